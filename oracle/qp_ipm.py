@@ -1,0 +1,321 @@
+"""Dense primal-dual interior-point QP solver (TEST INFRASTRUCTURE ONLY).
+
+The reference solves each rebalance date's QP through the third-party ``qpsolvers``
+package (``src/qp_problems.py:184-216``; default backend ``cvxopt``,
+``src/optimization.py:45``).  Neither ``qpsolvers`` (unpinned; the API used implies
+>= 3.x) nor any backend is present in the reference tree or in this image, so this
+module restates the published algorithm of cvxopt's ``coneqp`` for the nonnegative
+orthant: a Mehrotra predictor-corrector primal-dual path-following method on
+
+    min 0.5 x'Px + q'x   s.t.  Gx <= h,  Ax = b,  lb <= x <= ub
+
+followed by an active-set refinement (an exact equality-constrained solve on the
+detected active set) so that golden optima are accurate to ~1e-12 when P is PD on the
+active face.  The returned ``OracleSolution`` exposes the qpsolvers ``Solution``
+fields the reference reads (``found``, ``x``, ``obj``, ``y``, ``z``, ``z_box``) and the
+residual definitions of ``example/compare_solver.ipynb:212-216``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import scipy.linalg as sla
+
+
+@dataclass
+class OracleSolution:
+    P: np.ndarray
+    q: np.ndarray
+    G: np.ndarray | None
+    h: np.ndarray | None
+    A: np.ndarray | None
+    b: np.ndarray | None
+    lb: np.ndarray | None
+    ub: np.ndarray | None
+    x: np.ndarray | None = None
+    y: np.ndarray | None = None
+    z: np.ndarray | None = None
+    z_box: np.ndarray | None = None
+    found: bool = False
+    iterations: int = 0
+    extras: dict = field(default_factory=dict)
+
+    @property
+    def obj(self):
+        if self.x is None:
+            return None
+        return float(0.5 * self.x @ self.P @ self.x + self.q @ self.x)
+
+    def primal_residual(self) -> float:
+        """max(||Ax-b||inf, [Gx-h]+, [lb-x]+, [x-ub]+)  (compare_solver.ipynb:212-214)."""
+        x = self.x
+        r = 0.0
+        if self.A is not None:
+            r = max(r, float(np.max(np.abs(self.A @ x - self.b), initial=0.0)))
+        if self.G is not None:
+            r = max(r, float(np.max(np.maximum(self.G @ x - self.h, 0.0), initial=0.0)))
+        if self.lb is not None:
+            r = max(r, float(np.max(np.maximum(self.lb - x, 0.0), initial=0.0)))
+        if self.ub is not None:
+            r = max(r, float(np.max(np.maximum(x - self.ub, 0.0), initial=0.0)))
+        return r
+
+    def dual_residual(self) -> float:
+        """||Px + q + A'y + G'z + z_box||inf  (compare_solver.ipynb:215-216)."""
+        g = self.P @ self.x + self.q
+        if self.A is not None:
+            g = g + self.A.T @ self.y
+        if self.G is not None:
+            g = g + self.G.T @ self.z
+        if self.z_box is not None:
+            g = g + self.z_box
+        return float(np.max(np.abs(g)))
+
+    def duality_gap(self) -> float:
+        """|x'Px + q'x + b'y + h'z + lb'min(z_box,0) + ub'max(z_box,0)| (qpsolvers semantics)."""
+        x = self.x
+        gap = x @ self.P @ x + self.q @ x
+        if self.A is not None:
+            gap += self.b @ self.y
+        if self.G is not None:
+            gap += self.h @ self.z
+        if self.z_box is not None:
+            if self.lb is not None:
+                fin = np.isfinite(self.lb)
+                gap += self.lb[fin] @ np.minimum(self.z_box, 0.0)[fin]
+            if self.ub is not None:
+                fin = np.isfinite(self.ub)
+                gap += self.ub[fin] @ np.maximum(self.z_box, 0.0)[fin]
+        return float(abs(gap))
+
+
+def _as2d(M, n):
+    if M is None:
+        return None
+    M = np.asarray(M, dtype=np.float64)
+    return M.reshape(-1, n)
+
+
+def _kkt_solve(H, A, r1, r2, reg=0.0):
+    n = H.shape[0]
+    if A is None or A.shape[0] == 0:
+        M = H + reg * np.eye(n)
+        try:
+            return sla.solve(M, r1, assume_a="sym"), np.zeros(0)
+        except (sla.LinAlgError, ValueError):
+            return np.linalg.lstsq(M, r1, rcond=None)[0], np.zeros(0)
+    me = A.shape[0]
+    K = np.zeros((n + me, n + me))
+    K[:n, :n] = H + reg * np.eye(n)
+    K[:n, n:] = A.T
+    K[n:, :n] = A
+    if reg:
+        K[n:, n:] = -reg * np.eye(me)
+    rhs = np.concatenate([r1, r2])
+    try:
+        sol = sla.solve(K, rhs)
+        if not np.all(np.isfinite(sol)):
+            raise sla.LinAlgError
+    except (sla.LinAlgError, ValueError):
+        sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
+    return sol[:n], sol[n:]
+
+
+def solve_qp(P, q, G=None, h=None, A=None, b=None, lb=None, ub=None,
+             tol=1e-12, max_iter=200, refine=True) -> OracleSolution:
+    P = np.asarray(P, dtype=np.float64)
+    n = P.shape[0]
+    P = 0.5 * (P + P.T)
+    q = np.asarray(q, dtype=np.float64).reshape(n)
+    G = _as2d(G, n)
+    A = _as2d(A, n)
+    h = None if h is None else np.asarray(h, dtype=np.float64).reshape(-1)
+    b = None if b is None else np.asarray(b, dtype=np.float64).reshape(-1)
+    lb = None if lb is None else np.asarray(lb, dtype=np.float64).reshape(n)
+    ub = None if ub is None else np.asarray(ub, dtype=np.float64).reshape(n)
+    sol = OracleSolution(P, q, G, h, A, b, lb, ub)
+
+    # stacked inequalities  Gh x <= hh  :  [G; -I_L; I_U]
+    Lidx = np.flatnonzero(np.isfinite(lb)) if lb is not None else np.zeros(0, int)
+    Uidx = np.flatnonzero(np.isfinite(ub)) if ub is not None else np.zeros(0, int)
+    mi = 0 if G is None else G.shape[0]
+    rows = [G] if G is not None else []
+    hs = [h] if G is not None else []
+    if len(Lidx):
+        E = np.zeros((len(Lidx), n)); E[np.arange(len(Lidx)), Lidx] = -1.0
+        rows.append(E); hs.append(-lb[Lidx])
+    if len(Uidx):
+        E = np.zeros((len(Uidx), n)); E[np.arange(len(Uidx)), Uidx] = 1.0
+        rows.append(E); hs.append(ub[Uidx])
+    Gh = np.vstack(rows) if rows else np.zeros((0, n))
+    hh = np.concatenate(hs) if hs else np.zeros(0)
+    m = Gh.shape[0]
+    me = 0 if A is None else A.shape[0]
+    bb = np.zeros(0) if b is None else b
+
+    # initial point (coneqp style): [P A' Gh'; A 0 0; Gh 0 -I] [x;y;z] = [-q; b; hh]
+    H0 = P + Gh.T @ Gh
+    x, y = _kkt_solve(H0, A, -q + Gh.T @ hh, bb, reg=1e-12)
+    s = hh - Gh @ x
+    z = -s.copy()
+    if m:
+        a = -np.min(s)
+        if a >= -1e-8:
+            s = s + 1 + a
+        a = -np.min(z)
+        if a >= -1e-8:
+            z = z + 1 + a
+    nq = 1 + np.max(np.abs(q))
+    nb = 1 + (np.max(np.abs(bb)) if me else 0.0)
+    nh = 1 + (np.max(np.abs(hh)) if m else 0.0)
+    it = 0
+    best = (np.inf, None)
+    stall = 0
+    for it in range(1, max_iter + 1):
+        rd = P @ x + q + (A.T @ y if me else 0.0) + Gh.T @ z
+        rp = (A @ x - bb) if me else np.zeros(0)
+        ri = Gh @ x + s - hh
+        mu = (s @ z) / m if m else 0.0
+        pres = max(np.max(np.abs(rp), initial=0.0) / nb, np.max(np.abs(ri), initial=0.0) / nh)
+        dres = np.max(np.abs(rd)) / nq
+        gapr = mu * m / (1 + abs(0.5 * x @ P @ x + q @ x))
+        if pres < tol and dres < tol and gapr < tol:
+            break
+        merit = max(pres, dres, gapr)
+        if merit < 0.5 * best[0]:
+            best = (merit, (x.copy(), y.copy(), s.copy(), z.copy()))
+            stall = 0
+        else:
+            stall += 1
+            if stall >= 8:  # numerical floor reached: keep the best iterate
+                x, y, s, z = best[1]
+                break
+        w = z / s if m else np.zeros(0)
+        H = P + (Gh.T * w) @ Gh
+        reg = 1e-14 * (1 + np.max(np.abs(np.diag(H))))
+
+        def newton(rc):
+            # ds = -ri - Gh dx ; dz = (-rc + z*ri)/s + w*(Gh dx)
+            r1 = -rd - Gh.T @ ((-rc + z * ri) / s) if m else -rd
+            dx, dy = _kkt_solve(H, A, r1, -rp, reg=reg)
+            ds = -ri - Gh @ dx
+            dz = (-rc - z * ds) / s if m else np.zeros(0)
+            return dx, dy, ds, dz
+
+        def max_step(v, dv):
+            neg = dv < 0
+            if not np.any(neg):
+                return 1.0
+            return min(1.0, float(np.min(-v[neg] / dv[neg])))
+
+        if m:
+            dx_a, dy_a, ds_a, dz_a = newton(s * z)
+            a_aff = min(max_step(s, ds_a), max_step(z, dz_a))
+            mu_aff = ((s + a_aff * ds_a) @ (z + a_aff * dz_a)) / m
+            sigma = (mu_aff / mu) ** 3 if mu > 0 else 0.0
+            rc = s * z + ds_a * dz_a - sigma * mu
+            dx, dy, ds, dz = newton(rc)
+            a = min(1.0, 0.99 * min(max_step(s, ds), max_step(z, dz)))
+        else:
+            dx, dy, ds, dz = newton(np.zeros(0))
+            a = 1.0
+        x = x + a * dx
+        y = y + a * dy if me else y
+        s = s + a * ds
+        z = z + a * dz
+        if m:
+            s = np.maximum(s, 1e-300)
+            z = np.maximum(z, 1e-300)
+
+    zG = z[:mi] if mi else (np.zeros(0) if G is not None else None)
+    zbox = np.zeros(n)
+    if len(Lidx):
+        zbox[Lidx] -= z[mi:mi + len(Lidx)]
+    if len(Uidx):
+        zbox[Uidx] += z[mi + len(Lidx):]
+    sol.x, sol.y, sol.z = x, (y if me else (np.zeros(0) if A is not None else None)), zG
+    sol.z_box = zbox if (lb is not None or ub is not None) else None
+    sol.iterations = it
+    sol.found = bool(np.all(np.isfinite(x)))
+    if refine and sol.found:
+        _refine_active_set(sol)
+    sol.extras["kkt_primal"] = sol.primal_residual()
+    sol.extras["kkt_dual"] = sol.dual_residual()
+    return sol
+
+
+def _refine_active_set(sol: OracleSolution, max_rounds: int = 30):
+    """Exact solve on the detected active set (a short primal-dual active-set loop started
+    from the IPM classification); kept only if it improves the KKT residuals."""
+    P, q, G, h, A, b, lb, ub = sol.P, sol.q, sol.G, sol.h, sol.A, sol.b, sol.lb, sol.ub
+    n = P.shape[0]
+    x = sol.x
+    lo = np.full(n, -np.inf) if lb is None else lb
+    up = np.full(n, np.inf) if ub is None else ub
+    zbox = np.zeros(n) if sol.z_box is None else sol.z_box
+    at_lo = np.isfinite(lo) & (x - lo < -zbox)
+    at_up = np.isfinite(up) & (up - x < zbox) & ~at_lo
+    mi = 0 if G is None else G.shape[0]
+    act_G = np.zeros(mi, bool)
+    if mi:
+        act_G = (h - G @ x) < sol.z
+    me = 0 if A is None else A.shape[0]
+    best = None
+    for _ in range(max_rounds):
+        fixed = at_lo | at_up
+        xb = np.where(at_lo, lo, np.where(at_up, up, 0.0))
+        F = np.flatnonzero(~fixed)
+        Bi = np.flatnonzero(fixed)
+        rowsC, rhsC = [], []
+        if me:
+            rowsC.append(A); rhsC.append(b)
+        if act_G.any():
+            rowsC.append(G[act_G]); rhsC.append(h[act_G])
+        C = np.vstack(rowsC) if rowsC else np.zeros((0, n))
+        d = np.concatenate(rhsC) if rhsC else np.zeros(0)
+        rF = -q[F] - (P[np.ix_(F, Bi)] @ xb[Bi] if len(Bi) else 0.0)
+        dF = d - (C[:, Bi] @ xb[Bi] if len(Bi) else 0.0)
+        xF, lam = _kkt_solve(P[np.ix_(F, F)], C[:, F] if C.shape[0] else None, rF, dF)
+        xn = xb.copy()
+        xn[F] = xF
+        y = lam[:me] if me else None
+        zG = np.zeros(mi)
+        if act_G.any():
+            zG[act_G] = lam[me:]
+        g = P @ xn + q
+        if me:
+            g = g + A.T @ y
+        if mi:
+            g = g + G.T @ zG
+        zb = np.where(fixed, -g, 0.0)
+        tol = 1e-12 * (1 + np.max(np.abs(q)))
+        viol_lo = (~fixed) & (xn < lo - 1e-13)
+        viol_up = (~fixed) & (xn > up + 1e-13)
+        bad_lo = at_lo & (zb > tol)
+        bad_up = at_up & (zb < -tol)
+        viol_G = (~act_G) & ((G @ xn - h) > 1e-13) if mi else np.zeros(0, bool)
+        bad_G = act_G & (zG < -tol) if mi else np.zeros(0, bool)
+        if not (viol_lo.any() or viol_up.any() or bad_lo.any() or bad_up.any()
+                or viol_G.any() or bad_G.any()):
+            best = (xn, y, zG, zb)
+            break
+        # add the worst primal violators, release wrong-sign duals
+        at_lo = (at_lo & ~bad_lo) | viol_lo
+        at_up = (at_up & ~bad_up) | viol_up
+        if mi:
+            act_G = (act_G & ~bad_G) | viol_G
+    if best is None:
+        sol.extras["refined"] = False
+        return
+    cand = OracleSolution(P, q, G, h, A, b, lb, ub)
+    cand.x, cand.y = best[0], (best[1] if A is not None else None)
+    cand.z = best[2] if G is not None else None
+    cand.z_box = best[3] if sol.z_box is not None else None
+    old = max(sol.primal_residual(), sol.dual_residual())
+    new = max(cand.primal_residual(), cand.dual_residual())
+    if np.all(np.isfinite(cand.x)) and new <= max(old, 1e-12):
+        sol.x, sol.y, sol.z, sol.z_box = cand.x, cand.y, cand.z, cand.z_box
+        sol.extras["refined"] = True
+    else:
+        sol.extras["refined"] = False
