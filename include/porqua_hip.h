@@ -1,0 +1,140 @@
+/*
+ * porqua_hip.h -- C ABI of the MI355X (gfx950) engine for PorQua's backtest hot path.
+ *
+ * The reference (amolrpatil21/PorQua) is pure Python; each rebalance date estimates a
+ * covariance / Gram matrix and hands one dense QP to the third-party `qpsolvers`.
+ * This library replaces that per-date arithmetic with batched HIP kernels.  Every entry
+ * point names the reference interface it stands in for.  Conventions:
+ *   - all matrices FP64 row-major, device pointers owned by the caller (PyTorch-ROCm);
+ *   - square per-problem matrices use a leading dimension `ld` = round_up(n, 64) with a
+ *     zero-filled padding region; per-problem vectors use stride `ld` as well;
+ *   - `stream` is a hipStream_t passed as void*;  return 0 on success, < 0 on an
+ *     argument / HIP error (message via pq_last_error());  nothing throws across the ABI;
+ *   - the library allocates nothing persistent and keeps no global mutable state besides
+ *     the thread-local error string (reentrant; one device per call = the current one).
+ */
+#ifndef PORQUA_HIP_H
+#define PORQUA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PQ_VERSION 100
+
+/* per-problem status codes (pq_state.status) */
+#define PQ_UNSOLVED 0
+#define PQ_SOLVED 1             /* ADMM converged and the polished point passed its checks */
+#define PQ_SOLVED_INACCURATE 2  /* ADMM converged, polish rejected: ADMM point returned   */
+#define PQ_MAX_ITER 3
+#define PQ_NEED_REFACTOR 4      /* internal: adaptive rho asks for a new K^-1            */
+#define PQ_PRIMAL_INFEASIBLE (-3)
+#define PQ_DUAL_INFEASIBLE (-4)
+#define PQ_NON_CONVEX (-5)      /* KKT Cholesky failed                                   */
+
+/* per-problem output record (pq_state.out, PQ_OUT_FIELDS doubles each) */
+#define PQ_OUT_OBJ 0        /* 0.5 x'Px + q'x (no constant; test:72,82)               */
+#define PQ_OUT_PRIM 1       /* qpsolvers primal_residual()                              */
+#define PQ_OUT_DUAL 2       /* qpsolvers dual_residual()                                */
+#define PQ_OUT_GAP 3        /* qpsolvers duality_gap()                                  */
+#define PQ_OUT_RHO 4
+#define PQ_OUT_NFREE 5      /* variables strictly inside their box after polish         */
+#define PQ_OUT_ROUNDS 6     /* polish active-set rounds                                 */
+#define PQ_OUT_FIELDS 8
+
+/* polish scratch per problem (doubles) */
+#define PQ_WORK_DOUBLES(ld, mg_pad) ((int64_t)(5 + (mg_pad)) * (ld) + 512)
+
+/* A batch of dense QPs   min 0.5 x'Px + q'x  s.t.  lg <= Cg x <= ug,  lb <= x <= ub
+ * (the QuadraticProgram fields P, q, G, h, A, b, lb, ub of src/qp_problems.py:34-38 with
+ * A / G stacked into Cg: equality rows have lg == ug, G rows have lg = -inf).
+ * Effective P = p_scale[b] * P_b + p_diag[b] * I (p_scale / p_diag may be NULL).     */
+typedef struct pq_problem {
+  int32_t n, ld, batch, mg;
+  const double* P;   int64_t P_stride;
+  const double* p_scale;
+  const double* p_diag;
+  const double* q;   int64_t q_stride;
+  const double* Cg;  int64_t Cg_stride;   /* mg x ld per problem; stride 0 = shared   */
+  const double* lg;  const double* ug;  int64_t g_stride;    /* mg; stride 0 = shared */
+  const double* lb;  const double* ub;  int64_t box_stride;  /* ld; NULL = unbounded   */
+} pq_problem;
+
+/* Solver state / workspace, all device memory, indexed by problem id b < batch.       */
+typedef struct pq_state {
+  double* K;     int64_t K_stride;      /* ld x ld: KKT -> L -> K^-1 -> polish scratch  */
+  double* Dt;    int64_t Dt_stride;     /* (ld/64) x 64 x 64 transposed diag-block inverses */
+  double* x;     double* Px;            /* ld per problem                                 */
+  double* z;     double* y;             /* m_ld per problem: Cg rows at [0,mg), box at [mg_pad, mg_pad+n) */
+  int32_t m_ld, mg_pad;
+  double* rho;                          /* per problem                                    */
+  int32_t* iters; int32_t* status; int32_t* info;
+  double* out;                          /* PQ_OUT_FIELDS per problem                      */
+  double* work;  int64_t work_stride;   /* >= PQ_WORK_DOUBLES(ld, mg_pad) per problem      */
+} pq_state;
+
+typedef struct pq_settings {
+  double rho0, sigma, alpha, eps_abs, eps_rel, rho_min, rho_max, adapt_tol, eq_scale, delta,
+      dual_tol;
+  int32_t max_iter, adapt_interval, polish, polish_rounds, refine_iters;
+} pq_settings;
+
+int pq_version(void);
+const char* pq_last_error(void);
+
+/* Column means of each date's window (rows[b][0..tlen[b]) of the panel) -- the first pass
+ * of np.cov's two-pass algorithm behind DataFrame.cov() (src/covariance.py:65-66).      */
+int pq_window_mean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                   const int32_t* tlen, int32_t tmax, int32_t batch, double* mu,
+                   int64_t mu_stride, void* stream);
+
+/* K1: batched windowed SYRK on FP64 MFMA.  mode 0: centred covariance with ddof=1
+ * (Covariance.estimate 'pearson', src/covariance.py:40-56,65-66); mode 1: uncentred Gram
+ * X'X (LeastSquares.set_objective, src/optimization.py:215).  out: batch x ld x ld.     */
+int pq_cov_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                   const int32_t* tlen, int32_t tmax, int32_t batch, int32_t mode,
+                   const double* mu, int64_t mu_stride, double* out, int32_t ld,
+                   int64_t out_stride, void* stream);
+
+/* X'y and y'y of each window (LeastSquares q = -2 X'y, constant = y'y,
+ * src/optimization.py:216-217).                                                        */
+int pq_gram_xy_batched(const double* panel, int64_t ldp, int32_t n, const double* bm,
+                       const int32_t* rows, const int32_t* tlen, int32_t tmax, int32_t batch,
+                       double* xty, int64_t xty_stride, double* yty, void* stream);
+
+/* Geometric mean exp(mean(log1p X)) - 1 over each window (MeanEstimator.estimate_geometric,
+ * src/mean_estimation.py:39-48).                                                       */
+int pq_window_geomean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                      const int32_t* tlen, int32_t tmax, int32_t batch, double* mu,
+                      int64_t mu_stride, void* stream);
+
+/* Reset x, z, y, Px, iterations, status and set rho = settings.rho0 for problems idx[]. */
+int pq_init_state(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                  const pq_settings* s, void* stream);
+
+/* K2: form K = P_eff + sigma I + Cg' R Cg + R_box for the current rho, factor it with a
+ * batched blocked Cholesky on FP64 MFMA (info[] = first failing column + 1, the isPD test
+ * of src/helper_functions.py:61-67), and if `invert` overwrite K with K^-1 (trtri+lauum).
+ * With mg = 0, lb = ub = NULL and sigma = 0 this is a plain batched potrf of P_eff.     */
+int pq_factor_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                      const pq_settings* s, int32_t invert, void* stream);
+
+/* K3: up to `iters_this_call` OSQP-style ADMM iterations per problem idx[] (stops a
+ * problem at convergence, at settings.max_iter, or when adaptive rho requests a
+ * refactorisation: status PQ_NEED_REFACTOR and rho[] already updated).
+ * Replaces qpsolvers.solve_problem (src/qp_problems.py:211-214).                        */
+int pq_admm_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                    const pq_settings* s, int32_t iters_this_call, void* stream);
+
+/* K4: active-set polish of the ADMM point (reduced KKT by masked Cholesky + Schur +
+ * proximal iterative refinement), then exact residuals / objective of the final point
+ * into out[] (Solution.obj / primal_residual / dual_residual / duality_gap).            */
+int pq_polish_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                      const pq_settings* s, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -124,6 +124,25 @@ def _kkt_solve(H, A, r1, r2, reg=0.0):
 
 def solve_qp(P, q, G=None, h=None, A=None, b=None, lb=None, ub=None,
              tol=1e-12, max_iter=200, refine=True) -> OracleSolution:
+    """Solve with the objective scaled to unit magnitude (tolerances are then relative),
+    and report x / duals of the original problem."""
+    P = np.asarray(P, dtype=np.float64)
+    q = np.asarray(q, dtype=np.float64).reshape(-1)
+    s = max(float(np.max(np.abs(P), initial=0.0)), float(np.max(np.abs(q), initial=0.0)))
+    s = 1.0 if s == 0.0 or not np.isfinite(s) else 1.0 / s
+    sol = _solve_qp_scaled(P * s, q * s, G, h, A, b, lb, ub, tol, max_iter, refine)
+    out = OracleSolution(np.asarray(P, dtype=np.float64), q, sol.G, sol.h, sol.A, sol.b,
+                         sol.lb, sol.ub)
+    out.x, out.found, out.iterations, out.extras = sol.x, sol.found, sol.iterations, sol.extras
+    out.y = None if sol.y is None else sol.y / s
+    out.z = None if sol.z is None else sol.z / s
+    out.z_box = None if sol.z_box is None else sol.z_box / s
+    out.extras["kkt_primal"] = out.primal_residual()
+    out.extras["kkt_dual"] = out.dual_residual()
+    return out
+
+
+def _solve_qp_scaled(P, q, G, h, A, b, lb, ub, tol, max_iter, refine) -> OracleSolution:
     P = np.asarray(P, dtype=np.float64)
     n = P.shape[0]
     P = 0.5 * (P + P.T)
@@ -193,7 +212,7 @@ def solve_qp(P, q, G=None, h=None, A=None, b=None, lb=None, ub=None,
                 break
         w = z / s if m else np.zeros(0)
         H = P + (Gh.T * w) @ Gh
-        reg = 1e-14 * (1 + np.max(np.abs(np.diag(H))))
+        reg = 0.0
 
         def newton(rc):
             # ds = -ri - Gh dx ; dz = (-rc + z*ri)/s + w*(Gh dx)

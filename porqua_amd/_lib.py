@@ -1,0 +1,125 @@
+"""ctypes binding of the in-tree HIP library ``libporqua_hip.so`` (see include/porqua_hip.h).
+
+The product path has no CPU fallback: if the library is missing or no GPU is visible the
+calls raise ``PorquaHipError``.  Structures mirror the C ABI field for field.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libporqua_hip.so")
+
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_dp = ctypes.c_void_p   # device pointers are passed as plain integers
+
+PQ_UNSOLVED = 0
+PQ_SOLVED = 1
+PQ_SOLVED_INACCURATE = 2
+PQ_MAX_ITER = 3
+PQ_NEED_REFACTOR = 4
+PQ_PRIMAL_INFEASIBLE = -3
+PQ_DUAL_INFEASIBLE = -4
+PQ_NON_CONVEX = -5
+
+PQ_OUT_OBJ, PQ_OUT_PRIM, PQ_OUT_DUAL, PQ_OUT_GAP, PQ_OUT_RHO, PQ_OUT_NFREE, PQ_OUT_ROUNDS = range(7)
+PQ_OUT_FIELDS = 8
+
+
+def work_doubles(ld: int, mg_pad: int) -> int:
+    """PQ_WORK_DOUBLES of include/porqua_hip.h."""
+    return (5 + mg_pad) * ld + 512
+
+
+class PorquaHipError(RuntimeError):
+    pass
+
+
+class PQProblem(ctypes.Structure):
+    _fields_ = [
+        ("n", c_int32), ("ld", c_int32), ("batch", c_int32), ("mg", c_int32),
+        ("P", c_dp), ("P_stride", c_int64),
+        ("p_scale", c_dp), ("p_diag", c_dp),
+        ("q", c_dp), ("q_stride", c_int64),
+        ("Cg", c_dp), ("Cg_stride", c_int64),
+        ("lg", c_dp), ("ug", c_dp), ("g_stride", c_int64),
+        ("lb", c_dp), ("ub", c_dp), ("box_stride", c_int64),
+    ]
+
+
+class PQState(ctypes.Structure):
+    _fields_ = [
+        ("K", c_dp), ("K_stride", c_int64),
+        ("Dt", c_dp), ("Dt_stride", c_int64),
+        ("x", c_dp), ("Px", c_dp),
+        ("z", c_dp), ("y", c_dp),
+        ("m_ld", c_int32), ("mg_pad", c_int32),
+        ("rho", c_dp),
+        ("iters", c_dp), ("status", c_dp), ("info", c_dp),
+        ("out", c_dp),
+        ("work", c_dp), ("work_stride", c_int64),
+    ]
+
+
+class PQSettings(ctypes.Structure):
+    _fields_ = [
+        ("rho0", ctypes.c_double), ("sigma", ctypes.c_double), ("alpha", ctypes.c_double),
+        ("eps_abs", ctypes.c_double), ("eps_rel", ctypes.c_double),
+        ("rho_min", ctypes.c_double), ("rho_max", ctypes.c_double),
+        ("adapt_tol", ctypes.c_double), ("eq_scale", ctypes.c_double),
+        ("delta", ctypes.c_double), ("dual_tol", ctypes.c_double),
+        ("max_iter", c_int32), ("adapt_interval", c_int32), ("polish", c_int32),
+        ("polish_rounds", c_int32), ("refine_iters", c_int32),
+    ]
+
+
+_EXPORTS = {
+    "pq_version": ([], c_int32),
+    "pq_last_error": ([], ctypes.c_char_p),
+    "pq_window_mean": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_dp], c_int32),
+    "pq_window_geomean": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_dp], c_int32),
+    "pq_cov_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_int32, c_dp, c_int64,
+                        c_dp, c_int32, c_int64, c_dp], c_int32),
+    "pq_gram_xy_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64,
+                            c_dp, c_dp], c_int32),
+    "pq_init_state": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
+                       ctypes.POINTER(PQSettings), c_dp], c_int32),
+    "pq_factor_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
+                           ctypes.POINTER(PQSettings), c_int32, c_dp], c_int32),
+    "pq_admm_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
+                         ctypes.POINTER(PQSettings), c_int32, c_dp], c_int32),
+    "pq_polish_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
+                           ctypes.POINTER(PQSettings), c_dp], c_int32),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library (raises PorquaHipError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PorquaHipError(
+            f"{LIB_PATH} not found: build it with `make -C porqua_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (args, res) in _EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_EXPORTS)
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().pq_last_error().decode(errors="replace")
+        raise PorquaHipError(f"{what} failed (rc={rc}): {msg}")

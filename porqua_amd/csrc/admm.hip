@@ -1,0 +1,379 @@
+// K3: batched OSQP-style ADMM, one 512-thread workgroup per QP, iterations inside the
+// kernel with per-problem convergence (a converged problem's workgroup simply exits).
+//
+// Per iteration the only O(n^2) work is x~ = K^-1 rhs: every row of K^-1 (8 B x ld per
+// row, the whole matrix per iteration) is streamed from HBM exactly once with 16-byte
+// coalesced loads in "axpy" form -- wave w accumulates rhs_j * K^-1[j, :] for rows
+// j = w (mod 8) in registers (lane l owns columns 128 q + 2 l, 2 l + 1) -- and the eight
+// partial vectors are combined by a fixed-order LDS tree (bit-reproducible).  Everything
+// else is O(n + mg n) and lives in LDS: x, Px, z, y, rhs, q, bounds.
+//
+// P x is never formed with another mat-vec: K x~ = rhs gives P x~ = rhs - sigma x~ -
+// C'R C x~, and P x_{k+1} = alpha P x~ + (1 - alpha) P x_k, so the OSQP residuals and
+// the adaptive-rho estimate are evaluated every iteration for O(n).
+//
+// Replaces qpsolvers.solve_problem(...) (src/qp_problems.py:211-214) for the dense QPs
+// PorQua builds in Optimization.model_qpsolvers (src/optimization.py:91-143).
+#include "common.h"
+#include "capi_util.h"
+
+namespace pq {
+
+constexpr int AT = 512;   // threads per ADMM workgroup
+constexpr int AW = AT / 64;
+
+__device__ __forceinline__ double rho_row(double l, double u, double rho, const pq_settings& s) {
+  if (l == u) return rho * s.eq_scale;
+  if (isinf(l) && isinf(u)) return s.rho_min;
+  return rho;
+}
+
+// multi-value workgroup max: v[0..NV) per thread -> out[0..NV) for every thread
+template <int NV>
+__device__ __forceinline__ void block_maxv(double (&v)[NV], double* red) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = wave_max(v[k]);
+  __syncthreads();
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) red[k * AW + wave_id()] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double m = red[k * AW];
+    for (int w = 1; w < AW; ++w) m = fmax(m, red[k * AW + w]);
+    v[k] = m;
+  }
+}
+
+// dot products of the mg general rows with an LDS vector: out[r] = Cg[r] . v
+__device__ void rows_dot(const double* Cg, int64_t ld, int mg, int n, const double* v, double* out) {
+  const int w = wave_id(), l = lane_id();
+  for (int r = w; r < mg; r += AW) {
+    const double* c = Cg + (int64_t)r * ld;
+    double s = 0.0;
+    for (int i = l; i < n; i += 64) s += c[i] * v[i];
+    s = wave_sum(s);
+    if (l == 0) out[r] = s;
+  }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const int32_t* idx,
+                                             int nidx, pq_settings s, int iters_call) {
+  constexpr int LDMAX = NQ * 128;
+  __shared__ __attribute__((aligned(16))) double sm[9 * LDMAX + 4 * LDMAX + 8 * 64 + 16 * AW];
+  double* x = sm;
+  double* Px = x + LDMAX;
+  double* zb = Px + LDMAX;
+  double* yb = zb + LDMAX;
+  double* q = yb + LDMAX;
+  double* rhs = q + LDMAX;
+  double* xt = rhs + LDMAX;
+  double* lo = xt + LDMAX;
+  double* up = lo + LDMAX;
+  double* tree = up + LDMAX;       // 4 * LDMAX partial-vector scratch
+  double* zg = tree + 4 * LDMAX;   // mg <= 64 each
+  double* yg = zg + 64;
+  double* rg = yg + 64;
+  double* wg = rg + 64;            // rho z - y for the general rows
+  double* ztg = wg + 64;
+  double* cgx = ztg + 64;
+  double* lgs = cgx + 64;
+  double* ugs = lgs + 64;
+  double* red = ugs + 64;          // 16 * AW
+
+  const int b = idx ? idx[blockIdx.x] : (int)blockIdx.x;
+  if (st.status[b] != PQ_UNSOLVED && st.status[b] != PQ_NEED_REFACTOR) return;
+  const int n = pb.n, ld = pb.ld, mg = pb.mg;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const double* Kinv = st.K + (int64_t)b * st.K_stride;
+  const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
+  const bool has_box = pb.lb != nullptr;
+  double rho = st.rho[b];
+  const double sigma = s.sigma, alpha = s.alpha;
+
+  // ---- load state -----------------------------------------------------------------
+  {
+    const double* gq = pb.q + (int64_t)b * pb.q_stride;
+    const double* gx = st.x + (int64_t)b * ld;
+    const double* gpx = st.Px + (int64_t)b * ld;
+    const double* gz = st.z + (int64_t)b * st.m_ld + st.mg_pad;
+    const double* gy = st.y + (int64_t)b * st.m_ld + st.mg_pad;
+    const double* glb = has_box ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
+    const double* gub = has_box ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
+    for (int i = t; i < LDMAX; i += AT) {
+      const bool v = i < n;
+      x[i] = v ? gx[i] : 0.0;
+      Px[i] = v ? gpx[i] : 0.0;
+      zb[i] = v && has_box ? gz[i] : 0.0;
+      yb[i] = v && has_box ? gy[i] : 0.0;
+      q[i] = v ? gq[i] : 0.0;
+      lo[i] = v && has_box ? glb[i] : -INFINITY;
+      up[i] = v && has_box ? gub[i] : INFINITY;
+    }
+    if (t < mg) {
+      const double* gzg = st.z + (int64_t)b * st.m_ld;
+      const double* gyg = st.y + (int64_t)b * st.m_ld;
+      const double lgv = pb.lg[(int64_t)b * pb.g_stride + t];
+      const double ugv = pb.ug[(int64_t)b * pb.g_stride + t];
+      zg[t] = gzg[t];
+      yg[t] = gyg[t];
+      lgs[t] = lgv;
+      ugs[t] = ugv;
+      rg[t] = rho_row(lgv, ugv, rho, s);
+    }
+  }
+  __syncthreads();
+  if (mg) rows_dot(Cg, ld, mg, n, x, cgx);
+  __syncthreads();
+
+  int it = st.iters[b];
+  int status = PQ_UNSOLVED;
+  const int it_end = min(s.max_iter, it + iters_call);
+  while (it < it_end) {
+    ++it;
+    // ---- rhs = sigma x - q + C'(R z - y) ------------------------------------------
+    if (t < mg) wg[t] = rg[t] * zg[t] - yg[t];
+    __syncthreads();
+    for (int i = t; i < n; i += AT) {
+      double r = sigma * x[i] - q[i];
+      if (has_box) r += rho_row(lo[i], up[i], rho, s) * zb[i] - yb[i];
+      for (int k = 0; k < mg; ++k) r += Cg[(int64_t)k * ld + i] * wg[k];
+      rhs[i] = r;
+    }
+    for (int i = n + t; i < LDMAX; i += AT) rhs[i] = 0.0;
+    __syncthreads();
+    // ---- x~ = K^-1 rhs (the HBM stream) ---------------------------------------------
+    double2 acc[NQ];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) acc[qq] = double2{0.0, 0.0};
+    {
+      int j = w;
+      for (; j + AW < n; j += 2 * AW) {
+        const double2* r0 = reinterpret_cast<const double2*>(Kinv + (int64_t)j * ld) + l;
+        const double2* r1 = reinterpret_cast<const double2*>(Kinv + (int64_t)(j + AW) * ld) + l;
+        double2 v0[NQ], v1[NQ];
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const bool ok = 128 * qq + 2 * l < n;
+          v0[qq] = ok ? r0[64 * qq] : double2{0.0, 0.0};
+          v1[qq] = ok ? r1[64 * qq] : double2{0.0, 0.0};
+        }
+        const double a0 = rhs[j], a1 = rhs[j + AW];
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          acc[qq].x = fma(a0, v0[qq].x, acc[qq].x);
+          acc[qq].y = fma(a0, v0[qq].y, acc[qq].y);
+          acc[qq].x = fma(a1, v1[qq].x, acc[qq].x);
+          acc[qq].y = fma(a1, v1[qq].y, acc[qq].y);
+        }
+      }
+      if (j < n) {
+        const double2* r0 = reinterpret_cast<const double2*>(Kinv + (int64_t)j * ld) + l;
+        const double a0 = rhs[j];
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const double2 v = (128 * qq + 2 * l < n) ? r0[64 * qq] : double2{0.0, 0.0};
+          acc[qq].x = fma(a0, v.x, acc[qq].x);
+          acc[qq].y = fma(a0, v.y, acc[qq].y);
+        }
+      }
+    }
+    // fixed-order tree: waves 4-7 -> 0-3 -> 0-1 -> 0
+#pragma unroll
+    for (int half = AW / 2; half >= 1; half >>= 1) {
+      if (w >= half && w < 2 * half) {
+        double2* dst = reinterpret_cast<double2*>(tree + (w - half) * LDMAX) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
+      }
+      __syncthreads();
+      if (w < half) {
+        const double2* src = reinterpret_cast<const double2*>(tree + w * LDMAX) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const double2 v = src[64 * qq];
+          acc[qq].x += v.x;
+          acc[qq].y += v.y;
+        }
+      }
+      __syncthreads();
+    }
+    if (w == 0) {
+      double2* dst = reinterpret_cast<double2*>(xt) + l;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
+    }
+    __syncthreads();
+    // ---- z~ for the general rows ----------------------------------------------------
+    if (mg) rows_dot(Cg, ld, mg, n, xt, ztg);
+    __syncthreads();
+    // ---- updates and residual terms --------------------------------------------------
+    double mv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // mv: 0 |Cx - z|, 1 |Cx|, 2 |z|, 3 |Px + q + C'y|, 4 |Px|, 5 |C'y|, 6 |q|
+    for (int i = t; i < n; i += AT) {
+      const double xti = xt[i];
+      double pxt = rhs[i] - sigma * xti;
+      double rb = 0.0;
+      if (has_box) {
+        rb = rho_row(lo[i], up[i], rho, s);
+        pxt -= rb * xti;
+      }
+      for (int k = 0; k < mg; ++k) pxt -= Cg[(int64_t)k * ld + i] * rg[k] * ztg[k];
+      const double xn = alpha * xti + (1.0 - alpha) * x[i];
+      const double pxn = alpha * pxt + (1.0 - alpha) * Px[i];
+      x[i] = xn;
+      Px[i] = pxn;
+      double cty = 0.0;
+      if (has_box) {
+        const double zh = alpha * xti + (1.0 - alpha) * zb[i];
+        const double zn = fmin(fmax(zh + yb[i] / rb, lo[i]), up[i]);
+        const double yn = yb[i] + rb * (zh - zn);
+        zb[i] = zn;
+        yb[i] = yn;
+        cty = yn;
+        mv[0] = fmax(mv[0], fabs(xn - zn));
+        mv[1] = fmax(mv[1], fabs(xn));
+        mv[2] = fmax(mv[2], fabs(zn));
+      }
+      mv[4] = fmax(mv[4], fabs(pxn));
+      mv[6] = fmax(mv[6], fabs(q[i]));
+      // general-row part of C'y is added below once yg is updated
+      rhs[i] = pxn + q[i] + cty;   // reuse rhs as the dual-residual accumulator
+      xt[i] = cty;                 // reuse xt as C'y accumulator
+    }
+    __syncthreads();
+    if (t < mg) {
+      const double zh = alpha * ztg[t] + (1.0 - alpha) * zg[t];
+      const double zn = fmin(fmax(zh + yg[t] / rg[t], lgs[t]), ugs[t]);
+      yg[t] = yg[t] + rg[t] * (zh - zn);
+      zg[t] = zn;
+      cgx[t] = alpha * ztg[t] + (1.0 - alpha) * cgx[t];
+    }
+    __syncthreads();
+    if (t < mg) {
+      mv[0] = fmax(mv[0], fabs(cgx[t] - zg[t]));
+      mv[1] = fmax(mv[1], fabs(cgx[t]));
+      mv[2] = fmax(mv[2], fabs(zg[t]));
+    }
+    for (int i = t; i < n; i += AT) {
+      double cy = xt[i];
+      for (int k = 0; k < mg; ++k) cy += Cg[(int64_t)k * ld + i] * yg[k];
+      const double dres = rhs[i] + (cy - xt[i]);
+      mv[3] = fmax(mv[3], fabs(dres));
+      mv[5] = fmax(mv[5], fabs(cy));
+    }
+    block_maxv<8>(mv, red);
+    const double eps_p = s.eps_abs + s.eps_rel * fmax(mv[1], mv[2]);
+    const double eps_d = s.eps_abs + s.eps_rel * fmax(mv[4], fmax(mv[5], mv[6]));
+    if (mv[0] <= eps_p && mv[3] <= eps_d) {
+      status = PQ_SOLVED;
+      break;
+    }
+    if (s.adapt_interval > 0 && it % s.adapt_interval == 0) {
+      const double rp = mv[0] / (fmax(mv[1], mv[2]) + 1e-30);
+      const double rd = mv[3] / (fmax(mv[4], fmax(mv[5], mv[6])) + 1e-30);
+      double rn = rho * sqrt(rp / (rd + 1e-30));
+      rn = fmin(fmax(rn, s.rho_min), s.rho_max);
+      if (rn > rho * s.adapt_tol || rn < rho / s.adapt_tol) {
+        rho = rn;
+        status = PQ_NEED_REFACTOR;
+        break;
+      }
+    }
+    __syncthreads();
+  }
+  if (status == PQ_UNSOLVED && it >= s.max_iter) status = PQ_MAX_ITER;
+  __syncthreads();
+  // ---- save state --------------------------------------------------------------------
+  {
+    double* gx = st.x + (int64_t)b * ld;
+    double* gpx = st.Px + (int64_t)b * ld;
+    double* gz = st.z + (int64_t)b * st.m_ld;
+    double* gy = st.y + (int64_t)b * st.m_ld;
+    for (int i = t; i < n; i += AT) {
+      gx[i] = x[i];
+      gpx[i] = Px[i];
+      if (has_box) {
+        gz[st.mg_pad + i] = zb[i];
+        gy[st.mg_pad + i] = yb[i];
+      }
+    }
+    if (t < mg) {
+      gz[t] = zg[t];
+      gy[t] = yg[t];
+    }
+    if (t == 0) {
+      st.iters[b] = it;
+      st.status[b] = status;
+      st.rho[b] = rho;
+    }
+  }
+}
+
+__global__ void k_init_state(pq_problem pb, pq_state st, const int32_t* idx, pq_settings s) {
+  const int b = idx ? idx[blockIdx.x] : (int)blockIdx.x;
+  const int ld = pb.ld;
+  for (int i = threadIdx.x; i < ld; i += blockDim.x) {
+    st.x[(int64_t)b * ld + i] = 0.0;
+    st.Px[(int64_t)b * ld + i] = 0.0;
+  }
+  for (int i = threadIdx.x; i < st.m_ld; i += blockDim.x) {
+    st.z[(int64_t)b * st.m_ld + i] = 0.0;
+    st.y[(int64_t)b * st.m_ld + i] = 0.0;
+  }
+  if (threadIdx.x == 0) {
+    st.rho[b] = s.rho0;
+    st.iters[b] = 0;
+    st.status[b] = PQ_UNSOLVED;
+    st.info[b] = 0;
+    for (int k = 0; k < PQ_OUT_FIELDS; ++k) st.out[(int64_t)b * PQ_OUT_FIELDS + k] = 0.0;
+  }
+}
+
+}  // namespace pq
+
+extern "C" int pq_init_state(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                             const pq_settings* s, void* stream) {
+  PQ_CHECK_ARG(pb && st && s, "pq_init_state: null argument");
+  PQ_CHECK_ARG(st->x && st->Px && st->z && st->y && st->rho && st->iters && st->status &&
+                   st->info && st->out, "pq_init_state: state buffers missing");
+  PQ_CHECK_ARG(st->m_ld >= st->mg_pad + pb->ld && st->mg_pad >= pb->mg, "pq_init_state: bad m_ld / mg_pad");
+  const int grid = idx ? nidx : pb->batch;
+  if (grid <= 0) return 0;
+  hipLaunchKernelGGL(pq::k_init_state, dim3(grid), dim3(256), 0, (hipStream_t)stream, *pb, *st, idx, *s);
+  PQ_CHECK_LAUNCH("pq_init_state");
+  return 0;
+}
+
+extern "C" int pq_admm_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                               const pq_settings* s, int32_t iters_this_call, void* stream) {
+  PQ_CHECK_ARG(pb && st && s, "pq_admm_batched: null argument");
+  PQ_CHECK_ARG(pb->ld % 128 == 0 || pb->ld % 64 == 0, "pq_admm_batched: bad ld");
+  PQ_CHECK_ARG(pb->mg <= 64, "pq_admm_batched: mg must be <= 64");
+  PQ_CHECK_ARG(pb->mg == 0 || (pb->Cg && pb->lg && pb->ug), "pq_admm_batched: Cg/lg/ug missing");
+  const int grid = idx ? nidx : pb->batch;
+  if (grid <= 0) return 0;
+  const int nq = (pb->n + 127) / 128;
+  hipStream_t str = (hipStream_t)stream;
+#define PQ_ADMM_CASE(NQV) \
+  case NQV: hipLaunchKernelGGL(pq::k_admm<NQV>, dim3(grid), dim3(pq::AT), 0, str, *pb, *st, idx, nidx, *s, iters_this_call); break;
+  switch (nq) {
+    PQ_ADMM_CASE(1)
+    PQ_ADMM_CASE(2)
+    PQ_ADMM_CASE(3)
+    PQ_ADMM_CASE(4)
+    PQ_ADMM_CASE(5)
+    PQ_ADMM_CASE(6)
+    PQ_ADMM_CASE(7)
+    PQ_ADMM_CASE(8)
+    default:
+      pq::set_error("pq_admm_batched: n=%d exceeds the LDS-resident limit of 1024", pb->n);
+      return -1;
+  }
+#undef PQ_ADMM_CASE
+  PQ_CHECK_LAUNCH("pq_admm_batched");
+  return 0;
+}

@@ -1,0 +1,203 @@
+// K1: batched windowed covariance / Gram on FP64 MFMA, plus the O(T n) window reductions.
+//
+// The return panel (D_total x n, row-major, resident in HBM) is read through per-date row
+// index lists, so a window is `data[index <= rebdate].tail(width)` with weekend rows
+// removed exactly as src/builders.py:208-211 selects it; consecutive daily windows share
+// T-1 of their T rows, so the panel is served from L2 / Infinity Cache, not HBM.
+// Sigma = (X - 1 mu')'(X - 1 mu') * (1/(T-1)) is the two-pass np.cov that
+// DataFrame.cov() runs (src/covariance.py:65-66): the mean comes from pq_window_mean and
+// is subtracted while staging each 16-row chunk into LDS.  One 256-thread workgroup per
+// lower 64x64 output tile and date; each tile is written twice (tile and mirror) so the
+// result is the full symmetric matrix PorQua's Covariance.estimate returns.
+#include "common.h"
+#include "capi_util.h"
+
+namespace pq {
+
+__global__ __launch_bounds__(256) void k_window_mean(const double* panel, int64_t ldp, int n,
+                                                     const int32_t* rows, const int32_t* tlen,
+                                                     int tmax, double* mu, int64_t mu_stride,
+                                                     int geo) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int T = tlen[b];
+  const int32_t* rw = rows + (int64_t)b * tmax;
+  double s = 0.0;
+  if (geo) {
+    for (int k = 0; k < T; ++k) s += log(1.0 + panel[(int64_t)rw[k] * ldp + j]);
+    mu[(int64_t)b * mu_stride + j] = exp(s / T) - 1.0;
+  } else {
+    for (int k = 0; k < T; ++k) s += panel[(int64_t)rw[k] * ldp + j];
+    mu[(int64_t)b * mu_stride + j] = s / T;
+  }
+}
+
+__device__ __forceinline__ void tri_index(int t, int& I, int& J) {
+  // t enumerates lower tiles row by row: (0,0),(1,0),(1,1),(2,0),...
+  I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  J = t - I * (I + 1) / 2;
+}
+
+// stage one 16-row chunk of window columns [c0, c0+64) into image S[k][i] (centred)
+__device__ __forceinline__ void load_win(double (&v)[4], const double* panel, int64_t ldp, int n,
+                                         const int32_t* rw, int T, int k0, int c0,
+                                         const double* mu) {
+  const int t = threadIdx.x;
+  const int k = t >> 4, i = (t & 15) * 4;
+  const int kk = k0 + k;
+  const int64_t row = kk < T ? (int64_t)rw[kk] : -1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = c0 + i + e;
+    double x = 0.0;
+    if (row >= 0 && c < n) {
+      x = panel[row * ldp + c];
+      if (mu) x -= mu[c];
+    }
+    v[e] = x;
+  }
+}
+__device__ __forceinline__ void store_win(const double (&v)[4], double* S) {
+  const int t = threadIdx.x;
+  const int k = t >> 4, i = (t & 15) * 4;
+  double2* p = reinterpret_cast<double2*>(S + k * LDW + i);
+  p[0] = double2{v[0], v[1]};
+  p[1] = double2{v[2], v[3]};
+}
+
+__global__ __launch_bounds__(256) void k_syrk(const double* panel, int64_t ldp, int n,
+                                              const int32_t* rows, const int32_t* tlen, int tmax,
+                                              int mode, const double* mu, int64_t mu_stride,
+                                              double* out, int ld, int64_t out_stride) {
+  __shared__ __attribute__((aligned(16))) double smem[4 * STAGE];
+  const int b = blockIdx.y;
+  int I, J;
+  tri_index(blockIdx.x, I, J);
+  const int T = tlen[b];
+  const int32_t* rw = rows + (int64_t)b * tmax;
+  const double* m = (mode == 0) ? mu + (int64_t)b * mu_stride : nullptr;
+  Acc acc;
+  acc.zero();
+  double va[4], vb[4];
+  load_win(va, panel, ldp, n, rw, T, 0, I * TB, m);
+  load_win(vb, panel, ldp, n, rw, T, 0, J * TB, m);
+  store_win(va, smem);
+  store_win(vb, smem + STAGE);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < T; k0 += KC) {
+    const bool more = (k0 + KC) < T;
+    if (more) {
+      load_win(va, panel, ldp, n, rw, T, k0 + KC, I * TB, m);
+      load_win(vb, panel, ldp, n, rw, T, k0 + KC, J * TB, m);
+    }
+    mma_lds(acc, smem + buf * 2 * STAGE, smem + buf * 2 * STAGE + STAGE, KC);
+    if (more) {
+      store_win(va, smem + (buf ^ 1) * 2 * STAGE);
+      store_win(vb, smem + (buf ^ 1) * 2 * STAGE + STAGE);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (mode == 0) {
+    const double sc = 1.0 / (double)(T - 1);  // numpy: c *= 1/(N - ddof)
+#pragma unroll
+    for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) acc.c[mm][nn] *= sc;
+  }
+  double* o = out + (int64_t)b * out_stride;
+  acc_store(acc, o, ld, I * TB, J * TB);
+  if (I != J) acc_store_T(acc, o, ld, J * TB, I * TB);
+}
+
+__global__ __launch_bounds__(256) void k_gram_xy(const double* panel, int64_t ldp, int n,
+                                                 const double* bm, const int32_t* rows,
+                                                 const int32_t* tlen, int tmax, double* xty,
+                                                 int64_t xty_stride, double* yty) {
+  __shared__ double red[16];
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int T = tlen[b];
+  const int32_t* rw = rows + (int64_t)b * tmax;
+  if (j < n) {
+    double s = 0.0;
+    for (int k = 0; k < T; ++k) s += panel[(int64_t)rw[k] * ldp + j] * bm[rw[k]];
+    xty[(int64_t)b * xty_stride + j] = s;
+  }
+  if (blockIdx.x == 0) {
+    double s = 0.0;
+    for (int k = threadIdx.x; k < T; k += blockDim.x) {
+      const double v = bm[rw[k]];
+      s += v * v;
+    }
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) yty[b] = s;
+  }
+}
+
+}  // namespace pq
+
+static int check_win(const double* panel, int32_t n, const int32_t* rows, const int32_t* tlen,
+                     int32_t tmax, int32_t batch) {
+  PQ_CHECK_ARG(panel && rows && tlen, "window kernels: null pointer");
+  PQ_CHECK_ARG(n > 0 && tmax > 0 && batch >= 0, "window kernels: bad sizes n=%d tmax=%d batch=%d", n, tmax, batch);
+  return 0;
+}
+
+extern "C" int pq_window_mean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                              const int32_t* tlen, int32_t tmax, int32_t batch, double* mu,
+                              int64_t mu_stride, void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(mu != nullptr, "pq_window_mean: mu is null");
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(pq::k_window_mean, dim3((n + 255) / 256, batch), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mu, mu_stride, 0);
+  PQ_CHECK_LAUNCH("pq_window_mean");
+  return 0;
+}
+
+extern "C" int pq_window_geomean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                                 const int32_t* tlen, int32_t tmax, int32_t batch, double* mu,
+                                 int64_t mu_stride, void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(mu != nullptr, "pq_window_geomean: mu is null");
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(pq::k_window_mean, dim3((n + 255) / 256, batch), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mu, mu_stride, 1);
+  PQ_CHECK_LAUNCH("pq_window_geomean");
+  return 0;
+}
+
+extern "C" int pq_cov_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                              const int32_t* tlen, int32_t tmax, int32_t batch, int32_t mode,
+                              const double* mu, int64_t mu_stride, double* out, int32_t ld,
+                              int64_t out_stride, void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(mode == 0 || mode == 1, "pq_cov_batched: mode must be 0 (centred cov) or 1 (Gram)");
+  PQ_CHECK_ARG(mode == 1 || mu != nullptr, "pq_cov_batched: mode 0 needs the window means");
+  PQ_CHECK_ARG(out && ld >= n && ld % 64 == 0, "pq_cov_batched: ld must be a multiple of 64 >= n");
+  if (batch == 0) return 0;
+  const int nb = ld / 64;
+  hipLaunchKernelGGL(pq::k_syrk, dim3(nb * (nb + 1) / 2, batch), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mode, mu, mu_stride,
+                     out, ld, out_stride);
+  PQ_CHECK_LAUNCH("pq_cov_batched");
+  return 0;
+}
+
+extern "C" int pq_gram_xy_batched(const double* panel, int64_t ldp, int32_t n, const double* bm,
+                                  const int32_t* rows, const int32_t* tlen, int32_t tmax,
+                                  int32_t batch, double* xty, int64_t xty_stride, double* yty,
+                                  void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(bm && xty && yty, "pq_gram_xy_batched: null pointer");
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(pq::k_gram_xy, dim3((n + 255) / 256, batch), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, bm, rows, tlen, tmax, xty, xty_stride, yty);
+  PQ_CHECK_LAUNCH("pq_gram_xy_batched");
+  return 0;
+}

@@ -1,0 +1,396 @@
+"""Device engine: batched covariance + batched dense QP solve on MI355X through the C ABI.
+
+Host code only stages data (PyTorch-ROCm tensors for device memory and the current HIP
+stream) and drives the kernels of ``libporqua_hip.so``:
+
+  K1 pq_window_mean / pq_cov_batched / pq_gram_xy_batched / pq_window_geomean
+  K2 pq_factor_batched   (KKT formation + Cholesky [+ inverse])
+  K3 pq_admm_batched     (OSQP-style ADMM, per-problem convergence)
+  K4 pq_polish_batched   (active-set polish + exact residuals)
+
+There is deliberately no CPU fallback: without the library or a GPU every entry point
+raises ``PorquaHipError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+F64 = torch.float64
+
+
+def round_up(v: int, m: int) -> int:
+    return ((int(v) + m - 1) // m) * m
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise _lib.PorquaHipError("no HIP device visible: the MI355X engine has no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+@dataclass
+class Settings:
+    """ADMM / polish settings (OSQP defaults except the tighter eps: the polish needs a
+    correct active set).  Passed through ``params`` of the reference API."""
+    rho0: float = 0.1
+    sigma: float = 1e-6
+    alpha: float = 1.6
+    eps_abs: float = 1e-5
+    eps_rel: float = 1e-5
+    rho_min: float = 1e-6
+    rho_max: float = 1e6
+    adapt_tol: float = 5.0
+    eq_scale: float = 1e3
+    delta: float = 1e-9        # polish regularisation, relative to the problem scale
+    dual_tol: float = 1e-9     # multiplier sign tolerance, relative to the problem scale
+    max_iter: int = 4000
+    adapt_interval: int = 25
+    polish: int = 1
+    polish_rounds: int = 8
+    refine_iters: int = 8
+
+    def to_c(self) -> _lib.PQSettings:
+        return _lib.PQSettings(**{f.name: getattr(self, f.name) for f in dataclasses.fields(self)})
+
+    @classmethod
+    def from_params(cls, params) -> "Settings":
+        s = cls()
+        if params:
+            for f in dataclasses.fields(cls):
+                for key in (f.name, "admm_" + f.name):
+                    if key in params and params[key] is not None:
+                        setattr(s, f.name, type(getattr(s, f.name))(params[key]))
+        return s
+
+
+# ----------------------------------------------------------------------------------------
+# Problem batches
+# ----------------------------------------------------------------------------------------
+
+
+class QPBatch:
+    """A batch of dense QPs  min 0.5 x'(ps P + pd I)x + q'x  s.t. lg <= Cg x <= ug,
+    lb <= x <= ub, laid out as include/porqua_hip.h expects (ld = round_up(n, 64))."""
+
+    def __init__(self, n: int, batch: int, mg: int, device=None, shared_constraints=True,
+                 has_box=True, P=None):
+        self.device = device or default_device()
+        self.n, self.batch, self.mg = int(n), int(batch), int(mg)
+        self.ld = round_up(max(n, 1), 64)
+        self.mg_pad = round_up(max(mg, 1), 8)
+        ld, dev = self.ld, self.device
+        self.P = P if P is not None else torch.zeros((batch, ld, ld), dtype=F64, device=dev)
+        self.q = torch.zeros((batch, ld), dtype=F64, device=dev)
+        self.p_scale = None
+        self.p_diag = None
+        nc = 1 if shared_constraints else batch
+        self.shared = shared_constraints
+        self.Cg = torch.zeros((nc, max(mg, 1), ld), dtype=F64, device=dev)
+        self.lg = torch.full((nc, max(mg, 1)), -np.inf, dtype=F64, device=dev)
+        self.ug = torch.full((nc, max(mg, 1)), np.inf, dtype=F64, device=dev)
+        self.has_box = has_box
+        if has_box:
+            self.lb = torch.full((nc, ld), -np.inf, dtype=F64, device=dev)
+            self.ub = torch.full((nc, ld), np.inf, dtype=F64, device=dev)
+        else:
+            self.lb = self.ub = None
+
+    def c_struct(self) -> _lib.PQProblem:
+        ld = self.ld
+        cs = 0 if self.shared else self.Cg.stride(0)
+        gs = 0 if self.shared else self.lg.stride(0)
+        bs = 0 if (self.shared or not self.has_box) else self.lb.stride(0)
+        return _lib.PQProblem(
+            n=self.n, ld=ld, batch=self.batch, mg=self.mg,
+            P=self.P.data_ptr(), P_stride=self.P.stride(0),
+            p_scale=None if self.p_scale is None else self.p_scale.data_ptr(),
+            p_diag=None if self.p_diag is None else self.p_diag.data_ptr(),
+            q=self.q.data_ptr(), q_stride=self.q.stride(0),
+            Cg=self.Cg.data_ptr(), Cg_stride=cs,
+            lg=self.lg.data_ptr(), ug=self.ug.data_ptr(), g_stride=gs,
+            lb=None if self.lb is None else self.lb.data_ptr(),
+            ub=None if self.ub is None else self.ub.data_ptr(), box_stride=bs)
+
+    @classmethod
+    def from_dense(cls, P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, device=None):
+        """Build from host arrays: P (B,n,n), q (B,n); A (me,n)|(B,me,n), b; G, h; lb, ub
+        ((n,) shared or (B,n)).  Equality rows are stored first (lg == ug)."""
+        P = np.asarray(P, dtype=np.float64)
+        if P.ndim == 2:
+            P = P[None]
+        B, n, _ = P.shape
+        q = np.asarray(q, dtype=np.float64).reshape(B, n)
+
+        def per(M, rows):
+            if M is None:
+                return None
+            M = np.asarray(M, dtype=np.float64)
+            if M.ndim == 1 and rows is not None:
+                M = M.reshape(rows)
+            return M
+
+        A = None if A is None else np.asarray(A, dtype=np.float64)
+        G = None if G is None else np.asarray(G, dtype=np.float64)
+        if A is not None and A.ndim == 1:
+            A = A.reshape(1, n)
+        if G is not None and G.ndim == 1:
+            G = G.reshape(1, n)
+        me = 0 if A is None else A.shape[-2]
+        mi = 0 if G is None else G.shape[-2]
+        shared = (A is None or A.ndim == 2) and (G is None or G.ndim == 2)
+        b_ = None if b is None else np.asarray(b, dtype=np.float64)
+        h_ = None if h is None else np.asarray(h, dtype=np.float64)
+        if shared and b_ is not None and b_.size != me:
+            shared = False
+        if shared and h_ is not None and h_.size != mi:
+            shared = False
+        lb_ = None if lb is None else np.asarray(lb, dtype=np.float64)
+        ub_ = None if ub is None else np.asarray(ub, dtype=np.float64)
+        if shared and ((lb_ is not None and lb_.ndim == 2) or (ub_ is not None and ub_.ndim == 2)):
+            shared = False
+        has_box = lb_ is not None or ub_ is not None
+        self = cls(n, B, me + mi, device=device, shared_constraints=shared, has_box=has_box)
+        nc = 1 if shared else B
+        ld = self.ld
+        Cg = np.zeros((nc, max(me + mi, 1), ld))
+        lg = np.full((nc, max(me + mi, 1)), -np.inf)
+        ug = np.full((nc, max(me + mi, 1)), np.inf)
+        if me:
+            Ab = np.broadcast_to(A, (nc, me, n)) if A.ndim == 2 else A
+            bb = np.broadcast_to(b_.reshape(-1, me) if b_ is not None else 0.0, (nc, me))
+            Cg[:, :me, :n] = Ab
+            lg[:, :me] = bb
+            ug[:, :me] = bb
+        if mi:
+            Gb = np.broadcast_to(G, (nc, mi, n)) if G.ndim == 2 else G
+            hb = np.broadcast_to(h_.reshape(-1, mi), (nc, mi))
+            Cg[:, me:me + mi, :n] = Gb
+            ug[:, me:me + mi] = hb
+        dev = self.device
+        Pp = np.zeros((B, ld, ld))
+        Pp[:, :n, :n] = P
+        self.P = torch.from_numpy(Pp).to(dev)
+        qp = np.zeros((B, ld))
+        qp[:, :n] = q
+        self.q = torch.from_numpy(qp).to(dev)
+        self.Cg = torch.from_numpy(Cg).to(dev)
+        self.lg = torch.from_numpy(lg).to(dev)
+        self.ug = torch.from_numpy(ug).to(dev)
+        if has_box:
+            lo = np.full((nc, ld), -np.inf)
+            up = np.full((nc, ld), np.inf)
+            lo[:, n:] = 0.0
+            up[:, n:] = 0.0
+            if lb_ is not None:
+                lo[:, :n] = np.broadcast_to(lb_, (nc, n)) if lb_.ndim == 1 else lb_
+            if ub_ is not None:
+                up[:, :n] = np.broadcast_to(ub_, (nc, n)) if ub_.ndim == 1 else ub_
+            self.lb = torch.from_numpy(lo).to(dev)
+            self.ub = torch.from_numpy(up).to(dev)
+        self.me, self.mi = me, mi
+        return self
+
+
+class Workspace:
+    """Solver state for a QPBatch (all device memory; nothing persistent in the library)."""
+
+    def __init__(self, qb: QPBatch):
+        B, ld, dev = qb.batch, qb.ld, qb.device
+        self.mg_pad = qb.mg_pad
+        self.m_ld = qb.mg_pad + ld
+        self.K = torch.empty((B, ld, ld), dtype=F64, device=dev)
+        self.Dt = torch.empty((B, ld // 64, 64, 64), dtype=F64, device=dev)
+        self.x = torch.zeros((B, ld), dtype=F64, device=dev)
+        self.Px = torch.zeros((B, ld), dtype=F64, device=dev)
+        self.z = torch.zeros((B, self.m_ld), dtype=F64, device=dev)
+        self.y = torch.zeros((B, self.m_ld), dtype=F64, device=dev)
+        self.rho = torch.zeros(B, dtype=F64, device=dev)
+        self.iters = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.info = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.out = torch.zeros((B, _lib.PQ_OUT_FIELDS), dtype=F64, device=dev)
+        self.work_stride = _lib.work_doubles(ld, qb.mg_pad)
+        self.work = torch.zeros((B, self.work_stride), dtype=F64, device=dev)
+
+    def c_struct(self) -> _lib.PQState:
+        return _lib.PQState(
+            K=self.K.data_ptr(), K_stride=self.K.stride(0),
+            Dt=self.Dt.data_ptr(), Dt_stride=self.Dt.stride(0),
+            x=self.x.data_ptr(), Px=self.Px.data_ptr(),
+            z=self.z.data_ptr(), y=self.y.data_ptr(),
+            m_ld=self.m_ld, mg_pad=self.mg_pad,
+            rho=self.rho.data_ptr(),
+            iters=self.iters.data_ptr(), status=self.status.data_ptr(), info=self.info.data_ptr(),
+            out=self.out.data_ptr(),
+            work=self.work.data_ptr(), work_stride=self.work_stride)
+
+
+@dataclass
+class BatchResult:
+    x: torch.Tensor          # (B, n) weights (device)
+    y: torch.Tensor          # (B, mg) multipliers of the general rows (equalities first)
+    z_box: torch.Tensor      # (B, n)
+    status: torch.Tensor     # (B,) int32
+    iters: torch.Tensor      # (B,) int32
+    out: torch.Tensor        # (B, PQ_OUT_FIELDS)
+    refactors: int = 0
+    admm_launches: int = 0
+
+    @property
+    def obj(self):
+        return self.out[:, _lib.PQ_OUT_OBJ]
+
+    @property
+    def found(self):
+        return (self.status == _lib.PQ_SOLVED) | (self.status == _lib.PQ_SOLVED_INACCURATE)
+
+
+def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = None,
+          max_rounds: int = 64) -> BatchResult:
+    """Solve every QP of the batch on the current device/stream (K2 -> K3 [-> K2 -> K3 ...] -> K4)."""
+    lib = _lib.load()
+    s = (settings or Settings()).to_c()
+    ws = ws or Workspace(qb)
+    pb = qb.c_struct()
+    st = ws.c_struct()
+    strm = _stream()
+    P_, S_, SS = ctypes.byref(pb), ctypes.byref(st), ctypes.byref(s)
+    _lib.check(lib.pq_init_state(P_, S_, None, 0, SS, strm), "pq_init_state")
+    _lib.check(lib.pq_factor_batched(P_, S_, None, 0, SS, 1, strm), "pq_factor_batched")
+    idx = None
+    nidx = 0
+    refactors = launches = 0
+    for _ in range(max_rounds):
+        _lib.check(lib.pq_admm_batched(P_, S_, _ptr(idx), nidx, SS, int(s.max_iter), strm),
+                   "pq_admm_batched")
+        launches += 1
+        need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
+        k = int(need.numel())   # host sync: small status vector
+        if k == 0:
+            break
+        idx, nidx = need.contiguous(), k
+        _lib.check(lib.pq_factor_batched(P_, S_, _ptr(idx), nidx, SS, 1, strm), "pq_factor_batched")
+        refactors += k
+    if s.polish:
+        _lib.check(lib.pq_polish_batched(P_, S_, None, 0, SS, strm), "pq_polish_batched")
+    n, mg = qb.n, qb.mg
+    return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
+                       status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
+                       admm_launches=launches)
+
+
+def factor_only(qb: QPBatch, invert: bool = False, sigma: float = 0.0):
+    """Batched Cholesky of P_eff (mg = 0, no box): returns (Workspace, info) -- the isPD
+    test of src/helper_functions.py:61-67 on the device."""
+    lib = _lib.load()
+    s = Settings(sigma=sigma).to_c()
+    ws = Workspace(qb)
+    pb = qb.c_struct()
+    pb.mg = 0
+    pb.lb = pb.ub = None
+    st = ws.c_struct()
+    strm = _stream()
+    _lib.check(lib.pq_init_state(ctypes.byref(pb), ctypes.byref(st), None, 0, ctypes.byref(s), strm), "init")
+    _lib.check(lib.pq_factor_batched(ctypes.byref(pb), ctypes.byref(st), None, 0, ctypes.byref(s),
+                                     1 if invert else 0, strm), "pq_factor_batched")
+    return ws, ws.info
+
+
+# ----------------------------------------------------------------------------------------
+# Windows and K1
+# ----------------------------------------------------------------------------------------
+
+
+def window_rows(dates: np.ndarray, rebdates, width: int):
+    """Per-date row lists of ``data[data.index <= rebdate].tail(width)`` minus weekends
+    (src/builders.py:208-211).  Returns (rows int32 [B, Tmax], tlen int32 [B])."""
+    dates = np.asarray(dates, dtype="datetime64[D]")
+    reb = np.asarray(rebdates, dtype="datetime64[D]")
+    ends = np.searchsorted(dates, reb, side="right")
+    starts = np.maximum(0, ends - int(width))
+    wd = (dates.astype("int64") + 3) % 7
+    weekday = wd < 5
+    lists = []
+    for s, e in zip(starts, ends):
+        r = np.arange(s, e, dtype=np.int32)
+        if not weekday[s:e].all():
+            r = r[weekday[s:e]]
+        lists.append(r)
+    tmax = max(1, max(len(r) for r in lists)) if lists else 1
+    rows = np.zeros((len(lists), tmax), dtype=np.int32)
+    tlen = np.zeros(len(lists), dtype=np.int32)
+    for i, r in enumerate(lists):
+        rows[i, :len(r)] = r
+        tlen[i] = len(r)
+    return rows, tlen
+
+
+class Panel:
+    """A device-resident return panel (D_total x n, row-major) with optional benchmark."""
+
+    def __init__(self, returns, bm=None, device=None):
+        self.device = device or default_device()
+        R = returns if isinstance(returns, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(returns, dtype=np.float64))
+        self.R = R.to(self.device, dtype=F64).contiguous()
+        self.D, self.n = self.R.shape
+        self.bm = None
+        if bm is not None:
+            y = bm if isinstance(bm, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(bm, dtype=np.float64).reshape(-1))
+            self.bm = y.to(self.device, dtype=F64).contiguous()
+
+    def rows_to_device(self, rows, tlen):
+        r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int32)).to(self.device)
+        t = torch.from_numpy(np.ascontiguousarray(tlen, dtype=np.int32)).to(self.device)
+        return r, t
+
+    def window_means(self, rows, tlen, geometric=False):
+        lib = _lib.load()
+        B, tmax = rows.shape
+        mu = torch.zeros((B, round_up(self.n, 64)), dtype=F64, device=self.device)
+        fn = lib.pq_window_geomean if geometric else lib.pq_window_mean
+        _lib.check(fn(_ptr(self.R), self.n, self.n, _ptr(rows), _ptr(tlen), tmax, B, _ptr(mu),
+                      mu.stride(0), _stream()), "window means")
+        return mu
+
+    def cov(self, rows, tlen, mode=0, out=None, mu=None):
+        """K1: per-date centred covariance (mode 0, ddof=1) or Gram X'X (mode 1) -> (B, ld, ld)."""
+        lib = _lib.load()
+        B, tmax = rows.shape
+        ld = round_up(self.n, 64)
+        if mode == 0 and mu is None:
+            mu = self.window_means(rows, tlen)
+        if out is None:
+            out = torch.empty((B, ld, ld), dtype=F64, device=self.device)
+        _lib.check(lib.pq_cov_batched(_ptr(self.R), self.n, self.n, _ptr(rows), _ptr(tlen), tmax, B,
+                                      mode, _ptr(mu) if mode == 0 else None,
+                                      mu.stride(0) if mode == 0 else 0, _ptr(out), ld,
+                                      out.stride(0), _stream()), "pq_cov_batched")
+        return out
+
+    def gram_xy(self, rows, tlen):
+        lib = _lib.load()
+        if self.bm is None:
+            raise ValueError("Benchmark return series data is missing.")
+        B, tmax = rows.shape
+        ld = round_up(self.n, 64)
+        xty = torch.zeros((B, ld), dtype=F64, device=self.device)
+        yty = torch.zeros(B, dtype=F64, device=self.device)
+        _lib.check(lib.pq_gram_xy_batched(_ptr(self.R), self.n, self.n, _ptr(self.bm), _ptr(rows),
+                                          _ptr(tlen), tmax, B, _ptr(xty), xty.stride(0), _ptr(yty),
+                                          _stream()), "pq_gram_xy_batched")
+        return xty, yty

@@ -1,0 +1,109 @@
+"""GPU parity of the HIP kernels against the CPU oracle (run on an MI355X: -m gpu)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.ref_pipeline import cov_pearson, window_rows as oracle_window_rows
+from oracle.qp_ipm import solve_qp
+from porqua_amd import engine
+from porqua_amd.synthetic import factor_panel
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("n,T,D", [(24, 252, 400), (100, 60, 200), (130, 40, 120)])
+def test_cov_and_gram_match_numpy(device, n, T, D):
+    dates, R, y, _ = factor_panel(D, n, seed=n)
+    reb = dates[T::7][:9]
+    rows, tlen = engine.window_rows(dates, reb, T)
+    pan = engine.Panel(R, y, device=device)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    S = pan.cov(r_d, t_d, mode=0).cpu().numpy()
+    G = pan.cov(r_d, t_d, mode=1).cpu().numpy()
+    xty, yty = pan.gram_xy(r_d, t_d)
+    xty, yty = xty.cpu().numpy(), yty.cpu().numpy()
+    for b, rd in enumerate(reb):
+        rr = oracle_window_rows(dates, rd, T)
+        assert np.array_equal(rr, rows[b, :tlen[b]])
+        X = R[rr]
+        assert _rel(S[b, :n, :n], cov_pearson(X)) < 1e-12
+        assert _rel(G[b, :n, :n], X.T @ X) < 1e-12
+        assert _rel(xty[b, :n], X.T @ y[rr]) < 1e-12
+        assert abs(yty[b] - y[rr] @ y[rr]) <= 1e-12 * abs(yty[b])
+        assert np.all(S[b, n:, :] == 0) and np.all(S[b, :, n:] == 0)
+
+
+@pytest.mark.parametrize("n", [24, 64, 150, 300])
+def test_factor_and_inverse(device, n):
+    rng = np.random.default_rng(n)
+    B = 3
+    M = rng.standard_normal((B, n + 7, n))
+    P = np.einsum("bki,bkj->bij", M, M) / n + 0.1 * np.eye(n)
+    qb = engine.QPBatch.from_dense(P, np.zeros((B, n)), device=device)
+    ws, info = engine.factor_only(qb, invert=False)
+    assert int(info.abs().max()) == 0
+    L = torch.tril(ws.K).cpu().numpy()[:, :n, :n]
+    for b in range(B):
+        assert _rel(L[b], np.linalg.cholesky(P[b])) < 1e-12
+    ws, info = engine.factor_only(qb, invert=True)
+    Ki = ws.K.cpu().numpy()[:, :n, :n]
+    for b in range(B):
+        assert _rel(Ki[b], np.linalg.inv(P[b])) < 1e-10
+    # a non-PD matrix reports info > 0 (the isPD test)
+    P[1] = -P[1]
+    qb = engine.QPBatch.from_dense(P, np.zeros((B, n)), device=device)
+    _, info = engine.factor_only(qb)
+    info = info.cpu().numpy()
+    assert info[0] == 0 and info[1] == 1 and info[2] == 0
+
+
+@pytest.mark.parametrize("tag", ["msci_ls", "msci_ls_l2", "msci_ls_log", "msci_mv", "msci_mv_shrink", "msci_qeqw"])
+def test_qp_golden_msci(device, tag):
+    g = load_golden(tag)
+    P, q, A, b, lb, ub = g["P"], g["q"], g["A"], g["b"], g["lb"], g["ub"]
+    qb = engine.QPBatch.from_dense(P, q, A=A[0], b=b[0].reshape(-1), lb=lb[0], ub=ub[0], device=device)
+    res = engine.solve(qb)
+    x = res.x.cpu().numpy()
+    st = res.status.cpu().numpy()
+    obj = res.obj.cpu().numpy()
+    assert np.all(st == 1), (tag, np.unique(st, return_counts=True))
+    xg = g["x"]
+    og = g["obj"]
+    errs = np.abs(x - xg).max(axis=1)
+    assert errs.max() < 1e-5, (tag, errs.max(), int(errs.argmax()))
+    objd = np.array([0.5 * x[i] @ P[i] @ x[i] + q[i] @ x[i] for i in range(len(x))])
+    assert np.allclose(objd, obj, rtol=1e-9, atol=1e-15)
+    rel = np.abs(obj - og) / np.maximum(np.abs(og), 1e-12)
+    assert rel.max() < 1e-6, (tag, rel.max())
+    viol = np.maximum(np.abs(x.sum(1) - 1), np.maximum(lb - x, x - ub).max(1))
+    assert viol.max() <= 1e-7
+
+
+@pytest.mark.parametrize("shrink", [0.1, 0.0])
+def test_qp_synthetic_n1000_min_variance(device, shrink):
+    n, T = 1000, 252
+    dates, R, _, _ = factor_panel(520, n)
+    ends = [300, 519]
+    Ps = []
+    for e in ends:
+        S = cov_pearson(R[e - T + 1:e + 1])
+        if shrink:
+            S = S + shrink * np.mean(np.diag(S)) * np.eye(n)
+        Ps.append(2 * S)
+    P = np.stack(Ps)
+    q = np.zeros((len(ends), n))
+    qb = engine.QPBatch.from_dense(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), device=device)
+    res = engine.solve(qb)
+    x = res.x.cpu().numpy()
+    assert np.all(res.status.cpu().numpy() == 1)
+    for i in range(len(ends)):
+        s = solve_qp(P[i], q[i], A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n))
+        o = 0.5 * x[i] @ P[i] @ x[i]
+        assert abs(o - s.obj) <= 1e-6 * abs(s.obj)
+        assert np.abs(x[i] - s.x).max() < 1e-5
+        assert max(abs(x[i].sum() - 1), -x[i].min(), x[i].max() - 1) <= 1e-7
