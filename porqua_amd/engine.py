@@ -260,9 +260,31 @@ class BatchResult:
         return (self.status == _lib.PQ_SOLVED) | (self.status == _lib.PQ_SOLVED_INACCURATE)
 
 
+class _Timeline:
+    """Optional per-launch HIP event pairs on the launch stream (no host syncs)."""
+
+    def __init__(self, sink):
+        self.sink = sink
+
+    def __call__(self, name, fn):
+        if self.sink is None:
+            return fn()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn()
+        e1.record()
+        self.sink.append((name, e0, e1))
+        return r
+
+
 def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = None,
-          max_rounds: int = 64) -> BatchResult:
-    """Solve every QP of the batch on the current device/stream (K2 -> K3 [-> K2 -> K3 ...] -> K4)."""
+          max_rounds: int = 64, events: list | None = None) -> BatchResult:
+    """Solve every QP of the batch on the current device/stream (K2 -> K3 [-> K2 -> K3 ...] -> K4).
+
+    ``events``: if a list is given, (kernel name, start, end) torch.cuda.Event triples are
+    appended for every launch (recorded on the launch stream)."""
+    tl = _Timeline(events)
     lib = _lib.load()
     s = (settings or Settings()).to_c()
     ws = ws or Workspace(qb)
@@ -271,12 +293,14 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
     strm = _stream()
     P_, S_, SS = ctypes.byref(pb), ctypes.byref(st), ctypes.byref(s)
     _lib.check(lib.pq_init_state(P_, S_, None, 0, SS, strm), "pq_init_state")
-    _lib.check(lib.pq_factor_batched(P_, S_, None, 0, SS, 1, strm), "pq_factor_batched")
+    _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, None, 0, SS, 1, strm)),
+               "pq_factor_batched")
     idx = None
     nidx = 0
     refactors = launches = 0
     for _ in range(max_rounds):
-        _lib.check(lib.pq_admm_batched(P_, S_, _ptr(idx), nidx, SS, int(s.max_iter), strm),
+        _lib.check(tl("admm", lambda: lib.pq_admm_batched(P_, S_, _ptr(idx), nidx, SS,
+                                                          int(s.max_iter), strm)),
                    "pq_admm_batched")
         launches += 1
         need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
@@ -284,10 +308,12 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
         if k == 0:
             break
         idx, nidx = need.contiguous(), k
-        _lib.check(lib.pq_factor_batched(P_, S_, _ptr(idx), nidx, SS, 1, strm), "pq_factor_batched")
+        _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, _ptr(idx), nidx, SS, 1, strm)),
+                   "pq_factor_batched")
         refactors += k
     if s.polish:
-        _lib.check(lib.pq_polish_batched(P_, S_, None, 0, SS, strm), "pq_polish_batched")
+        _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, None, 0, SS, strm)),
+                   "pq_polish_batched")
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,

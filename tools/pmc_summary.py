@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarise a round's rocprofv3 output (tools/profile_round.sh) into profiles/<round>_*.
+
+HBM traffic per kernel follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB
+from separate --pmc passes; on gfx950 FETCH_SIZE counts exactly half of a 16 B/lane
+coalesced stream, so read bytes = 2 * FETCH_SIZE * 1024 (the ADMM K^-1 stream and the
+factor kernel's tile staging are 16 B/lane loads); WRITE_SIZE is exact for 16 B stores.
+
+Usage: python tools/pmc_summary.py r01
+"""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path, counter):
+    agg = collections.defaultdict(float)
+    calls = collections.Counter()
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            agg[r["Kernel_Name"]] += float(r["Counter_Value"])
+            calls[r["Kernel_Name"]] += 1
+    return agg, calls
+
+
+def main():
+    rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{rnd}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
+                os.path.join(dst, f"{rnd}_kernel_stats.csv"))
+    fetch, calls = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write, _ = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    line = [l for l in open(os.path.join(src, "pmc_fetch.log")) if l.startswith('{"metric"')][-1]
+    bench_pmc = json.loads(line)
+    iters = bench_pmc["roofline"]["admm_iterations_per_step"]
+    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
+    out = {"round": rnd, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of "
+                                   "`bench.py --steps 1 --warmup 0` (one step = the whole backtest)",
+           "admm_iterations_per_step": iters, "kernels": {}}
+    for k in sorted(fetch, key=lambda k: -fetch[k]):
+        rd = 2.0 * fetch[k] * 1024.0
+        wr = write.get(k, 0.0) * 1024.0
+        e = {"calls_per_step": calls[k], "read_bytes_per_step": rd, "write_bytes_per_step": wr,
+             "hbm_bytes_per_step": rd + wr}
+        if k in stats:
+            e["trace_avg_ns"] = float(stats[k]["AverageNs"])
+            e["trace_calls"] = int(stats[k]["Calls"])
+        out["kernels"][k] = e
+    adm = out["kernels"].get("k_admm")
+    if adm:
+        adm["hbm_bytes_per_admm_iteration"] = adm["hbm_bytes_per_step"] / iters
+        adm["algorithmic_bytes_per_admm_iteration"] = 8.0 * bench_pmc["config"]["n_assets"] ** 2
+    with open(os.path.join(dst, f"{rnd}_pmc_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    full = os.path.join(src, "bench_full.log")
+    if os.path.exists(full):
+        shutil.copy(full, os.path.join(dst, f"{rnd}_bench.log"))
+    print(json.dumps(out["kernels"].get("k_admm"), indent=1))
+
+
+if __name__ == "__main__":
+    main()
