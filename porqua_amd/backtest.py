@@ -1,0 +1,395 @@
+"""Backtest service and rebalance loop (mirror of src/backtest.py:42-270).
+
+``Backtest.run(bs)`` keeps the reference semantics.  When the optimization's solver is the
+device engine ('mi355x') and the builders are the standard ones (src/builders.py), the
+loop runs in two phases instead of one serial QP per date:
+
+  A (host, once): selection + constraints from the first date (they are date-invariant
+    for the standard builders), window row lists for every rebalance date
+    (``data[index <= rebdate].tail(width)`` minus weekends, src/builders.py:208-211);
+  B (device): the whole panel is uploaded once; K1 builds every date's covariance / Gram,
+    K2-K4 solve every date's QP in one batch (chunked to bound HBM use), sharded across
+    ranks when torch.distributed is initialised (contiguous date blocks, one all-gather of
+    the weight panel -- SURVEY.md §8(e));
+  C (host): Portfolio objects in date order, ``append_fun`` called per date.
+
+Dates are independent in the reference; an ``append_fun`` that mutates
+state read by later dates is not supported in batched mode (set settings['batched'] = False
+to force the serial loop, which still solves each date on the device).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+from typing import Optional
+
+import numpy as np
+import pandas as pd
+
+from . import builders as _b
+from .constraints import Constraints
+from .optimization import EmptyOptimization, Optimization
+from .optimization_data import OptimizationData
+from .portfolio import Portfolio, Strategy
+from .selection import Selection
+
+
+class BacktestData:
+    def __init__(self):
+        pass
+
+
+class BacktestService:
+
+    def __init__(self, data, selection_item_builders: dict, optimization_item_builders: dict,
+                 optimization: Optional[Optimization] = None, settings: Optional[dict] = None, **kwargs) -> None:
+        self.data = data
+        self.optimization = EmptyOptimization() if optimization is None else optimization
+        self.selection_item_builders = selection_item_builders
+        self.optimization_item_builders = optimization_item_builders
+        self.settings = settings if settings is not None else {}
+        self.settings.update(kwargs)
+        self.selection = Selection()
+        self.optimization_data = OptimizationData([])
+
+    @property
+    def selection(self):
+        return self._selection
+
+    @selection.setter
+    def selection(self, value):
+        if not isinstance(value, Selection):
+            raise TypeError("Expected a Selection instance for 'selection'")
+        self._selection = value
+
+    @property
+    def selection_item_builders(self):
+        return self._selection_item_builders
+
+    @selection_item_builders.setter
+    def selection_item_builders(self, value):
+        if not isinstance(value, dict) or not all(isinstance(v, _b.SelectionItemBuilder) for v in value.values()):
+            raise TypeError("Expected a dictionary containing SelectionItemBuilder instances "
+                            "for 'selection_item_builders'")
+        self._selection_item_builders = value
+
+    @property
+    def optimization(self):
+        return self._optimization
+
+    @optimization.setter
+    def optimization(self, value):
+        if not isinstance(value, Optimization):
+            raise TypeError("Expected an Optimization instance for 'optimization'")
+        self._optimization = value
+
+    @property
+    def optimization_item_builders(self):
+        return self._optimization_item_builders
+
+    @optimization_item_builders.setter
+    def optimization_item_builders(self, value):
+        if not isinstance(value, dict) or not all(isinstance(v, _b.OptimizationItemBuilder) for v in value.values()):
+            raise TypeError("Expected a dictionary containing OptimizationItemBuilder instances "
+                            "for 'optimization_item_builders'")
+        self._optimization_item_builders = value
+
+    @property
+    def settings(self):
+        return self._settings
+
+    @settings.setter
+    def settings(self, value):
+        if not isinstance(value, dict):
+            raise TypeError("Expected a dictionary for 'settings'")
+        self._settings = value
+
+    def build_selection(self, rebdate: str) -> None:
+        for key, item_builder in self.selection_item_builders.items():
+            item_builder.arguments["item_name"] = key
+            item_builder(self, rebdate)
+
+    def build_optimization(self, rebdate: str) -> None:
+        self.optimization.constraints = Constraints(selection=self.selection.selected)
+        for item_builder in self.optimization_item_builders.values():
+            item_builder(self, rebdate)
+
+    def prepare_rebalancing(self, rebalancing_date: str) -> None:
+        self.build_selection(rebdate=rebalancing_date)
+        self.build_optimization(rebdate=rebalancing_date)
+
+
+# ------------------------------------------------------------------------------------------
+# batched staging
+# ------------------------------------------------------------------------------------------
+
+
+def shard_range(total: int, rank: int, world: int):
+    """Contiguous block of dates for ``rank`` (sizes differ by at most one)."""
+    base, extra = divmod(total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+class BatchStage:
+    """Device staging of one backtest (or one chunk of it) for objective_batch()."""
+
+    def __init__(self, panel, rows_host, tlen_host, device):
+        import torch
+        self.panel = panel
+        self.device = device
+        self.rows_host = np.ascontiguousarray(rows_host, dtype=np.int32)
+        self.tlen_host = np.ascontiguousarray(tlen_host, dtype=np.int32)
+        self.rows = torch.from_numpy(self.rows_host).to(device)
+        self.tlen = torch.from_numpy(self.tlen_host).to(device)
+        self.batch = len(self.tlen_host)
+        self.n = panel.n
+        self.ld = ((panel.n + 63) // 64) * 64
+        self._P = None
+        self._log_panel = None
+
+    def P_buffer(self):
+        import torch
+        if self._P is None:
+            self._P = torch.empty((self.batch, self.ld, self.ld), dtype=torch.float64, device=self.device)
+        return self._P
+
+    def identity_P(self):
+        import torch
+        P = self.P_buffer()
+        P.zero_()
+        idx = torch.arange(self.n, device=self.device)
+        P[:, idx, idx] = 1.0
+        return P
+
+    def sub_windows(self, a: int, b: int):
+        """Rows [a, b) of every window (for estimators that use a sub-window)."""
+        import torch
+        T = int(self.tlen_host.max())
+        if (a, b) == (0, T):
+            return self.rows, self.tlen
+        r = self.rows_host[:, a:b].copy()
+        t = np.clip(self.tlen_host - a, 0, b - a).astype(np.int32)
+        return torch.from_numpy(np.ascontiguousarray(r)).to(self.device), torch.from_numpy(t).to(self.device)
+
+    def log1p_panel(self):
+        import torch
+        from . import engine
+        if self._log_panel is None:
+            p = engine.Panel(torch.log1p(self.panel.R), None if self.panel.bm is None else torch.log1p(self.panel.bm),
+                             device=self.device)
+            self._log_panel = p
+        return self._log_panel
+
+
+def _batchable(bs) -> bool:
+    fns = [b.arguments.get("bibfn") for b in list(bs.selection_item_builders.values()) +
+           list(bs.optimization_item_builders.values())]
+    return all(f in _b.STANDARD_BIBFNS for f in fns) and bs.settings.get("batched", True)
+
+
+class Backtest:
+
+    def __init__(self) -> None:
+        self._strategy = Strategy([])
+        self._output = {}
+        self.stats = {}
+
+    @property
+    def strategy(self):
+        return self._strategy
+
+    @property
+    def output(self):
+        return self._output
+
+    def append_output(self, date_key=None, output_key=None, value=None):
+        if value is None:
+            return True
+        if date_key in self.output:
+            if output_key in self.output[date_key]:
+                raise Warning(f"Output key '{output_key}' for date key '{date_key}' already exists and will be overwritten.")
+            self.output[date_key][output_key] = value
+        else:
+            self.output[date_key] = {output_key: value}
+        return True
+
+    def rebalance(self, bs: BacktestService, rebalancing_date: str) -> None:
+        bs.prepare_rebalancing(rebalancing_date=rebalancing_date)
+        try:
+            bs.optimization.set_objective(optimization_data=bs.optimization_data)
+            bs.optimization.solve()
+        except Exception as error:
+            raise RuntimeError(error)
+
+    def run(self, bs: BacktestService) -> None:
+        from .qp_problems import ENGINE_SOLVERS
+        if bs.optimization.params.get("solver_name") in ENGINE_SOLVERS and _batchable(bs):
+            if self._run_batched(bs):
+                return None
+        return self._run_serial(bs)
+
+    def _after_solve(self, bs, rebalancing_date):
+        portfolio = Portfolio(rebalancing_date=rebalancing_date, weights=bs.optimization.results["weights"])
+        self.strategy.portfolios.append(portfolio)
+        append_fun = bs.settings.get("append_fun")
+        if append_fun is not None:
+            append_fun(backtest=self, bs=bs, rebalancing_date=rebalancing_date,
+                       what=bs.settings.get("append_fun_args"))
+
+    def _run_serial(self, bs) -> None:
+        for rebalancing_date in bs.settings["rebdates"]:
+            if not bs.settings.get("quiet"):
+                print(f"Rebalancing date: {rebalancing_date}")
+            self.rebalance(bs=bs, rebalancing_date=rebalancing_date)
+            self._after_solve(bs, rebalancing_date)
+
+    def _run_batched(self, bs) -> bool:
+        import torch
+        from . import engine
+        rebdates = list(bs.settings["rebdates"])
+        if not rebdates:
+            return True
+        opt = bs.optimization
+        # ---- phase A: static selection / constraints, window row lists ------------------
+        bs.prepare_rebalancing(rebalancing_date=rebdates[0])
+        cons = opt.constraints
+        if cons.l1:
+            return False                      # l1 linearisations: serial path
+        universe = bs.selection.selected
+        X = bs.data.get("return_series")
+        if X is None:
+            raise ValueError("Return series data is missing.")
+        width = None
+        for bld in bs.optimization_item_builders.values():
+            if bld.arguments.get("bibfn") is _b.bibfn_return_series:
+                width = bld.arguments.get("width")
+        if width is None:
+            return False
+        Xs = X[universe]
+        if Xs.isna().to_numpy().any():
+            return False                      # NaN windows: pairwise covariance, serial path
+        idx = pd.DatetimeIndex(Xs.index)
+        dates = idx.values.astype("datetime64[D]")
+        rows, tlen = engine.window_rows(dates, np.array(rebdates, dtype="datetime64[D]"), width)
+        bm = None
+        ys = bs.data.get("bm_series")
+        if ys is not None:
+            yv = ys.reindex(idx)
+            yv = yv.iloc[:, 0] if isinstance(yv, pd.DataFrame) else yv
+            bm = yv.to_numpy(dtype=np.float64)
+            need = np.unique(rows[tlen > 0].ravel())
+            if np.isnan(bm[need]).any():
+                bm = None                     # benchmark not aligned with the returns
+        GhAb = cons.to_GhAb()
+        boxed = cons.box["box_type"] != "NA"
+        lb = cons.box["lower"].to_numpy(dtype=np.float64) if boxed else None
+        ub = cons.box["upper"].to_numpy(dtype=np.float64) if boxed else None
+
+        # ---- phase B: device ---------------------------------------------------------------
+        dev = engine.default_device()
+        world, rank = 1, 0
+        dist = None
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            dist = torch.distributed
+            world, rank = dist.get_world_size(), dist.get_rank()
+        lo, hi = shard_range(len(rebdates), rank, world)
+        settings = engine.Settings.from_params(opt.params)
+        panel = engine.Panel(Xs.to_numpy(dtype=np.float64), bm, device=dev)
+        n = panel.n
+        chunk = int(bs.settings.get("batch_chunk", 0) or _auto_chunk(n))
+        W = np.zeros((hi - lo, n))
+        ST = np.zeros(hi - lo, dtype=np.int32)
+        OBJ = np.zeros(hi - lo)
+        for s in range(lo, hi, chunk):
+            e = min(hi, s + chunk)
+            stage = BatchStage(panel, rows[s:e], tlen[s:e], dev)
+            obj = opt.objective_batch(stage)
+            if obj is None:
+                return False
+            Pm, scale, pdiag, q, _const = obj
+            qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=GhAb["A"], b=GhAb["b"],
+                                           G=GhAb["G"], h=GhAb["h"], lb=lb, ub=ub, device=dev)
+            qb.batch = e - s
+            qb.P = Pm
+            qb.p_scale = scale
+            qb.p_diag = pdiag
+            qq = torch.zeros((e - s, qb.ld), dtype=torch.float64, device=dev)
+            qq[:, :n] = q[:, :n]
+            qb.q = qq
+            res = engine.solve(qb, settings)
+            W[s - lo:e - lo] = res.x.cpu().numpy()
+            ST[s - lo:e - lo] = res.status.cpu().numpy()
+            OBJ[s - lo:e - lo] = res.obj.cpu().numpy()
+        if dist is not None:
+            W, ST, OBJ = gather_shards(W, ST, OBJ, len(rebdates), world, dist, dev)
+        # ---- phase C: portfolios -----------------------------------------------------------
+        from . import _lib
+        solved = (ST == _lib.PQ_SOLVED) | (ST == _lib.PQ_SOLVED_INACCURATE)
+        self.stats = {"dates": len(rebdates), "solved": int(solved.sum()), "status": ST, "objective": OBJ}
+        if not bs.settings.get("quiet"):
+            print(f"Rebalanced {len(rebdates)} dates on the device ({int(solved.sum())} solved)")
+        for i, d in enumerate(rebdates):
+            w = W[i] if solved[i] else [None] * n
+            opt.results = {"weights": pd.Series(w, index=universe).to_dict(), "status": bool(solved[i])}
+            self._after_solve(bs, d)
+        return True
+
+    def save(self, filename: str, path: Optional[str] = None) -> None:
+        try:
+            if path is not None and filename is not None:
+                filename = os.path.join(path, filename)
+            with open(filename, "wb") as f:
+                pickle.dump(self, f, protocol=pickle.HIGHEST_PROTOCOL)
+        except Exception as ex:
+            print("Error during pickling object:", ex)
+
+
+def _auto_chunk(n: int) -> int:
+    """Dates per device batch: P + K^-1 (2 x 8 ld^2 B) per date within ~96 GiB."""
+    ld = ((n + 63) // 64) * 64
+    per = 2 * 8 * ld * ld + 64 * ld * 8
+    return max(1, int((96 << 30) // per))
+
+
+def gather_shards(W, ST, OBJ, total, world, dist, device):
+    """All-gather every rank's contiguous block (RCCL over xGMI on GPUs, gloo on CPU)."""
+    import torch
+    per = -(-total // world)
+    n = W.shape[1]
+    be = dist.get_backend()
+    dev = device if be == "nccl" else torch.device("cpu")
+    buf = torch.zeros((per, n + 2), dtype=torch.float64, device=dev)
+    k = W.shape[0]
+    buf[:k, :n] = torch.from_numpy(W).to(dev)
+    buf[:k, n] = torch.from_numpy(ST.astype(np.float64)).to(dev)
+    buf[:k, n + 1] = torch.from_numpy(OBJ).to(dev)
+    if be == "nccl":
+        out = torch.zeros((world * per, n + 2), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(out, buf)
+    else:
+        parts_t = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(parts_t, buf)
+        out = torch.cat(parts_t)
+    out = out.cpu().numpy()
+    parts = []
+    for r in range(world):
+        s, e = shard_range(total, r, world)
+        parts.append(out[r * per:r * per + (e - s)])
+    full = np.concatenate(parts)
+    return full[:, :n], full[:, n].astype(np.int32), full[:, n + 1]
+
+
+def append_custom(backtest: Backtest, bs: BacktestService, rebalancing_date: Optional[str] = None,
+                  what: Optional[list] = None) -> None:
+    """src/backtest.py:245-270."""
+    what = ["w_dict", "objective"] if what is None else what
+    for key in what:
+        if key == "w_dict":
+            for k, weights in bs.optimization.results["w_dict"].items():
+                if hasattr(weights, "to_dict"):
+                    weights = weights.to_dict()
+                backtest.append_output(date_key=rebalancing_date, output_key=f"weights_{k}",
+                                       value=pd.Series(Portfolio(rebalancing_date, weights).weights))
+        elif key in bs.optimization.results:
+            backtest.append_output(date_key=rebalancing_date, output_key=key, value=bs.optimization.results[key])

@@ -1,0 +1,118 @@
+"""Covariance estimation on the device (mirror of src/covariance.py:21-84).
+
+``Covariance.estimate(X)`` keeps the reference signature (T x n DataFrame in, n x n
+DataFrame out) and computes the two-pass np.cov / DataFrame.cov() result with K1
+(window mean + FP64-MFMA SYRK), the PD check with K2's Cholesky info and the repair with
+``helper_functions.nearestPD``.  ``estimate_batch`` is the batched backtest entry: all
+rebalance dates of a device-resident panel at once, results left on the device.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+from .helper_functions import isPD, nearestPD
+
+
+class CovarianceSpecification(dict):
+    """Defaults: method 'pearson', check_positive_definite True (src/covariance.py:21-28)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.__dict__ = self
+        self.setdefault("method", "pearson")
+        if self.get("method") is None:
+            self["method"] = "pearson"
+        if self.get("check_positive_definite") is None:
+            self["check_positive_definite"] = True
+
+
+def _shrink_lambda(lam):
+    if lam is None or np.isnan(lam) or lam < 0:
+        return 0.0
+    return float(lam)
+
+
+class Covariance:
+
+    def __init__(self, spec: CovarianceSpecification = None, *args, **kwargs):
+        self.spec = CovarianceSpecification(*args, **kwargs) if spec is None else spec
+
+    def set_ctrl(self, *args, **kwargs) -> None:
+        self.spec = CovarianceSpecification(*args, **kwargs)
+
+    def estimate(self, X: pd.DataFrame):
+        method = self.spec["method"]
+        if method == "pearson":
+            covmat = cov_pearson(X)
+        elif method == "duv":
+            covmat = cov_duv(X)
+        elif method == "linear_shrinkage":
+            covmat = cov_linear_shrinkage(X, self.spec.get("lambda_covmat_regularization"))
+        else:
+            raise NotImplementedError("This method is not implemented yet")
+        if self.spec.get("check_positive_definite") and not isPD(covmat):
+            fixed = nearestPD(covmat)
+            covmat = pd.DataFrame(fixed, index=covmat.index, columns=covmat.columns) \
+                if isinstance(covmat, pd.DataFrame) else fixed
+        return covmat
+
+    # -- batched (backtest) entry --------------------------------------------------------
+    def estimate_batch(self, panel, rows, tlen, out=None):
+        """All dates at once on the device.  Returns (S, p_diag): S is the (B, ld, ld)
+        device tensor of raw sample covariances; p_diag (B,) is the diagonal term the spec
+        adds (linear shrinkage: lam * mean(diag S)); 'duv' returns (None, None)."""
+        import torch
+        method = self.spec["method"]
+        if method == "duv":
+            return None, None
+        if method not in ("pearson", "linear_shrinkage"):
+            raise NotImplementedError("This method is not implemented yet")
+        S = panel.cov(rows, tlen, mode=0, out=out)
+        B = S.shape[0]
+        pdiag = torch.zeros(B, dtype=torch.float64, device=S.device)
+        if method == "linear_shrinkage":
+            lam = _shrink_lambda(self.spec.get("lambda_covmat_regularization"))
+            if lam > 0:
+                n = panel.n
+                pdiag = lam * torch.diagonal(S, dim1=1, dim2=2)[:, :n].mean(dim=1)
+        return S, pdiag
+
+
+def _device_cov(X, mode=0):
+    from . import engine
+    Xv = np.ascontiguousarray(X.to_numpy() if hasattr(X, "to_numpy") else X, dtype=np.float64)
+    if np.isnan(Xv).any():
+        raise NotImplementedError(
+            "windows with NaN (pandas' pairwise-complete covariance) are not supported by the device path")
+    T, n = Xv.shape
+    pan = engine.Panel(Xv)
+    rows, tlen = pan.rows_to_device(np.arange(T, dtype=np.int32)[None], np.array([T], dtype=np.int32))
+    S = pan.cov(rows, tlen, mode=mode)
+    return S[0, :n, :n].cpu().numpy()
+
+
+def cov_pearson(X):
+    """X.cov() (src/covariance.py:65-66) on the device."""
+    S = _device_cov(X, mode=0)
+    if isinstance(X, pd.DataFrame):
+        return pd.DataFrame(S, index=X.columns, columns=X.columns)
+    return S
+
+
+def cov_duv(X):
+    """Identity, returned as an ndarray like the reference (src/covariance.py:68-69)."""
+    return np.identity(X.shape[1])
+
+
+def cov_linear_shrinkage(X, lambda_covmat_regularization=None):
+    """Sigma + lambda * mean(diag Sigma) * I (src/covariance.py:71-84); the reference's
+    unused correlation loop (:78-82) is not reproduced (it has no effect on the result)."""
+    lam = _shrink_lambda(lambda_covmat_regularization)
+    S = cov_pearson(X)
+    if lam > 0:
+        vals = S.to_numpy() if isinstance(S, pd.DataFrame) else S
+        d = vals.shape[0]
+        vals = vals + lam * np.mean(np.diag(vals)) * np.eye(d)
+        S = pd.DataFrame(vals, index=S.index, columns=S.columns) if isinstance(S, pd.DataFrame) else vals
+    return S

@@ -1,0 +1,247 @@
+"""Optimization classes (mirror of the hot-path part of src/optimization.py:40-259).
+
+Each class keeps the reference API (``set_objective(optimization_data)``, ``solve()``,
+``model_qpsolvers()``, ``results``) and adds a batched objective builder used by the
+batched backtest: ``objective_batch(stage)`` returns the device-resident P (as the K1
+output plus a per-date scale / diagonal term), q and the constant for every date at once.
+
+Deliberate differences from the reference ("Reference defects"):
+* ``OptimizationParameter`` defaults ``solver_name`` to 'mi355x' (the engine of this
+  package) and lets ``verbose=False`` stick (src/optimization.py:45-46).
+* ``MeanVariance`` uses the mean estimator that is passed in; the reference stores the
+  class instead of the instance (src/optimization.py:165).
+LAD and PercentilePortfolios (LP / ranking, not the QP path) are out of scope.
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from typing import Optional
+
+import numpy as np
+import pandas as pd
+
+from . import qp_problems
+from .constraints import Constraints
+from .covariance import Covariance
+from .helper_functions import to_numpy
+from .mean_estimation import MeanEstimator
+from .optimization_data import OptimizationData
+
+
+class OptimizationParameter(dict):
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.__dict__ = self
+        if not self.get("solver_name"):
+            self["solver_name"] = qp_problems.ENGINE_SOLVER
+        self.setdefault("verbose", True)
+        self.setdefault("allow_suboptimal", False)
+
+
+class Objective(dict):
+    pass
+
+
+def _device_gram(X, y=None):
+    """(X'X, X'y, y'y) of one window on the device (K1 Gram mode + pq_gram_xy)."""
+    from . import engine
+    Xv = np.ascontiguousarray(to_numpy(X), dtype=np.float64)
+    T, n = Xv.shape
+    yv = None if y is None else np.ascontiguousarray(to_numpy(y), dtype=np.float64).reshape(-1)
+    pan = engine.Panel(Xv, yv)
+    rows, tlen = pan.rows_to_device(np.arange(T, dtype=np.int32)[None], np.array([T], dtype=np.int32))
+    G = pan.cov(rows, tlen, mode=1)[0, :n, :n].cpu().numpy()
+    if yv is None:
+        return G, None, None
+    xty, yty = pan.gram_xy(rows, tlen)
+    return G, xty[0, :n].cpu().numpy(), float(yty[0].item())
+
+
+class Optimization(ABC):
+
+    def __init__(self, params: OptimizationParameter = None, constraints: Constraints = None, **kwargs):
+        self.params = OptimizationParameter(**kwargs) if params is None else params
+        self.objective = Objective()
+        self.constraints = Constraints() if constraints is None else constraints
+        self.model = None
+        self.results = None
+
+    @abstractmethod
+    def set_objective(self, optimization_data: OptimizationData) -> None:
+        raise NotImplementedError("Method 'set_objective' must be implemented in derived class.")
+
+    def objective_batch(self, stage):
+        """Batched objective for the device backtest; ``None`` = not batchable."""
+        return None
+
+    @abstractmethod
+    def solve(self) -> bool:
+        self.solve_qpsolvers()
+        return self.results["status"]
+
+    def solve_qpsolvers(self) -> None:
+        self.model_qpsolvers()
+        self.model.solve()
+        universe = self.constraints.selection
+        sol = self.model["solution"]
+        w = sol.x[:len(universe)] if sol.found else [None] * len(universe)
+        self.results = {"weights": pd.Series(w, index=universe).to_dict(), "status": sol.found}
+
+    def model_qpsolvers(self) -> None:
+        """Assemble the QuadraticProgram exactly as src/optimization.py:91-143."""
+        if "P" not in self.objective:
+            raise ValueError("Missing matrix 'P' in objective.")
+        P = to_numpy(self.objective["P"])
+        q = to_numpy(self.objective["q"]) if "q" in self.objective else np.zeros(len(self.constraints.selection))
+        self.objective["P"], self.objective["q"] = P, q
+        universe = self.constraints.selection
+        GhAb = self.constraints.to_GhAb()
+        boxed = self.constraints.box["box_type"] != "NA"
+        lb = self.constraints.box["lower"].to_numpy() if boxed else None
+        ub = self.constraints.box["upper"].to_numpy() if boxed else None
+        self.model = qp_problems.QuadraticProgram(P=P, q=q, constant=self.objective.get("constant"),
+                                                  G=GhAb["G"], h=GhAb["h"], A=GhAb["A"], b=GhAb["b"],
+                                                  lb=lb, ub=ub, params=self.params)
+        tocon = self.constraints.l1.get("turnover")
+        x0 = tocon["x0"] if tocon is not None and tocon.get("x0") is not None else self.params.get("x0")
+        x_init = {a: x0.get(a, 0) for a in universe} if x0 is not None else None
+        tc = self.params.get("transaction_cost")
+        if tc is not None and x_init is not None:
+            self.model.linearize_turnover_objective(pd.Series(x_init), tc)
+        if tocon and not tc and x_init is not None:
+            self.model.linearize_turnover_constraint(pd.Series(x_init), tocon["rhs"])
+        levcon = self.constraints.l1.get("leverage")
+        if levcon is not None:
+            self.model.linearize_leverage_constraint(N=len(universe), leverage_budget=levcon["rhs"])
+
+
+class EmptyOptimization(Optimization):
+
+    def set_objective(self, optimization_data=None) -> None:
+        pass
+
+    def solve(self) -> bool:
+        return super().solve()
+
+
+class MeanVariance(Optimization):
+    """P = 2 * risk_aversion * Sigma, q = -mu_geometric (src/optimization.py:157-177)."""
+
+    def __init__(self, covariance: Optional[Covariance] = None,
+                 mean_estimator: Optional[MeanEstimator] = None, **kwargs):
+        super().__init__(**kwargs)
+        self.covariance = Covariance() if covariance is None else covariance
+        self.mean_estimator = MeanEstimator() if mean_estimator is None else mean_estimator
+        self.params.setdefault("risk_aversion", 1)
+
+    def set_objective(self, optimization_data: OptimizationData) -> None:
+        X = optimization_data["return_series"]
+        covmat = self.covariance.estimate(X=X) * self.params["risk_aversion"] * 2
+        mu = self.mean_estimator.estimate(X=X) * (-1)
+        self.objective = Objective(q=mu, P=covmat)
+
+    def objective_batch(self, stage):
+        import torch
+        S, pdiag = self.covariance.estimate_batch(stage.panel, stage.rows, stage.tlen, out=stage.P_buffer())
+        ra = float(self.params["risk_aversion"])
+        B = stage.batch
+        dev = stage.device
+        if S is None:  # duv: identity covariance
+            S = stage.identity_P()
+            pdiag = torch.zeros(B, dtype=torch.float64, device=dev)
+        me = self.mean_estimator
+        if me.spec.get("method") != "geometric":
+            return None
+        a, b = me.window(int(stage.tlen_host.max()))
+        if not np.all(stage.tlen_host == stage.tlen_host[0]) and (a, b) != (0, int(stage.tlen_host[0])):
+            return None
+        mrows, mtlen = stage.sub_windows(a, b)
+        mu = stage.panel.window_means(mrows, mtlen, geometric=True)
+        sf = me.spec.get("scalefactor")
+        if sf not in (None, 1):
+            mu = torch.expm1(torch.log1p(mu) * sf)
+        scale = torch.full((B,), 2.0 * ra, dtype=torch.float64, device=dev)
+        return S, scale, scale * pdiag, -mu, None
+
+
+class QEQW(Optimization):
+    """P = 2 I, q = 0 (src/optimization.py:180-194)."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.covariance = Covariance(method="duv")
+
+    def set_objective(self, optimization_data: OptimizationData) -> None:
+        X = optimization_data["return_series"]
+        self.objective = Objective(P=self.covariance.estimate(X=X) * 2, q=np.zeros(X.shape[1]))
+
+    def objective_batch(self, stage):
+        import torch
+        B, dev = stage.batch, stage.device
+        return (stage.identity_P(), torch.full((B,), 2.0, dtype=torch.float64, device=dev),
+                None, torch.zeros((B, stage.ld), dtype=torch.float64, device=dev), None)
+
+
+class LeastSquares(Optimization):
+    """P = 2 X'X (+ 2 l2 I), q = -2 X'y, constant y'y (src/optimization.py:198-229)."""
+
+    def __init__(self, covariance: Optional[Covariance] = None, **kwargs):
+        super().__init__(**kwargs)
+        self.covariance = covariance
+
+    def set_objective(self, optimization_data: OptimizationData) -> None:
+        X = optimization_data["return_series"]
+        y = optimization_data["bm_series"]
+        if self.params.get("log_transform"):
+            X = np.log(1 + X)
+            y = np.log(1 + y)
+        if isinstance(X, pd.DataFrame) and isinstance(y, (pd.DataFrame, pd.Series)):
+            if not X.index.equals(y.index):
+                # the reference's X.T @ y raises on misaligned dates (src/optimization.py:215-217)
+                raise ValueError("matrices are not aligned")
+        G, xty, yty = _device_gram(X, y)
+        P = 2 * G
+        l2 = self.params.get("l2_penalty")
+        if l2 is not None and l2 != 0:
+            P = P + 2 * l2 * np.eye(P.shape[0])
+        if isinstance(X, pd.DataFrame):
+            P = pd.DataFrame(P, index=X.columns, columns=X.columns)
+        self.objective = Objective(P=P, q=-2 * xty, constant=yty)
+
+    def objective_batch(self, stage):
+        import torch
+        if stage.panel.bm is None:
+            return None
+        if self.params.get("log_transform"):
+            pan = stage.log1p_panel()
+        else:
+            pan = stage.panel
+        G = pan.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer())
+        xty, yty = pan.gram_xy(stage.rows, stage.tlen)
+        B, dev = stage.batch, stage.device
+        l2 = self.params.get("l2_penalty")
+        scale = torch.full((B,), 2.0, dtype=torch.float64, device=dev)
+        pdiag = torch.full((B,), 2.0 * float(l2), dtype=torch.float64, device=dev) if l2 else None
+        return G, scale, pdiag, -2.0 * xty, yty
+
+
+class WeightedLeastSquares(Optimization):
+    """P = 2 X'WX, q = -2 X'Wy with half-life tau weights (src/optimization.py:232-259)."""
+
+    def _weights(self, T):
+        lam = np.exp(-np.log(2) / self.params["tau"])
+        w = lam ** np.arange(T)
+        return np.flip(w / np.sum(w) * len(w))
+
+    def set_objective(self, optimization_data: OptimizationData) -> None:
+        X = optimization_data["return_series"]
+        y = optimization_data["bm_series"]
+        if self.params.get("log_transform"):
+            X = np.log(1 + X)
+            y = np.log(1 + y)
+        Xv = np.asarray(to_numpy(X), dtype=np.float64)
+        yv = np.asarray(to_numpy(y), dtype=np.float64).reshape(-1)
+        sw = np.sqrt(self._weights(Xv.shape[0]))
+        G, xty, yty = _device_gram(Xv * sw[:, None], yv * sw)
+        self.objective = Objective(P=2 * G, q=-2 * xty, constant=yty)

@@ -1,0 +1,230 @@
+"""QuadraticProgram -- drop-in for src/qp_problems.py with the MI355X engine behind a new
+``solver_name``.
+
+The reference dispatches every QP to the third-party ``qpsolvers.solve_problem``
+(src/qp_problems.py:184-216).  Here ``solver_name='mi355x'`` routes it to the batched HIP
+engine (``porqua_amd.engine``); the problem data, the ``solution`` record and
+``objective_value`` keep the reference's meaning.  Any other solver name is handed to
+``qpsolvers`` exactly as the reference does (ImportError when it is not installed) -- the
+engine itself never falls back to a CPU solver.
+"""
+from __future__ import annotations
+
+import pickle
+
+import numpy as np
+
+from .solution import Solution
+
+ENGINE_SOLVER = "mi355x"
+ENGINE_SOLVERS = {ENGINE_SOLVER}
+
+# reference solver sets (src/qp_problems.py:19-30), extended by the dense device engine
+IGNORED_SOLVERS = {"gurobi", "mosek", "ecos", "scs", "piqp", "proxqp", "clarabel"}
+SPARSE_SOLVERS = {"clarabel", "ecos", "gurobi", "mosek", "highs", "qpalm", "osqp", "qpswift", "scs"}
+ALL_SOLVERS = {"clarabel", "cvxopt", "daqp", "ecos", "gurobi", "highs", "mosek", "osqp", "piqp",
+               "proxqp", "qpalm", "quadprog", "scs"} | ENGINE_SOLVERS
+USABLE_SOLVERS = ALL_SOLVERS - IGNORED_SOLVERS
+
+
+def _arr(v):
+    return None if v is None else np.asarray(v, dtype=np.float64)
+
+
+class QuadraticProgram(dict):
+    """min 0.5 x'Px + q'x (+ constant)  s.t.  Gx <= h, Ax = b, lb <= x <= ub."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.solver = self["params"]["solver_name"]
+
+    # -- l1 linearisations (src/qp_problems.py:40-157): auxiliary variables d >= |x - x0| ----
+    def linearize_turnover_constraint(self, x_init, to_budget=float("inf")) -> None:
+        """Turnover budget sum|x - x0| <= to_budget via d: [x; d], x - d <= x0, -x - d <= -x0."""
+        x0 = np.asarray(x_init, dtype=np.float64).reshape(-1)
+        n = len(self["q"])
+        eye = np.eye(n)
+        rows = [np.hstack([eye, -eye]), np.hstack([-eye, -eye]),
+                np.concatenate([np.zeros(n), np.ones(n)])[None, :]]
+        rhs = [x0, -x0, np.array([to_budget], dtype=np.float64)]
+        self._extend_aux(n, rows, rhs, q_aux=np.zeros(n))
+
+    def linearize_turnover_objective(self, x_init, transaction_cost=0.002) -> None:
+        """Proportional cost transaction_cost * sum|x - x0| in the objective via d."""
+        x0 = np.asarray(x_init, dtype=np.float64).reshape(-1)
+        n = len(self["q"])
+        eye = np.eye(n)
+        rows = [np.hstack([eye, -eye]), np.hstack([-eye, -eye])]
+        self._extend_aux(n, rows, [x0, -x0], q_aux=np.full(n, float(transaction_cost)))
+
+    def linearize_leverage_constraint(self, N=None, leverage_budget=2) -> None:
+        """sum|x| <= leverage_budget via x = x+ - x-, x+, x- >= 0 (src/qp_problems.py:79-118)."""
+        n = len(self["q"])
+        N = n if N is None else int(N)
+        P = self.get("P")
+        if P is not None:
+            P = np.pad(P, (0, 2 * N))
+        q = np.pad(self["q"], (0, 2 * N))
+        G_old = self.get("G")
+        mG = 0 if G_old is None else G_old.shape[0]
+        G = np.zeros((mG + 1, n + 2 * N))
+        if G_old is not None:
+            G[:mG, :n] = G_old
+        G[mG, n:] = 1.0
+        h_old = self.get("h")
+        h = np.append(np.empty(0) if h_old is None else h_old, leverage_budget)
+        A_old = self.get("A")
+        A_old = A_old.reshape(-1, n) if A_old is not None else np.zeros((0, n))
+        mA = A_old.shape[0]
+        A = np.zeros((mA + N, n + 2 * N))
+        A[:mA, :n] = A_old
+        A[mA:, :N] = np.eye(N)
+        A[mA:, n:n + N] = np.eye(N)
+        A[mA:, n + N:] = -np.eye(N)
+        b_old = self.get("b")
+        b = np.concatenate([np.asarray(b_old, dtype=np.float64).reshape(-1) if b_old is not None else np.empty(0),
+                            np.zeros(N)])
+        lb = np.pad(self["lb"], (0, 2 * N)) if self.get("lb") is not None else None
+        ub = np.pad(self["ub"], (0, 2 * N), constant_values=np.inf) if self.get("ub") is not None else None
+        self.update({"P": P, "q": q, "G": G, "h": h, "A": A, "b": b, "lb": lb, "ub": ub})
+
+    def _extend_aux(self, n, g_rows, h_parts, q_aux):
+        P = self.get("P")
+        if P is not None:
+            P = np.pad(P, (0, n))
+        q = np.concatenate([self["q"], q_aux])
+        G_old = self.get("G")
+        blocks = []
+        if G_old is not None:
+            blocks.append(np.hstack([G_old, np.zeros((G_old.shape[0], n))]))
+        G = np.vstack(blocks + g_rows)
+        h_old = self.get("h")
+        h = np.concatenate(([] if h_old is None else [np.asarray(h_old, dtype=np.float64).reshape(-1)]) + h_parts)
+        A = self.get("A")
+        if A is not None:
+            A = np.pad(A.reshape(-1, A.shape[-1]), [(0, 0), (0, n)])
+        lb = np.pad(self["lb"], (0, n)) if self.get("lb") is not None else None
+        ub = np.pad(self["ub"], (0, n), constant_values=np.inf) if self.get("ub") is not None else None
+        self.update({"P": P, "q": q, "G": G, "h": h, "A": A, "lb": lb, "ub": ub})
+
+    # -- solving ------------------------------------------------------------------------
+    def is_feasible(self) -> bool:
+        """Feasibility of the constraint set (a zero objective, src/qp_problems.py:159-182)."""
+        P = self.get("P")
+        n = len(self["q"])
+        probe = QuadraticProgram(P=np.zeros((n, n)) if P is None else np.zeros_like(P), q=np.zeros(n),
+                                 G=self.get("G"), h=self.get("h"), A=self.get("A"), b=self.get("b"),
+                                 lb=self.get("lb"), ub=self.get("ub"), params=self["params"])
+        probe.solve()
+        return bool(probe["solution"].found)
+
+    def solve(self) -> None:
+        if self.solver in ENGINE_SOLVERS:
+            self["solution"] = solve_batch([self])[0]
+            return None
+        return self._solve_qpsolvers()
+
+    def _solve_qpsolvers(self) -> None:
+        """Non-engine solver names keep the reference behaviour (third-party qpsolvers)."""
+        import qpsolvers  # noqa: F401  (ImportError when absent, as in the reference)
+        import scipy.sparse as sp
+        from .helper_functions import isPD, nearestPD
+        if self.solver in ("ecos", "scs", "clarabel") and self.get("b") is not None and np.size(self["b"]) == 1:
+            self["b"] = np.asarray(self["b"]).reshape(-1)
+        P = self.get("P")
+        if P is not None and not isPD(P):
+            self["P"] = nearestPD(P)
+        problem = qpsolvers.Problem(P=self.get("P"), q=self.get("q"), G=self.get("G"), h=self.get("h"),
+                                    A=self.get("A"), b=self.get("b"), lb=self.get("lb"), ub=self.get("ub"))
+        if self.solver in SPARSE_SOLVERS and self["params"].get("sparse"):
+            for f in ("P", "A", "G"):
+                if getattr(problem, f) is not None:
+                    setattr(problem, f, sp.csc_matrix(getattr(problem, f)))
+        self["solution"] = qpsolvers.solve_problem(problem=problem, solver=self.solver,
+                                                   initvals=self.get("x0"), verbose=False)
+        return None
+
+    def objective_value(self, x: np.ndarray, with_const: bool = True) -> float:
+        """0.5 x'Px + q'x (+ constant), src/qp_problems.py:219-221."""
+        const = self.get("constant")
+        c = 0 if const is None or not with_const else const
+        return float(0.5 * (x @ self.get("P") @ x) + self.get("q") @ x) + c
+
+    def serialize(self, path, **kwargs):
+        with open(path, "wb") as f:
+            pickle.dump(self, f, **kwargs)
+
+    @staticmethod
+    def load(path, **kwargs):
+        # NB: the reference passes the *path* to pickle.load (src/qp_problems.py:228-230); fixed.
+        with open(path, "rb") as f:
+            return pickle.load(f, **kwargs)
+
+
+def solve_batch(qps, settings=None, device=None):
+    """Solve a list of QuadraticPrograms of equal dimension on the device in one batch.
+
+    Problems whose constraint matrices are identical share them on the device; the
+    solutions are ``Solution`` objects with the qpsolvers fields the reference reads."""
+    from . import engine
+    if not qps:
+        return []
+    params = qps[0]["params"]
+    settings = settings or engine.Settings.from_params(params)
+    P = np.stack([_arr(qp["P"]) for qp in qps])
+    n = P.shape[-1]
+    q = np.stack([_arr(qp["q"]).reshape(-1) for qp in qps])
+
+    def stack_opt(key, reshape=None):
+        vals = [qp.get(key) for qp in qps]
+        if all(v is None for v in vals):
+            return None
+        if any(v is None for v in vals):
+            raise ValueError(f"solve_batch: '{key}' present in some problems only")
+        arrs = [_arr(v) if reshape is None else _arr(v).reshape(reshape) for v in vals]
+        if all(np.array_equal(arrs[0], a) for a in arrs[1:]):
+            return arrs[0]
+        return np.stack(arrs)
+
+    A = stack_opt("A", (-1, n))
+    b = stack_opt("b", (-1,))
+    G = stack_opt("G", (-1, n))
+    h = stack_opt("h", (-1,))
+    lb = stack_opt("lb", (n,))
+    ub = stack_opt("ub", (n,))
+    if A is not None and A.ndim == 3 and b is not None and b.ndim == 1:
+        b = np.broadcast_to(b, (len(qps), b.size)).copy()
+    if G is not None and G.ndim == 3 and h is not None and h.ndim == 1:
+        h = np.broadcast_to(h, (len(qps), h.size)).copy()
+    qb = engine.QPBatch.from_dense(P, q, A=A, b=b, G=G, h=h, lb=lb, ub=ub, device=device)
+    res = engine.solve(qb, settings)
+    return batch_result_to_solutions(res, qb)
+
+
+def batch_result_to_solutions(res, qb):
+    """Device BatchResult -> list of Solution (one host copy of each array)."""
+    from . import _lib
+    x = res.x.cpu().numpy()
+    y = res.y.cpu().numpy()
+    zb = res.z_box.cpu().numpy() if qb.has_box else None
+    st = res.status.cpu().numpy()
+    it = res.iters.cpu().numpy()
+    out = res.out.cpu().numpy()
+    me = getattr(qb, "me", qb.mg)
+    sols = []
+    for i in range(x.shape[0]):
+        s = Solution(x=x[i].copy(), status=int(st[i]), iterations=int(it[i]))
+        s.found = int(st[i]) in (_lib.PQ_SOLVED, _lib.PQ_SOLVED_INACCURATE)
+        s.y = y[i, :me].copy() if me else None
+        s.z = y[i, me:qb.mg].copy() if qb.mg > me else None
+        s.z_box = zb[i].copy() if zb is not None else None
+        s.obj = float(out[i, _lib.PQ_OUT_OBJ]) if s.found else None
+        s._prim = float(out[i, _lib.PQ_OUT_PRIM])
+        s._dual = float(out[i, _lib.PQ_OUT_DUAL])
+        s._gap = float(out[i, _lib.PQ_OUT_GAP])
+        s.extras = {"rho": float(out[i, _lib.PQ_OUT_RHO]), "n_free": int(out[i, _lib.PQ_OUT_NFREE]),
+                    "polish_rounds": int(out[i, _lib.PQ_OUT_ROUNDS])}
+        if not s.found:
+            s.x = None if int(st[i]) == _lib.PQ_NON_CONVEX else s.x
+        sols.append(s)
+    return sols

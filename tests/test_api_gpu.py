@@ -1,0 +1,140 @@
+"""Reference-API parity on the device: the same calls the reference's tests and
+quick-and-dirty script make (test/tests_quadratic_program.py, src/_quick_and_dirty_
+interactive_testing.py), with solver_name='mi355x'."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import ref_pipeline as rp
+from porqua_amd.backtest import Backtest, BacktestService
+from porqua_amd.builders import (OptimizationItemBuilder, SelectionItemBuilder, bibfn_box_constraints,
+                                 bibfn_bm_series, bibfn_budget_constraint, bibfn_return_series,
+                                 bibfn_selection_data)
+from porqua_amd.constraints import Constraints
+from porqua_amd.covariance import Covariance
+from porqua_amd.helper_functions import isPD, nearestPD
+from porqua_amd.mean_estimation import MeanEstimator
+from porqua_amd.optimization import LeastSquares, MeanVariance, QEQW
+from porqua_amd.optimization_data import OptimizationData
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def msci():
+    g = load_golden("msci_panel")
+    idx = pd.DatetimeIndex(g["dates"].astype("datetime64[D]"))
+    cols = [str(c) for c in g["columns"]]
+    return pd.DataFrame(g["returns"], index=idx, columns=cols), pd.DataFrame({"NDDLWI": g["bm"]}, index=idx)
+
+
+def test_least_squares_reference_test(device):
+    """TestLeastSquares (test:61-126): found, and solution.obj == objective_value(x, False)."""
+    X, y = msci()
+    opt = LeastSquares(solver_name="mi355x", sparse=True)
+    opt.params["l2_penalty"] = 0
+    c = Constraints(selection=X.columns)
+    c.add_budget()
+    c.add_box("LongOnly")
+    opt.constraints = c
+    opt.set_objective(OptimizationData(return_series=X, bm_series=y, align=True))
+    opt.model_qpsolvers()
+    opt.model.solve()
+    sol = opt.model["solution"]
+    assert sol.found
+    assert sol.obj == pytest.approx(opt.model.objective_value(sol.x, False), abs=1e-7)
+    assert sol.primal_residual() < 1e-9 and sol.dual_residual() < 1e-9
+    from oracle.qp_ipm import solve_qp
+    m = opt.model
+    ref = solve_qp(m["P"], m["q"], A=m["A"], b=np.atleast_1d(m["b"]), lb=m["lb"], ub=m["ub"])
+    assert np.abs(sol.x - ref.x).max() < 1e-5
+    assert abs(sol.obj - ref.obj) <= 1e-6 * abs(ref.obj)
+
+
+def test_covariance_estimate_matches_reference_golden(device):
+    g = load_golden("cov_cases")
+    for name in ["pearson_n_lt_T", "pearson_n_gt_T", "shrink_0p1", "shrink_neg"]:
+        X = pd.DataFrame(g[f"{name}__X"])
+        spec = eval(str(g[f"{name}__spec"]))
+        S = Covariance(**spec).estimate(X)
+        S = S.to_numpy() if hasattr(S, "to_numpy") else S
+        ref = g[f"{name}__cov"]
+        assert np.linalg.norm(S - ref) <= 1e-12 * np.linalg.norm(ref), name
+    S = Covariance(method="duv").estimate(pd.DataFrame(g["duv__X"]))
+    assert np.array_equal(S, g["duv__cov"])
+
+
+def test_pd_check_and_repair_on_device(device):
+    g = load_golden("cov_cases")
+    raw = g["pearson_n_gt_T__raw"]
+    assert not isPD(raw) and isPD(g["pearson_n_lt_T__raw"])
+    rep = nearestPD(raw)
+    assert isPD(rep) and np.linalg.norm(rep - raw) <= 1e-12 * np.linalg.norm(raw)
+
+
+def test_geometric_mean(device):
+    X = pd.DataFrame(np.random.default_rng(3).normal(3e-4, 0.02, (120, 9)))
+    for kw in [{}, {"n_mom": 60, "n_rev": 5}, {"scalefactor": 252}]:
+        mu = MeanEstimator(**kw).estimate(X).to_numpy()
+        ref = rp.mean_geometric(X.to_numpy(), kw.get("n_mom"), kw.get("n_rev"), kw.get("scalefactor"))
+        assert np.allclose(mu, ref, rtol=1e-12, atol=1e-15)
+
+
+def _service(opt, X, y, rebdates, box_kw):
+    return BacktestService(
+        data={"return_series": X, "bm_series": y},
+        selection_item_builders={"data": SelectionItemBuilder(bibfn=bibfn_selection_data)},
+        optimization_item_builders={
+            "return_series": OptimizationItemBuilder(bibfn=bibfn_return_series, width=252),
+            "bm_series": OptimizationItemBuilder(bibfn=bibfn_bm_series, width=252),
+            "budget_constraint": OptimizationItemBuilder(bibfn=bibfn_budget_constraint, budget=1),
+            "box_constraints": OptimizationItemBuilder(bibfn=bibfn_box_constraints, **box_kw)},
+        optimization=opt, rebdates=rebdates, quiet=True)
+
+
+@pytest.mark.parametrize("tag,make,box", [
+    ("msci_ls", lambda: LeastSquares(solver_name="mi355x"), {}),
+    ("msci_ls_l2", lambda: LeastSquares(solver_name="mi355x", l2_penalty=1e-3), {"upper": 0.2}),
+    ("msci_ls_log", lambda: LeastSquares(solver_name="mi355x", log_transform=True), {"upper": 0.3}),
+    ("msci_mv", lambda: MeanVariance(solver_name="mi355x"), {"upper": 0.25}),
+    ("msci_mv_shrink", lambda: MeanVariance(covariance=Covariance(method="linear_shrinkage",
+                                                                  lambda_covmat_regularization=0.1),
+                                            solver_name="mi355x", risk_aversion=3.0), {"upper": 0.25}),
+])
+def test_backtest_batched_matches_golden(device, tag, make, box):
+    X, y = msci()
+    g = load_golden(tag)
+    rebdates = [str(d) for d in g["rebdates"]]
+    bt = Backtest()
+    bt.run(_service(make(), X, y, rebdates, box))
+    assert bt.stats["solved"] == len(rebdates)          # the batched path ran
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    assert W.shape == g["x"].shape
+    assert np.abs(W - g["x"]).max() < 1e-5
+    obj = np.array([0.5 * w @ P @ w + q @ w for w, P, q in zip(W, g["P"], g["q"])])
+    assert np.max(np.abs(obj - g["obj"]) / np.maximum(np.abs(g["obj"]), 1e-12)) < 1e-6
+
+
+def test_backtest_serial_equals_batched(device):
+    X, y = msci()
+    g = load_golden("msci_mv")
+    rebdates = [str(d) for d in g["rebdates"][:12]]
+    bt1 = Backtest()
+    bt1.run(_service(MeanVariance(solver_name="mi355x"), X, y, rebdates, {"upper": 0.25}))
+    bs = _service(MeanVariance(solver_name="mi355x"), X, y, rebdates, {"upper": 0.25})
+    bs.settings["batched"] = False
+    bt2 = Backtest()
+    bt2.run(bs)
+    W1 = bt1.strategy.get_weights_df().to_numpy(dtype=float)
+    W2 = bt2.strategy.get_weights_df().to_numpy(dtype=float)
+    assert np.abs(W1 - W2).max() < 1e-7
+    assert np.abs(W1 - g["x"][:12]).max() < 1e-5
+
+
+def test_qeqw_backtest(device):
+    X, y = msci()
+    rebdates = [str(d.date()) for d in X.index[400:1400:200]]
+    bt = Backtest()
+    bt.run(_service(QEQW(solver_name="mi355x"), X, y, rebdates, {}))
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    assert np.allclose(W, 1.0 / 24, atol=1e-9)

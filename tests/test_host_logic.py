@@ -1,0 +1,164 @@
+"""Host-side logic of the product package (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from oracle import ref_pipeline as rp
+from porqua_amd import _lib, engine
+from porqua_amd.backtest import shard_range
+from porqua_amd.constraints import Constraints
+from porqua_amd.synthetic import business_days, factor_panel
+from tests.conftest import ROOT, load_golden
+
+
+def test_window_rows_match_reference_semantics():
+    g = load_golden("msci_panel")
+    dates = g["dates"].astype("datetime64[D]")
+    reb = dates[300::97]
+    rows, tlen = engine.window_rows(dates, reb, 252)
+    for b, d in enumerate(reb):
+        assert np.array_equal(rows[b, :tlen[b]], rp.window_rows(dates, d, 252))
+    # calendars with weekend rows: they are dropped, as src/builders.py:211 does
+    cal = np.datetime64("2020-01-01") + np.arange(60)
+    rows, tlen = engine.window_rows(cal, cal[[20, 59]], 10)
+    for b, d in enumerate(cal[[20, 59]]):
+        r = rp.window_rows(cal, d, 10)
+        assert np.array_equal(rows[b, :tlen[b]], r) and len(r) < 10
+    # a rebalance date before the data starts -> empty window
+    rows, tlen = engine.window_rows(cal, [np.datetime64("2019-01-01")], 10)
+    assert tlen[0] == 0
+
+
+def test_business_days_and_panel_are_deterministic():
+    d = business_days("2005-01-03", 10)
+    assert ((d.astype(np.int64) + 3) % 7 < 5).all() and len(d) == 10
+    a = factor_panel(50, 7)[1]
+    b = factor_panel(50, 7)[1]
+    assert np.array_equal(a, b)
+
+
+def test_shard_range_covers_dates():
+    for total in [1, 7, 4749, 10000]:
+        for world in [1, 2, 3, 8]:
+            parts = [shard_range(total, r, world) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == total
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+            sizes = [e - s for s, e in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_qpbatch_layout_cpu():
+    rng = np.random.default_rng(0)
+    B, n = 3, 70
+    P = rng.standard_normal((B, n, n))
+    qb = engine.QPBatch.from_dense(P, rng.standard_normal((B, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=rng.random((2, n)), h=np.ones(2), lb=np.zeros(n), ub=np.ones(n),
+                                   device=torch.device("cpu"))
+    assert qb.ld == 128 and qb.mg == 3 and qb.shared
+    assert np.array_equal(qb.P[:, :n, :n].numpy(), P) and float(qb.P[:, n:, :].abs().sum()) == 0
+    assert qb.lg[0, 0] == qb.ug[0, 0] == 1.0 and np.isinf(qb.lg[0, 1].item()) and qb.ug[0, 2] == 1.0
+    assert float(qb.lb[0, n:].abs().sum()) == 0 and float(qb.ub[0, n:].abs().sum()) == 0
+    cs = qb.c_struct()
+    assert cs.n == n and cs.ld == 128 and cs.Cg_stride == 0 and cs.P_stride == 128 * 128
+    # per-problem constraints switch to strided storage
+    qb2 = engine.QPBatch.from_dense(P, np.zeros((B, n)), A=np.ones((B, 1, n)), b=np.ones((B, 1)),
+                                    device=torch.device("cpu"))
+    assert not qb2.shared and qb2.c_struct().Cg_stride == qb2.Cg.stride(0)
+
+
+def test_settings_from_params():
+    s = engine.Settings.from_params({"eps_abs": 1e-7, "admm_max_iter": 50, "solver_name": "mi355x"})
+    assert s.eps_abs == 1e-7 and s.max_iter == 50 and isinstance(s.max_iter, int)
+    c = s.to_c()
+    assert abs(c.eps_abs - 1e-7) < 1e-20 and c.max_iter == 50
+
+
+def test_constraints_mirror_reference_shapes():
+    """The reference's own known-answer test (test/tests_quadratic_program.py:28-58)."""
+    g = load_golden("msci_panel")
+    universe = pd.Index([str(c) for c in g["columns"]])
+    c = Constraints(selection=universe)
+    c.add_budget()
+    c.add_box("LongOnly")
+    rng = np.random.default_rng(1)
+    c.add_linear(None, pd.Series(rng.random(universe.size), index=universe), "<=", 1)
+    c.add_linear(None, pd.Series(rng.random(universe.size), index=universe), ">=", -1)
+    c.add_linear(None, pd.Series(rng.random(universe.size), index=universe), "=", 0.5)
+    sub = universe[: universe.size // 2]
+    c.add_linear(pd.DataFrame(rng.random((3, sub.size)), columns=sub), None, pd.Series(np.repeat("=", 3)),
+                 pd.Series(np.ones(3)), None)
+    o = c.to_GhAb()
+    assert o["G"].shape == (2, universe.size) and o["h"].shape == (2,)
+    assert o["A"].shape == (5, universe.size) and o["b"].shape == (5,)
+    o = c.to_GhAb(True)
+    assert o["G"].shape == (2 + 2 * universe.size, universe.size) and o["h"].shape == (2 + 2 * universe.size,)
+
+
+def test_constraints_values_match_reference_golden():
+    g = load_golden("ghab")
+    cols = [f"c{i}" for i in range(24)]
+    u = pd.Index(cols)
+    c = Constraints(selection=u)
+    c.add_budget()
+    c.add_box("LongOnly")
+    c.add_linear(None, pd.Series(g["a1"], index=u), "<=", 1)
+    c.add_linear(None, pd.Series(g["a2"], index=u), ">=", -1)
+    c.add_linear(None, pd.Series(g["a3"], index=u), "=", 0.5)
+    c.add_linear(pd.DataFrame(g["blk"], columns=u[:12]), None, pd.Series(np.repeat("=", 3)), pd.Series(np.ones(3)), None)
+    for lbub, s in [(False, "0"), (True, "1")]:
+        o = c.to_GhAb(lbub)
+        for k in "GhAb":
+            assert np.allclose(o[k], g[k + s])
+    c2 = Constraints(selection=u)
+    c2.add_budget()
+    c2.add_box("LongShort")
+    c2.add_linear(None, pd.Series(g["a3"], index=u), "=", 0.5)
+    c2.add_linear(pd.DataFrame(g["blk"], columns=u[:12]), None, pd.Series(np.repeat("=", 3)), pd.Series(np.ones(3)), None)
+    o = c2.to_GhAb(True)
+    assert np.allclose(o["G"], g["G2"]) and np.allclose(o["h"], g["h2"])
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = _lib.load()
+    header = open(os.path.join(ROOT, "include", "porqua_hip.h")).read()
+    declared = set(re.findall(r"^(?:int|const char\*)\s+(pq_\w+)\(", header, flags=re.M))
+    assert declared and declared == set(_lib.exported_symbols())
+    for name in declared:
+        assert hasattr(lib, name)
+    assert lib.pq_version() == 100
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared:
+        assert re.search(rf"\bT {name}\b", nm), name
+
+
+def test_ctypes_structs_match_c_layout(tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text('#include "porqua_hip.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(pq_problem), sizeof(pq_state),'
+                   ' sizeof(pq_settings), offsetof(pq_problem, lb), offsetof(pq_state, work),'
+                   ' offsetof(pq_settings, refine_iters)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()))
+    exp = [ctypes.sizeof(_lib.PQProblem), ctypes.sizeof(_lib.PQState), ctypes.sizeof(_lib.PQSettings),
+           _lib.PQProblem.lb.offset, _lib.PQState.work.offset, _lib.PQSettings.refine_iters.offset]
+    assert got == exp
+
+
+def test_product_path_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.PorquaHipError):
+        engine.default_device()
+    from porqua_amd.qp_problems import QuadraticProgram
+    n = 4
+    qp = QuadraticProgram(P=np.eye(n), q=np.zeros(n), A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n),
+                          ub=np.ones(n), params={"solver_name": "mi355x"})
+    with pytest.raises(_lib.PorquaHipError):
+        qp.solve()

@@ -1,0 +1,96 @@
+"""The CPU oracle is pinned against golden vectors captured from the reference itself
+(tools/capture_golden.py imports /root/reference/src with a capturing qpsolvers stub)."""
+import numpy as np
+import pytest
+
+from oracle import ref_pipeline as rp
+from oracle.qp_ipm import solve_qp
+from tests.conftest import load_golden
+
+
+def _panel():
+    g = load_golden("msci_panel")
+    return g["dates"].astype("datetime64[D]"), g["returns"], g["bm"]
+
+
+def test_cov_cases_match_reference():
+    g = load_golden("cov_cases")
+    names = sorted({k.split("__")[0] for k in g.files})
+    assert len(names) == 6
+    for name in names:
+        X = g[f"{name}__X"]
+        spec = eval(str(g[f"{name}__spec"]))   # dict literal written by the capture script
+        kw = {"method": spec.get("method", "pearson"),
+              "check_positive_definite": spec.get("check_positive_definite", True),
+              "lam": spec.get("lambda_covmat_regularization")}
+        S = rp.covariance_estimate(X, **kw)
+        ref = g[f"{name}__cov"]
+        assert np.linalg.norm(S - ref) <= 1e-12 * np.linalg.norm(ref), name
+        assert np.linalg.norm(rp.cov_pearson(X) - g[f"{name}__raw"]) <= 1e-13 * np.linalg.norm(g[f"{name}__raw"])
+
+
+def test_nearest_pd_fires_for_singular_window():
+    g = load_golden("cov_cases")
+    raw, rep = g["pearson_n_gt_T__raw"], g["pearson_n_gt_T__cov"]
+    assert not rp.is_pd(raw) and rp.is_pd(rep)
+    assert np.linalg.norm(rep - raw) <= 1e-12 * np.linalg.norm(raw)   # repair is rounding-level
+
+
+@pytest.mark.parametrize("tag", ["msci_ls", "msci_ls_l2", "msci_ls_log"])
+def test_least_squares_objective_matches_reference(tag):
+    dates, R, y = _panel()
+    g = load_golden(tag)
+    params = eval(str(g["params"]))
+    for d, rb in enumerate(g["rebdates"][::11]):
+        i = d * 11
+        rows = rp.window_rows(dates, rb, int(g["width"]))
+        assert len(rows) == g["win_len"][i]
+        assert dates[rows[0]].astype(np.int64) == g["win_first"][i]
+        P, q, c = rp.objective_least_squares(R[rows], y[rows], l2_penalty=params.get("l2_penalty"),
+                                             log_transform=params.get("log_transform", False))
+        assert np.allclose(P, g["P"][i], rtol=1e-12, atol=1e-15)
+        assert np.allclose(q, g["q"][i], rtol=1e-12, atol=1e-15)
+        assert abs(c - g["const"][i]) <= 1e-12 * abs(c)
+
+
+@pytest.mark.parametrize("tag", ["msci_mv", "msci_mv_shrink"])
+def test_mean_variance_objective_matches_reference(tag):
+    dates, R, _ = _panel()
+    g = load_golden(tag)
+    cov = eval(str(g["cov"]))
+    for i in range(0, len(g["rebdates"]), 13):
+        rows = rp.window_rows(dates, g["rebdates"][i], int(g["width"]))
+        P, q, _ = rp.objective_mean_variance(R[rows], risk_aversion=float(g["risk_aversion"]),
+                                             method=cov.get("method", "pearson"),
+                                             lam=cov.get("lambda_covmat_regularization"))
+        assert np.allclose(P, g["P"][i], rtol=1e-12, atol=1e-17)
+        assert np.allclose(q, g["q"][i], rtol=1e-12, atol=1e-17)
+
+
+def test_constraints_to_GhAb_matches_reference():
+    g = load_golden("ghab")
+    n = 24
+    sub = 12
+    blk = np.zeros((3, n)); blk[:, :sub] = g["blk"]
+    linear = (np.vstack([g["a1"], g["a2"], g["a3"], blk]), ["<=", ">=", "=", "=", "=", "="],
+              np.array([1, -1, 0.5, 1, 1, 1.0]))
+    budget = (np.ones(n), "=", 1)
+    box = rp.box_bounds(n, "LongOnly")
+    for lbub, sfx in [(False, "0"), (True, "1")]:
+        out = rp.to_GhAb(n, budget, box, linear, lbub_to_G=lbub)
+        for k in "GhAb":
+            assert np.allclose(out[k], g[k + sfx]), (k, sfx)
+    out = rp.to_GhAb(n, budget, rp.box_bounds(n, "LongShort"),
+                     (np.vstack([g["a3"], blk]), ["="] * 4, np.array([0.5, 1, 1, 1.0])), lbub_to_G=True)
+    assert out["G"].shape == g["G2"].shape == (4 * n, n)      # box rows stacked twice (quirk)
+    assert np.allclose(out["G"], g["G2"]) and np.allclose(out["h"], g["h2"])
+
+
+@pytest.mark.parametrize("tag", ["msci_ls", "msci_mv", "msci_qeqw"])
+def test_ipm_oracle_is_kkt_certified(tag):
+    g = load_golden(tag)
+    for i in range(0, len(g["P"]), 20):
+        s = solve_qp(g["P"][i], g["q"][i], A=g["A"][i], b=np.atleast_1d(g["b"][i]), lb=g["lb"][i], ub=g["ub"][i])
+        assert s.primal_residual() < 1e-12 and s.dual_residual() < 1e-12
+        assert np.abs(s.x - g["x"][i]).max() < 1e-9
+        assert abs(s.obj - g["obj"][i]) <= 1e-12 * max(1.0, abs(g["obj"][i]))
