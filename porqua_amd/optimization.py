@@ -75,8 +75,8 @@ class Optimization(ABC):
         """Batched objective for the device backtest; ``None`` = not batchable."""
         return None
 
-    @abstractmethod
     def solve(self) -> bool:
+        """src/optimization.py:72-75 (subclasses in the reference only forward here)."""
         self.solve_qpsolvers()
         return self.results["status"]
 

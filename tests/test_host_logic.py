@@ -162,3 +162,20 @@ def test_product_path_fails_loudly_without_gpu():
                           ub=np.ones(n), params={"solver_name": "mi355x"})
     with pytest.raises(_lib.PorquaHipError):
         qp.solve()
+
+
+def test_api_objects_construct_without_gpu():
+    from porqua_amd.backtest import Backtest, BacktestService
+    from porqua_amd.builders import OptimizationItemBuilder, SelectionItemBuilder, bibfn_selection_data
+    from porqua_amd.covariance import Covariance
+    from porqua_amd.optimization import (EmptyOptimization, LeastSquares, MeanVariance, QEQW,
+                                         WeightedLeastSquares)
+    for cls in (LeastSquares, MeanVariance, QEQW, WeightedLeastSquares, EmptyOptimization):
+        o = cls(solver_name="mi355x")
+        assert o.params["solver_name"] == "mi355x"
+    assert LeastSquares().params["solver_name"] == "mi355x" and LeastSquares(verbose=False).params["verbose"] is False
+    mv = MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1))
+    assert mv.params["risk_aversion"] == 1 and mv.covariance.spec["method"] == "linear_shrinkage"
+    bs = BacktestService(data={}, selection_item_builders={"d": SelectionItemBuilder(bibfn=bibfn_selection_data)},
+                         optimization_item_builders={}, optimization=mv, rebdates=[])
+    Backtest().run(bs)
