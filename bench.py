@@ -14,8 +14,8 @@ its own contiguous block of 4749 dates of a longer panel (weak scaling); the onl
 collective is the all-gather of the weight panels.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with a `roofline` object
-for the dominant kernel (K3 ADMM, HBM-bound: algorithmic bytes = 8 n^2 per iteration for
-the K^-1 stream, timed with HIP events on the launch stream) and a `cpu_baseline` object
+for the dominant kernel (K3 ADMM, HBM-bound: algorithmic bytes = 8 n(n+1)/2 per iteration
+for the lower-triangle K^-1 stream, timed with HIP events on the launch stream) and a `cpu_baseline` object
 (the reference per-date path restated in numpy, oracle/cpu_baseline.py, on a bounded
 sample of dates).
 """
@@ -137,7 +137,7 @@ def main():
     iters = res.iters.to(torch.int64)
     total_iters = int(iters.sum().item()) * args.steps   # identical work every step
     status = res.status.cpu().numpy()
-    admm_bytes = 8.0 * n * n * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
+    admm_bytes = 8.0 * n * (n + 1) / 2 * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
     admm_gbs = admm_bytes / tk["admm"] / 1e9
     ld = qb.ld
     nb = ld // 64
@@ -152,7 +152,7 @@ def main():
         try:
             pm = json.load(open(f))
             k = pm["kernels"]["k_admm"]
-            if int(round(k["algorithmic_bytes_per_admm_iteration"])) == 8 * n * n:
+            if int(round(k["algorithmic_bytes_per_admm_iteration"])) == 8 * n * (n + 1) // 2:
                 traffic, traffic_src = k["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
         except Exception:
             pass
@@ -180,7 +180,7 @@ def main():
                      "traffic_unit": "HBM bytes per ADMM iteration (PMC: 2*FETCH_SIZE + WRITE_SIZE, "
                                      "gfx950 correction; committed rocprofv3 pass)",
                      "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_iteration": 8 * n * n,
+                     "algorithmic_bytes_per_iteration": 8 * n * (n + 1) // 2,
                      "admm_iterations_per_step": total_iters // args.steps},
         "stages_s_per_step": {k: v / args.steps for k, v in tk.items()},
         "stage_rates": {

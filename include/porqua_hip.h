@@ -75,9 +75,11 @@ typedef struct pq_state {
   double* work;  int64_t work_stride;   /* >= PQ_WORK_DOUBLES(ld, mg_pad) per problem      */
 } pq_state;
 
+/* rho0_rel > 0: the initial rho of problem b is rho0_rel * mean(diag(P_eff_b)) (clamped to
+ * [rho_min, rho_max]) instead of rho0 -- one scale-aware value per problem.           */
 typedef struct pq_settings {
-  double rho0, sigma, alpha, eps_abs, eps_rel, rho_min, rho_max, adapt_tol, eq_scale, delta,
-      dual_tol;
+  double rho0, rho0_rel, sigma, alpha, eps_abs, eps_rel, rho_min, rho_max, adapt_tol, eq_scale,
+      delta, dual_tol;
   int32_t max_iter, adapt_interval, polish, polish_rounds, refine_iters;
 } pq_settings;
 
@@ -110,14 +112,17 @@ int pq_window_geomean(const double* panel, int64_t ldp, int32_t n, const int32_t
                       const int32_t* tlen, int32_t tmax, int32_t batch, double* mu,
                       int64_t mu_stride, void* stream);
 
-/* Reset x, z, y, Px, iterations, status and set rho = settings.rho0 for problems idx[]. */
+/* Reset x, z, y, Px, iterations, status and set the initial rho (rho0, or rho0_rel times
+ * the mean diagonal of P_eff) for problems idx[].                                      */
 int pq_init_state(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
                   const pq_settings* s, void* stream);
 
 /* K2: form K = P_eff + sigma I + Cg' R Cg + R_box for the current rho, factor it with a
  * batched blocked Cholesky on FP64 MFMA (info[] = first failing column + 1, the isPD test
- * of src/helper_functions.py:61-67), and if `invert` overwrite K with K^-1 (trtri+lauum).
- * With mg = 0, lb = ub = NULL and sigma = 0 this is a plain batched potrf of P_eff.     */
+ * of src/helper_functions.py:61-67), and if `invert` overwrite K with K^-1 (trtri+lauum):
+ * invert = 1 writes the lower triangle only (what pq_admm_batched reads), invert = 2 the
+ * full symmetric matrix.  With mg = 0, lb = ub = NULL and sigma = 0 this is a plain
+ * batched potrf of P_eff.                                                              */
 int pq_factor_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
                       const pq_settings* s, int32_t invert, void* stream);
 

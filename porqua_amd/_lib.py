@@ -65,7 +65,8 @@ class PQState(ctypes.Structure):
 
 class PQSettings(ctypes.Structure):
     _fields_ = [
-        ("rho0", ctypes.c_double), ("sigma", ctypes.c_double), ("alpha", ctypes.c_double),
+        ("rho0", ctypes.c_double), ("rho0_rel", ctypes.c_double),
+        ("sigma", ctypes.c_double), ("alpha", ctypes.c_double),
         ("eps_abs", ctypes.c_double), ("eps_rel", ctypes.c_double),
         ("rho_min", ctypes.c_double), ("rho_max", ctypes.c_double),
         ("adapt_tol", ctypes.c_double), ("eq_scale", ctypes.c_double),

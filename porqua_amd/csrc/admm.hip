@@ -1,12 +1,13 @@
 // K3: batched OSQP-style ADMM, one 512-thread workgroup per QP, iterations inside the
 // kernel with per-problem convergence (a converged problem's workgroup simply exits).
 //
-// Per iteration the only O(n^2) work is x~ = K^-1 rhs: every row of K^-1 (8 B x ld per
-// row, the whole matrix per iteration) is streamed from HBM exactly once with 16-byte
-// coalesced loads in "axpy" form -- wave w accumulates rhs_j * K^-1[j, :] for rows
-// j = w (mod 8) in registers (lane l owns columns 128 q + 2 l, 2 l + 1) -- and the eight
-// partial vectors are combined by a fixed-order LDS tree (bit-reproducible).  Everything
-// else is O(n + mg n) and lives in LDS: x, Px, z, y, rhs, q, bounds.
+// Per iteration the only O(n^2) work is x~ = K^-1 rhs.  K^-1 is symmetric, so only its
+// lower triangle (8 B x n(n+1)/2) is streamed from HBM, once per iteration, with 16-byte
+// coalesced loads: wave w takes rows j = w (mod 8); row j adds K[j][c] rhs[j] to x~[c]
+// for c < j in register accumulators (lane l owns columns 128 q + 2 l, 2 l + 1) and
+// sum_{c<=j} K[j][c] rhs[c] to x~[j] through one wave reduction.  The eight partial
+// vectors are combined by a fixed-order LDS tree (bit-reproducible).  Everything else is
+// O(n + mg n) and lives in LDS: x, Px, z, y, rhs, q, bounds.
 //
 // P x is never formed with another mat-vec: K x~ = rhs gives P x~ = rhs - sigma x~ -
 // C'R C x~, and P x_{k+1} = alpha P x~ + (1 - alpha) P x_k, so the OSQP residuals and
@@ -63,7 +64,7 @@ template <int NQ>
 __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const int32_t* idx,
                                              int nidx, pq_settings s, int iters_call) {
   constexpr int LDMAX = NQ * 128;
-  __shared__ __attribute__((aligned(16))) double sm[9 * LDMAX + 4 * LDMAX + 8 * 64 + 16 * AW];
+  __shared__ __attribute__((aligned(16))) double sm[10 * LDMAX + 4 * LDMAX + 8 * 64 + 16 * AW];
   double* x = sm;
   double* Px = x + LDMAX;
   double* zb = Px + LDMAX;
@@ -73,7 +74,8 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
   double* xt = rhs + LDMAX;
   double* lo = xt + LDMAX;
   double* up = lo + LDMAX;
-  double* tree = up + LDMAX;       // 4 * LDMAX partial-vector scratch
+  double* dotv = up + LDMAX;       // per-row dot products of the lower-triangle mat-vec
+  double* tree = dotv + LDMAX;     // 4 * LDMAX partial-vector scratch
   double* zg = tree + 4 * LDMAX;   // mg <= 64 each
   double* yg = zg + 64;
   double* rg = yg + 64;
@@ -145,40 +147,65 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
     }
     for (int i = n + t; i < LDMAX; i += AT) rhs[i] = 0.0;
     __syncthreads();
-    // ---- x~ = K^-1 rhs (the HBM stream) ---------------------------------------------
+    // ---- x~ = K^-1 rhs (the HBM stream): lower triangle only ------------------------
+    // row j contributes K[j][c] rhs[j] to x~[c] for c < j (axpy, register accumulators)
+    // and sum_{c <= j} K[j][c] rhs[c] to x~[j] (dot, one wave reduction per row).
     double2 acc[NQ];
+    double2 rv[NQ];
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) acc[qq] = double2{0.0, 0.0};
+    for (int qq = 0; qq < NQ; ++qq) {
+      acc[qq] = double2{0.0, 0.0};
+      rv[qq] = reinterpret_cast<const double2*>(rhs)[64 * qq + l];
+    }
     {
       int j = w;
       for (; j + AW < n; j += 2 * AW) {
+        const int j1 = j + AW;
         const double2* r0 = reinterpret_cast<const double2*>(Kinv + (int64_t)j * ld) + l;
-        const double2* r1 = reinterpret_cast<const double2*>(Kinv + (int64_t)(j + AW) * ld) + l;
+        const double2* r1 = reinterpret_cast<const double2*>(Kinv + (int64_t)j1 * ld) + l;
         double2 v0[NQ], v1[NQ];
 #pragma unroll
         for (int qq = 0; qq < NQ; ++qq) {
-          const bool ok = 128 * qq + 2 * l < n;
-          v0[qq] = ok ? r0[64 * qq] : double2{0.0, 0.0};
-          v1[qq] = ok ? r1[64 * qq] : double2{0.0, 0.0};
+          const int c = 128 * qq + 2 * l;
+          v0[qq] = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
+          v1[qq] = (c <= j1) ? r1[64 * qq] : double2{0.0, 0.0};
         }
-        const double a0 = rhs[j], a1 = rhs[j + AW];
+        const double a0 = rhs[j], a1 = rhs[j1];
+        double d0 = 0.0, d1 = 0.0;
 #pragma unroll
         for (int qq = 0; qq < NQ; ++qq) {
-          acc[qq].x = fma(a0, v0[qq].x, acc[qq].x);
-          acc[qq].y = fma(a0, v0[qq].y, acc[qq].y);
-          acc[qq].x = fma(a1, v1[qq].x, acc[qq].x);
-          acc[qq].y = fma(a1, v1[qq].y, acc[qq].y);
+          const int c = 128 * qq + 2 * l;
+          const double y0 = (c + 1 <= j) ? v0[qq].y : 0.0;
+          const double y1 = (c + 1 <= j1) ? v1[qq].y : 0.0;
+          d0 = fma(v0[qq].x, rv[qq].x, fma(y0, rv[qq].y, d0));
+          d1 = fma(v1[qq].x, rv[qq].x, fma(y1, rv[qq].y, d1));
+          acc[qq].x = fma(a0, (c < j) ? v0[qq].x : 0.0, acc[qq].x);
+          acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
+          acc[qq].x = fma(a1, (c < j1) ? v1[qq].x : 0.0, acc[qq].x);
+          acc[qq].y = fma(a1, (c + 1 < j1) ? y1 : 0.0, acc[qq].y);
+        }
+        d0 = wave_sum(d0);
+        d1 = wave_sum(d1);
+        if (l == 0) {
+          dotv[j] = d0;
+          dotv[j1] = d1;
         }
       }
       if (j < n) {
         const double2* r0 = reinterpret_cast<const double2*>(Kinv + (int64_t)j * ld) + l;
         const double a0 = rhs[j];
+        double d0 = 0.0;
 #pragma unroll
         for (int qq = 0; qq < NQ; ++qq) {
-          const double2 v = (128 * qq + 2 * l < n) ? r0[64 * qq] : double2{0.0, 0.0};
-          acc[qq].x = fma(a0, v.x, acc[qq].x);
-          acc[qq].y = fma(a0, v.y, acc[qq].y);
+          const int c = 128 * qq + 2 * l;
+          const double2 v = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
+          const double y0 = (c + 1 <= j) ? v.y : 0.0;
+          d0 = fma(v.x, rv[qq].x, fma(y0, rv[qq].y, d0));
+          acc[qq].x = fma(a0, (c < j) ? v.x : 0.0, acc[qq].x);
+          acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
         }
+        d0 = wave_sum(d0);
+        if (l == 0) dotv[j] = d0;
       }
     }
     // fixed-order tree: waves 4-7 -> 0-3 -> 0-1 -> 0
@@ -203,8 +230,12 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
     }
     if (w == 0) {
       double2* dst = reinterpret_cast<double2*>(xt) + l;
+      const double2* dv = reinterpret_cast<const double2*>(dotv) + l;
 #pragma unroll
-      for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
+      for (int qq = 0; qq < NQ; ++qq) {
+        const double2 d = dv[64 * qq];
+        dst[64 * qq] = double2{acc[qq].x + d.x, acc[qq].y + d.y};
+      }
     }
     __syncthreads();
     // ---- z~ for the general rows ----------------------------------------------------
@@ -324,8 +355,20 @@ __global__ void k_init_state(pq_problem pb, pq_state st, const int32_t* idx, pq_
     st.z[(int64_t)b * st.m_ld + i] = 0.0;
     st.y[(int64_t)b * st.m_ld + i] = 0.0;
   }
+  double rho0 = s.rho0;
+  if (s.rho0_rel > 0.0) {
+    __shared__ double red[16];
+    const double* P = pb.P + (int64_t)b * pb.P_stride;
+    const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
+    const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+    double sdiag = 0.0;
+    for (int i = threadIdx.x; i < pb.n; i += blockDim.x) sdiag += ps * P[(int64_t)i * ld + i] + pd;
+    sdiag = block_sum(sdiag, red);
+    const double md = sdiag / pb.n;
+    rho0 = (md > 0.0 && isfinite(md)) ? fmin(fmax(s.rho0_rel * md, s.rho_min), s.rho_max) : s.rho0;
+  }
   if (threadIdx.x == 0) {
-    st.rho[b] = s.rho0;
+    st.rho[b] = rho0;
     st.iters[b] = 0;
     st.status[b] = PQ_UNSOLVED;
     st.info[b] = 0;

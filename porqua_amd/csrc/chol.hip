@@ -23,7 +23,8 @@ struct FormCtx {
   int n, mg;
   double ps, pd, sigma;
   const double* Cg;
-  const double* rg;   // LDS, mg entries: rho of each general row
+  const double* lg;   // general-row bounds (rho of each row derived on the fly)
+  const double* ug;
   const double* lb;
   const double* ub;
   double rho, rho_min, eq_scale;
@@ -39,7 +40,9 @@ __device__ __forceinline__ double rho_for(double l, double u, double rho, double
 __device__ __forceinline__ double form_elem(const FormCtx& f, int gi, int gj) {
   if (gi >= f.n || gj >= f.n) return gi == gj ? 1.0 : 0.0;
   double v = f.ps * f.P[(int64_t)gi * f.ld + gj];
-  for (int r = 0; r < f.mg; ++r) v += f.rg[r] * f.Cg[(int64_t)r * f.ld + gi] * f.Cg[(int64_t)r * f.ld + gj];
+  for (int r = 0; r < f.mg; ++r)
+    v += rho_for(f.lg[r], f.ug[r], f.rho, f.rho_min, f.eq_scale) * f.Cg[(int64_t)r * f.ld + gi] *
+         f.Cg[(int64_t)r * f.ld + gj];
   if (gi == gj) {
     v += f.pd + f.sigma;
     if (f.lb != nullptr) v += rho_for(f.lb[gi], f.ub[gi], f.rho, f.rho_min, f.eq_scale);
@@ -52,13 +55,12 @@ struct FormOp {
   __device__ __forceinline__ double operator()(int gi, int gj) const { return form_elem(*f, gi, gj); }
 };
 
-__global__ __launch_bounds__(256) void k_factor(pq_problem pb, pq_state st, const int32_t* idx,
+__global__ __launch_bounds__(256, 2) void k_factor(pq_problem pb, pq_state st, const int32_t* idx,
                                                 int nidx, pq_settings s, int invert) {
-  __shared__ __attribute__((aligned(16))) double smem[4 * STAGE + TB * LDW + 64 + 8];
+  // exactly CHOL_LDS (80 KiB): two workgroups per CU
+  __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS];
   double* stg = smem;                      // 4*STAGE: stream buffers / W image / diag tile
   double* sD = smem + 4 * STAGE;           // 64 x LDW: Dinv image for the current column
-  double* rg = sD + TB * LDW;              // 64: rho per general row
-  int* flag = reinterpret_cast<int*>(rg + 64);
 
   const int b = idx ? idx[blockIdx.x] : (int)blockIdx.x;
   const int ld = pb.ld, n = pb.n, nb = ld / TB;
@@ -76,13 +78,8 @@ __global__ __launch_bounds__(256) void k_factor(pq_problem pb, pq_state st, cons
   f.lb = pb.lb ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
   f.ub = pb.ub ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
   f.rho = rho; f.rho_min = s.rho_min; f.eq_scale = s.eq_scale;
-  f.rg = rg;
-  if (threadIdx.x < pb.mg) {
-    const double* lg = pb.lg + (int64_t)b * pb.g_stride;
-    const double* ug = pb.ug + (int64_t)b * pb.g_stride;
-    rg[threadIdx.x] = rho_for(lg[threadIdx.x], ug[threadIdx.x], rho, s.rho_min, s.eq_scale);
-  }
-  __syncthreads();
+  f.lg = pb.mg ? pb.lg + (int64_t)b * pb.g_stride : nullptr;
+  f.ug = pb.mg ? pb.ug + (int64_t)b * pb.g_stride : nullptr;
 
   int info = wg_cholesky(FormOp{&f}, K, ld, nb, Dt, smem);
   if (threadIdx.x == 0) {
@@ -128,7 +125,7 @@ __global__ __launch_bounds__(256) void k_factor(pq_problem pb, pq_state st, cons
       gemm_stream<MODE_KI, MODE_KI>(acc, stg, K, ld, I * TB, I * TB, K, ld, J * TB, I * TB,
                                     (nb - I) * TB);
       acc_store(acc, K, ld, I * TB, J * TB);
-      if (J < I) acc_store_T(acc, K, ld, J * TB, I * TB);
+      if (J < I && invert == 2) acc_store_T(acc, K, ld, J * TB, I * TB);
     }
   }
 }

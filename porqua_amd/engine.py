@@ -45,9 +45,13 @@ def default_device() -> torch.device:
 
 @dataclass
 class Settings:
-    """ADMM / polish settings (OSQP defaults except the tighter eps: the polish needs a
-    correct active set).  Passed through ``params`` of the reference API."""
+    """ADMM / polish settings.  OSQP defaults except: tighter eps (the polish needs a
+    correct active set) and a scale-aware initial rho (4 x mean diag P, adapted every 60
+    iterations) -- measured on the n = 1000 min-variance windows this converges in ~40
+    iterations with no refactorisation, against ~85 + 1 refactor for rho0 = 0.1 / 25
+    (tests/engine_model.py).  Passed through ``params`` of the reference API."""
     rho0: float = 0.1
+    rho0_rel: float = 4.0      # initial rho = rho0_rel * mean(diag P) (0: use rho0)
     sigma: float = 1e-6
     alpha: float = 1.6
     eps_abs: float = 1e-5
@@ -59,7 +63,7 @@ class Settings:
     delta: float = 1e-9        # polish regularisation, relative to the problem scale
     dual_tol: float = 1e-9     # multiplier sign tolerance, relative to the problem scale
     max_iter: int = 4000
-    adapt_interval: int = 25
+    adapt_interval: int = 60
     polish: int = 1
     polish_rounds: int = 8
     refine_iters: int = 8
@@ -333,7 +337,7 @@ def factor_only(qb: QPBatch, invert: bool = False, sigma: float = 0.0):
     strm = _stream()
     _lib.check(lib.pq_init_state(ctypes.byref(pb), ctypes.byref(st), None, 0, ctypes.byref(s), strm), "init")
     _lib.check(lib.pq_factor_batched(ctypes.byref(pb), ctypes.byref(st), None, 0, ctypes.byref(s),
-                                     1 if invert else 0, strm), "pq_factor_batched")
+                                     2 if invert else 0, strm), "pq_factor_batched")
     return ws, ws.info
 
 

@@ -189,6 +189,8 @@ class LeastSquares(Optimization):
     def __init__(self, covariance: Optional[Covariance] = None, **kwargs):
         super().__init__(**kwargs)
         self.covariance = covariance
+        # tracking problems: P = 2 X'X is well scaled, a smaller initial rho converges faster
+        self.params.setdefault("rho0_rel", 0.5)
 
     def set_objective(self, optimization_data: OptimizationData) -> None:
         X = optimization_data["return_series"]

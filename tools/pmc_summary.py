@@ -56,7 +56,7 @@ def main():
     adm = out["kernels"].get("k_admm")
     if adm:
         adm["hbm_bytes_per_admm_iteration"] = adm["hbm_bytes_per_step"] / iters
-        adm["algorithmic_bytes_per_admm_iteration"] = 8.0 * bench_pmc["config"]["n_assets"] ** 2
+        adm["algorithmic_bytes_per_admm_iteration"] = float(bench_pmc["roofline"]["algorithmic_bytes_per_iteration"])
     with open(os.path.join(dst, f"{rnd}_pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     full = os.path.join(src, "bench_full.log")
