@@ -45,7 +45,7 @@ extern "C" {
 #define PQ_OUT_FIELDS 8
 
 /* polish scratch per problem (doubles) */
-#define PQ_WORK_DOUBLES(ld, mg_pad) ((int64_t)(5 + (mg_pad)) * (ld) + 512)
+#define PQ_WORK_DOUBLES(ld, mg_pad) ((int64_t)(4 + (mg_pad)) * (ld) + 512)
 
 /* A batch of dense QPs   min 0.5 x'Px + q'x  s.t.  lg <= Cg x <= ug,  lb <= x <= ub
  * (the QuadraticProgram fields P, q, G, h, A, b, lb, ub of src/qp_problems.py:34-38 with

@@ -38,7 +38,7 @@ struct PolishForm {
 
 // y = L^-1 r  (L in K with ld, block inverses in Dt); r, y, t64 in LDS, length nbk*64.
 __device__ void fwd_solve(const double* K, int64_t ld, const double* Dt, int nbk, const double* r,
-                          double* y, double* t64) {
+                          double* y, double* t64, double* y64p) {
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   for (int I = 0; I < nbk; ++I) {
     for (int i = w; i < TB; i += PW) {
@@ -49,19 +49,23 @@ __device__ void fwd_solve(const double* K, int64_t ld, const double* Dt, int nbk
       if (l == 0) t64[i] = r[I * TB + i] - s;
     }
     __syncthreads();
-    if (t < TB) {
+    {  // y_I = Dinv_I t_I : 4 threads per output row, 16 independent loads each
       const double* D = Dt + (int64_t)I * TB * TB;
+      const int o = t & 63, part = t >> 6;
       double s = 0.0;
-      for (int c = 0; c < TB; ++c) s += D[c * TB + t] * t64[c];   // Dinv[t][c] = Dt[c][t]
-      y[I * TB + t] = s;
+#pragma unroll
+      for (int c = part * 16; c < part * 16 + 16; ++c) s += D[c * TB + o] * t64[c];   // Dinv[o][c] = Dt[c][o]
+      y64p[part * TB + o] = s;
     }
+    __syncthreads();
+    if (t < TB) y[I * TB + t] = (y64p[t] + y64p[TB + t]) + (y64p[2 * TB + t] + y64p[3 * TB + t]);
     __syncthreads();
   }
 }
 
 // x = L^-T y ; part[] is 4*64 LDS scratch.
 __device__ void bwd_solve(const double* K, int64_t ld, const double* Dt, int nbk, const double* y,
-                          double* x, double* t64, double* part) {
+                          double* x, double* t64, double* part, double* part_out) {
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   for (int I = nbk - 1; I >= 0; --I) {
     // t_I = y_I - sum_{r >= 64(I+1)} L[r][64I + i] x[r]   (lanes over i, waves split r)
@@ -71,12 +75,16 @@ __device__ void bwd_solve(const double* K, int64_t ld, const double* Dt, int nbk
     __syncthreads();
     if (t < TB) t64[t] = y[I * TB + t] - (part[t] + part[TB + t] + part[2 * TB + t] + part[3 * TB + t]);
     __syncthreads();
-    if (t < TB) {
+    {  // x_I = Dinv_I' t_I : (Dinv')[o][c] = Dt[o][c], 4 threads per output
       const double* D = Dt + (int64_t)I * TB * TB;
+      const int o = t & 63, part = t >> 6;
       double v = 0.0;
-      for (int c = 0; c < TB; ++c) v += D[t * TB + c] * t64[c];   // (Dinv^T)[t][c] = Dinv[c][t] = Dt[t][c]
-      x[I * TB + t] = v;
+#pragma unroll
+      for (int c = part * 16; c < part * 16 + 16; ++c) v += D[o * TB + c] * t64[c];
+      part_out[part * TB + o] = v;
     }
+    __syncthreads();
+    if (t < TB) x[I * TB + t] = (part_out[t] + part_out[TB + t]) + (part_out[2 * TB + t] + part_out[3 * TB + t]);
     __syncthreads();
   }
 }
@@ -88,7 +96,7 @@ __device__ __forceinline__ int block_or(int v, double* red) {
 __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const int32_t* idx,
                                                int nidx, pq_settings s) {
   constexpr int LDMAX = 1024;
-  __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS + 2 * LDMAX + 10 * 64 + 64];
+  __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS + 2 * LDMAX + 14 * 64 + 64 + LDMAX + 256];
   double* stg = smem;                  // Cholesky stream buffers; S factor during refinement
   double* vec = smem + 4 * STAGE;      // sD region: 3 LDMAX vectors during refinement
   double* solx = smem + CHOL_LDS;      // compact solution x_F
@@ -101,6 +109,15 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
   double* part = t64 + 64;             // 4*64 (also reduction scratch)
   double* red = part + 4 * 64;         // 64
   double* lamF = red + 64;             // 64: multipliers of all general rows (by row)
+  double* y64p = lamF + 64;            // 4*64 partial sums of the diagonal-block products
+  // index bookkeeping lives in LDS: these arrays are rewritten every active-set round and
+  // read at wave-uniform addresses, which hipcc serves from the (non-coherent) scalar
+  // cache when they sit in global memory -- stale values in round >= 2.
+  int* fl = reinterpret_cast<int*>(y64p + 4 * 64);   // LDMAX: 0 free, 1 at lower, 2 at upper
+  int* Fl = fl + LDMAX;                               // LDMAX: free-variable list
+  int* act = Fl + LDMAX;                              // 64
+  int* Al = act + 64;                                 // 64
+  int* cnt = Al + 64;                                 // PT + 8
 
   const int b = idx ? idx[blockIdx.x] : (int)blockIdx.x;
   const int st0 = st.status[b];
@@ -122,18 +139,13 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
   double* sx = st.x + (int64_t)b * ld;
   double* sz = st.z + (int64_t)b * st.m_ld;
   double* sy = st.y + (int64_t)b * st.m_ld;
-  // work layout (doubles): xs | xb | g | Px | U (mg_pad rows) | ints: fl | Flist
+  // work layout (doubles): xs | xb | g | Px | U (mg_pad rows)
   double* W = st.work + (int64_t)b * st.work_stride;
   double* xs = W;
   double* xb = xs + ld;
   double* g = xb + ld;
   double* Px = g + ld;
   double* U = Px + ld;
-  int* fl = reinterpret_cast<int*>(U + (int64_t)st.mg_pad * ld);
-  int* Fl = fl + ld;
-  int* act = Fl + ld;     // 64
-  int* Al = act + 64;     // 64
-  int* cnt = Al + 64;     // 256 + 8 scratch
 
   // ---- problem scale -> tolerances ----------------------------------------------------
   double sc = 0.0;
@@ -196,6 +208,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     const int nbk = (k + TB - 1) / TB;
     for (int i = t; i < n; i += PT) xb[i] = fl[i] == 1 ? lb[i] : (fl[i] == 2 ? ub[i] : 0.0);
     __syncthreads();
+    __builtin_amdgcn_s_dcache_inv();
     // ---- reduced rhs: rF = -q_F - ps P_FB x_B ;  d_a = rhs_a - C_aB x_B -----------------
     for (int p = w; p < k; p += PW) {
       const int i = Fl[p];
@@ -229,10 +242,11 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
       const int r = Al[a];
       for (int p = t; p < nbk * TB; p += PT) rx[p] = p < k ? Cg[(int64_t)r * ld + Fl[p]] : 0.0;
       __syncthreads();
-      fwd_solve(K, ld, Dt, nbk, rx, t1, t64);
+      fwd_solve(K, ld, Dt, nbk, rx, t1, t64, y64p);
       for (int p = t; p < nbk * TB; p += PT) U[(int64_t)a * ld + p] = t1[p];
       __syncthreads();
     }
+    __builtin_amdgcn_s_dcache_inv();   // U is re-read below, partly at uniform addresses
     for (int e = t; e < TB * TB; e += PT) {
       const int i = e >> 6, j = e & 63;
       double v = (i == j) ? 1.0 : 0.0;
@@ -271,7 +285,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
         }
       }
       __syncthreads();
-      fwd_solve(K, ld, Dt, nbk, rx, t1, t64);
+      fwd_solve(K, ld, Dt, nbk, rx, t1, t64, y64p);
       // wl = U' t1 - rl ; dlam = S^-1 wl (S = Ls Ls', tiny, one thread)
       for (int a = w; a < ma; a += PW) {
         double sum = 0.0;
@@ -300,7 +314,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
         t1[p] = v;
       }
       __syncthreads();
-      bwd_solve(K, ld, Dt, nbk, t1, dx, t64, part);
+      bwd_solve(K, ld, Dt, nbk, t1, dx, t64, part, y64p);
       for (int p = t; p < k; p += PT) solx[p] += dx[p];
       if (t < ma) solL[t] += wl[t];
       __syncthreads();
@@ -313,6 +327,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     __syncthreads();
     if (t < ma) lamF[Al[t]] = solL[t];  // full-length general multipliers
     __syncthreads();
+    __builtin_amdgcn_s_dcache_inv();   // xs was rewritten: no stale scalar-cache reads
     for (int i = w; i < n; i += PW) {
       const double* row = P + (int64_t)i * ld;
       double sum = 0.0;
@@ -361,6 +376,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     for (int i = t; i < n; i += PT) xs[i] = sx[i];
     if (t < 64) lamF[t] = (t < mg) ? sy[t] : 0.0;
     __syncthreads();
+    __builtin_amdgcn_s_dcache_inv();
     for (int i = w; i < n; i += PW) {
       const double* row = P + (int64_t)i * ld;
       double sum = 0.0;

@@ -66,7 +66,7 @@ class Settings:
     adapt_interval: int = 60
     polish: int = 1
     polish_rounds: int = 8
-    refine_iters: int = 8
+    refine_iters: int = 4
 
     def to_c(self) -> _lib.PQSettings:
         return _lib.PQSettings(**{f.name: getattr(self, f.name) for f in dataclasses.fields(self)})
