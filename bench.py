@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--window", type=int, default=252)
     ap.add_argument("--dates", type=int, default=4749, help="rebalance dates per rank")
+    ap.add_argument("--path", choices=["auto", "dense", "lowrank"], default="auto",
+                    help="dense K^-1 (K2 n^3 + K3 n^2 stream) or Woodbury low-rank (T + mg < n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     return ap.parse_args()
@@ -86,18 +88,24 @@ def main():
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)   # P = 2 * Sigma
     ws = engine.Workspace(qb)
     settings = engine.Settings()
+    mu_lr = pan.window_means(rows_d, tlen_d)
+    lr = engine.LowRank(pan, rows_d, tlen_d, mu=mu_lr, w_scale=1.0 / (tlen_d.to(torch.float64) - 1.0))
+    use_lr = args.path == "lowrank" or (args.path == "auto" and engine.lowrank_applicable(qb, lr))
     w_host = torch.empty((D * world, n), dtype=torch.float64).pin_memory() if rank == 0 else None
     gather_buf = torch.empty((world, D, n), dtype=torch.float64, device=dev) if world > 1 else None
 
     def step(events=None):
-        mu = pan.window_means(rows_d, tlen_d)
+        mu = pan.window_means(rows_d, tlen_d, out=mu_lr)
         if events is not None:
             e0 = torch.cuda.Event(enable_timing=True); e0.record()
         pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu)
         if events is not None:
             e1 = torch.cuda.Event(enable_timing=True); e1.record()
             events.append(("cov", e0, e1))
-        res = engine.solve(qb, settings, ws, events=events)
+        if use_lr:
+            res = engine.solve_lowrank(qb, lr, settings, ws, events=events)
+        else:
+            res = engine.solve(qb, settings, ws, events=events)
         x = res.x.contiguous()
         if world > 1:
             dist.all_gather_into_tensor(gather_buf, x)
@@ -137,12 +145,15 @@ def main():
     iters = res.iters.to(torch.int64)
     total_iters = int(iters.sum().item()) * args.steps   # identical work every step
     status = res.status.cpu().numpy()
-    admm_bytes = 8.0 * n * (n + 1) / 2 * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
+    k_lr = T + 1
+    it_bytes = (8.0 * (2 * T * n + k_lr * (k_lr + 1) / 2)) if use_lr else 8.0 * n * (n + 1) / 2
+    admm_bytes = it_bytes * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
     admm_gbs = admm_bytes / tk["admm"] / 1e9
     ld = qb.ld
     nb = ld // 64
     syrk_flops = D * (nb * (nb + 1) // 2) * 64 * 64 * 2.0 * T * args.steps
-    factor_flops_per = ld ** 3  # potrf + trtri + lauum ~ ld^3 (n^3/3 each)
+    kld = ((T + 1 + 63) // 64) * 64
+    factor_flops_per = (2.0 * kld * kld * n + kld ** 3) if use_lr else ld ** 3  # (capacitance SYRK +) potrf+trtri+lauum
     n_factor = D * args.steps + res.refactors * args.steps
     factor_flops = factor_flops_per * n_factor
 
@@ -152,7 +163,7 @@ def main():
         try:
             pm = json.load(open(f))
             k = pm["kernels"]["k_admm"]
-            if int(round(k["algorithmic_bytes_per_admm_iteration"])) == 8 * n * (n + 1) // 2:
+            if int(round(k["algorithmic_bytes_per_admm_iteration"])) == int(it_bytes):
                 traffic, traffic_src = k["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
         except Exception:
             pass
@@ -180,7 +191,8 @@ def main():
                      "traffic_unit": "HBM bytes per ADMM iteration (PMC: 2*FETCH_SIZE + WRITE_SIZE, "
                                      "gfx950 correction; committed rocprofv3 pass)",
                      "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_iteration": 8 * n * (n + 1) // 2,
+                     "algorithmic_bytes_per_iteration": int(it_bytes),
+                     "path": "lowrank (Woodbury: window rows + M^-1)" if use_lr else "dense K^-1 (lower)",
                      "admm_iterations_per_step": total_iters // args.steps},
         "stages_s_per_step": {k: v / args.steps for k, v in tk.items()},
         "stage_rates": {

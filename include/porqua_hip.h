@@ -83,6 +83,21 @@ typedef struct pq_settings {
   int32_t max_iter, adapt_interval, polish, polish_rounds, refine_iters;
 } pq_settings;
 
+/* Low-rank description of P for T < n (the backtest path): P_eff = p_scale[b] *
+ * w_scale[b] * Xc'Xc + p_diag[b] * I, Xc = the T x n window of the panel
+ * (rows[b][0..tlen[b])) centred by mu (mu == NULL: uncentred Gram, the LeastSquares case);
+ * w_scale (NULL = 1) is 1/(T-1) when pq_problem.P holds the covariance of the same window.
+ * With D = diag(sigma + p_diag + rho_box) and
+ * U' = [sqrt(p_scale w_scale) Xc' | sqrt(rho_r) Cg_r'] (n x k, k = tmax + mg) the ADMM
+ * system is K = D + U'U, so K^-1 = D^-1 - D^-1 U' M^-1 U D^-1 with the k x k capacitance
+ * matrix M = I + U D^-1 U' (Woodbury): no n x n matrix is formed or factored.          */
+typedef struct pq_lowrank {
+  const double* panel; int64_t ldp;
+  const int32_t* rows; const int32_t* tlen; int32_t tmax;
+  const double* mu; int64_t mu_stride;
+  const double* w_scale;
+} pq_lowrank;
+
 int pq_version(void);
 const char* pq_last_error(void);
 
@@ -132,6 +147,19 @@ int pq_factor_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, in
  * Replaces qpsolvers.solve_problem (src/qp_problems.py:211-214).                        */
 int pq_admm_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
                     const pq_settings* s, int32_t iters_this_call, void* stream);
+
+/* Low-rank K2: capacitance matrices M_b = I + U D^-1 U' (lower 64x64 tiles, k_ld =
+ * round_up(tmax + mg, 64)) for the current rho[], as an MFMA SYRK over the n assets.
+ * Factor / invert them with pq_factor_batched on a pq_problem {n = k_ld, P = M}.       */
+int pq_lr_capacitance(const pq_lowrank* lr, const pq_problem* pb, const pq_state* st,
+                      const int32_t* idx, int32_t nidx, const pq_settings* s, double* M,
+                      int32_t k_ld, int64_t M_stride, void* stream);
+
+/* Low-rank K3: the ADMM of pq_admm_batched with x~ = K^-1 rhs applied through the window
+ * (two passes over its T rows) and the lower-triangle M^-1 (Minv, k_ld x k_ld).        */
+int pq_admm_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
+                       const double* Minv, int32_t k_ld, int64_t M_stride, const int32_t* idx,
+                       int32_t nidx, const pq_settings* s, int32_t iters_this_call, void* stream);
 
 /* K4: active-set polish of the ADMM point (reduced KKT by masked Cholesky + Schur +
  * proximal iterative refinement), then exact residuals / objective of the final point

@@ -76,6 +76,15 @@ class PQSettings(ctypes.Structure):
     ]
 
 
+class PQLowRank(ctypes.Structure):
+    _fields_ = [
+        ("panel", c_dp), ("ldp", c_int64),
+        ("rows", c_dp), ("tlen", c_dp), ("tmax", c_int32),
+        ("mu", c_dp), ("mu_stride", c_int64),
+        ("w_scale", c_dp),
+    ]
+
+
 _EXPORTS = {
     "pq_version": ([], c_int32),
     "pq_last_error": ([], ctypes.c_char_p),
@@ -93,6 +102,11 @@ _EXPORTS = {
                          ctypes.POINTER(PQSettings), c_int32, c_dp], c_int32),
     "pq_polish_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
                            ctypes.POINTER(PQSettings), c_dp], c_int32),
+    "pq_lr_capacitance": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                           c_dp, c_int32, ctypes.POINTER(PQSettings), c_dp, c_int32, c_int64, c_dp], c_int32),
+    "pq_admm_lr_batched": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                            c_dp, c_int32, c_int64, c_dp, c_int32, ctypes.POINTER(PQSettings), c_int32,
+                            c_dp], c_int32),
 }
 
 _lib = None

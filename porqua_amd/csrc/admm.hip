@@ -60,11 +60,246 @@ __device__ void rows_dot(const double* Cg, int64_t ld, int mg, int n, const doub
   }
 }
 
+// fixed-order combination of the AW waves' register vectors into wave 0's acc:
+// waves 4-7 -> 0-3 -> 0-1 -> 0 through LDS (tree: 4 * NQ*128 doubles)
 template <int NQ>
-__global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const int32_t* idx,
-                                             int nidx, pq_settings s, int iters_call) {
+__device__ __forceinline__ void tree_reduce(double2 (&acc)[NQ], double* tree) {
+  constexpr int LM = NQ * 128;
+  const int w = wave_id(), l = lane_id();
+#pragma unroll
+  for (int half = AW / 2; half >= 1; half >>= 1) {
+    if (w >= half && w < 2 * half) {
+      double2* dst = reinterpret_cast<double2*>(tree + (w - half) * LM) + l;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
+    }
+    __syncthreads();
+    if (w < half) {
+      const double2* src = reinterpret_cast<const double2*>(tree + w * LM) + l;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const double2 vv = src[64 * qq];
+        acc[qq].x += vv.x;
+        acc[qq].y += vv.y;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// y = A v for a symmetric A of which only the lower triangle (rows j < n, leading
+// dimension ld) is read: row j adds A[j][c] v[j] to y[c] for c < j (axpy, register
+// accumulators; lane l owns columns 128 q + 2 l, 2 l + 1) and sum_{c<=j} A[j][c] v[c] to
+// y[j] (one wave reduction per row).  Partial vectors of the AW waves are combined by a
+// fixed-order LDS tree (bit-reproducible).  v, y, dotv: LDS, >= NQ*128 entries (v zero
+// beyond n); tree: 4 * NQ*128 doubles.  All threads must call.
+template <int NQ>
+__device__ void symv_lower(const double* A, int64_t ld, int n, const double* v, double* y,
+                           double* dotv, double* tree) {
+  constexpr int LM = NQ * 128;
+  const int w = wave_id(), l = lane_id();
+  double2 acc[NQ];
+  double2 rv[NQ];
+#pragma unroll
+  for (int qq = 0; qq < NQ; ++qq) {
+    acc[qq] = double2{0.0, 0.0};
+    rv[qq] = reinterpret_cast<const double2*>(v)[64 * qq + l];
+  }
+  int j = w;
+  for (; j + AW < n; j += 2 * AW) {
+    const int j1 = j + AW;
+    const double2* r0 = reinterpret_cast<const double2*>(A + (int64_t)j * ld) + l;
+    const double2* r1 = reinterpret_cast<const double2*>(A + (int64_t)j1 * ld) + l;
+    double2 v0[NQ], v1[NQ];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const int c = 128 * qq + 2 * l;
+      v0[qq] = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
+      v1[qq] = (c <= j1) ? r1[64 * qq] : double2{0.0, 0.0};
+    }
+    const double a0 = v[j], a1 = v[j1];
+    double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const int c = 128 * qq + 2 * l;
+      const double y0 = (c + 1 <= j) ? v0[qq].y : 0.0;
+      const double y1 = (c + 1 <= j1) ? v1[qq].y : 0.0;
+      d0 = fma(v0[qq].x, rv[qq].x, fma(y0, rv[qq].y, d0));
+      d1 = fma(v1[qq].x, rv[qq].x, fma(y1, rv[qq].y, d1));
+      acc[qq].x = fma(a0, (c < j) ? v0[qq].x : 0.0, acc[qq].x);
+      acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
+      acc[qq].x = fma(a1, (c < j1) ? v1[qq].x : 0.0, acc[qq].x);
+      acc[qq].y = fma(a1, (c + 1 < j1) ? y1 : 0.0, acc[qq].y);
+    }
+    d0 = wave_sum(d0);
+    d1 = wave_sum(d1);
+    if (l == 0) {
+      dotv[j] = d0;
+      dotv[j1] = d1;
+    }
+  }
+  if (j < n) {
+    const double2* r0 = reinterpret_cast<const double2*>(A + (int64_t)j * ld) + l;
+    const double a0 = v[j];
+    double d0 = 0.0;
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const int c = 128 * qq + 2 * l;
+      const double2 vv = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
+      const double y0 = (c + 1 <= j) ? vv.y : 0.0;
+      d0 = fma(vv.x, rv[qq].x, fma(y0, rv[qq].y, d0));
+      acc[qq].x = fma(a0, (c < j) ? vv.x : 0.0, acc[qq].x);
+      acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
+    }
+    d0 = wave_sum(d0);
+    if (l == 0) dotv[j] = d0;
+  }
+  tree_reduce<NQ>(acc, tree);
+  if (w == 0) {
+    double2* dst = reinterpret_cast<double2*>(y) + l;
+    const double2* dv = reinterpret_cast<const double2*>(dotv) + l;
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const int c = 128 * qq + 2 * l;
+      const double2 d = dv[64 * qq];
+      dst[64 * qq] = double2{c < n ? acc[qq].x + d.x : 0.0, c + 1 < n ? acc[qq].y + d.y : 0.0};
+    }
+  }
+  __syncthreads();
+  (void)LM;
+}
+
+// Low-rank x~ = K^-1 rhs with K = D + U'U (see include/porqua_hip.h, pq_lowrank):
+//   v = D^-1 rhs;  w = U v (T window-row dots + mg general rows);  u = M^-1 w (lower
+//   symv);  x~ = v - D^-1 U' u (one axpy pass over the window rows).
+// The window rows are read straight from the shared panel (2 passes per iteration).
+template <int NQ, int NQK>
+__device__ void lr_apply(const pq_lowrank& lr, int b, const pq_problem& pb, const pq_settings& s,
+                         double rho, const double* rhs, double* xt, double* vv, double* kw,
+                         double* ku, double* kdot, double* tree, double* red, const double* lo,
+                         const double* up, const double* rg, const double* Cg, const double* Minv,
+                         int k_ld) {
   constexpr int LDMAX = NQ * 128;
-  __shared__ __attribute__((aligned(16))) double sm[10 * LDMAX + 4 * LDMAX + 8 * 64 + 16 * AW];
+  constexpr int KMAX = NQK * 128;
+  const int n = pb.n, ld = pb.ld, mg = pb.mg;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const bool has_box = pb.lb != nullptr;
+  const double ps = (pb.p_scale ? pb.p_scale[b] : 1.0) * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double sps = sqrt(fmax(ps, 0.0));
+  const int T = lr.tlen[b], tmax = lr.tmax, k = tmax + mg;
+  const int32_t* rws = lr.rows + (int64_t)b * tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const bool vec2 = (lr.ldp & 1) == 0;
+  // (1) v = D^-1 rhs
+  for (int i = t; i < LDMAX; i += AT) {
+    double d = 0.0;
+    if (i < n) d = rhs[i] / (s.sigma + pd + (has_box ? rho_row(lo[i], up[i], rho, s) : 0.0));
+    vv[i] = d;
+  }
+  __syncthreads();
+  double muv = 0.0;
+  if (mu) {
+    double a = 0.0;
+    for (int i = t; i < n; i += AT) a += mu[i] * vv[i];
+    muv = block_sum(a, red);
+  }
+  // (2) w = U v
+  for (int tt = w; tt < tmax; tt += AW) {
+    double d = 0.0;
+    if (tt < T) {
+      const double* row = lr.panel + (int64_t)rws[tt] * lr.ldp;
+      if (vec2) {
+        const double2* r2 = reinterpret_cast<const double2*>(row) + l;
+        const double2* v2 = reinterpret_cast<const double2*>(vv) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          if (128 * qq + 2 * l < n) {
+            const double2 a = r2[64 * qq], c = v2[64 * qq];
+            d = fma(a.x, c.x, fma(a.y, c.y, d));
+          }
+        }
+      } else {
+        for (int c = l; c < n; c += 64) d = fma(row[c], vv[c], d);
+      }
+      d = wave_sum(d);
+    }
+    if (l == 0) kw[tt] = (tt < T) ? sps * (d - muv) : 0.0;
+  }
+  for (int r = w; r < mg; r += AW) {
+    const double* c = Cg + (int64_t)r * ld;
+    double d = 0.0;
+    for (int i = l; i < n; i += 64) d = fma(c[i], vv[i], d);
+    d = wave_sum(d);
+    if (l == 0) kw[tmax + r] = sqrt(rg[r]) * d;
+  }
+  for (int i = k + t; i < KMAX; i += AT) kw[i] = 0.0;
+  __syncthreads();
+  // (3) u = M^-1 w
+  symv_lower<NQK>(Minv, k_ld, k, kw, ku, kdot, tree);
+  // (4) x~ = v - D^-1 U' u
+  double su = 0.0;
+  if (mu) {
+    double a = 0.0;
+    for (int tt = t; tt < T; tt += AT) a += ku[tt];
+    su = block_sum(a, red);
+  }
+  double2 acc[NQ];
+#pragma unroll
+  for (int qq = 0; qq < NQ; ++qq) acc[qq] = double2{0.0, 0.0};
+  for (int tt = w; tt < T; tt += AW) {
+    const double a = ku[tt];
+    const double* row = lr.panel + (int64_t)rws[tt] * lr.ldp;
+    if (vec2) {
+      const double2* r2 = reinterpret_cast<const double2*>(row) + l;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        if (128 * qq + 2 * l < n) {
+          const double2 v = r2[64 * qq];
+          acc[qq].x = fma(a, v.x, acc[qq].x);
+          acc[qq].y = fma(a, v.y, acc[qq].y);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int c = 128 * qq + 2 * l;
+        if (c < n) acc[qq].x = fma(a, row[c], acc[qq].x);
+        if (c + 1 < n) acc[qq].y = fma(a, row[c + 1], acc[qq].y);
+      }
+    }
+  }
+  tree_reduce<NQ>(acc, tree);
+  if (w == 0) {
+    double2* dst = reinterpret_cast<double2*>(xt) + l;
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += AT) {
+    double corr = sps * (xt[i] - (mu ? su * mu[i] : 0.0));
+    for (int r = 0; r < mg; ++r) corr = fma(sqrt(rg[r]) * ku[tmax + r], Cg[(int64_t)r * ld + i], corr);
+    const double D = s.sigma + pd + (has_box ? rho_row(lo[i], up[i], rho, s) : 0.0);
+    xt[i] = vv[i] - corr / D;
+  }
+  __syncthreads();
+}
+
+// Grid position -> problem slot so that the blocks sharing an XCD (g = x mod 8) take a
+// contiguous range of dates: neighbouring windows overlap in T-1 rows, so the low-rank
+// kernels then find the panel rows in that XCD's L2 (speed only, bijective for any N).
+__device__ __forceinline__ int xcd_slot(int g, int N) {
+  const int x = g & 7, q = N >> 3, r = N & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (g >> 3);
+}
+
+template <int NQ, int NQK, int MODE>
+__global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const int32_t* idx,
+                                             int nidx, pq_settings s, int iters_call, pq_lowrank lr,
+                                             const double* Minv_all, int k_ld, int64_t M_stride) {
+  constexpr int LDMAX = NQ * 128;
+  constexpr int KMAX = NQK * 128;
+  __shared__ __attribute__((aligned(16))) double sm[10 * LDMAX + 4 * LDMAX + 8 * 64 + 16 * AW + 3 * KMAX];
   double* x = sm;
   double* Px = x + LDMAX;
   double* zb = Px + LDMAX;
@@ -85,8 +320,12 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
   double* lgs = cgx + 64;
   double* ugs = lgs + 64;
   double* red = ugs + 64;          // 16 * AW
+  double* kw = red + 16 * AW;      // low-rank: U D^-1 rhs (k)
+  double* ku = kw + KMAX;          // low-rank: M^-1 kw
+  double* kdot = ku + KMAX;        // low-rank: symv scratch
 
-  const int b = idx ? idx[blockIdx.x] : (int)blockIdx.x;
+  const int gslot = MODE == 1 ? xcd_slot(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int b = idx ? idx[gslot] : gslot;
   if (st.status[b] != PQ_UNSOLVED && st.status[b] != PQ_NEED_REFACTOR) return;
   const int n = pb.n, ld = pb.ld, mg = pb.mg;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
@@ -147,97 +386,12 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
     }
     for (int i = n + t; i < LDMAX; i += AT) rhs[i] = 0.0;
     __syncthreads();
-    // ---- x~ = K^-1 rhs (the HBM stream): lower triangle only ------------------------
-    // row j contributes K[j][c] rhs[j] to x~[c] for c < j (axpy, register accumulators)
-    // and sum_{c <= j} K[j][c] rhs[c] to x~[j] (dot, one wave reduction per row).
-    double2 acc[NQ];
-    double2 rv[NQ];
-#pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) {
-      acc[qq] = double2{0.0, 0.0};
-      rv[qq] = reinterpret_cast<const double2*>(rhs)[64 * qq + l];
+    if constexpr (MODE == 0) {
+      symv_lower<NQ>(Kinv, ld, n, rhs, xt, dotv, tree);
+    } else {
+      lr_apply<NQ, NQK>(lr, b, pb, s, rho, rhs, xt, dotv, kw, ku, kdot, tree, red, lo, up, rg, Cg,
+                        Minv_all + (int64_t)b * M_stride, k_ld);
     }
-    {
-      int j = w;
-      for (; j + AW < n; j += 2 * AW) {
-        const int j1 = j + AW;
-        const double2* r0 = reinterpret_cast<const double2*>(Kinv + (int64_t)j * ld) + l;
-        const double2* r1 = reinterpret_cast<const double2*>(Kinv + (int64_t)j1 * ld) + l;
-        double2 v0[NQ], v1[NQ];
-#pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) {
-          const int c = 128 * qq + 2 * l;
-          v0[qq] = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
-          v1[qq] = (c <= j1) ? r1[64 * qq] : double2{0.0, 0.0};
-        }
-        const double a0 = rhs[j], a1 = rhs[j1];
-        double d0 = 0.0, d1 = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) {
-          const int c = 128 * qq + 2 * l;
-          const double y0 = (c + 1 <= j) ? v0[qq].y : 0.0;
-          const double y1 = (c + 1 <= j1) ? v1[qq].y : 0.0;
-          d0 = fma(v0[qq].x, rv[qq].x, fma(y0, rv[qq].y, d0));
-          d1 = fma(v1[qq].x, rv[qq].x, fma(y1, rv[qq].y, d1));
-          acc[qq].x = fma(a0, (c < j) ? v0[qq].x : 0.0, acc[qq].x);
-          acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
-          acc[qq].x = fma(a1, (c < j1) ? v1[qq].x : 0.0, acc[qq].x);
-          acc[qq].y = fma(a1, (c + 1 < j1) ? y1 : 0.0, acc[qq].y);
-        }
-        d0 = wave_sum(d0);
-        d1 = wave_sum(d1);
-        if (l == 0) {
-          dotv[j] = d0;
-          dotv[j1] = d1;
-        }
-      }
-      if (j < n) {
-        const double2* r0 = reinterpret_cast<const double2*>(Kinv + (int64_t)j * ld) + l;
-        const double a0 = rhs[j];
-        double d0 = 0.0;
-#pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) {
-          const int c = 128 * qq + 2 * l;
-          const double2 v = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
-          const double y0 = (c + 1 <= j) ? v.y : 0.0;
-          d0 = fma(v.x, rv[qq].x, fma(y0, rv[qq].y, d0));
-          acc[qq].x = fma(a0, (c < j) ? v.x : 0.0, acc[qq].x);
-          acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
-        }
-        d0 = wave_sum(d0);
-        if (l == 0) dotv[j] = d0;
-      }
-    }
-    // fixed-order tree: waves 4-7 -> 0-3 -> 0-1 -> 0
-#pragma unroll
-    for (int half = AW / 2; half >= 1; half >>= 1) {
-      if (w >= half && w < 2 * half) {
-        double2* dst = reinterpret_cast<double2*>(tree + (w - half) * LDMAX) + l;
-#pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
-      }
-      __syncthreads();
-      if (w < half) {
-        const double2* src = reinterpret_cast<const double2*>(tree + w * LDMAX) + l;
-#pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) {
-          const double2 v = src[64 * qq];
-          acc[qq].x += v.x;
-          acc[qq].y += v.y;
-        }
-      }
-      __syncthreads();
-    }
-    if (w == 0) {
-      double2* dst = reinterpret_cast<double2*>(xt) + l;
-      const double2* dv = reinterpret_cast<const double2*>(dotv) + l;
-#pragma unroll
-      for (int qq = 0; qq < NQ; ++qq) {
-        const double2 d = dv[64 * qq];
-        dst[64 * qq] = double2{acc[qq].x + d.x, acc[qq].y + d.y};
-      }
-    }
-    __syncthreads();
     // ---- z~ for the general rows ----------------------------------------------------
     if (mg) rows_dot(Cg, ld, mg, n, xt, ztg);
     __syncthreads();
@@ -401,8 +555,9 @@ extern "C" int pq_admm_batched(const pq_problem* pb, pq_state* st, const int32_t
   if (grid <= 0) return 0;
   const int nq = (pb->n + 127) / 128;
   hipStream_t str = (hipStream_t)stream;
+  pq_lowrank nolr = {};
 #define PQ_ADMM_CASE(NQV) \
-  case NQV: hipLaunchKernelGGL(pq::k_admm<NQV>, dim3(grid), dim3(pq::AT), 0, str, *pb, *st, idx, nidx, *s, iters_this_call); break;
+  case NQV: hipLaunchKernelGGL((pq::k_admm<NQV, 1, 0>), dim3(grid), dim3(pq::AT), 0, str, *pb, *st, idx, nidx, *s, iters_this_call, nolr, nullptr, 0, 0); break;
   switch (nq) {
     PQ_ADMM_CASE(1)
     PQ_ADMM_CASE(2)
@@ -419,4 +574,33 @@ extern "C" int pq_admm_batched(const pq_problem* pb, pq_state* st, const int32_t
 #undef PQ_ADMM_CASE
   PQ_CHECK_LAUNCH("pq_admm_batched");
   return 0;
+}
+
+extern "C" int pq_admm_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
+                                  const double* Minv, int32_t k_ld, int64_t M_stride,
+                                  const int32_t* idx, int32_t nidx, const pq_settings* s,
+                                  int32_t iters_this_call, void* stream) {
+  PQ_CHECK_ARG(lr && pb && st && s && Minv, "pq_admm_lr_batched: null argument");
+  PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0, "pq_admm_lr_batched: window missing");
+  PQ_CHECK_ARG(pb->mg <= 64 && (pb->mg == 0 || (pb->Cg && pb->lg && pb->ug)), "pq_admm_lr_batched: bad general rows");
+  const int k = lr->tmax + pb->mg;
+  PQ_CHECK_ARG(k_ld % 64 == 0 && k_ld >= k && k_ld <= 512, "pq_admm_lr_batched: need k <= k_ld <= 512 (k=%d k_ld=%d)", k, k_ld);
+  const int grid = idx ? nidx : pb->batch;
+  if (grid <= 0) return 0;
+  const int nq = (pb->n + 127) / 128;
+  const int nqk = (k_ld + 127) / 128;
+  PQ_CHECK_ARG(nqk <= nq, "pq_admm_lr_batched: the low-rank form needs k <= n");
+  hipStream_t str = (hipStream_t)stream;
+#define PQ_LR_CASE(NQV, NQKV) \
+  if (nq == NQV && nqk == NQKV) { hipLaunchKernelGGL((pq::k_admm<NQV, NQKV, 1>), dim3(grid), dim3(pq::AT), 0, str, *pb, *st, idx, nidx, *s, iters_this_call, *lr, Minv, k_ld, M_stride); PQ_CHECK_LAUNCH("pq_admm_lr_batched"); return 0; }
+  PQ_LR_CASE(2, 1) PQ_LR_CASE(2, 2)
+  PQ_LR_CASE(3, 1) PQ_LR_CASE(3, 2) PQ_LR_CASE(3, 3)
+  PQ_LR_CASE(4, 1) PQ_LR_CASE(4, 2) PQ_LR_CASE(4, 3) PQ_LR_CASE(4, 4)
+  PQ_LR_CASE(5, 1) PQ_LR_CASE(5, 2) PQ_LR_CASE(5, 3) PQ_LR_CASE(5, 4)
+  PQ_LR_CASE(6, 1) PQ_LR_CASE(6, 2) PQ_LR_CASE(6, 3) PQ_LR_CASE(6, 4)
+  PQ_LR_CASE(7, 1) PQ_LR_CASE(7, 2) PQ_LR_CASE(7, 3) PQ_LR_CASE(7, 4)
+  PQ_LR_CASE(8, 1) PQ_LR_CASE(8, 2) PQ_LR_CASE(8, 3) PQ_LR_CASE(8, 4)
+#undef PQ_LR_CASE
+  pq::set_error("pq_admm_lr_batched: unsupported sizes n=%d k_ld=%d", pb->n, k_ld);
+  return -1;
 }

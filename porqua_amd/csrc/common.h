@@ -126,8 +126,11 @@ __device__ void gemm_stream(Acc& acc, double* lds, const double* GA, int64_t lda
                             const double* GB, int64_t ldb, int b_j0, int kb0, int K) {
   if (K <= 0) return;
   Stage4 ra, rb;
+  // Barrier BEFORE the first global load: callers stream tiles that other waves of the
+  // workgroup have just stored (e.g. L_{J,J-1} in wg_cholesky), and the stage buffers'
+  // previous users must be done before they are overwritten.
+  __syncthreads();
   stage_load<MA, MB>(ra, rb, GA, lda, a_i0, GB, ldb, b_j0, 0, ka0, kb0);
-  __syncthreads();  // previous users of the stage buffers are done
   stage_store<MA, MB>(ra, rb, lds, lds + STAGE);
   __syncthreads();
   int buf = 0;

@@ -213,12 +213,15 @@ class QPBatch:
 class Workspace:
     """Solver state for a QPBatch (all device memory; nothing persistent in the library)."""
 
-    def __init__(self, qb: QPBatch):
+    def __init__(self, qb: QPBatch, dense: bool = True):
         B, ld, dev = qb.batch, qb.ld, qb.device
+        self.B, self.device = B, dev
         self.mg_pad = qb.mg_pad
         self.m_ld = qb.mg_pad + ld
+        # K / Dt: the dense KKT inverse (K2 / K3) and the polish scratch (K4)
         self.K = torch.empty((B, ld, ld), dtype=F64, device=dev)
         self.Dt = torch.empty((B, ld // 64, 64, 64), dtype=F64, device=dev)
+        self._lr = None
         self.x = torch.zeros((B, ld), dtype=F64, device=dev)
         self.Px = torch.zeros((B, ld), dtype=F64, device=dev)
         self.z = torch.zeros((B, self.m_ld), dtype=F64, device=dev)
@@ -230,6 +233,19 @@ class Workspace:
         self.out = torch.zeros((B, _lib.PQ_OUT_FIELDS), dtype=F64, device=dev)
         self.work_stride = _lib.work_doubles(ld, qb.mg_pad)
         self.work = torch.zeros((B, self.work_stride), dtype=F64, device=dev)
+
+    def lr_buffers(self, k_ld: int):
+        """Capacitance matrices M, their inverses and factor scratch (low-rank path)."""
+        if self._lr is None or self._lr["k_ld"] != k_ld:
+            B, dev = self.B, self.device
+            self._lr = {"k_ld": k_ld,
+                        "M": torch.empty((B, k_ld, k_ld), dtype=F64, device=dev),
+                        "Minv": torch.empty((B, k_ld, k_ld), dtype=F64, device=dev),
+                        "Dt": torch.empty((B, k_ld // 64, 64, 64), dtype=F64, device=dev),
+                        "iters": torch.zeros(B, dtype=torch.int32, device=dev),
+                        "status": torch.zeros(B, dtype=torch.int32, device=dev),
+                        "info": torch.zeros(B, dtype=torch.int32, device=dev)}
+        return self._lr
 
     def c_struct(self) -> _lib.PQState:
         return _lib.PQState(
@@ -324,6 +340,92 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
                        admm_launches=launches)
 
 
+class LowRank:
+    """Device description of P_eff = p_scale Xc'Xc + p_diag I through the date windows
+    (pq_lowrank): nothing n x n is formed.  ``mu`` None = uncentred Gram (LeastSquares)."""
+
+    def __init__(self, panel, rows, tlen, mu=None, w_scale=None):
+        self.panel, self.rows, self.tlen, self.mu, self.w_scale = panel, rows, tlen, mu, w_scale
+        self.tmax = int(rows.shape[1])
+
+    def c_struct(self) -> _lib.PQLowRank:
+        return _lib.PQLowRank(panel=self.panel.R.data_ptr(), ldp=self.panel.R.stride(0),
+                              rows=self.rows.data_ptr(), tlen=self.tlen.data_ptr(), tmax=self.tmax,
+                              mu=None if self.mu is None else self.mu.data_ptr(),
+                              mu_stride=0 if self.mu is None else self.mu.stride(0),
+                              w_scale=None if self.w_scale is None else self.w_scale.data_ptr())
+
+
+def lowrank_applicable(qb: QPBatch, lr: LowRank) -> bool:
+    k_ld = round_up(lr.tmax + qb.mg, 64)
+    return k_ld <= 512 and (k_ld + 127) // 128 <= (qb.n + 127) // 128 and lr.tmax + qb.mg < qb.n
+
+
+def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
+                  ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
+                  polish: bool = True) -> BatchResult:
+    """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
+    k x k matrices M, K3 = low-rank ADMM over the shared window rows, K4 = polish (needs the
+    dense P in qb.P)."""
+    tl = _Timeline(events)
+    lib = _lib.load()
+    s = (settings or Settings()).to_c()
+    ws = ws or Workspace(qb, dense=False)
+    B, dev = qb.batch, qb.device
+    k = lr.tmax + qb.mg
+    k_ld = round_up(k, 64)
+    if not lowrank_applicable(qb, lr):
+        raise _lib.PorquaHipError(f"low-rank form not applicable (k={k}, n={qb.n})")
+    M = ws.lr_buffers(k_ld)
+    pb = qb.c_struct()
+    st = ws.c_struct()
+    lrs = lr.c_struct()
+    pbM = _lib.PQProblem(n=k_ld, ld=k_ld, batch=B, mg=0, P=M["M"].data_ptr(), P_stride=k_ld * k_ld,
+                         q=qb.q.data_ptr(), q_stride=qb.q.stride(0), Cg=qb.Cg.data_ptr(), lg=qb.lg.data_ptr(),
+                         ug=qb.ug.data_ptr())
+    stM = _lib.PQState(K=M["Minv"].data_ptr(), K_stride=k_ld * k_ld, Dt=M["Dt"].data_ptr(),
+                       Dt_stride=(k_ld // 64) * 4096, x=ws.x.data_ptr(), Px=ws.Px.data_ptr(),
+                       z=ws.z.data_ptr(), y=ws.y.data_ptr(), m_ld=ws.m_ld, mg_pad=ws.mg_pad,
+                       rho=ws.rho.data_ptr(), iters=M["iters"].data_ptr(), status=M["status"].data_ptr(),
+                       info=M["info"].data_ptr(), out=ws.out.data_ptr(), work=ws.work.data_ptr(),
+                       work_stride=ws.work_stride)
+    sM = (settings or Settings()).to_c()
+    sM.sigma = 0.0
+    strm = _stream()
+    P_, S_, SS, L_ = ctypes.byref(pb), ctypes.byref(st), ctypes.byref(s), ctypes.byref(lrs)
+    PM_, SM_, SSM = ctypes.byref(pbM), ctypes.byref(stM), ctypes.byref(sM)
+    _lib.check(lib.pq_init_state(P_, S_, None, 0, SS, strm), "pq_init_state")
+
+    def refactor(idx, nidx):
+        _lib.check(lib.pq_lr_capacitance(L_, P_, S_, _ptr(idx), nidx, SS, M["M"].data_ptr(), k_ld,
+                                         k_ld * k_ld, strm), "pq_lr_capacitance")
+        _lib.check(lib.pq_factor_batched(PM_, SM_, _ptr(idx), nidx, SSM, 1, strm), "pq_factor_batched(M)")
+
+    tl("factor", lambda: refactor(None, 0))
+    idx, nidx = None, 0
+    refactors = launches = 0
+    for _ in range(max_rounds):
+        _lib.check(tl("admm", lambda: lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld,
+                                                             k_ld * k_ld, _ptr(idx), nidx, SS,
+                                                             int(s.max_iter), strm)),
+                   "pq_admm_lr_batched")
+        launches += 1
+        need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
+        kk = int(need.numel())
+        if kk == 0:
+            break
+        idx, nidx = need.contiguous(), kk
+        tl("factor", lambda: refactor(idx, nidx))
+        refactors += kk
+    if s.polish and polish:
+        _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, None, 0, SS, strm)),
+                   "pq_polish_batched")
+    n, mg = qb.n, qb.mg
+    return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
+                       status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
+                       admm_launches=launches)
+
+
 def factor_only(qb: QPBatch, invert: bool = False, sigma: float = 0.0):
     """Batched Cholesky of P_eff (mg = 0, no box): returns (Workspace, info) -- the isPD
     test of src/helper_functions.py:61-67 on the device."""
@@ -388,10 +490,10 @@ class Panel:
         t = torch.from_numpy(np.ascontiguousarray(tlen, dtype=np.int32)).to(self.device)
         return r, t
 
-    def window_means(self, rows, tlen, geometric=False):
+    def window_means(self, rows, tlen, geometric=False, out=None):
         lib = _lib.load()
         B, tmax = rows.shape
-        mu = torch.zeros((B, round_up(self.n, 64)), dtype=F64, device=self.device)
+        mu = out if out is not None else torch.zeros((B, round_up(self.n, 64)), dtype=F64, device=self.device)
         fn = lib.pq_window_geomean if geometric else lib.pq_window_mean
         _lib.check(fn(_ptr(self.R), self.n, self.n, _ptr(rows), _ptr(tlen), tmax, B, _ptr(mu),
                       mu.stride(0), _stream()), "window means")

@@ -1,0 +1,82 @@
+"""Woodbury (low-rank) engine path for T + mg < n: same QP, same polished optimum as the
+dense path and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.qp_ipm import solve_qp
+from oracle.ref_pipeline import cov_pearson
+from porqua_amd import engine
+from porqua_amd.synthetic import factor_panel
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(n, T, ends, centred=True, D=None, seed=None):
+    D = D or (max(ends) + 1)
+    dates, R, y, sec = factor_panel(D, n, seed=seed or 20240314)
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    pan = engine.Panel(R, y)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    mu = pan.window_means(r_d, t_d) if centred else None
+    return dates, R, y, sec, pan, r_d, t_d, mu
+
+
+@pytest.mark.parametrize("shrink,groups", [(0.0, False), (0.1, False), (0.0, True)])
+def test_lowrank_matches_dense_and_oracle_min_variance(device, shrink, groups):
+    n, T = 1000, 252
+    ends = [300, 451, 599]
+    dates, R, y, sec, pan, r_d, t_d, mu = _setup(n, T, ends)
+    B = len(ends)
+    G = h = None
+    if groups:
+        G = np.stack([(sec == g).astype(float) for g in range(3)])
+        h = np.full(3, 0.12)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=G, h=h, lb=np.zeros(n), ub=np.ones(n), device=device)
+    qb.batch = B
+    qb.P = pan.cov(r_d, t_d, mode=0, mu=mu)
+    qb.q = torch.zeros((B, qb.ld), dtype=torch.float64, device=device)
+    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
+    if shrink:
+        qb.p_diag = 2.0 * shrink * torch.diagonal(qb.P, dim1=1, dim2=2)[:, :n].mean(dim=1)
+    lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+    res_lr = engine.solve_lowrank(qb, lr)
+    x_lr = res_lr.x.cpu().numpy().copy()
+    st_lr = res_lr.status.cpu().numpy().copy()
+    it_lr = res_lr.iters.cpu().numpy().copy()
+    res_d = engine.solve(qb)
+    x_d = res_d.x.cpu().numpy()
+    assert np.all(st_lr == 1) and np.all(res_d.status.cpu().numpy() == 1)
+    assert np.abs(x_lr - x_d).max() < 1e-9
+    assert np.abs(it_lr - res_d.iters.cpu().numpy()).max() <= 2   # same iterates up to rounding
+    for i, e in enumerate(ends):
+        S = cov_pearson(R[e - T + 1:e + 1])
+        P = 2 * S + (2 * shrink * np.mean(np.diag(S)) * np.eye(n) if shrink else 0)
+        o = solve_qp(P, np.zeros(n), G=G, h=h, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n))
+        assert np.abs(x_lr[i] - o.x).max() < 1e-5
+        assert abs(0.5 * x_lr[i] @ P @ x_lr[i] - o.obj) <= 1e-6 * abs(o.obj)
+
+
+def test_lowrank_least_squares_uncentred(device):
+    n, T = 600, 120
+    ends = [200, 333]
+    dates, R, y, sec, pan, r_d, t_d, _ = _setup(n, T, ends, centred=False, D=400)
+    B = len(ends)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   lb=np.zeros(n), ub=np.full(n, 0.05), device=device)
+    qb.batch = B
+    qb.P = pan.cov(r_d, t_d, mode=1)
+    xty, _ = pan.gram_xy(r_d, t_d)
+    qb.q = (-2.0 * xty).contiguous()
+    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
+    lr = engine.LowRank(pan, r_d, t_d, mu=None)
+    res = engine.solve_lowrank(qb, lr, engine.Settings(rho0_rel=0.5))
+    x = res.x.cpu().numpy()
+    assert np.all(res.status.cpu().numpy() == 1)
+    for i, e in enumerate(ends):
+        X = R[e - T + 1:e + 1]
+        P, q = 2 * X.T @ X, -2 * X.T @ y[e - T + 1:e + 1]
+        o = solve_qp(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.full(n, 0.05))
+        assert np.abs(x[i] - o.x).max() < 1e-5
+        assert abs((0.5 * x[i] @ P @ x[i] + q @ x[i]) - o.obj) <= 1e-6 * abs(o.obj)
