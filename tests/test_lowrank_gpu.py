@@ -72,11 +72,19 @@ def test_lowrank_least_squares_uncentred(device):
     qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
     lr = engine.LowRank(pan, r_d, t_d, mu=None)
     res = engine.solve_lowrank(qb, lr, engine.Settings(rho0_rel=0.5))
-    x = res.x.cpu().numpy()
+    x = res.x.cpu().numpy().copy()
     assert np.all(res.status.cpu().numpy() == 1)
+    res_d = engine.solve(qb, engine.Settings(rho0_rel=0.5))
+    assert np.all(res_d.status.cpu().numpy() == 1)
+    # flat optimal face (see below): rounding differences between the two K^-1 forms move
+    # the iterates along it, so the paths agree to the weight tolerance, not to 1e-9
+    assert np.abs(x - res_d.x.cpu().numpy()).max() < 1e-5
     for i, e in enumerate(ends):
         X = R[e - T + 1:e + 1]
         P, q = 2 * X.T @ X, -2 * X.T @ y[e - T + 1:e + 1]
         o = solve_qp(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.full(n, 0.05))
-        assert np.abs(x[i] - o.x).max() < 1e-5
+        # rank(P) <= T = 120 < n = 600: the minimiser is a face, not a point, so the oracle
+        # and the engine may return different optimal x -- compare value and feasibility.
         assert abs((0.5 * x[i] @ P @ x[i] + q @ x[i]) - o.obj) <= 1e-6 * abs(o.obj)
+        assert abs(x[i].sum() - 1.0) <= 1e-7
+        assert x[i].min() >= -1e-7 and x[i].max() <= 0.05 + 1e-7
