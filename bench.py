@@ -52,6 +52,8 @@ def parse():
                     help="dense K^-1 (K2 n^3 + K3 n^2 stream) or Woodbury low-rank (T + mg < n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="override an engine.Settings field (experiments)")
     return ap.parse_args()
 
 
@@ -87,7 +89,7 @@ def main():
     qb.q = torch.zeros((D, ld), dtype=torch.float64, device=dev)
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)   # P = 2 * Sigma
     ws = engine.Workspace(qb)
-    settings = engine.Settings()
+    settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))
     mu_lr = pan.window_means(rows_d, tlen_d)
     lr = engine.LowRank(pan, rows_d, tlen_d, mu=mu_lr, w_scale=1.0 / (tlen_d.to(torch.float64) - 1.0))
     use_lr = args.path == "lowrank" or (args.path == "auto" and engine.lowrank_applicable(qb, lr))
@@ -145,6 +147,10 @@ def main():
     iters = res.iters.to(torch.int64)
     total_iters = int(iters.sum().item()) * args.steps   # identical work every step
     status = res.status.cpu().numpy()
+    out_rec = res.out.cpu().numpy()
+    from porqua_amd import _lib
+    nfree = out_rec[:, _lib.PQ_OUT_NFREE]
+    prounds = out_rec[:, _lib.PQ_OUT_ROUNDS]
     k_lr = T + 1
     it_bytes = (8.0 * (2 * T * n + k_lr * (k_lr + 1) / 2)) if use_lr else 8.0 * n * (n + 1) / 2
     admm_bytes = it_bytes * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
@@ -203,7 +209,10 @@ def main():
         "solver": {"status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
                    "mean_iters": float(iters.float().mean().item()),
                    "max_iters": int(iters.max().item()),
-                   "refactors_per_step": res.refactors, "admm_launches_per_step": res.admm_launches},
+                   "refactors_per_step": res.refactors, "admm_launches_per_step": res.admm_launches,
+                   "polish_nfree_mean": float(nfree.mean()), "polish_nfree_max": int(nfree.max()),
+                   "polish_rounds_mean": float(prounds.mean()), "polish_rounds_max": int(prounds.max()),
+                   "settings_overrides": args.set},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -23,6 +23,35 @@ namespace pq {
 constexpr int AT = 512;   // threads per ADMM workgroup
 constexpr int AW = AT / 64;
 
+// Optional per-phase timing (build with -DPQ_PROFILE): wall-clock ticks per phase summed
+// over iterations, added into doubles [16, 24) after each problem's polish work layout.
+struct PhaseClock {
+#ifdef PQ_PROFILE
+  long long a[8];
+  long long t;
+  __device__ void init() {
+    for (int i = 0; i < 8; ++i) a[i] = 0;
+    t = wall_clock64();
+  }
+  __device__ void stamp(int k) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const long long now = wall_clock64();
+      a[k] += now - t;
+      t = now;
+    }
+  }
+  __device__ void flush(double* dst) {
+    if (threadIdx.x == 0)
+      for (int i = 0; i < 8; ++i) dst[i] += (double)a[i];
+  }
+#else
+  __device__ void init() {}
+  __device__ void stamp(int) {}
+  __device__ void flush(double*) {}
+#endif
+};
+
 __device__ __forceinline__ double rho_row(double l, double u, double rho, const pq_settings& s) {
   if (l == u) return rho * s.eq_scale;
   if (isinf(l) && isinf(u)) return s.rho_min;
@@ -92,11 +121,11 @@ __device__ __forceinline__ void tree_reduce(double2 (&acc)[NQ], double* tree) {
 // accumulators; lane l owns columns 128 q + 2 l, 2 l + 1) and sum_{c<=j} A[j][c] v[c] to
 // y[j] (one wave reduction per row).  Partial vectors of the AW waves are combined by a
 // fixed-order LDS tree (bit-reproducible).  v, y, dotv: LDS, >= NQ*128 entries (v zero
-// beyond n); tree: 4 * NQ*128 doubles.  All threads must call.
-template <int NQ>
+// beyond n); tree: 4 * NQ*128 doubles.  RU rows per wave are in flight at a time (their
+// loads are issued together; the accumulation order is fixed).  All threads must call.
+template <int NQ, int RU>
 __device__ void symv_lower(const double* A, int64_t ld, int n, const double* v, double* y,
                            double* dotv, double* tree) {
-  constexpr int LM = NQ * 128;
   const int w = wave_id(), l = lane_id();
   double2 acc[NQ];
   double2 rv[NQ];
@@ -105,55 +134,44 @@ __device__ void symv_lower(const double* A, int64_t ld, int n, const double* v, 
     acc[qq] = double2{0.0, 0.0};
     rv[qq] = reinterpret_cast<const double2*>(v)[64 * qq + l];
   }
-  int j = w;
-  for (; j + AW < n; j += 2 * AW) {
-    const int j1 = j + AW;
-    const double2* r0 = reinterpret_cast<const double2*>(A + (int64_t)j * ld) + l;
-    const double2* r1 = reinterpret_cast<const double2*>(A + (int64_t)j1 * ld) + l;
-    double2 v0[NQ], v1[NQ];
+  // process RU rows j0, j0 + AW, ... (rows >= n are skipped)
+  auto rows = [&](int j0) {
+    double2 r[RU][NQ];
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) {
-      const int c = 128 * qq + 2 * l;
-      v0[qq] = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
-      v1[qq] = (c <= j1) ? r1[64 * qq] : double2{0.0, 0.0};
-    }
-    const double a0 = v[j], a1 = v[j1];
-    double d0 = 0.0, d1 = 0.0;
+    for (int u = 0; u < RU; ++u) {
+      const int j = j0 + u * AW;
+      const double2* rp = reinterpret_cast<const double2*>(A + (int64_t)(j < n ? j : 0) * ld) + l;
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) {
-      const int c = 128 * qq + 2 * l;
-      const double y0 = (c + 1 <= j) ? v0[qq].y : 0.0;
-      const double y1 = (c + 1 <= j1) ? v1[qq].y : 0.0;
-      d0 = fma(v0[qq].x, rv[qq].x, fma(y0, rv[qq].y, d0));
-      d1 = fma(v1[qq].x, rv[qq].x, fma(y1, rv[qq].y, d1));
-      acc[qq].x = fma(a0, (c < j) ? v0[qq].x : 0.0, acc[qq].x);
-      acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
-      acc[qq].x = fma(a1, (c < j1) ? v1[qq].x : 0.0, acc[qq].x);
-      acc[qq].y = fma(a1, (c + 1 < j1) ? y1 : 0.0, acc[qq].y);
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int c = 128 * qq + 2 * l;
+        r[u][qq] = (j < n && c <= j) ? rp[64 * qq] : double2{0.0, 0.0};
+      }
     }
-    d0 = wave_sum(d0);
-    d1 = wave_sum(d1);
+    double d[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int j = j0 + u * AW;
+      const double a = j < n ? v[j] : 0.0;
+      double s = 0.0;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int c = 128 * qq + 2 * l;
+        const double yy = (c + 1 <= j) ? r[u][qq].y : 0.0;
+        s = fma(r[u][qq].x, rv[qq].x, fma(yy, rv[qq].y, s));
+        acc[qq].x = fma(a, (c < j) ? r[u][qq].x : 0.0, acc[qq].x);
+        acc[qq].y = fma(a, (c + 1 < j) ? yy : 0.0, acc[qq].y);
+      }
+      d[u] = s;
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) d[u] = wave_sum(d[u]);
     if (l == 0) {
-      dotv[j] = d0;
-      dotv[j1] = d1;
-    }
-  }
-  if (j < n) {
-    const double2* r0 = reinterpret_cast<const double2*>(A + (int64_t)j * ld) + l;
-    const double a0 = v[j];
-    double d0 = 0.0;
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) {
-      const int c = 128 * qq + 2 * l;
-      const double2 vv = (c <= j) ? r0[64 * qq] : double2{0.0, 0.0};
-      const double y0 = (c + 1 <= j) ? vv.y : 0.0;
-      d0 = fma(vv.x, rv[qq].x, fma(y0, rv[qq].y, d0));
-      acc[qq].x = fma(a0, (c < j) ? vv.x : 0.0, acc[qq].x);
-      acc[qq].y = fma(a0, (c + 1 < j) ? y0 : 0.0, acc[qq].y);
+      for (int u = 0; u < RU; ++u)
+        if (j0 + u * AW < n) dotv[j0 + u * AW] = d[u];
     }
-    d0 = wave_sum(d0);
-    if (l == 0) dotv[j] = d0;
-  }
+  };
+  for (int j0 = w; j0 < n; j0 += RU * AW) rows(j0);
   tree_reduce<NQ>(acc, tree);
   if (w == 0) {
     double2* dst = reinterpret_cast<double2*>(y) + l;
@@ -166,7 +184,6 @@ __device__ void symv_lower(const double* A, int64_t ld, int n, const double* v, 
     }
   }
   __syncthreads();
-  (void)LM;
 }
 
 // Low-rank x~ = K^-1 rhs with K = D + U'U (see include/porqua_hip.h, pq_lowrank):
@@ -178,7 +195,7 @@ __device__ void lr_apply(const pq_lowrank& lr, int b, const pq_problem& pb, cons
                          double rho, const double* rhs, double* xt, double* vv, double* kw,
                          double* ku, double* kdot, double* tree, double* red, const double* lo,
                          const double* up, const double* rg, const double* Cg, const double* Minv,
-                         int k_ld) {
+                         int k_ld, PhaseClock& pc) {
   constexpr int LDMAX = NQ * 128;
   constexpr int KMAX = NQK * 128;
   const int n = pb.n, ld = pb.ld, mg = pb.mg;
@@ -204,27 +221,52 @@ __device__ void lr_apply(const pq_lowrank& lr, int b, const pq_problem& pb, cons
     for (int i = t; i < n; i += AT) a += mu[i] * vv[i];
     muv = block_sum(a, red);
   }
-  // (2) w = U v
-  for (int tt = w; tt < tmax; tt += AW) {
-    double d = 0.0;
-    if (tt < T) {
-      const double* row = lr.panel + (int64_t)rws[tt] * lr.ldp;
-      if (vec2) {
-        const double2* r2 = reinterpret_cast<const double2*>(row) + l;
-        const double2* v2 = reinterpret_cast<const double2*>(vv) + l;
+  pc.stamp(1);
+  // (2) w = U v: RU window rows per wave in flight (16-B loads, v in registers)
+  constexpr int RU = 3;
+  if (vec2) {
+    double2 vr[NQ];
 #pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) {
-          if (128 * qq + 2 * l < n) {
-            const double2 a = r2[64 * qq], c = v2[64 * qq];
-            d = fma(a.x, c.x, fma(a.y, c.y, d));
-          }
-        }
-      } else {
-        for (int c = l; c < n; c += 64) d = fma(row[c], vv[c], d);
+    for (int qq = 0; qq < NQ; ++qq) vr[qq] = reinterpret_cast<const double2*>(vv)[64 * qq + l];
+    for (int t0 = w; t0 < tmax; t0 += RU * AW) {
+      double2 r[RU][NQ];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int tt = t0 + u * AW;
+        const int64_t ri = tt < T ? (int64_t)rws[tt] : 0;
+        const double2* rp = reinterpret_cast<const double2*>(lr.panel + ri * lr.ldp) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq)
+          r[u][qq] = (tt < T && 128 * qq + 2 * l < n) ? rp[64 * qq] : double2{0.0, 0.0};
       }
-      d = wave_sum(d);
+      double d[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        double s0 = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) s0 = fma(r[u][qq].x, vr[qq].x, fma(r[u][qq].y, vr[qq].y, s0));
+        d[u] = s0;
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) d[u] = wave_sum(d[u]);
+      if (l == 0) {
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int tt = t0 + u * AW;
+          if (tt < tmax) kw[tt] = (tt < T) ? sps * (d[u] - muv) : 0.0;
+        }
+      }
     }
-    if (l == 0) kw[tt] = (tt < T) ? sps * (d - muv) : 0.0;
+  } else {
+    for (int tt = w; tt < tmax; tt += AW) {
+      double d = 0.0;
+      if (tt < T) {
+        const double* row = lr.panel + (int64_t)rws[tt] * lr.ldp;
+        for (int c = l; c < n; c += 64) d = fma(row[c], vv[c], d);
+        d = wave_sum(d);
+      }
+      if (l == 0) kw[tt] = (tt < T) ? sps * (d - muv) : 0.0;
+    }
   }
   for (int r = w; r < mg; r += AW) {
     const double* c = Cg + (int64_t)r * ld;
@@ -235,8 +277,10 @@ __device__ void lr_apply(const pq_lowrank& lr, int b, const pq_problem& pb, cons
   }
   for (int i = k + t; i < KMAX; i += AT) kw[i] = 0.0;
   __syncthreads();
+  pc.stamp(2);
   // (3) u = M^-1 w
-  symv_lower<NQK>(Minv, k_ld, k, kw, ku, kdot, tree);
+  symv_lower<NQK, 4>(Minv, k_ld, k, kw, ku, kdot, tree);
+  pc.stamp(3);
   // (4) x~ = v - D^-1 U' u
   double su = 0.0;
   if (mu) {
@@ -247,20 +291,32 @@ __device__ void lr_apply(const pq_lowrank& lr, int b, const pq_problem& pb, cons
   double2 acc[NQ];
 #pragma unroll
   for (int qq = 0; qq < NQ; ++qq) acc[qq] = double2{0.0, 0.0};
-  for (int tt = w; tt < T; tt += AW) {
-    const double a = ku[tt];
-    const double* row = lr.panel + (int64_t)rws[tt] * lr.ldp;
-    if (vec2) {
-      const double2* r2 = reinterpret_cast<const double2*>(row) + l;
+  if (vec2) {
+    for (int t0 = w; t0 < T; t0 += RU * AW) {
+      double2 r[RU][NQ];
+      double a[RU];
 #pragma unroll
-      for (int qq = 0; qq < NQ; ++qq) {
-        if (128 * qq + 2 * l < n) {
-          const double2 v = r2[64 * qq];
-          acc[qq].x = fma(a, v.x, acc[qq].x);
-          acc[qq].y = fma(a, v.y, acc[qq].y);
-        }
+      for (int u = 0; u < RU; ++u) {
+        const int tt = t0 + u * AW;
+        const int64_t ri = tt < T ? (int64_t)rws[tt] : 0;
+        a[u] = tt < T ? ku[tt] : 0.0;
+        const double2* rp = reinterpret_cast<const double2*>(lr.panel + ri * lr.ldp) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq)
+          r[u][qq] = (tt < T && 128 * qq + 2 * l < n) ? rp[64 * qq] : double2{0.0, 0.0};
       }
-    } else {
+#pragma unroll
+      for (int u = 0; u < RU; ++u)
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          acc[qq].x = fma(a[u], r[u][qq].x, acc[qq].x);
+          acc[qq].y = fma(a[u], r[u][qq].y, acc[qq].y);
+        }
+    }
+  } else {
+    for (int tt = w; tt < T; tt += AW) {
+      const double a = ku[tt];
+      const double* row = lr.panel + (int64_t)rws[tt] * lr.ldp;
 #pragma unroll
       for (int qq = 0; qq < NQ; ++qq) {
         const int c = 128 * qq + 2 * l;
@@ -283,6 +339,7 @@ __device__ void lr_apply(const pq_lowrank& lr, int b, const pq_problem& pb, cons
     xt[i] = vv[i] - corr / D;
   }
   __syncthreads();
+  pc.stamp(4);
 }
 
 // Grid position -> problem slot so that the blocks sharing an XCD (g = x mod 8) take a
@@ -373,6 +430,8 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
   int it = st.iters[b];
   int status = PQ_UNSOLVED;
   const int it_end = min(s.max_iter, it + iters_call);
+  PhaseClock pc;
+  pc.init();
   while (it < it_end) {
     ++it;
     // ---- rhs = sigma x - q + C'(R z - y) ------------------------------------------
@@ -386,11 +445,12 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
     }
     for (int i = n + t; i < LDMAX; i += AT) rhs[i] = 0.0;
     __syncthreads();
+    pc.stamp(0);
     if constexpr (MODE == 0) {
-      symv_lower<NQ>(Kinv, ld, n, rhs, xt, dotv, tree);
+      symv_lower<NQ, 2>(Kinv, ld, n, rhs, xt, dotv, tree);
     } else {
       lr_apply<NQ, NQK>(lr, b, pb, s, rho, rhs, xt, dotv, kw, ku, kdot, tree, red, lo, up, rg, Cg,
-                        Minv_all + (int64_t)b * M_stride, k_ld);
+                        Minv_all + (int64_t)b * M_stride, k_ld, pc);
     }
     // ---- z~ for the general rows ----------------------------------------------------
     if (mg) rows_dot(Cg, ld, mg, n, xt, ztg);
@@ -451,6 +511,7 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
       mv[5] = fmax(mv[5], fabs(cy));
     }
     block_maxv<8>(mv, red);
+    pc.stamp(5);
     const double eps_p = s.eps_abs + s.eps_rel * fmax(mv[1], mv[2]);
     const double eps_d = s.eps_abs + s.eps_rel * fmax(mv[4], fmax(mv[5], mv[6]));
     if (mv[0] <= eps_p && mv[3] <= eps_d) {
@@ -472,6 +533,7 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
   }
   if (status == PQ_UNSOLVED && it >= s.max_iter) status = PQ_MAX_ITER;
   __syncthreads();
+  pc.flush(st.work + (int64_t)b * st.work_stride + (int64_t)(4 + st.mg_pad) * ld + 16);
   // ---- save state --------------------------------------------------------------------
   {
     double* gx = st.x + (int64_t)b * ld;

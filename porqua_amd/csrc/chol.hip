@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256, 2) void k_factor(pq_problem pb, pq_state st, c
   f.lg = pb.mg ? pb.lg + (int64_t)b * pb.g_stride : nullptr;
   f.ug = pb.mg ? pb.ug + (int64_t)b * pb.g_stride : nullptr;
 
-  int info = wg_cholesky(FormOp{&f}, K, ld, nb, Dt, smem);
+  int info = wg_cholesky(FormOp{&f}, K, ld, nb, n, Dt, smem);
   if (threadIdx.x == 0) {
     st.info[b] = info;
     if (info) st.status[b] = PQ_NON_CONVEX;

@@ -8,11 +8,13 @@ namespace pq {
 constexpr int DP = 65;  // pitch of the row-major diagonal work tile
 
 // Unblocked Cholesky of the 64x64 row-major tile T (pitch DP, lower used).  Returns the
-// 1-based local column of the first non-positive pivot, 0 on success (uniform).
-__device__ int tile_potrf(double* T, int nvalid_dummy) {
-  (void)nvalid_dummy;
+// 1-based local column of the first non-positive pivot, 0 on success (uniform).  Rows and
+// columns >= nvalid must already hold the identity (the zero-padded tail of a matrix whose
+// padding is the identity): their pivot steps are skipped.
+__device__ int tile_potrf(double* T, int nvalid) {
   const int t = threadIdx.x;
-  for (int k = 0; k < TB; ++k) {
+  const int kend = nvalid < TB ? (nvalid > 0 ? nvalid : 0) : TB;
+  for (int k = 0; k < kend; ++k) {
     __syncthreads();
     const double d = T[k * DP + k];
     if (!(d > 0.0) || !isfinite(d)) return k + 1;
@@ -23,7 +25,7 @@ __device__ int tile_potrf(double* T, int nvalid_dummy) {
       else if (t > k) T[t * DP + k] /= s;
     }
     __syncthreads();
-    const int rem = TB - 1 - k;
+    const int rem = kend - 1 - k;
     for (int e = t; e < rem * rem; e += blockDim.x) {
       const int i = k + 1 + e / rem, j = k + 1 + e % rem;
       if (j <= i) T[i * DP + j] -= T[i * DP + k] * T[j * DP + k];
@@ -34,15 +36,16 @@ __device__ int tile_potrf(double* T, int nvalid_dummy) {
 }
 
 // Inverse of the lower-triangular tile T (pitch DP) into X (row c = column c of T^-1,
-// pitch DP).  Thread c < 64 owns column c.
-__device__ void tile_trinv(const double* T, double* X) {
+// pitch DP).  Thread c < 64 owns column c.  Rows / columns >= nvalid are the identity.
+__device__ void tile_trinv(const double* T, double* X, int nvalid) {
   const int c = threadIdx.x;
   if (c < TB) {
     for (int r = 0; r < c; ++r) X[c * DP + r] = 0.0;
     X[c * DP + c] = 1.0 / T[c * DP + c];
     for (int r = c + 1; r < TB; ++r) {
       double acc = 0.0;
-      for (int k = c; k < r; ++k) acc += T[r * DP + k] * X[c * DP + k];
+      if (r < nvalid)
+        for (int k = c; k < r; ++k) acc += T[r * DP + k] * X[c * DP + k];
       X[c * DP + r] = -acc / T[r * DP + r];
     }
   }
@@ -58,7 +61,7 @@ constexpr int CHOL_LDS = 4 * STAGE + TB * LDW;
 // inverses of the diagonal blocks in Dt.  Returns info (0 = success, else first failing
 // column + 1).  All threads of the (256-thread) workgroup must call it.
 template <typename Form>
-__device__ int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, double* Dt, double* smem) {
+__device__ int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, int nv, double* Dt, double* smem) {
   double* stg = smem;
   double* sD = smem + 4 * STAGE;
   for (int J = 0; J < nb; ++J) {
@@ -75,10 +78,10 @@ __device__ int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, double*
           const int i = acc_row(m, r), j = acc_col(nn);
           stg[i * DP + j] = f(J * TB + i, J * TB + j) - acc.c[m][nn][r];
         }
-    const int bad = tile_potrf(stg, 0);
+    const int bad = tile_potrf(stg, nv - J * TB);
     if (bad) return J * TB + bad;
     double* X = sD;  // inverse computed with pitch DP inside the sD region
-    tile_trinv(stg, X);
+    tile_trinv(stg, X, nv - J * TB);
     double xr[TB * TB / 256];
 #pragma unroll
     for (int q = 0; q < TB * TB / 256; ++q) {

@@ -22,6 +22,22 @@ namespace pq {
 constexpr int PT = 256;
 constexpr int PW = PT / 64;
 
+// Optional phase timing (build with -DPQ_PROFILE): wall-clock ticks per phase accumulated
+// into the 16 doubles after the work layout of each problem (tools/prof_polish.py).
+#ifdef PQ_PROFILE
+#define PQ_STAMP(k)                                              \
+  do {                                                           \
+    __syncthreads();                                             \
+    if (threadIdx.x == 0) {                                      \
+      const long long now_ = wall_clock64();                     \
+      prof[k] += (double)(now_ - t_last_);                       \
+      t_last_ = now_;                                            \
+    }                                                            \
+  } while (0)
+#else
+#define PQ_STAMP(k) do { } while (0)
+#endif
+
 struct PolishForm {
   const double* P;
   int64_t ld;
@@ -93,6 +109,48 @@ __device__ __forceinline__ int block_or(int v, double* red) {
   return block_max((double)v, red) > 0.5;
 }
 
+// emit(p, P[row(p)] . v) for p < cnt: full rows of the dense symmetric P (n <= 1024
+// columns), v held in registers (lane l owns columns 128 q + 2 l, 2 l + 1; v must be zero
+// from n up to the next even index), 16-B loads, two rows per wave in flight.  Called by
+// every thread; emit runs on lane 0 of the wave that owns the row.
+template <typename RowF, typename EmitF>
+__device__ __forceinline__ void rows_dot_vec(const double* P, int64_t ld, int n, int cnt, RowF row_of,
+                                             const double* v, EmitF emit) {
+  constexpr int NQ = 8;
+  const int w = wave_id(), l = lane_id();
+  double2 vr[NQ];
+#pragma unroll
+  for (int qq = 0; qq < NQ; ++qq) {
+    const int c = 128 * qq + 2 * l;
+    vr[qq] = c < n ? reinterpret_cast<const double2*>(v + c)[0] : double2{0.0, 0.0};
+  }
+  for (int p = w; p < cnt; p += 2 * PW) {
+    const int p1 = p + PW;
+    const bool two = p1 < cnt;
+    const double2* r0 = reinterpret_cast<const double2*>(P + (int64_t)row_of(p) * ld) + l;
+    const double2* r1 = reinterpret_cast<const double2*>(P + (int64_t)row_of(two ? p1 : p) * ld) + l;
+    double2 a[NQ], b[NQ];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const bool ok = 128 * qq + 2 * l < n;
+      a[qq] = ok ? r0[64 * qq] : double2{0.0, 0.0};
+      b[qq] = (ok && two) ? r1[64 * qq] : double2{0.0, 0.0};
+    }
+    double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      d0 = fma(a[qq].x, vr[qq].x, fma(a[qq].y, vr[qq].y, d0));
+      d1 = fma(b[qq].x, vr[qq].x, fma(b[qq].y, vr[qq].y, d1));
+    }
+    d0 = wave_sum(d0);
+    d1 = wave_sum(d1);
+    if (l == 0) {
+      emit(p, d0);
+      if (two) emit(p1, d1);
+    }
+  }
+}
+
 __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const int32_t* idx,
                                                int nidx, pq_settings s) {
   constexpr int LDMAX = 1024;
@@ -146,6 +204,11 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
   double* g = xb + ld;
   double* Px = g + ld;
   double* U = Px + ld;
+#ifdef PQ_PROFILE
+  double* prof = W + (int64_t)(4 + st.mg_pad) * ld;
+  if (t < 16) prof[t] = 0.0;
+  long long t_last_ = wall_clock64();
+#endif
 
   // ---- problem scale -> tolerances ----------------------------------------------------
   double sc = 0.0;
@@ -178,6 +241,16 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     lamF[t] = yr;   // multipliers start at the ADMM duals
   }
   __syncthreads();
+  PQ_STAMP(0);
+
+  // exact P x and gradient g = P x + q + Cg' lam of the point in xs (rows_dot_vec emit)
+  auto emit_g = [&](int i, double sum) {
+    const double pxi = ps * sum + pd * xs[i];
+    double gi = pxi + q[i];
+    for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * lamF[r];
+    Px[i] = pxi;
+    g[i] = gi;
+  };
 
   int accepted = 0, rounds = 0, nfree = 0;
   for (int round = 0; round < s.polish_rounds && !accepted; ++round) {
@@ -206,17 +279,21 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     const int ma = cnt[PT + 1];
     nfree = k;
     const int nbk = (k + TB - 1) / TB;
-    for (int i = t; i < n; i += PT) xb[i] = fl[i] == 1 ? lb[i] : (fl[i] == 2 ? ub[i] : 0.0);
-    __syncthreads();
+    int nzb = 0;
+    for (int i = t; i < ld; i += PT) {
+      const double v = i < n ? (fl[i] == 1 ? lb[i] : (fl[i] == 2 ? ub[i] : 0.0)) : 0.0;
+      xb[i] = v;
+      nzb |= (v != 0.0);
+    }
+    nzb = block_or(nzb, red);
+    PQ_STAMP(1);
     __builtin_amdgcn_s_dcache_inv();
     // ---- reduced rhs: rF = -q_F - ps P_FB x_B ;  d_a = rhs_a - C_aB x_B -----------------
-    for (int p = w; p < k; p += PW) {
-      const int i = Fl[p];
-      const double* row = P + (int64_t)i * ld;
-      double sum = 0.0;
-      for (int j = l; j < n; j += 64) sum += row[j] * xb[j];
-      sum = wave_sum(sum);
-      if (l == 0) rF[p] = -q[i] - ps * sum;
+    if (nzb) {   // (long-only: every fixed weight is 0 and P_FB x_B vanishes)
+      rows_dot_vec(P, ld, n, k, [&](int p) { return Fl[p]; }, xb,
+                   [&](int p, double sum) { rF[p] = -q[Fl[p]] - ps * sum; });
+    } else {
+      for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]];
     }
     for (int a = w; a < ma; a += PW) {
       const int r = Al[a];
@@ -230,10 +307,12 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     for (int p = t; p < k; p += PT) solx[p] = xs[Fl[p]];
     if (t < ma) solL[t] = lamF[Al[t]];
     __syncthreads();
+    PQ_STAMP(2);
     // ---- factor M = ps P_FF + (pd + delta) I ---------------------------------------------
     int info = 0;
-    if (k > 0) info = wg_cholesky(PolishForm{P, ld, Fl, k, ps, pd + delta}, K, ld, nbk, Dt, smem);
+    if (k > 0) info = wg_cholesky(PolishForm{P, ld, Fl, k, ps, pd + delta}, K, ld, nbk, k, Dt, smem);
     if (info) break;
+    PQ_STAMP(3);
     double* t1 = vec;                 // LDMAX each, inside the sD region
     double* dx = vec + LDMAX;
     double* rx = vec + 2 * LDMAX;
@@ -257,7 +336,8 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
       stg[i * DP + j] = v;
     }
     __syncthreads();
-    if (tile_potrf(stg, 0)) break;
+    if (tile_potrf(stg, ma)) break;
+    PQ_STAMP(4);
     // ---- proximal iterative refinement -------------------------------------------------
     for (int itr = 0; itr < s.refine_iters; ++itr) {
       // rx = rF - (ps P_FF + pd I) solx - C_aF' solL ;  rl = dA - C_aF solx
@@ -285,6 +365,12 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
         }
       }
       __syncthreads();
+      {  // converged to rounding level: further refinement steps change nothing
+        double rm = 0.0;
+        for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
+        if (t < ma) rm = fmax(rm, fabs(rl[t]));
+        if (block_max(rm, red) <= 1e-13 * sc) break;
+      }
       fwd_solve(K, ld, Dt, nbk, rx, t1, t64, y64p);
       // wl = U' t1 - rl ; dlam = S^-1 wl (S = Ls Ls', tiny, one thread)
       for (int a = w; a < ma; a += PW) {
@@ -319,6 +405,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
       if (t < ma) solL[t] += wl[t];
       __syncthreads();
     }
+    PQ_STAMP(5);
     // ---- expand, exact gradient, checks -------------------------------------------------
     for (int i = t; i < n; i += PT) xs[i] = xb[i];
     __syncthreads();
@@ -328,20 +415,9 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     if (t < ma) lamF[Al[t]] = solL[t];  // full-length general multipliers
     __syncthreads();
     __builtin_amdgcn_s_dcache_inv();   // xs was rewritten: no stale scalar-cache reads
-    for (int i = w; i < n; i += PW) {
-      const double* row = P + (int64_t)i * ld;
-      double sum = 0.0;
-      for (int j = l; j < n; j += 64) sum += row[j] * xs[j];
-      sum = wave_sum(sum);
-      if (l == 0) {
-        const double pxi = ps * sum + pd * xs[i];
-        double gi = pxi + q[i];
-        for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * lamF[r];
-        Px[i] = pxi;
-        g[i] = gi;
-      }
-    }
+    rows_dot_vec(P, ld, n, n, [](int p) { return p; }, xs, emit_g);
     __syncthreads();
+    PQ_STAMP(6);
     int bad = 0;
     for (int i = t; i < n; i += PT) {
       const int f = fl[i];
@@ -369,6 +445,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     bad = block_or(bad, red);
     if (!bad) accepted = 1;
     __syncthreads();
+    PQ_STAMP(7);
   }
   __syncthreads();
   // ---- final point: polished or ADMM --------------------------------------------------
@@ -377,19 +454,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     if (t < 64) lamF[t] = (t < mg) ? sy[t] : 0.0;
     __syncthreads();
     __builtin_amdgcn_s_dcache_inv();
-    for (int i = w; i < n; i += PW) {
-      const double* row = P + (int64_t)i * ld;
-      double sum = 0.0;
-      for (int j = l; j < n; j += 64) sum += row[j] * xs[j];
-      sum = wave_sum(sum);
-      if (l == 0) {
-        const double pxi = ps * sum + pd * xs[i];
-        double gi = pxi + q[i];
-        for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * lamF[r];
-        Px[i] = pxi;
-        g[i] = gi;
-      }
-    }
+    rows_dot_vec(P, ld, n, n, [](int p) { return p; }, xs, emit_g);
     __syncthreads();
   }
   // z_box: polished -> -g on fixed, 0 on free; ADMM -> ADMM box duals
@@ -443,6 +508,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     if (st0 == PQ_SOLVED) st.status[b] = accepted ? PQ_SOLVED : PQ_SOLVED_INACCURATE;
     else st.status[b] = accepted ? PQ_SOLVED : PQ_MAX_ITER;
   }
+  PQ_STAMP(8);
 }
 
 }  // namespace pq

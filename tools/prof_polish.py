@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-phase wall-clock split of the polish kernel (library built with EXTRA=-DPQ_PROFILE).
+
+Runs the bench workload (config 3, low-rank path) once and prints the mean ticks of each
+polish phase per problem (wall_clock64, 100 MHz) -- experiment tooling, not a test."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from porqua_amd import engine  # noqa: E402
+from porqua_amd.synthetic import factor_panel  # noqa: E402
+
+PHASES = ["setup+classify", "free list", "rF/dA", "cholesky", "U+S", "refine", "expand+Px",
+          "checks", "final"]
+
+
+def main():
+    n, T, D = 1000, 252, int(sys.argv[1]) if len(sys.argv) > 1 else 4749
+    dates, R, _, _ = factor_panel(T - 1 + D, n)
+    rows, tlen = engine.window_rows(dates, dates[T - 1:T - 1 + D], T)
+    pan = engine.Panel(R)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   lb=np.zeros(n), ub=np.ones(n))
+    qb.batch = D
+    mu = pan.window_means(r_d, t_d)
+    qb.P = pan.cov(r_d, t_d, mode=0, mu=mu)
+    qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=qb.P.device)
+    qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=qb.P.device)
+    lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+    ws = engine.Workspace(qb)
+    off = (4 + ws.mg_pad) * qb.ld
+    for _ in range(2):
+        ev = []
+        ws.work[:, off + 16:off + 24].zero_()
+        res = engine.solve_lowrank(qb, lr, engine.Settings(), ws, events=ev)
+        torch.cuda.synchronize()
+    ad = ws.work[:, off + 16:off + 24].cpu().numpy() * 10e-3
+    its = res.iters.cpu().numpy().astype(float)
+    atot = ad.sum(1)
+    print("admm us per problem: mean %.1f  (%.2f us per iteration)" % (atot.mean(), (atot / its).mean()))
+    for i, p in enumerate(["rhs", "v, mu.v", "w = U v", "M^-1 symv", "U'u + tree + corr", "updates+resid"]):
+        print("  %-18s %8.2f us/iter (%4.1f %%)" % (p, (ad[:, i] / its).mean(), 100 * ad[:, i].mean() / atot.mean()))
+    prof = ws.work[:, off:off + 16].cpu().numpy() * 10e-3   # ticks (10 ns) -> us
+    tot = prof[:, :9].sum(1)
+    print("polish us per problem: mean %.1f  p50 %.1f  p90 %.1f" % (tot.mean(), np.median(tot), np.percentile(tot, 90)))
+    for i, p in enumerate(PHASES):
+        print("  %-16s %8.1f us  (%4.1f %%)" % (p, prof[:, i].mean(), 100 * prof[:, i].mean() / tot.mean()))
+    for name, a, b in ev:
+        print("stage", name, "%.1f ms" % a.elapsed_time(b))
+    out = res.out.cpu().numpy()
+    print("nfree mean %.1f rounds mean %.2f" % (out[:, 5].mean(), out[:, 6].mean()))
+
+
+if __name__ == "__main__":
+    main()
