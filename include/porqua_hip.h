@@ -167,6 +167,12 @@ int pq_admm_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
 int pq_polish_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
                       const pq_settings* s, void* stream);
 
+/* K4 with the exact P x products taken from the window form of P (lr, as for
+ * pq_admm_lr_batched: two passes over the date's window rows instead of n^2 bytes of P;
+ * tmax <= 1024, even ldp).  pb.P (the K1 output) is still read for P_FF.               */
+int pq_polish_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
+                         const int32_t* idx, int32_t nidx, const pq_settings* s, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

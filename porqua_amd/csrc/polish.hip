@@ -151,8 +151,120 @@ __device__ __forceinline__ void rows_dot_vec(const double* P, int64_t ld, int n,
   }
 }
 
+// emit(i, w_scale * (Xc' Xc x)_i) for i < n from the window form of P (pq_lowrank): two
+// passes over the date's window rows (shared by neighbouring dates, so L2-resident)
+// instead of n^2 bytes of P.  x: global, zero from n to the next even index.  u: LDS
+// >= tmax doubles; tree: LDS >= 2 * 1024 doubles; red: LDS reduction scratch.
+template <typename EmitF>
+__device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* tree,
+                      double* red, EmitF emit) {
+  constexpr int NQ = 8, RU = 4, LM = NQ * 128;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
+  double mux = 0.0;
+  if (mu) {
+    double a = 0.0;
+    for (int i = t; i < n; i += PT) a += mu[i] * x[i];
+    mux = block_sum(a, red);
+  }
+  // pass 1: u_t = X_t . x - mu . x
+  {
+    double2 vr[NQ];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const int c = 128 * qq + 2 * l;
+      vr[qq] = c < n ? reinterpret_cast<const double2*>(x + c)[0] : double2{0.0, 0.0};
+    }
+    for (int t0 = w; t0 < T; t0 += RU * PW) {
+      double2 r[RU][NQ];
+#pragma unroll
+      for (int e = 0; e < RU; ++e) {
+        const int tt = t0 + e * PW;
+        const double2* rp = reinterpret_cast<const double2*>(lr.panel + (tt < T ? (int64_t)rws[tt] : 0) * lr.ldp) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq)
+          r[e][qq] = (tt < T && 128 * qq + 2 * l < n) ? rp[64 * qq] : double2{0.0, 0.0};
+      }
+      double d[RU];
+#pragma unroll
+      for (int e = 0; e < RU; ++e) {
+        double s0 = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) s0 = fma(r[e][qq].x, vr[qq].x, fma(r[e][qq].y, vr[qq].y, s0));
+        d[e] = wave_sum(s0);
+      }
+      if (l == 0) {
+#pragma unroll
+        for (int e = 0; e < RU; ++e)
+          if (t0 + e * PW < T) u[t0 + e * PW] = d[e] - mux;
+      }
+    }
+  }
+  __syncthreads();
+  double su = 0.0;
+  if (mu) {
+    double a = 0.0;
+    for (int tt = t; tt < T; tt += PT) a += u[tt];
+    su = block_sum(a, red);
+  }
+  // pass 2: acc = sum_t u_t X_t (register accumulators), then a fixed-order wave tree
+  double2 acc[NQ];
+#pragma unroll
+  for (int qq = 0; qq < NQ; ++qq) acc[qq] = double2{0.0, 0.0};
+  for (int t0 = w; t0 < T; t0 += RU * PW) {
+    double2 r[RU][NQ];
+    double a[RU];
+#pragma unroll
+    for (int e = 0; e < RU; ++e) {
+      const int tt = t0 + e * PW;
+      a[e] = tt < T ? u[tt] : 0.0;
+      const double2* rp = reinterpret_cast<const double2*>(lr.panel + (tt < T ? (int64_t)rws[tt] : 0) * lr.ldp) + l;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq)
+        r[e][qq] = (tt < T && 128 * qq + 2 * l < n) ? rp[64 * qq] : double2{0.0, 0.0};
+    }
+#pragma unroll
+    for (int e = 0; e < RU; ++e)
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        acc[qq].x = fma(a[e], r[e][qq].x, acc[qq].x);
+        acc[qq].y = fma(a[e], r[e][qq].y, acc[qq].y);
+      }
+  }
+#pragma unroll
+  for (int half = PW / 2; half >= 1; half >>= 1) {
+    if (w >= half && w < 2 * half) {
+      double2* dst = reinterpret_cast<double2*>(tree + (w - half) * LM) + l;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
+    }
+    __syncthreads();
+    if (w < half) {
+      const double2* src = reinterpret_cast<const double2*>(tree + w * LM) + l;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const double2 vv = src[64 * qq];
+        acc[qq].x += vv.x;
+        acc[qq].y += vv.y;
+      }
+    }
+    __syncthreads();
+  }
+  if (w == 0) {
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const int c = 128 * qq + 2 * l;
+      if (c < n) emit(c, wsc * (acc[qq].x - (mu ? mu[c] * su : 0.0)));
+      if (c + 1 < n) emit(c + 1, wsc * (acc[qq].y - (mu ? mu[c + 1] * su : 0.0)));
+    }
+  }
+}
+
 __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const int32_t* idx,
-                                               int nidx, pq_settings s) {
+                                               int nidx, pq_settings s, pq_lowrank lr) {
   constexpr int LDMAX = 1024;
   __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS + 2 * LDMAX + 14 * 64 + 64 + LDMAX + 256];
   double* stg = smem;                  // Cholesky stream buffers; S factor during refinement
@@ -250,6 +362,12 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * lamF[r];
     Px[i] = pxi;
     g[i] = gi;
+  };
+  // P x of the point in xs: window form when given (vec / stg are free at the call sites:
+  // after refinement and in the final scoring), else the dense rows of P
+  auto full_px = [&]() {
+    if (lr.panel) lr_px(lr, b, n, xs, vec, stg, red, emit_g);
+    else rows_dot_vec(P, ld, n, n, [](int p) { return p; }, xs, emit_g);
   };
 
   int accepted = 0, rounds = 0, nfree = 0;
@@ -415,7 +533,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     if (t < ma) lamF[Al[t]] = solL[t];  // full-length general multipliers
     __syncthreads();
     __builtin_amdgcn_s_dcache_inv();   // xs was rewritten: no stale scalar-cache reads
-    rows_dot_vec(P, ld, n, n, [](int p) { return p; }, xs, emit_g);
+    full_px();
     __syncthreads();
     PQ_STAMP(6);
     int bad = 0;
@@ -454,7 +572,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     if (t < 64) lamF[t] = (t < mg) ? sy[t] : 0.0;
     __syncthreads();
     __builtin_amdgcn_s_dcache_inv();
-    rows_dot_vec(P, ld, n, n, [](int p) { return p; }, xs, emit_g);
+    full_px();
     __syncthreads();
   }
   // z_box: polished -> -g on fixed, 0 on free; ADMM -> ADMM box duals
@@ -513,16 +631,35 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
 
 }  // namespace pq
 
-extern "C" int pq_polish_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
-                                 const pq_settings* s, void* stream) {
-  PQ_CHECK_ARG(pb && st && s, "pq_polish_batched: null argument");
-  PQ_CHECK_ARG(pb->ld <= 1024, "pq_polish_batched: ld=%d exceeds the LDS-resident limit 1024", pb->ld);
-  PQ_CHECK_ARG(pb->mg <= 64, "pq_polish_batched: mg must be <= 64");
+static int polish_launch(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const int32_t* idx,
+                         int32_t nidx, const pq_settings* s, void* stream, const char* who) {
+  PQ_CHECK_ARG(pb && st && s, "%s: null argument", who);
+  PQ_CHECK_ARG(pb->ld <= 1024, "%s: ld=%d exceeds the LDS-resident limit 1024", who, pb->ld);
+  PQ_CHECK_ARG(pb->mg <= 64, "%s: mg must be <= 64", who);
   PQ_CHECK_ARG(st->work && st->work_stride >= PQ_WORK_DOUBLES(pb->ld, st->mg_pad),
-               "pq_polish_batched: work buffer too small");
+               "%s: work buffer too small", who);
+  pq_lowrank l = {};
+  if (lr) {
+    PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0 && lr->tmax <= 1024,
+                 "%s: window missing or tmax > 1024", who);
+    PQ_CHECK_ARG((lr->ldp & 1) == 0, "%s: the window form needs an even panel stride", who);
+    l = *lr;
+  }
   const int grid = idx ? nidx : pb->batch;
   if (grid <= 0) return 0;
-  hipLaunchKernelGGL(pq::k_polish, dim3(grid), dim3(pq::PT), 0, (hipStream_t)stream, *pb, *st, idx, nidx, *s);
-  PQ_CHECK_LAUNCH("pq_polish_batched");
+  hipLaunchKernelGGL(pq::k_polish, dim3(grid), dim3(pq::PT), 0, (hipStream_t)stream, *pb, *st, idx, nidx, *s, l);
+  PQ_CHECK_LAUNCH(who);
   return 0;
+}
+
+extern "C" int pq_polish_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                                 const pq_settings* s, void* stream) {
+  return polish_launch(nullptr, pb, st, idx, nidx, s, stream, "pq_polish_batched");
+}
+
+extern "C" int pq_polish_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
+                                    const int32_t* idx, int32_t nidx, const pq_settings* s,
+                                    void* stream) {
+  PQ_CHECK_ARG(lr != nullptr, "pq_polish_lr_batched: null window description");
+  return polish_launch(lr, pb, st, idx, nidx, s, stream, "pq_polish_lr_batched");
 }

@@ -380,7 +380,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     pb = qb.c_struct()
     st = ws.c_struct()
     lrs = lr.c_struct()
-    pbM = _lib.PQProblem(n=k_ld, ld=k_ld, batch=B, mg=0, P=M["M"].data_ptr(), P_stride=k_ld * k_ld,
+    # n = k: the padded tail of M is the identity, so the factor skips its pivot steps
+    pbM = _lib.PQProblem(n=k, ld=k_ld, batch=B, mg=0, P=M["M"].data_ptr(), P_stride=k_ld * k_ld,
                          q=qb.q.data_ptr(), q_stride=qb.q.stride(0), Cg=qb.Cg.data_ptr(), lg=qb.lg.data_ptr(),
                          ug=qb.ug.data_ptr())
     stM = _lib.PQState(K=M["Minv"].data_ptr(), K_stride=k_ld * k_ld, Dt=M["Dt"].data_ptr(),
@@ -418,8 +419,12 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         tl("factor", lambda: refactor(idx, nidx))
         refactors += kk
     if s.polish and polish:
-        _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, None, 0, SS, strm)),
-                   "pq_polish_batched")
+        if lr.tmax <= 1024 and lr.panel.R.stride(0) % 2 == 0:
+            _lib.check(tl("polish", lambda: lib.pq_polish_lr_batched(L_, P_, S_, None, 0, SS, strm)),
+                       "pq_polish_lr_batched")
+        else:
+            _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, None, 0, SS, strm)),
+                       "pq_polish_batched")
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
