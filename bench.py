@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--path", choices=["auto", "dense", "lowrank"], default="auto",
                     help="dense K^-1 (K2 n^3 + K3 n^2 stream) or Woodbury low-rank (T + mg < n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-slide", action="store_true",
+                    help="K1 as one full T-deep SYRK per date instead of anchor SYRK + rank-2 slides")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="override an engine.Settings field (experiments)")
@@ -80,6 +82,7 @@ def main():
 
     pan = engine.Panel(R_rank, device=dev)
     rows_d, tlen_d = pan.rows_to_device(rows, tlen)
+    plan = None if args.no_slide else engine.SlidePlan(rows, tlen, dev)
     qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)),
                                    b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), device=dev)
     # re-shape the batch to D problems sharing constraints; P is written by K1 every step
@@ -100,7 +103,7 @@ def main():
         mu = pan.window_means(rows_d, tlen_d, out=mu_lr)
         if events is not None:
             e0 = torch.cuda.Event(enable_timing=True); e0.record()
-        pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu)
+        pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu, plan=plan)
         if events is not None:
             e1 = torch.cuda.Event(enable_timing=True); e1.record()
             events.append(("cov", e0, e1))
@@ -157,7 +160,12 @@ def main():
     admm_gbs = admm_bytes / tk["admm"] / 1e9
     ld = qb.ld
     nb = ld // 64
-    syrk_flops = D * (nb * (nb + 1) // 2) * 64 * 64 * 2.0 * T * args.steps
+    tiles = nb * (nb + 1) // 2
+    if plan is None:
+        syrk_flops = D * tiles * 64 * 64 * 2.0 * T * args.steps
+    else:   # anchors: full T-deep SYRK; slid dates: one 4-deep (2 s padded) MFMA update
+        syrk_flops = (plan.ngroups * T + (D - plan.ngroups) * 4) * tiles * 64 * 64 * 2.0 * args.steps
+    cov_write_gbs = D * ld * ld * 8.0 * args.steps / tk.get("cov", float("nan")) / 1e9
     kld = ((T + 1 + 63) // 64) * 64
     factor_flops_per = (2.0 * kld * kld * n + kld ** 3) if use_lr else ld ** 3  # (capacitance SYRK +) potrf+trtri+lauum
     n_factor = D * args.steps + res.refactors * args.steps
@@ -203,6 +211,9 @@ def main():
         "stages_s_per_step": {k: v / args.steps for k, v in tk.items()},
         "stage_rates": {
             "cov_syrk_tflops": syrk_flops / tk.get("cov", float("nan")) / 1e12,
+            "cov_write_gbs": cov_write_gbs,
+            "cov_mode": "full SYRK per date" if plan is None else
+                        f"sliding: {plan.ngroups} anchor SYRKs + rank-2 updates",
             "factor_tflops": factor_flops / tk.get("factor", float("nan")) / 1e12,
             "fp64_peak_tflops": FP64_PEAK_TFLOPS,
         },

@@ -115,6 +115,18 @@ int pq_cov_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* r
                    const double* mu, int64_t mu_stride, double* out, int32_t ld,
                    int64_t out_stride, void* stream);
 
+/* K1 for overlapping windows (the same outputs as pq_cov_batched): dates are cut into
+ * ngroups groups [gstart[g], gstart[g+1]); the first date of a group is a full SYRK, and
+ * every later date d must hold the window of date d-1 shifted by shift[d] >= 1 rows
+ * (rows[d][0..T-s) == rows[d-1][s..T), equal tlen), which is applied as a rank-2s MFMA
+ * update: 2 s n^2 instead of 2 T n^2 flops per date.  The host builds the plan
+ * (porqua_amd.engine.slide_plan).                                                      */
+int pq_cov_slide_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                         const int32_t* tlen, int32_t tmax, int32_t batch, int32_t mode,
+                         const double* mu, int64_t mu_stride, double* out, int32_t ld,
+                         int64_t out_stride, const int32_t* gstart, int32_t ngroups,
+                         const int32_t* shift, void* stream);
+
 /* X'y and y'y of each window (LeastSquares q = -2 X'y, constant = y'y,
  * src/optimization.py:216-217).                                                        */
 int pq_gram_xy_batched(const double* panel, int64_t ldp, int32_t n, const double* bm,

@@ -114,6 +114,139 @@ __global__ __launch_bounds__(256) void k_syrk(const double* panel, int64_t ldp, 
   if (I != J) acc_store_T(acc, o, ld, J * TB, I * TB);
 }
 
+// ---- sliding windows: anchor SYRK + rank-2s updates -----------------------------------
+//
+// A daily backtest's consecutive windows share T - s of their T rows (s = 1 for daily,
+// 21 for monthly rebalancing).  Dates are cut into groups; the first date of a group (the
+// anchor) is a full SYRK of its window, shifted by the anchor's own mean c; every later
+// date d of the group updates the shifted Gram in registers,
+//     S_d = S_{d-1} + sum_{added rows} (x - c)(x - c)' - sum_{dropped rows} (x - c)(x - c)',
+// as one MFMA pass over a 2s-deep [added; -dropped] operand, and is written out centred
+// by its own two-pass mean mu_d (pq_window_mean):
+//     Sigma_d = (S_d - T (mu_d - c)(mu_d - c)') / (T - 1)
+// -- algebraically np.cov's two-pass result (src/covariance.py:65-66); the shift keeps
+// the correction term at the size of the drift of the mean inside one group.  mode 1
+// (uncentred Gram X'X, src/optimization.py:215) uses c = 0 and no correction.  Flops per
+// date: 2 s n^2 instead of 2 T n^2; the output (8 n^2 B per date) is the remaining cost,
+// written through an LDS tile with 16-B row stores (tile and mirror).
+constexpr int SP = 65;   // pitch of the LDS output tile
+
+__device__ __forceinline__ void slide_load(double (&va)[4], double (&vb)[4], const double* panel,
+                                           int64_t ldp, int n, const int32_t* add, const int32_t* drop,
+                                           int na, int i0, int j0, const double* c) {
+  // rows k < na: added (+), na <= k < 2 na: dropped (- on the A side), else zero
+  const int t = threadIdx.x;
+  const int k = t >> 4, i = (t & 15) * 4;
+  int64_t row = -1;
+  double sg = 1.0;
+  if (k < na) row = add[k];
+  else if (k < 2 * na) { row = drop[k - na]; sg = -1.0; }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    double a = 0.0, b = 0.0;
+    if (row >= 0) {
+      const int ca = i0 + i + e, cb = j0 + i + e;
+      if (ca < n) a = sg * (panel[row * ldp + ca] - (c ? c[ca] : 0.0));
+      if (cb < n) b = panel[row * ldp + cb] - (c ? c[cb] : 0.0);
+    }
+    va[e] = a;
+    vb[e] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_syrk_slide(const double* panel, int64_t ldp, int n,
+                                                    const int32_t* rows, const int32_t* tlen, int tmax,
+                                                    int mode, const double* mu, int64_t mu_stride,
+                                                    double* out, int ld, int64_t out_stride,
+                                                    const int32_t* gstart, const int32_t* shift) {
+  __shared__ __attribute__((aligned(16))) double smem[4 * STAGE + TB * SP];
+  double* tile = smem + 4 * STAGE;
+  int I, J;
+  tri_index(blockIdx.x, I, J);
+  const int g = blockIdx.y;
+  const int d0 = gstart[g], d1 = gstart[g + 1];
+  const int T = tlen[d0];
+  const double* c = (mode == 0) ? mu + (int64_t)d0 * mu_stride : nullptr;   // the shift
+  const int t = threadIdx.x;
+  // ---- anchor: full SYRK of the anchor window (identical to k_syrk) ---------------------
+  Acc acc;
+  acc.zero();
+  {
+    const int32_t* rw = rows + (int64_t)d0 * tmax;
+    double va[4], vb[4];
+    load_win(va, panel, ldp, n, rw, T, 0, I * TB, c);
+    load_win(vb, panel, ldp, n, rw, T, 0, J * TB, c);
+    store_win(va, smem);
+    store_win(vb, smem + STAGE);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < T; k0 += KC) {
+      const bool more = (k0 + KC) < T;
+      if (more) {
+        load_win(va, panel, ldp, n, rw, T, k0 + KC, I * TB, c);
+        load_win(vb, panel, ldp, n, rw, T, k0 + KC, J * TB, c);
+      }
+      mma_lds(acc, smem + buf * 2 * STAGE, smem + buf * 2 * STAGE + STAGE, KC);
+      if (more) {
+        store_win(va, smem + (buf ^ 1) * 2 * STAGE);
+        store_win(vb, smem + (buf ^ 1) * 2 * STAGE + STAGE);
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  const double sc = (mode == 0) ? 1.0 / (double)(T - 1) : 1.0;
+  for (int d = d0; d < d1; ++d) {
+    if (d > d0) {
+      // ---- slide: + rows entering the window, - rows leaving it (chunks of 8 each) ------
+      const int s = shift[d];
+      const int32_t* add = rows + (int64_t)d * tmax + (T - s);
+      const int32_t* drop = rows + (int64_t)(d - 1) * tmax;
+      for (int k0 = 0; k0 < s; k0 += KC / 2) {
+        const int na = min(KC / 2, s - k0);
+        double va[4], vb[4];
+        slide_load(va, vb, panel, ldp, n, add + k0, drop + k0, na, I * TB, J * TB, c);
+        store_win(va, smem);
+        store_win(vb, smem + STAGE);
+        __syncthreads();
+        mma_lds(acc, smem, smem + STAGE, (2 * na + 3) & ~3);
+        __syncthreads();
+      }
+    }
+    // ---- emit date d: centre by its own mean, scale, stage through LDS ----------------
+    const double* md = (mode == 0) ? mu + (int64_t)d * mu_stride : nullptr;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = acc_row(m, r), j = acc_col(nn);
+          double v = acc.c[m][nn][r];
+          if (md && d > d0) {
+            const int gi = I * TB + i, gj = J * TB + j;
+            const double di = gi < n ? md[gi] - c[gi] : 0.0;
+            const double dj = gj < n ? md[gj] - c[gj] : 0.0;
+            v -= (double)T * (di * dj);   // (di dj) first: bitwise symmetric tiles
+          }
+          tile[i * SP + j] = v * sc;
+        }
+    __syncthreads();
+    double* o = out + (int64_t)d * out_stride;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = t + 256 * e;
+      const int r = idx >> 5, c2 = (idx & 31) * 2;
+      reinterpret_cast<double2*>(o + (int64_t)(I * TB + r) * ld + J * TB)[c2 >> 1] =
+          double2{tile[r * SP + c2], tile[r * SP + c2 + 1]};
+      if (I != J)
+        reinterpret_cast<double2*>(o + (int64_t)(J * TB + r) * ld + I * TB)[c2 >> 1] =
+            double2{tile[c2 * SP + r], tile[(c2 + 1) * SP + r]};
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void k_gram_xy(const double* panel, int64_t ldp, int n,
                                                  const double* bm, const int32_t* rows,
                                                  const int32_t* tlen, int tmax, double* xty,
@@ -186,6 +319,25 @@ extern "C" int pq_cov_batched(const double* panel, int64_t ldp, int32_t n, const
                      (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mode, mu, mu_stride,
                      out, ld, out_stride);
   PQ_CHECK_LAUNCH("pq_cov_batched");
+  return 0;
+}
+
+extern "C" int pq_cov_slide_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                                    const int32_t* tlen, int32_t tmax, int32_t batch, int32_t mode,
+                                    const double* mu, int64_t mu_stride, double* out, int32_t ld,
+                                    int64_t out_stride, const int32_t* gstart, int32_t ngroups,
+                                    const int32_t* shift, void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(mode == 0 || mode == 1, "pq_cov_slide_batched: mode must be 0 (centred cov) or 1 (Gram)");
+  PQ_CHECK_ARG(mode == 1 || mu != nullptr, "pq_cov_slide_batched: mode 0 needs the window means");
+  PQ_CHECK_ARG(out && ld >= n && ld % 64 == 0, "pq_cov_slide_batched: ld must be a multiple of 64 >= n");
+  PQ_CHECK_ARG(gstart && shift && ngroups >= 0, "pq_cov_slide_batched: slide plan missing");
+  if (batch == 0 || ngroups == 0) return 0;
+  const int nb = ld / 64;
+  hipLaunchKernelGGL(pq::k_syrk_slide, dim3(nb * (nb + 1) / 2, ngroups), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mode, mu, mu_stride,
+                     out, ld, out_stride, gstart, shift);
+  PQ_CHECK_LAUNCH("pq_cov_slide_batched");
   return 0;
 }
 

@@ -477,6 +477,46 @@ def window_rows(dates: np.ndarray, rebdates, width: int):
     return rows, tlen
 
 
+def slide_plan(rows, tlen, group: int = 32, smax: int = 64):
+    """Host plan for pq_cov_slide_batched: ``(gstart int32 [G+1], shift int32 [B])``.
+
+    Date d joins the group of date d-1 when its window is that window shifted by
+    1 <= s <= smax rows (same length, rows[d][:T-s] == rows[d-1][s:T]) and the group holds
+    fewer than ``group`` dates; otherwise d starts a new group (a full-SYRK anchor)."""
+    rows = np.asarray(rows)
+    tlen = np.asarray(tlen)
+    B, tmax = rows.shape
+    shift = np.zeros(B, dtype=np.int32)
+    if B > 1:
+        col = np.arange(tmax)[None, :]
+        prev, cur = rows[:-1], rows[1:]
+        tp, tc = tlen[:-1], tlen[1:]
+        s = ((prev < cur[:, :1]) & (col < tp[:, None])).sum(1)
+        gathered = np.take_along_axis(prev, np.minimum(col + s[:, None], tmax - 1), axis=1)
+        match = np.where(col < (tc - s)[:, None], gathered == cur, True).all(1)
+        good = (tp == tc) & (tc > 1) & match & (s >= 1) & (s <= smax)
+        shift[1:] = np.where(good, s, 0)
+    gstart = []
+    cnt = 0
+    for d in range(B):
+        if shift[d] == 0 or cnt == group:
+            gstart.append(d)
+            cnt = 0
+        cnt += 1
+    gstart.append(B)
+    return np.asarray(gstart, dtype=np.int32), shift
+
+
+class SlidePlan:
+    """Device copy of a slide_plan (see pq_cov_slide_batched)."""
+
+    def __init__(self, rows, tlen, device, group: int = 32, smax: int = 64):
+        gs, sh = slide_plan(rows, tlen, group, smax)
+        self.ngroups = len(gs) - 1
+        self.gstart = torch.from_numpy(gs).to(device)
+        self.shift = torch.from_numpy(sh).to(device)
+
+
 class Panel:
     """A device-resident return panel (D_total x n, row-major) with optional benchmark."""
 
@@ -504,8 +544,9 @@ class Panel:
                       mu.stride(0), _stream()), "window means")
         return mu
 
-    def cov(self, rows, tlen, mode=0, out=None, mu=None):
-        """K1: per-date centred covariance (mode 0, ddof=1) or Gram X'X (mode 1) -> (B, ld, ld)."""
+    def cov(self, rows, tlen, mode=0, out=None, mu=None, plan: SlidePlan | None = None):
+        """K1: per-date centred covariance (mode 0, ddof=1) or Gram X'X (mode 1) -> (B, ld, ld).
+        With a SlidePlan, overlapping windows are built by rank-2s updates (same result)."""
         lib = _lib.load()
         B, tmax = rows.shape
         ld = round_up(self.n, 64)
@@ -513,10 +554,16 @@ class Panel:
             mu = self.window_means(rows, tlen)
         if out is None:
             out = torch.empty((B, ld, ld), dtype=F64, device=self.device)
-        _lib.check(lib.pq_cov_batched(_ptr(self.R), self.n, self.n, _ptr(rows), _ptr(tlen), tmax, B,
-                                      mode, _ptr(mu) if mode == 0 else None,
-                                      mu.stride(0) if mode == 0 else 0, _ptr(out), ld,
-                                      out.stride(0), _stream()), "pq_cov_batched")
+        mp = _ptr(mu) if mode == 0 else None
+        ms = mu.stride(0) if mode == 0 else 0
+        if plan is not None:
+            _lib.check(lib.pq_cov_slide_batched(_ptr(self.R), self.R.stride(0), self.n, _ptr(rows), _ptr(tlen),
+                                                tmax, B, mode, mp, ms, _ptr(out), ld, out.stride(0),
+                                                _ptr(plan.gstart), plan.ngroups, _ptr(plan.shift), _stream()),
+                       "pq_cov_slide_batched")
+            return out
+        _lib.check(lib.pq_cov_batched(_ptr(self.R), self.R.stride(0), self.n, _ptr(rows), _ptr(tlen), tmax, B,
+                                      mode, mp, ms, _ptr(out), ld, out.stride(0), _stream()), "pq_cov_batched")
         return out
 
     def gram_xy(self, rows, tlen):

@@ -38,6 +38,33 @@ def test_cov_and_gram_match_numpy(device, n, T, D):
         assert np.all(S[b, n:, :] == 0) and np.all(S[b, :, n:] == 0)
 
 
+@pytest.mark.parametrize("n,T,stride,offset", [(24, 252, 1, 0.0), (130, 60, 1, 0.0), (200, 252, 21, 0.0),
+                                               (70, 40, 3, 50.0)])
+def test_sliding_cov_matches_full_syrk_and_numpy(device, n, T, stride, offset):
+    """pq_cov_slide_batched (anchor SYRK + rank-2s updates) == pq_cov_batched == np.cov;
+    offset: price-like data with a large common mean (the shift keeps it exact)."""
+    D = T + 70 * stride
+    dates, R, y, _ = factor_panel(D, n, seed=n + stride)
+    R = R + offset
+    reb = dates[T - 1::stride][:70]
+    rows, tlen = engine.window_rows(dates, reb, T)
+    plan = engine.SlidePlan(rows, tlen, device, group=16)
+    assert plan.ngroups < len(reb)
+    pan = engine.Panel(R, y, device=device)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    for mode in (0, 1):
+        full = pan.cov(r_d, t_d, mode=mode).cpu().numpy()
+        sl = pan.cov(r_d, t_d, mode=mode, plan=plan).cpu().numpy()
+        gs = plan.gstart.cpu().numpy()
+        assert np.array_equal(full[gs[:-1]], sl[gs[:-1]])          # anchors: same arithmetic
+        for b in range(len(reb)):
+            X = R[rows[b, :tlen[b]]]
+            ref = cov_pearson(X) if mode == 0 else X.T @ X
+            assert _rel(sl[b, :n, :n], ref) < 1e-12, (mode, b, _rel(sl[b, :n, :n], ref))
+            assert np.array_equal(sl[b, :n, :n], sl[b, :n, :n].T)
+            assert np.all(sl[b, n:, :] == 0) and np.all(sl[b, :, n:] == 0)
+
+
 @pytest.mark.parametrize("n", [24, 64, 150, 300])
 def test_factor_and_inverse(device, n):
     rng = np.random.default_rng(n)

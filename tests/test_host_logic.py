@@ -35,6 +35,30 @@ def test_window_rows_match_reference_semantics():
     assert tlen[0] == 0
 
 
+def test_slide_plan_groups_overlapping_windows():
+    dates, _, _, _ = factor_panel(600, 3)
+    # daily: every window is the previous one shifted by one row -> groups of 32
+    rows, tlen = engine.window_rows(dates, dates[251:600], 252)
+    gs, sh = engine.slide_plan(rows, tlen, group=32)
+    assert list(gs[:3]) == [0, 32, 64] and gs[-1] == len(tlen)
+    assert np.all(sh[gs[:-1]] <= 1) and np.all(np.delete(sh, gs[:-1]) == 1)
+    # monthly stride 21 -> shift 21; beyond smax -> anchors only
+    rows, tlen = engine.window_rows(dates, dates[251:600:21], 252)
+    gs, sh = engine.slide_plan(rows, tlen)
+    assert len(gs) == 2 and np.all(sh[1:] == 21)
+    gs, sh = engine.slide_plan(rows, tlen, smax=20)
+    assert len(gs) == len(tlen) + 1 and np.all(sh == 0)
+    # every slid window really is its predecessor shifted by s rows
+    cal = np.datetime64("2020-01-01") + np.arange(400)
+    rows, tlen = engine.window_rows(cal, cal[100:160], 30)
+    gs, sh = engine.slide_plan(rows, tlen)
+    for d in np.flatnonzero(sh):
+        T, s = tlen[d], sh[d]
+        assert tlen[d - 1] == T and np.array_equal(rows[d, :T - s], rows[d - 1, s:T])
+    # ragged (weekend-filtered) windows break groups
+    assert len(gs) - 1 > 1 and sh[0] == 0
+
+
 def test_business_days_and_panel_are_deterministic():
     d = business_days("2005-01-03", 10)
     assert ((d.astype(np.int64) + 3) % 7 < 5).all() and len(d) == 10
