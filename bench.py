@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--path", choices=["auto", "dense", "lowrank"], default="auto",
                     help="dense K^-1 (K2 n^3 + K3 n^2 stream) or Woodbury low-rank (T + mg < n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-group", action="store_true",
+                    help="low-rank ADMM one workgroup per date instead of per group of sliding windows")
     ap.add_argument("--no-slide", action="store_true",
                     help="K1 as one full T-deep SYRK per date instead of anchor SYRK + rank-2 slides")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -83,6 +85,7 @@ def main():
     pan = engine.Panel(R_rank, device=dev)
     rows_d, tlen_d = pan.rows_to_device(rows, tlen)
     plan = None if args.no_slide else engine.SlidePlan(rows, tlen, dev)
+    gplan = None if args.no_group else engine.GroupPlan(rows, tlen, dev)
     qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)),
                                    b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), device=dev)
     # re-shape the batch to D problems sharing constraints; P is written by K1 every step
@@ -108,7 +111,7 @@ def main():
             e1 = torch.cuda.Event(enable_timing=True); e1.record()
             events.append(("cov", e0, e1))
         if use_lr:
-            res = engine.solve_lowrank(qb, lr, settings, ws, events=events)
+            res = engine.solve_lowrank(qb, lr, settings, ws, events=events, groups=gplan)
         else:
             res = engine.solve(qb, settings, ws, events=events)
         x = res.x.contiguous()

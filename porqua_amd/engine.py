@@ -361,12 +361,18 @@ def lowrank_applicable(qb: QPBatch, lr: LowRank) -> bool:
     return k_ld <= 512 and (k_ld + 127) // 128 <= (qb.n + 127) // 128 and lr.tmax + qb.mg < qb.n
 
 
+def grouped_applicable(qb: QPBatch, lr: LowRank, groups: "GroupPlan | None", ws: "Workspace") -> bool:
+    k_ld = round_up(lr.tmax + qb.mg, 64)
+    return (groups is not None and groups.ok and qb.n % 2 == 0 and lr.panel.R.stride(0) % 2 == 0
+            and qb.mg <= 4 and k_ld <= 384 and ws.work_stride >= 3 * qb.ld)
+
+
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
-                  polish: bool = True) -> BatchResult:
+                  polish: bool = True, groups: "GroupPlan | None" = None) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
-    k x k matrices M, K3 = low-rank ADMM over the shared window rows, K4 = polish (needs the
-    dense P in qb.P)."""
+    k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
+    windows when a GroupPlan is given), K4 = polish (needs the dense P in qb.P)."""
     tl = _Timeline(events)
     lib = _lib.load()
     s = (settings or Settings()).to_c()
@@ -405,11 +411,19 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     tl("factor", lambda: refactor(None, 0))
     idx, nidx = None, 0
     refactors = launches = 0
+    grouped = grouped_applicable(qb, lr, groups, ws)
+
+    def admm(idx, nidx):
+        if grouped:   # every group relaunches; solved dates are skipped inside
+            return lib.pq_admm_lr_grouped(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
+                                          _ptr(groups.gdates), groups.ngroups, _ptr(groups.urows),
+                                          _ptr(groups.ucnt), _ptr(groups.uoff), groups.umax, SS,
+                                          int(s.max_iter), strm)
+        return lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld, _ptr(idx),
+                                      nidx, SS, int(s.max_iter), strm)
+
     for _ in range(max_rounds):
-        _lib.check(tl("admm", lambda: lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld,
-                                                             k_ld * k_ld, _ptr(idx), nidx, SS,
-                                                             int(s.max_iter), strm)),
-                   "pq_admm_lr_batched")
+        _lib.check(tl("admm", lambda: admm(idx, nidx)), "pq_admm_lr")
         launches += 1
         need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
         kk = int(need.numel())
@@ -515,6 +529,63 @@ class SlidePlan:
         self.ngroups = len(gs) - 1
         self.gstart = torch.from_numpy(gs).to(device)
         self.shift = torch.from_numpy(sh).to(device)
+
+
+GROUP_MAX_DATES = 16     # MFMA N of the grouped ADMM (admm_grp.hip GMAX)
+GROUP_MAX_UNION = 320    # union rows per group (admm_grp.hip UMAXG)
+
+
+class GroupPlan:
+    """Date groups for pq_admm_lr_grouped: runs of consecutive dates whose windows slide
+    (slide_plan), at most ``gmax`` dates and ``umax`` union rows each.  ``ok`` is False
+    when some window cannot be grouped (the per-date kernel is used then)."""
+
+    def __init__(self, rows, tlen, device, gmax: int = GROUP_MAX_DATES, umax: int = GROUP_MAX_UNION,
+                 smax: int = 64, cus: int = 256, gmin: int = 4):
+        rows = np.asarray(rows)
+        tlen = np.asarray(tlen)
+        B = len(tlen)
+        # balance: one group per CU per round (one 512-thread workgroup fits a CU), as few
+        # rounds as gmax allows, groups as even as possible within them
+        rounds = max(1, -(-B // (gmax * cus)))
+        gmax = max(1, min(gmax, max(gmin, -(-B // (rounds * cus)))))
+        self.ok = B > 0 and int(tlen.min()) >= 2 and int(tlen.max()) <= umax
+        gs, sh = slide_plan(rows, tlen, group=gmax, smax=smax)
+        groups = []
+        for a, b in zip(gs[:-1], gs[1:]):
+            start, U = a, int(tlen[a])
+            for d in range(a + 1, b):
+                if U + int(sh[d]) > umax:
+                    groups.append((start, d))
+                    start, U = d, int(tlen[d])
+                else:
+                    U += int(sh[d])
+            groups.append((start, b))
+        self.ngroups = len(groups)
+        self.umax = umax
+        gdates = np.array([a for a, _ in groups] + [B], dtype=np.int32)
+        urows = np.zeros((max(1, self.ngroups), umax), dtype=np.int32)
+        ucnt = np.zeros(max(1, self.ngroups), dtype=np.int32)
+        uoff = np.zeros(B, dtype=np.int32)
+        for gi, (a, b) in enumerate(groups):
+            u = [rows[a, :tlen[a]]]
+            off = 0
+            for d in range(a + 1, b):
+                s = int(sh[d])
+                off += s
+                uoff[d] = off
+                u.append(rows[d, tlen[d] - s:tlen[d]])
+            u = np.concatenate(u)
+            if len(u) > umax:
+                self.ok = False
+                continue
+            urows[gi, :len(u)] = u
+            ucnt[gi] = len(u)
+        self.sizes = np.diff(gdates)
+        self.gdates = torch.from_numpy(gdates).to(device)
+        self.urows = torch.from_numpy(urows).to(device)
+        self.ucnt = torch.from_numpy(ucnt).to(device)
+        self.uoff = torch.from_numpy(uoff).to(device)
 
 
 class Panel:

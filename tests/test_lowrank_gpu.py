@@ -88,3 +88,44 @@ def test_lowrank_least_squares_uncentred(device):
         assert abs((0.5 * x[i] @ P @ x[i] + q @ x[i]) - o.obj) <= 1e-6 * abs(o.obj)
         assert abs(x[i].sum() - 1.0) <= 1e-7
         assert x[i].min() >= -1e-7 and x[i].max() <= 0.05 + 1e-7
+
+
+@pytest.mark.parametrize("n,T,D,stride,groups_rows", [(300, 120, 40, 1, False), (300, 120, 40, 1, True),
+                                                      (1000, 252, 35, 1, False), (200, 60, 24, 5, True)])
+def test_grouped_admm_matches_per_date_lowrank(device, n, T, D, stride, groups_rows):
+    """pq_admm_lr_grouped (one workgroup per group of sliding windows, MFMA passes over the
+    union rows) reaches the same iterates as the per-date low-rank kernel: the same
+    iteration counts up to rounding and the same polished weights."""
+    ends = list(range(T + 5, T + 5 + D * stride, stride))
+    dates, R, y, sec, pan, r_d, t_d, mu = _setup(n, T, ends, D=max(ends) + 1)
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    B = len(ends)
+    G = h = None
+    if groups_rows:
+        G = np.stack([(sec == g).astype(float) for g in range(3)])
+        h = np.full(3, 0.3)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=G, h=h, lb=np.zeros(n), ub=np.full(n, 0.2), device=device)
+    qb.batch = B
+    qb.P = pan.cov(r_d, t_d, mode=0, mu=mu)
+    qb.q = torch.zeros((B, qb.ld), dtype=torch.float64, device=device)
+    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
+    lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+    gp = engine.GroupPlan(rows, tlen, device)
+    assert gp.ok and gp.ngroups < B
+    ws_g = engine.Workspace(qb)
+    assert engine.grouped_applicable(qb, lr, gp, ws_g)
+    res_g = engine.solve_lowrank(qb, lr, ws=ws_g, groups=gp)
+    xg, itg, stg = res_g.x.cpu().numpy().copy(), res_g.iters.cpu().numpy().copy(), res_g.status.cpu().numpy().copy()
+    res_d = engine.solve_lowrank(qb, lr)
+    xd, itd = res_d.x.cpu().numpy(), res_d.iters.cpu().numpy()
+    assert np.all(stg == 1) and np.all(res_d.status.cpu().numpy() == 1)
+    assert np.abs(itg - itd).max() <= 2, (itg, itd)
+    assert np.abs(xg - xd).max() < 1e-8
+    assert np.abs(xg.sum(1) - 1).max() < 1e-9 and xg.min() > -1e-9 and xg.max() < 0.2 + 1e-9
+    for i in (0, B - 1):
+        e = ends[i]
+        P = 2 * cov_pearson(R[e - T + 1:e + 1])
+        o = solve_qp(P, np.zeros(n), G=G, h=h, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n),
+                     ub=np.full(n, 0.2))
+        assert abs(0.5 * xg[i] @ P @ xg[i] - o.obj) <= 1e-6 * abs(o.obj)

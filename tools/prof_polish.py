@@ -19,7 +19,8 @@ PHASES = ["setup+classify", "free list", "rF/dA", "cholesky", "U+S", "refine", "
 
 
 def main():
-    n, T, D = 1000, 252, int(sys.argv[1]) if len(sys.argv) > 1 else 4749
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    n, T, D = 1000, 252, int(args[0]) if args else 4749
     dates, R, _, _ = factor_panel(T - 1 + D, n)
     rows, tlen = engine.window_rows(dates, dates[T - 1:T - 1 + D], T)
     pan = engine.Panel(R)
@@ -33,15 +34,22 @@ def main():
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=qb.P.device)
     lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
     ws = engine.Workspace(qb)
+    gp = engine.GroupPlan(rows, tlen, qb.P.device) if "--group" in sys.argv else None
     off = (4 + ws.mg_pad) * qb.ld
     for _ in range(2):
         ev = []
         ws.work[:, off + 16:off + 24].zero_()
-        res = engine.solve_lowrank(qb, lr, engine.Settings(), ws, events=ev)
+        res = engine.solve_lowrank(qb, lr, engine.Settings(), ws, events=ev, groups=gp)
         torch.cuda.synchronize()
     ad = ws.work[:, off + 16:off + 24].cpu().numpy() * 10e-3
     its = res.iters.cpu().numpy().astype(float)
     atot = ad.sum(1)
+    if gp is not None:
+        names = ["pass 1 (MFMA)", "M^-1 symv", "pass 2 (MFMA)", "updates/resid/rhs"]
+        print("grouped admm, chip-wide ms per phase (sum over groups / 256 CUs):")
+        for i, p in enumerate(names):
+            print("  %-18s %8.2f ms" % (p, ad[:, i].sum() / 256 / 1e3))
+        print("  groups %d, mean size %.1f" % (gp.ngroups, gp.sizes.mean()))
     print("admm us per problem: mean %.1f  (%.2f us per iteration)" % (atot.mean(), (atot / its).mean()))
     for i, p in enumerate(["rhs", "v, mu.v", "w = U v", "M^-1 symv", "U'u + tree + corr", "updates+resid"]):
         print("  %-18s %8.2f us/iter (%4.1f %%)" % (p, (ad[:, i] / its).mean(), 100 * ad[:, i].mean() / atot.mean()))
