@@ -157,9 +157,27 @@ def main():
     from porqua_amd import _lib
     nfree = out_rec[:, _lib.PQ_OUT_NFREE]
     prounds = out_rec[:, _lib.PQ_OUT_ROUNDS]
-    k_lr = T + 1
-    it_bytes = (8.0 * (2 * T * n + k_lr * (k_lr + 1) / 2)) if use_lr else 8.0 * n * (n + 1) / 2
-    admm_bytes = it_bytes * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
+    # ---- roofline of the ADMM kernel: algorithmic bytes per date-iteration ---------------
+    k_lr = T + qb.mg
+    grouped = use_lr and engine.grouped_applicable(qb, lr, gplan, ws)
+    l2_bytes = None
+    if grouped:
+        # HBM level: the date's lower-triangle M^-1 (the only per-date O(k^2) stream; 4749 x
+        # 512 KB is far beyond the caches) + the ADMM state read and written (x, z, y, Px);
+        # the window passes read the group's union rows, which sit in the XCD's L2
+        kern = "k_admm_grp"
+        it_bytes = 8.0 * k_lr * (k_lr + 1) / 2 + 8.0 * 8 * n
+        u_mean = float(gplan.ucnt.double().mean().item())
+        l2_bytes = 2 * 8.0 * u_mean * n / float(gplan.sizes.mean())
+        admm_bytes = it_bytes * total_iters
+    elif use_lr:
+        kern = "k_admm"
+        it_bytes = 8.0 * (2 * T * n + k_lr * (k_lr + 1) / 2)
+        admm_bytes = it_bytes * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
+    else:
+        kern = "k_admm"
+        it_bytes = 8.0 * n * (n + 1) / 2
+        admm_bytes = it_bytes * total_iters + 8.0 * 8 * n * D * cnt.get("admm", 1)
     admm_gbs = admm_bytes / tk["admm"] / 1e9
     ld = qb.ld
     nb = ld // 64
@@ -179,7 +197,7 @@ def main():
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
         try:
             pm = json.load(open(f))
-            k = pm["kernels"]["k_admm"]
+            k = pm["kernels"][kern]
             if int(round(k["algorithmic_bytes_per_admm_iteration"])) == int(it_bytes):
                 traffic, traffic_src = k["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
         except Exception:
@@ -202,14 +220,23 @@ def main():
         "config": {"workload": "config3: long-only min-variance (P=2*Pearson cov, budget + box [0,1]), "
                                "daily rebalance", "n_assets": n, "window": T,
                    "dates_per_gpu": D, "global_batch": D * world, "parallelism": f"dates-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_admm (K3)", "achieved": admm_gbs,
+        "roofline": {"bound": "hbm", "kernel": kern + (" (K3, grouped low-rank)" if grouped else " (K3)"),
+                     "achieved": admm_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": admm_gbs / HBM_PEAK_GBS,
                      "traffic": traffic,
-                     "traffic_unit": "HBM bytes per ADMM iteration (PMC: 2*FETCH_SIZE + WRITE_SIZE, "
+                     "traffic_unit": "HBM bytes per date-iteration (PMC: 2*FETCH_SIZE + WRITE_SIZE, "
                                      "gfx950 correction; committed rocprofv3 pass)",
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_iteration": int(it_bytes),
-                     "path": "lowrank (Woodbury: window rows + M^-1)" if use_lr else "dense K^-1 (lower)",
+                     "algorithmic_bytes_note": ("per date-iteration: lower-triangle M^-1 8k(k+1)/2 (k = T + mg) "
+                                                "+ ADMM state 8 x 8n" if grouped else
+                                                "per date-iteration: window rows 2 x 8Tn + M^-1 8k(k+1)/2"
+                                                if use_lr else "per date-iteration: lower-triangle K^-1 8n(n+1)/2"),
+                     "l2_window_bytes_per_iteration": None if l2_bytes is None else int(l2_bytes),
+                     "l2_window_gbs": None if l2_bytes is None else l2_bytes * total_iters / tk["admm"] / 1e9,
+                     "path": ("lowrank grouped (Woodbury; MFMA passes over the union of sliding windows)"
+                              if grouped else "lowrank (Woodbury: window rows + M^-1)" if use_lr
+                              else "dense K^-1 (lower)"),
                      "admm_iterations_per_step": total_iters // args.steps},
         "stages_s_per_step": {k: v / args.steps for k, v in tk.items()},
         "stage_rates": {

@@ -53,16 +53,18 @@ def main():
             e["trace_avg_ns"] = float(stats[k]["AverageNs"])
             e["trace_calls"] = int(stats[k]["Calls"])
         out["kernels"][k] = e
-    adm = out["kernels"].get("k_admm")
+    kern = bench_pmc["roofline"]["kernel"].split()[0]
+    adm = out["kernels"].get(kern)
     if adm:
         adm["hbm_bytes_per_admm_iteration"] = adm["hbm_bytes_per_step"] / iters
         adm["algorithmic_bytes_per_admm_iteration"] = float(bench_pmc["roofline"]["algorithmic_bytes_per_iteration"])
+    out["admm_kernel"] = kern
     with open(os.path.join(dst, f"{rnd}_pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     full = os.path.join(src, "bench_full.log")
     if os.path.exists(full):
         shutil.copy(full, os.path.join(dst, f"{rnd}_bench.log"))
-    print(json.dumps(out["kernels"].get("k_admm"), indent=1))
+    print(json.dumps(out["kernels"].get(kern), indent=1))
 
 
 if __name__ == "__main__":
