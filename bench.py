@@ -106,7 +106,7 @@ def main():
         mu = pan.window_means(rows_d, tlen_d, out=mu_lr)
         if events is not None:
             e0 = torch.cuda.Event(enable_timing=True); e0.record()
-        pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu, plan=plan)
+        pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu, plan=plan, lower_only=use_lr)
         if events is not None:
             e1 = torch.cuda.Event(enable_timing=True); e1.record()
             events.append(("cov", e0, e1))

@@ -120,12 +120,14 @@ int pq_cov_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* r
  * every later date d must hold the window of date d-1 shifted by shift[d] >= 1 rows
  * (rows[d][0..T-s) == rows[d-1][s..T), equal tlen), which is applied as a rank-2s MFMA
  * update: 2 s n^2 instead of 2 T n^2 flops per date.  The host builds the plan
- * (porqua_amd.engine.slide_plan).                                                      */
+ * (porqua_amd.engine.slide_plan).  lower_only != 0 writes the lower 64x64 tiles and the
+ * full diagonal tiles only (LAPACK uplo = 'L' storage: half the bytes), which is all the
+ * low-rank path reads.                                                                  */
 int pq_cov_slide_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
                          const int32_t* tlen, int32_t tmax, int32_t batch, int32_t mode,
                          const double* mu, int64_t mu_stride, double* out, int32_t ld,
                          int64_t out_stride, const int32_t* gstart, int32_t ngroups,
-                         const int32_t* shift, void* stream);
+                         const int32_t* shift, int32_t lower_only, void* stream);
 
 /* X'y and y'y of each window (LeastSquares q = -2 X'y, constant = y'y,
  * src/optimization.py:216-217).                                                        */

@@ -93,7 +93,7 @@ _EXPORTS = {
     "pq_cov_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_int32, c_dp, c_int64,
                         c_dp, c_int32, c_int64, c_dp], c_int32),
     "pq_cov_slide_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_int32, c_dp, c_int64,
-                              c_dp, c_int32, c_int64, c_dp, c_int32, c_dp, c_dp], c_int32),
+                              c_dp, c_int32, c_int64, c_dp, c_int32, c_dp, c_int32, c_dp], c_int32),
     "pq_gram_xy_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64,
                             c_dp, c_dp], c_int32),
     "pq_init_state": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,

@@ -158,7 +158,8 @@ __global__ __launch_bounds__(256) void k_syrk_slide(const double* panel, int64_t
                                                     const int32_t* rows, const int32_t* tlen, int tmax,
                                                     int mode, const double* mu, int64_t mu_stride,
                                                     double* out, int ld, int64_t out_stride,
-                                                    const int32_t* gstart, const int32_t* shift) {
+                                                    const int32_t* gstart, const int32_t* shift,
+                                                    int mirror) {
   __shared__ __attribute__((aligned(16))) double smem[4 * STAGE + TB * SP];
   double* tile = smem + 4 * STAGE;
   int I, J;
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(256) void k_syrk_slide(const double* panel, int64_t
       const int r = idx >> 5, c2 = (idx & 31) * 2;
       reinterpret_cast<double2*>(o + (int64_t)(I * TB + r) * ld + J * TB)[c2 >> 1] =
           double2{tile[r * SP + c2], tile[r * SP + c2 + 1]};
-      if (I != J)
+      if (I != J && mirror)
         reinterpret_cast<double2*>(o + (int64_t)(J * TB + r) * ld + I * TB)[c2 >> 1] =
             double2{tile[c2 * SP + r], tile[(c2 + 1) * SP + r]};
     }
@@ -326,7 +327,7 @@ extern "C" int pq_cov_slide_batched(const double* panel, int64_t ldp, int32_t n,
                                     const int32_t* tlen, int32_t tmax, int32_t batch, int32_t mode,
                                     const double* mu, int64_t mu_stride, double* out, int32_t ld,
                                     int64_t out_stride, const int32_t* gstart, int32_t ngroups,
-                                    const int32_t* shift, void* stream) {
+                                    const int32_t* shift, int32_t lower_only, void* stream) {
   if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
   PQ_CHECK_ARG(mode == 0 || mode == 1, "pq_cov_slide_batched: mode must be 0 (centred cov) or 1 (Gram)");
   PQ_CHECK_ARG(mode == 1 || mu != nullptr, "pq_cov_slide_batched: mode 0 needs the window means");
@@ -336,7 +337,7 @@ extern "C" int pq_cov_slide_batched(const double* panel, int64_t ldp, int32_t n,
   const int nb = ld / 64;
   hipLaunchKernelGGL(pq::k_syrk_slide, dim3(nb * (nb + 1) / 2, ngroups), dim3(256), 0,
                      (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mode, mu, mu_stride,
-                     out, ld, out_stride, gstart, shift);
+                     out, ld, out_stride, gstart, shift, lower_only ? 0 : 1);
   PQ_CHECK_LAUNCH("pq_cov_slide_batched");
   return 0;
 }

@@ -407,7 +407,11 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     PQ_STAMP(1);
     __builtin_amdgcn_s_dcache_inv();
     // ---- reduced rhs: rF = -q_F - ps P_FB x_B ;  d_a = rhs_a - C_aB x_B -----------------
-    if (nzb) {   // (long-only: every fixed weight is 0 and P_FB x_B vanishes)
+    if (nzb && lr.panel) {   // window form (P may hold its lower triangle only): P x_B -> g
+      lr_px(lr, b, n, xb, vec, stg, red, [&](int i, double sum) { g[i] = sum; });
+      __syncthreads();
+      for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]] - ps * g[Fl[p]];
+    } else if (nzb) {   // (long-only: every fixed weight is 0 and P_FB x_B vanishes)
       rows_dot_vec(P, ld, n, k, [&](int p) { return Fl[p]; }, xb,
                    [&](int p, double sum) { rF[p] = -q[Fl[p]] - ps * sum; });
     } else {
@@ -460,9 +464,12 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     for (int itr = 0; itr < s.refine_iters; ++itr) {
       // rx = rF - (ps P_FF + pd I) solx - C_aF' solL ;  rl = dA - C_aF solx
       for (int p = w; p < k; p += PW) {
-        const double* row = P + (int64_t)Fl[p] * ld;
+        const int fi = Fl[p];
         double sum = 0.0;
-        for (int qq = l; qq < k; qq += 64) sum += row[Fl[qq]] * solx[qq];
+        for (int qq = l; qq < k; qq += 64) {   // lower triangle only: P[max][min]
+          const int fj = Fl[qq];
+          sum += P[(int64_t)max(fi, fj) * ld + min(fi, fj)] * solx[qq];
+        }
         sum = wave_sum(sum);
         if (l == 0) {
           double v = rF[p] - ps * sum - pd * solx[p];

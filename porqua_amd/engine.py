@@ -615,9 +615,11 @@ class Panel:
                       mu.stride(0), _stream()), "window means")
         return mu
 
-    def cov(self, rows, tlen, mode=0, out=None, mu=None, plan: SlidePlan | None = None):
+    def cov(self, rows, tlen, mode=0, out=None, mu=None, plan: SlidePlan | None = None,
+            lower_only: bool = False):
         """K1: per-date centred covariance (mode 0, ddof=1) or Gram X'X (mode 1) -> (B, ld, ld).
-        With a SlidePlan, overlapping windows are built by rank-2s updates (same result)."""
+        With a SlidePlan, overlapping windows are built by rank-2s updates (same result);
+        ``lower_only`` (SlidePlan only) leaves the strictly-upper off-diagonal tiles unwritten."""
         lib = _lib.load()
         B, tmax = rows.shape
         ld = round_up(self.n, 64)
@@ -630,7 +632,8 @@ class Panel:
         if plan is not None:
             _lib.check(lib.pq_cov_slide_batched(_ptr(self.R), self.R.stride(0), self.n, _ptr(rows), _ptr(tlen),
                                                 tmax, B, mode, mp, ms, _ptr(out), ld, out.stride(0),
-                                                _ptr(plan.gstart), plan.ngroups, _ptr(plan.shift), _stream()),
+                                                _ptr(plan.gstart), plan.ngroups, _ptr(plan.shift),
+                                                1 if lower_only else 0, _stream()),
                        "pq_cov_slide_batched")
             return out
         _lib.check(lib.pq_cov_batched(_ptr(self.R), self.R.stride(0), self.n, _ptr(rows), _ptr(tlen), tmax, B,

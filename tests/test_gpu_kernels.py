@@ -57,6 +57,12 @@ def test_sliding_cov_matches_full_syrk_and_numpy(device, n, T, stride, offset):
         sl = pan.cov(r_d, t_d, mode=mode, plan=plan).cpu().numpy()
         gs = plan.gstart.cpu().numpy()
         assert np.array_equal(full[gs[:-1]], sl[gs[:-1]])          # anchors: same arithmetic
+        lo = torch.full_like(torch.from_numpy(sl), float("nan")).to(device)
+        lo = pan.cov(r_d, t_d, mode=mode, plan=plan, out=lo, lower_only=True).cpu().numpy()
+        ld = lo.shape[-1]
+        tile = np.arange(ld) // 64
+        upper = tile[:, None] < tile[None, :]                          # strictly-upper 64x64 tiles
+        assert np.array_equal(lo[:, ~upper], sl[:, ~upper]) and np.isnan(lo[:, upper]).all()
         for b in range(len(reb)):
             X = R[rows[b, :tlen[b]]]
             ref = cov_pearson(X) if mode == 0 else X.T @ X

@@ -107,7 +107,11 @@ def test_grouped_admm_matches_per_date_lowrank(device, n, T, D, stride, groups_r
     qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
                                    G=G, h=h, lb=np.zeros(n), ub=np.full(n, 0.2), device=device)
     qb.batch = B
-    qb.P = pan.cov(r_d, t_d, mode=0, mu=mu)
+    # the bench layout: sliding K1 writing the lower triangle only (upper tiles stay NaN --
+    # nothing on the low-rank path may read them)
+    Pbuf = torch.full((B, qb.ld, qb.ld), float("nan"), dtype=torch.float64, device=device)
+    qb.P = pan.cov(r_d, t_d, mode=0, mu=mu, out=Pbuf, plan=engine.SlidePlan(rows, tlen, device),
+                   lower_only=True)
     qb.q = torch.zeros((B, qb.ld), dtype=torch.float64, device=device)
     qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
     lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
