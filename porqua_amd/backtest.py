@@ -147,6 +147,26 @@ class BatchStage:
         self.ld = ((panel.n + 63) // 64) * 64
         self._P = None
         self._log_panel = None
+        self._slide = None
+        self._groups = None
+        # set by Backtest before objective_batch: the objective may hand back the factored
+        # (window) form of P in .lowrank, and then stores P's lower triangle only
+        self.prefer_lowrank = False
+        self.lowrank = None
+
+    def slide_plan(self):
+        """SlidePlan of the windows (sliding K1), None when no window slides."""
+        from . import engine
+        if self._slide is None:
+            plan = engine.SlidePlan(self.rows_host, self.tlen_host, self.device)
+            self._slide = plan if plan.ngroups < self.batch else False
+        return self._slide or None
+
+    def group_plan(self):
+        from . import engine
+        if self._groups is None:
+            self._groups = engine.GroupPlan(self.rows_host, self.tlen_host, self.device)
+        return self._groups
 
     def P_buffer(self):
         import torch
@@ -301,9 +321,14 @@ class Backtest:
         W = np.zeros((hi - lo, n))
         ST = np.zeros(hi - lo, dtype=np.int32)
         OBJ = np.zeros(hi - lo)
+        mg = sum(0 if GhAb[k] is None else np.atleast_2d(GhAb[k]).shape[0] for k in ("A", "G"))
         for s in range(lo, hi, chunk):
             e = min(hi, s + chunk)
             stage = BatchStage(panel, rows[s:e], tlen[s:e], dev)
+            # T + mg < n: the Woodbury (window-form) solver; its consumers read P's lower
+            # triangle only (engine.lowrank_shape_ok: same test as solve_lowrank's)
+            stage.prefer_lowrank = (bs.settings.get("lowrank", True)
+                                    and engine.lowrank_shape_ok(n, int(stage.rows_host.shape[1]), mg))
             obj = opt.objective_batch(stage)
             if obj is None:
                 return False
@@ -317,7 +342,10 @@ class Backtest:
             qq = torch.zeros((e - s, qb.ld), dtype=torch.float64, device=dev)
             qq[:, :n] = q[:, :n]
             qb.q = qq
-            res = engine.solve(qb, settings)
+            if stage.lowrank is not None:
+                res = engine.solve_lowrank(qb, stage.lowrank, settings, groups=stage.group_plan())
+            else:
+                res = engine.solve(qb, settings)
             W[s - lo:e - lo] = res.x.cpu().numpy()
             ST[s - lo:e - lo] = res.status.cpu().numpy()
             OBJ[s - lo:e - lo] = res.obj.cpu().numpy()
@@ -326,7 +354,8 @@ class Backtest:
         # ---- phase C: portfolios -----------------------------------------------------------
         from . import _lib
         solved = (ST == _lib.PQ_SOLVED) | (ST == _lib.PQ_SOLVED_INACCURATE)
-        self.stats = {"dates": len(rebdates), "solved": int(solved.sum()), "status": ST, "objective": OBJ}
+        self.stats = {"dates": len(rebdates), "solved": int(solved.sum()), "status": ST, "objective": OBJ,
+                      "path": "lowrank" if stage.lowrank is not None else "dense"}
         if not bs.settings.get("quiet"):
             print(f"Rebalanced {len(rebdates)} dates on the device ({int(solved.sum())} solved)")
         for i, d in enumerate(rebdates):

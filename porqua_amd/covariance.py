@@ -58,17 +58,25 @@ class Covariance:
         return covmat
 
     # -- batched (backtest) entry --------------------------------------------------------
-    def estimate_batch(self, panel, rows, tlen, out=None):
+    def estimate_batch(self, panel, rows, tlen, out=None, plan=None, lower_only=False):
         """All dates at once on the device.  Returns (S, p_diag): S is the (B, ld, ld)
         device tensor of raw sample covariances; p_diag (B,) is the diagonal term the spec
         adds (linear shrinkage: lam * mean(diag S)); 'duv' returns (None, None)."""
+        S, pdiag, _ = self.estimate_batch_lr(panel, rows, tlen, out=out, plan=plan, lower_only=lower_only)
+        return S, pdiag
+
+    def estimate_batch_lr(self, panel, rows, tlen, out=None, plan=None, lower_only=False):
+        """estimate_batch plus the window means (the centring of the factored form
+        S = Xc'Xc / (T-1) that the low-rank solver uses).  ``plan``: an engine.SlidePlan for
+        overlapping windows; ``lower_only``: lower-triangle storage (low-rank consumers)."""
         import torch
         method = self.spec["method"]
         if method == "duv":
-            return None, None
+            return None, None, None
         if method not in ("pearson", "linear_shrinkage"):
             raise NotImplementedError("This method is not implemented yet")
-        S = panel.cov(rows, tlen, mode=0, out=out)
+        mu = panel.window_means(rows, tlen)
+        S = panel.cov(rows, tlen, mode=0, out=out, mu=mu, plan=plan, lower_only=lower_only and plan is not None)
         B = S.shape[0]
         pdiag = torch.zeros(B, dtype=torch.float64, device=S.device)
         if method == "linear_shrinkage":
@@ -76,7 +84,7 @@ class Covariance:
             if lam > 0:
                 n = panel.n
                 pdiag = lam * torch.diagonal(S, dim1=1, dim2=2)[:, :n].mean(dim=1)
-        return S, pdiag
+        return S, pdiag, mu
 
 
 def _device_cov(X, mode=0):

@@ -356,9 +356,16 @@ class LowRank:
                               w_scale=None if self.w_scale is None else self.w_scale.data_ptr())
 
 
+def lowrank_shape_ok(n: int, tmax: int, mg: int) -> bool:
+    """The Woodbury path applies (and pays): T + mg < n, k <= 512, and the window-form polish
+    can run (even panel stride n, tmax <= 1024) so nothing needs the dense upper triangle."""
+    k_ld = round_up(tmax + mg, 64)
+    return (k_ld <= 512 and (k_ld + 127) // 128 <= (n + 127) // 128 and tmax + mg < n
+            and n % 2 == 0 and tmax <= 1024 and mg <= 64)
+
+
 def lowrank_applicable(qb: QPBatch, lr: LowRank) -> bool:
-    k_ld = round_up(lr.tmax + qb.mg, 64)
-    return k_ld <= 512 and (k_ld + 127) // 128 <= (qb.n + 127) // 128 and lr.tmax + qb.mg < qb.n
+    return lowrank_shape_ok(qb.n, lr.tmax, qb.mg) and lr.panel.R.stride(0) % 2 == 0
 
 
 def grouped_applicable(qb: QPBatch, lr: LowRank, groups: "GroupPlan | None", ws: "Workspace") -> bool:

@@ -143,13 +143,20 @@ class MeanVariance(Optimization):
 
     def objective_batch(self, stage):
         import torch
-        S, pdiag = self.covariance.estimate_batch(stage.panel, stage.rows, stage.tlen, out=stage.P_buffer())
+        from . import engine
+        lowrank = stage.prefer_lowrank and self.covariance.spec["method"] != "duv"
+        S, pdiag, mu_c = self.covariance.estimate_batch_lr(
+            stage.panel, stage.rows, stage.tlen, out=stage.P_buffer(), plan=stage.slide_plan(),
+            lower_only=lowrank)
         ra = float(self.params["risk_aversion"])
         B = stage.batch
         dev = stage.device
         if S is None:  # duv: identity covariance
             S = stage.identity_P()
             pdiag = torch.zeros(B, dtype=torch.float64, device=dev)
+        elif lowrank:   # factored form S = Xc'Xc / (T - 1) for the Woodbury solver
+            stage.lowrank = engine.LowRank(stage.panel, stage.rows, stage.tlen, mu=mu_c,
+                                           w_scale=1.0 / (stage.tlen.to(torch.float64) - 1.0))
         me = self.mean_estimator
         if me.spec.get("method") != "geometric":
             return None
@@ -215,11 +222,15 @@ class LeastSquares(Optimization):
         import torch
         if stage.panel.bm is None:
             return None
+        from . import engine
         if self.params.get("log_transform"):
             pan = stage.log1p_panel()
         else:
             pan = stage.panel
-        G = pan.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer())
+        G = pan.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer(), plan=stage.slide_plan(),
+                    lower_only=stage.prefer_lowrank)
+        if stage.prefer_lowrank:   # factored form X'X (uncentred) for the Woodbury solver
+            stage.lowrank = engine.LowRank(pan, stage.rows, stage.tlen, mu=None)
         xty, yty = pan.gram_xy(stage.rows, stage.tlen)
         B, dev = stage.batch, stage.device
         l2 = self.params.get("l2_penalty")

@@ -80,13 +80,13 @@ def test_geometric_mean(device):
         assert np.allclose(mu, ref, rtol=1e-12, atol=1e-15)
 
 
-def _service(opt, X, y, rebdates, box_kw):
+def _service(opt, X, y, rebdates, box_kw, width=252):
     return BacktestService(
         data={"return_series": X, "bm_series": y},
         selection_item_builders={"data": SelectionItemBuilder(bibfn=bibfn_selection_data)},
         optimization_item_builders={
-            "return_series": OptimizationItemBuilder(bibfn=bibfn_return_series, width=252),
-            "bm_series": OptimizationItemBuilder(bibfn=bibfn_bm_series, width=252),
+            "return_series": OptimizationItemBuilder(bibfn=bibfn_return_series, width=width),
+            "bm_series": OptimizationItemBuilder(bibfn=bibfn_bm_series, width=width),
             "budget_constraint": OptimizationItemBuilder(bibfn=bibfn_budget_constraint, budget=1),
             "box_constraints": OptimizationItemBuilder(bibfn=bibfn_box_constraints, **box_kw)},
         optimization=opt, rebdates=rebdates, quiet=True)
@@ -138,3 +138,48 @@ def test_qeqw_backtest(device):
     bt.run(_service(QEQW(solver_name="mi355x"), X, y, rebdates, {}))
     W = bt.strategy.get_weights_df().to_numpy(dtype=float)
     assert np.allclose(W, 1.0 / 24, atol=1e-9)
+
+
+def _synthetic(n, D, seed):
+    from porqua_amd.synthetic import factor_panel
+    dates, R, y, _ = factor_panel(D, n, seed=seed)
+    idx = pd.DatetimeIndex(dates)
+    return (pd.DataFrame(R, index=idx, columns=[f"a{i}" for i in range(n)]),
+            pd.DataFrame({"bm": y}, index=idx))
+
+
+@pytest.mark.parametrize("kind", ["mv", "mv_shrink", "ls"])
+def test_backtest_lowrank_path_matches_oracle(device, kind):
+    """Backtest.run with n > width: sliding K1 (lower triangle), Woodbury factor, grouped
+    ADMM and window-form polish; weights checked against the oracle IPM per date."""
+    from oracle.qp_ipm import solve_qp
+    n, D, width = 300, 160, 60
+    X, y = _synthetic(n, D, seed=11)
+    rebdates = [str(d.date()) for d in X.index[width + 5:width + 5 + 24]]
+    make = {"mv": lambda: MeanVariance(solver_name="mi355x"),
+            "mv_shrink": lambda: MeanVariance(covariance=Covariance(method="linear_shrinkage",
+                                                                    lambda_covmat_regularization=0.1),
+                                              solver_name="mi355x", risk_aversion=2.0),
+            "ls": lambda: LeastSquares(solver_name="mi355x")}[kind]
+    bt = Backtest()
+    bt.run(_service(make(), X, y, rebdates, {"upper": 0.1}, width=width))
+    assert bt.stats["solved"] == len(rebdates) and bt.stats["path"] == "lowrank"
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    Xv, yv = X.to_numpy(), y.to_numpy()[:, 0]
+    for i in (0, 11, len(rebdates) - 1):
+        e = X.index.get_loc(pd.Timestamp(rebdates[i]))
+        Xw, yw = Xv[e - width + 1:e + 1], yv[e - width + 1:e + 1]
+        if kind == "ls":
+            P, q = 2 * Xw.T @ Xw, -2 * Xw.T @ yw
+        else:
+            S = rp.cov_pearson(Xw)
+            ra = 2.0 if kind == "mv_shrink" else 1.0
+            if kind == "mv_shrink":
+                S = S + 0.1 * np.mean(np.diag(S)) * np.eye(n)
+            P, q = 2 * ra * S, -rp.mean_geometric(Xw, None, None, None)
+        o = solve_qp(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.full(n, 0.1))
+        obj = 0.5 * W[i] @ P @ W[i] + q @ W[i]
+        assert abs(obj - o.obj) <= 1e-6 * max(abs(o.obj), 1e-12), (kind, i, obj, o.obj)
+        if kind != "ls":   # LS: rank(X'X) <= width < n, the optimum is a face (compare value)
+            assert np.abs(W[i] - o.x).max() < 1e-5, (kind, i, np.abs(W[i] - o.x).max())
+        assert abs(W[i].sum() - 1) < 1e-7 and W[i].min() > -1e-7 and W[i].max() < 0.1 + 1e-7
