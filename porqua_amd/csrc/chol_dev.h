@@ -11,7 +11,51 @@ constexpr int DP = 65;  // pitch of the row-major diagonal work tile
 // 1-based local column of the first non-positive pivot, 0 on success (uniform).  Rows and
 // columns >= nvalid must already hold the identity (the zero-padded tail of a matrix whose
 // padding is the identity): their pivot steps are skipped.
+//
+// One wave does the whole tile with lane i holding row i in registers (fully unrolled, so
+// every register index is static); the pivot column of each step is exchanged through the
+// tile's padding column T[j][64] (LDS broadcast reads: a wave's LDS operations complete in
+// order, so no barrier is needed inside the wave).  All threads must call.
 __device__ int tile_potrf(double* T, int nvalid) {
+  const int kend = nvalid < TB ? (nvalid > 0 ? nvalid : 0) : TB;
+  __syncthreads();   // the tile was written by every wave
+  if (wave_id() == 0) {
+    const int i = lane_id();
+    double r[TB];
+#pragma unroll
+    for (int j = 0; j < TB; ++j) r[j] = T[i * DP + j];
+    int bad = 0;
+#pragma unroll
+    for (int k = 0; k < TB; ++k) {
+      if (k < kend && !bad) {
+        T[i * DP + TB] = r[k];
+        const double d = T[k * DP + TB];
+        if (!(d > 0.0) || !isfinite(d)) {
+          bad = k + 1;
+        } else {
+          const double s = sqrt(d);
+          const double lik = (i > k) ? r[k] / s : (i == k ? s : 0.0);
+          r[k] = lik;
+          T[i * DP + TB] = lik;
+#pragma unroll
+          for (int j = k + 1; j < TB; ++j) r[j] = fma(-lik, T[j * DP + TB], r[j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TB; ++j)
+      if (j <= i) T[i * DP + j] = r[j];
+    if (i == 0) T[TB] = (double)bad;   // padding slot of row 0 carries the result
+  }
+  __syncthreads();
+  const int bad = (int)T[TB];
+  __syncthreads();
+  return bad;
+}
+
+// The same factorisation with the whole workgroup and LDS only (few registers): for the
+// small Schur-complement tile of the polish, whose valid size is the number of active rows.
+__device__ int tile_potrf_lds(double* T, int nvalid) {
   const int t = threadIdx.x;
   const int kend = nvalid < TB ? (nvalid > 0 ? nvalid : 0) : TB;
   for (int k = 0; k < kend; ++k) {
@@ -36,18 +80,25 @@ __device__ int tile_potrf(double* T, int nvalid) {
 }
 
 // Inverse of the lower-triangular tile T (pitch DP) into X (row c = column c of T^-1,
-// pitch DP).  Thread c < 64 owns column c.  Rows / columns >= nvalid are the identity.
+// pitch DP).  One wave: lane c builds column c in registers by forward substitution over
+// the broadcast rows of T.  Rows / columns >= nvalid are the identity.  All threads call.
 __device__ void tile_trinv(const double* T, double* X, int nvalid) {
-  const int c = threadIdx.x;
-  if (c < TB) {
-    for (int r = 0; r < c; ++r) X[c * DP + r] = 0.0;
-    X[c * DP + c] = 1.0 / T[c * DP + c];
-    for (int r = c + 1; r < TB; ++r) {
+  __syncthreads();
+  if (wave_id() == 0) {
+    const int c = lane_id();
+    double x[TB];
+#pragma unroll
+    for (int r = 0; r < TB; ++r) {
       double acc = 0.0;
-      if (r < nvalid)
-        for (int k = c; k < r; ++k) acc += T[r * DP + k] * X[c * DP + k];
-      X[c * DP + r] = -acc / T[r * DP + r];
+      if (r < nvalid) {
+#pragma unroll
+        for (int k = 0; k < r; ++k) acc = fma(T[r * DP + k], x[k], acc);
+      }
+      const double dg = T[r * DP + r];
+      x[r] = (r < c) ? 0.0 : (r == c ? 1.0 / dg : -acc / dg);
     }
+#pragma unroll
+    for (int r = 0; r < TB; ++r) X[c * DP + r] = x[r];
   }
   __syncthreads();
 }

@@ -458,7 +458,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
       stg[i * DP + j] = v;
     }
     __syncthreads();
-    if (tile_potrf(stg, ma)) break;
+    if (tile_potrf_lds(stg, ma)) break;
     PQ_STAMP(4);
     // ---- proximal iterative refinement -------------------------------------------------
     for (int itr = 0; itr < s.refine_iters; ++itr) {
