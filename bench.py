@@ -55,6 +55,9 @@ def parse():
                     help="low-rank ADMM one workgroup per date instead of per group of sliding windows")
     ap.add_argument("--no-slide", action="store_true",
                     help="K1 as one full T-deep SYRK per date instead of anchor SYRK + rank-2 slides")
+    ap.add_argument("--with-cov", action="store_true",
+                    help="low-rank path: also materialise every date's n x n covariance with K1 "
+                         "(nothing on that path reads it)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="override an engine.Settings field (experiments)")
@@ -88,28 +91,34 @@ def main():
     gplan = None if args.no_group else engine.GroupPlan(rows, tlen, dev)
     qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)),
                                    b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), device=dev)
-    # re-shape the batch to D problems sharing constraints; P is written by K1 every step
+    # re-shape the batch to D problems sharing constraints
     ld = qb.ld
     qb.batch = D
-    qb.P = torch.empty((D, ld, ld), dtype=torch.float64, device=dev)
+    qb.P = None
     qb.q = torch.zeros((D, ld), dtype=torch.float64, device=dev)
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)   # P = 2 * Sigma
-    ws = engine.Workspace(qb)
     settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))
     mu_lr = pan.window_means(rows_d, tlen_d)
     lr = engine.LowRank(pan, rows_d, tlen_d, mu=mu_lr, w_scale=1.0 / (tlen_d.to(torch.float64) - 1.0))
     use_lr = args.path == "lowrank" or (args.path == "auto" and engine.lowrank_applicable(qb, lr))
+    with_cov = (not use_lr) or args.with_cov
+    if with_cov:   # K1 writes Sigma every step (dense path: P = 2 Sigma is what K2 factors)
+        qb.P = torch.empty((D, ld, ld), dtype=torch.float64, device=dev)
+    ws = engine.Workspace(qb, dense=not use_lr)
     w_host = torch.empty((D * world, n), dtype=torch.float64).pin_memory() if rank == 0 else None
     gather_buf = torch.empty((world, D, n), dtype=torch.float64, device=dev) if world > 1 else None
 
     def step(events=None):
-        mu = pan.window_means(rows_d, tlen_d, out=mu_lr)
         if events is not None:
             e0 = torch.cuda.Event(enable_timing=True); e0.record()
-        pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu, plan=plan, lower_only=use_lr)
+        mu = pan.window_means(rows_d, tlen_d, out=mu_lr)
+        if use_lr:
+            lr.refresh()   # diag(Xc'Xc) of the windows: the only O(n) per-date moment besides mu
+        if with_cov:
+            pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu, plan=plan, lower_only=use_lr)
         if events is not None:
             e1 = torch.cuda.Event(enable_timing=True); e1.record()
-            events.append(("cov", e0, e1))
+            events.append(("moments+cov" if with_cov else "moments", e0, e1))
         if use_lr:
             res = engine.solve_lowrank(qb, lr, settings, ws, events=events, groups=gplan)
         else:
@@ -186,7 +195,8 @@ def main():
         syrk_flops = D * tiles * 64 * 64 * 2.0 * T * args.steps
     else:   # anchors: full T-deep SYRK; slid dates: one 4-deep (2 s padded) MFMA update
         syrk_flops = (plan.ngroups * T + (D - plan.ngroups) * 4) * tiles * 64 * 64 * 2.0 * args.steps
-    cov_write_gbs = D * ld * ld * 8.0 * args.steps / tk.get("cov", float("nan")) / 1e9
+    cov_t = tk.get("moments+cov") if with_cov else None
+    cov_write_gbs = D * ld * ld * 8.0 * args.steps / cov_t / 1e9 if cov_t else None
     kld = ((T + 1 + 63) // 64) * 64
     factor_flops_per = (2.0 * kld * kld * n + kld ** 3) if use_lr else ld ** 3  # (capacitance SYRK +) potrf+trtri+lauum
     n_factor = D * args.steps + res.refactors * args.steps
@@ -240,9 +250,11 @@ def main():
                      "admm_iterations_per_step": total_iters // args.steps},
         "stages_s_per_step": {k: v / args.steps for k, v in tk.items()},
         "stage_rates": {
-            "cov_syrk_tflops": syrk_flops / tk.get("cov", float("nan")) / 1e12,
+            "cov_syrk_tflops": syrk_flops / cov_t / 1e12 if cov_t else None,
             "cov_write_gbs": cov_write_gbs,
-            "cov_mode": "full SYRK per date" if plan is None else
+            "cov_mode": ("not materialised: P = 2 Xc'Xc/(T-1) stays in window form; moments = "
+                         "window means + diag(Xc'Xc)") if not with_cov else
+                        "full SYRK per date" if plan is None else
                         f"sliding: {plan.ngroups} anchor SYRKs + rank-2 updates",
             "factor_tflops": factor_flops / tk.get("factor", float("nan")) / 1e12,
             "fp64_peak_tflops": FP64_PEAK_TFLOPS,

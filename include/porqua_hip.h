@@ -44,8 +44,10 @@ extern "C" {
 #define PQ_OUT_ROUNDS 6     /* polish active-set rounds                                 */
 #define PQ_OUT_FIELDS 8
 
-/* polish scratch per problem (doubles) */
-#define PQ_WORK_DOUBLES(ld, mg_pad) ((int64_t)(4 + (mg_pad)) * (ld) + 512)
+/* polish scratch per problem (doubles): xs | xb | g | Px | U (mg_pad rows) | flags (ld
+ * int32) | 512 spare (the PQ_PROFILE phase timers sit at PQ_WORK_PROF)                  */
+#define PQ_WORK_DOUBLES(ld, mg_pad) ((int64_t)(5 + (mg_pad)) * (ld) + 512)
+#define PQ_WORK_PROF(ld, mg_pad) ((int64_t)(5 + (mg_pad)) * (ld))
 
 /* A batch of dense QPs   min 0.5 x'Px + q'x  s.t.  lg <= Cg x <= ug,  lb <= x <= ub
  * (the QuadraticProgram fields P, q, G, h, A, b, lb, ub of src/qp_problems.py:34-38 with
@@ -90,12 +92,15 @@ typedef struct pq_settings {
  * With D = diag(sigma + p_diag + rho_box) and
  * U' = [sqrt(p_scale w_scale) Xc' | sqrt(rho_r) Cg_r'] (n x k, k = tmax + mg) the ADMM
  * system is K = D + U'U, so K^-1 = D^-1 - D^-1 U' M^-1 U D^-1 with the k x k capacitance
- * matrix M = I + U D^-1 U' (Woodbury): no n x n matrix is formed or factored.          */
+ * matrix M = I + U D^-1 U' (Woodbury): no n x n matrix is formed or factored.
+ * dg (stride dg_stride, from pq_window_sumsq) is diag(Xc'Xc) per date: the diagonal of P
+ * that pq_init_state_lr and pq_polish_w_batched need without P itself.                  */
 typedef struct pq_lowrank {
   const double* panel; int64_t ldp;
   const int32_t* rows; const int32_t* tlen; int32_t tmax;
   const double* mu; int64_t mu_stride;
   const double* w_scale;
+  const double* dg; int64_t dg_stride;
 } pq_lowrank;
 
 int pq_version(void);
@@ -106,6 +111,14 @@ const char* pq_last_error(void);
 int pq_window_mean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
                    const int32_t* tlen, int32_t tmax, int32_t batch, double* mu,
                    int64_t mu_stride, void* stream);
+
+/* Column sums of squared deviations sum_t (X_ti - mu_i)^2 of each window (mu == NULL:
+ * sum_t X_ti^2): diag(Xc'Xc), i.e. (T - 1) times the variances of Covariance.estimate
+ * (src/covariance.py:65-66) or the Gram diagonal of LeastSquares (src/optimization.py:215).
+ * Second pass of the two-pass moments over the same (L2-resident) window rows.        */
+int pq_window_sumsq(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                    const int32_t* tlen, int32_t tmax, int32_t batch, const double* mu,
+                    int64_t mu_stride, double* out, int64_t out_stride, void* stream);
 
 /* K1: batched windowed SYRK on FP64 MFMA.  mode 0: centred covariance with ddof=1
  * (Covariance.estimate 'pearson', src/covariance.py:40-56,65-66); mode 1: uncentred Gram
@@ -146,6 +159,11 @@ int pq_window_geomean(const double* panel, int64_t ldp, int32_t n, const int32_t
 int pq_init_state(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
                   const pq_settings* s, void* stream);
 
+/* pq_init_state for the window form: P is not read (pb->P may be NULL); the initial rho
+ * uses mean(diag P_eff) = mean(p_scale w_scale dg + p_diag).                           */
+int pq_init_state_lr(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const int32_t* idx,
+                     int32_t nidx, const pq_settings* s, void* stream);
+
 /* K2: form K = P_eff + sigma I + Cg' R Cg + R_box for the current rho, factor it with a
  * batched blocked Cholesky on FP64 MFMA (info[] = first failing column + 1, the isPD test
  * of src/helper_functions.py:61-67), and if `invert` overwrite K with K^-1 (trtri+lauum):
@@ -180,7 +198,7 @@ int pq_admm_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
  * union rows are urows[g * umax + u] (u < ucnt[g] <= 320) and date b's window is union
  * rows [uoff[b], uoff[b] + tlen[b]).  One workgroup per group runs the dates' iterations
  * in lock step with both window passes as FP64 MFMA GEMMs over the union; results are
- * those of pq_admm_lr_batched up to summation order.  Needs even n and ldp, mg <= 4,
+ * those of pq_admm_lr_batched up to summation order.  Needs even n and ldp, mg <= 32,
  * k_ld <= 384, work_stride >= 3 ld (work holds each date's V / rhs / x~ scratch).      */
 int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const double* Minv,
                        int32_t k_ld, int64_t M_stride, const int32_t* gdates, int32_t ngroups,
@@ -198,6 +216,17 @@ int pq_polish_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, in
  * tmax <= 1024, even ldp).  pb.P (the K1 output) is still read for P_FF.               */
 int pq_polish_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
                          const int32_t* idx, int32_t nidx, const pq_settings* s, void* stream);
+
+/* K4 entirely in the window form (pb->P is not read; any n): each active-set round forms
+ * the reduced P_FF from the free columns of the window with FP64 MFMA tile products into
+ * a compact ldk x ldk scratch (st->K, K_stride >= ldk^2; st->Dt, Dt_stride >=
+ * (ldk/64) 4096), indexed by launch slot (blockIdx: the problem's position in idx[] or
+ * its id when idx == NULL).  64 <= ldk <= min(ld, 1024).  A problem whose free set
+ * exceeds ldk is left unchanged with out[PQ_OUT_ROUNDS] = -1 unless final_try != 0 (then
+ * it is scored at its ADMM point, status PQ_SOLVED_INACCURATE).  Needs lr->dg.          */
+int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const int32_t* idx,
+                        int32_t nidx, const pq_settings* s, int32_t ldk, int32_t final_try,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libporqua_hip.so")
+# PQ_LIB_PATH: an alternative build of the same library (e.g. the PQ_PROFILE phase-timing build)
+LIB_PATH = os.environ.get("PQ_LIB_PATH") or os.path.join(_HERE, "libporqua_hip.so")
 
 c_int32 = ctypes.c_int32
 c_int64 = ctypes.c_int64
@@ -30,7 +31,7 @@ PQ_OUT_FIELDS = 8
 
 def work_doubles(ld: int, mg_pad: int) -> int:
     """PQ_WORK_DOUBLES of include/porqua_hip.h."""
-    return (4 + mg_pad) * ld + 512
+    return (5 + mg_pad) * ld + 512
 
 
 class PorquaHipError(RuntimeError):
@@ -82,6 +83,7 @@ class PQLowRank(ctypes.Structure):
         ("rows", c_dp), ("tlen", c_dp), ("tmax", c_int32),
         ("mu", c_dp), ("mu_stride", c_int64),
         ("w_scale", c_dp),
+        ("dg", c_dp), ("dg_stride", c_int64),
     ]
 
 
@@ -94,6 +96,12 @@ _EXPORTS = {
                         c_dp, c_int32, c_int64, c_dp], c_int32),
     "pq_cov_slide_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_int32, c_dp, c_int64,
                               c_dp, c_int32, c_int64, c_dp, c_int32, c_dp, c_int32, c_dp], c_int32),
+    "pq_window_sumsq": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_dp, c_int64,
+                         c_dp], c_int32),
+    "pq_init_state_lr": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp,
+                          c_int32, ctypes.POINTER(PQSettings), c_dp], c_int32),
+    "pq_polish_w_batched": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                             c_dp, c_int32, ctypes.POINTER(PQSettings), c_int32, c_int32, c_dp], c_int32),
     "pq_gram_xy_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64,
                             c_dp, c_dp], c_int32),
     "pq_init_state": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,

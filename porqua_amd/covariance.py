@@ -62,29 +62,39 @@ class Covariance:
         """All dates at once on the device.  Returns (S, p_diag): S is the (B, ld, ld)
         device tensor of raw sample covariances; p_diag (B,) is the diagonal term the spec
         adds (linear shrinkage: lam * mean(diag S)); 'duv' returns (None, None)."""
-        S, pdiag, _ = self.estimate_batch_lr(panel, rows, tlen, out=out, plan=plan, lower_only=lower_only)
+        S, pdiag, _, _ = self.estimate_batch_lr(panel, rows, tlen, out=out, plan=plan, lower_only=lower_only)
         return S, pdiag
 
-    def estimate_batch_lr(self, panel, rows, tlen, out=None, plan=None, lower_only=False):
+    def estimate_batch_lr(self, panel, rows, tlen, out=None, plan=None, lower_only=False,
+                          materialise=True):
         """estimate_batch plus the window means (the centring of the factored form
-        S = Xc'Xc / (T-1) that the low-rank solver uses).  ``plan``: an engine.SlidePlan for
-        overlapping windows; ``lower_only``: lower-triangle storage (low-rank consumers)."""
+        S = Xc'Xc / (T-1) that the low-rank solver uses) -> (S, p_diag, mu, dg).
+        ``plan``: an engine.SlidePlan for overlapping windows; ``lower_only``: lower-triangle
+        storage.  ``materialise=False`` (the window-form solver, which never reads an n x n
+        S): S is None and dg = diag(Xc'Xc) per date carries what the shrinkage term needs."""
         import torch
         method = self.spec["method"]
         if method == "duv":
-            return None, None, None
+            return None, None, None, None
         if method not in ("pearson", "linear_shrinkage"):
             raise NotImplementedError("This method is not implemented yet")
         mu = panel.window_means(rows, tlen)
-        S = panel.cov(rows, tlen, mode=0, out=out, mu=mu, plan=plan, lower_only=lower_only and plan is not None)
-        B = S.shape[0]
-        pdiag = torch.zeros(B, dtype=torch.float64, device=S.device)
+        B, n = int(rows.shape[0]), panel.n
+        S = dg = None
+        if materialise:
+            S = panel.cov(rows, tlen, mode=0, out=out, mu=mu, plan=plan,
+                          lower_only=lower_only and plan is not None)
+        else:
+            dg = panel.window_sumsq(rows, tlen, mu)
+        pdiag = torch.zeros(B, dtype=torch.float64, device=mu.device)
         if method == "linear_shrinkage":
             lam = _shrink_lambda(self.spec.get("lambda_covmat_regularization"))
             if lam > 0:
-                n = panel.n
-                pdiag = lam * torch.diagonal(S, dim1=1, dim2=2)[:, :n].mean(dim=1)
-        return S, pdiag, mu
+                if S is not None:
+                    pdiag = lam * torch.diagonal(S, dim1=1, dim2=2)[:, :n].mean(dim=1)
+                else:   # mean(diag S) = mean(diag Xc'Xc) / (T - 1)
+                    pdiag = lam * dg[:, :n].mean(dim=1) / (tlen.to(torch.float64) - 1.0)
+        return S, pdiag, mu, dg
 
 
 def _device_cov(X, mode=0):

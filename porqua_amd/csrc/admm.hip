@@ -560,7 +560,9 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
   }
 }
 
-__global__ void k_init_state(pq_problem pb, pq_state st, const int32_t* idx, pq_settings s) {
+// dg: diag of the unscaled window Gram (pq_lowrank.dg) when P is given in window form
+__global__ void k_init_state(pq_problem pb, pq_state st, const int32_t* idx, pq_settings s,
+                             const double* dg, int64_t dg_stride, const double* w_scale) {
   const int b = idx ? idx[blockIdx.x] : (int)blockIdx.x;
   const int ld = pb.ld;
   for (int i = threadIdx.x; i < ld; i += blockDim.x) {
@@ -578,7 +580,12 @@ __global__ void k_init_state(pq_problem pb, pq_state st, const int32_t* idx, pq_
     const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
     const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
     double sdiag = 0.0;
-    for (int i = threadIdx.x; i < pb.n; i += blockDim.x) sdiag += ps * P[(int64_t)i * ld + i] + pd;
+    if (dg) {
+      const double psw = ps * (w_scale ? w_scale[b] : 1.0);
+      for (int i = threadIdx.x; i < pb.n; i += blockDim.x) sdiag += psw * dg[(int64_t)b * dg_stride + i] + pd;
+    } else {
+      for (int i = threadIdx.x; i < pb.n; i += blockDim.x) sdiag += ps * P[(int64_t)i * ld + i] + pd;
+    }
     sdiag = block_sum(sdiag, red);
     const double md = sdiag / pb.n;
     rho0 = (md > 0.0 && isfinite(md)) ? fmin(fmax(s.rho0_rel * md, s.rho_min), s.rho_max) : s.rho0;
@@ -602,8 +609,25 @@ extern "C" int pq_init_state(const pq_problem* pb, pq_state* st, const int32_t* 
   PQ_CHECK_ARG(st->m_ld >= st->mg_pad + pb->ld && st->mg_pad >= pb->mg, "pq_init_state: bad m_ld / mg_pad");
   const int grid = idx ? nidx : pb->batch;
   if (grid <= 0) return 0;
-  hipLaunchKernelGGL(pq::k_init_state, dim3(grid), dim3(256), 0, (hipStream_t)stream, *pb, *st, idx, *s);
+  PQ_CHECK_ARG(pb->P || s->rho0_rel <= 0.0, "pq_init_state: rho0_rel > 0 needs P (pq_init_state_lr for the window form)");
+  hipLaunchKernelGGL(pq::k_init_state, dim3(grid), dim3(256), 0, (hipStream_t)stream, *pb, *st, idx, *s,
+                     nullptr, 0, nullptr);
   PQ_CHECK_LAUNCH("pq_init_state");
+  return 0;
+}
+
+extern "C" int pq_init_state_lr(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const int32_t* idx,
+                                int32_t nidx, const pq_settings* s, void* stream) {
+  PQ_CHECK_ARG(lr && pb && st && s, "pq_init_state_lr: null argument");
+  PQ_CHECK_ARG(lr->dg || s->rho0_rel <= 0.0, "pq_init_state_lr: rho0_rel > 0 needs lr->dg (pq_window_sumsq)");
+  PQ_CHECK_ARG(st->x && st->Px && st->z && st->y && st->rho && st->iters && st->status &&
+                   st->info && st->out, "pq_init_state_lr: state buffers missing");
+  PQ_CHECK_ARG(st->m_ld >= st->mg_pad + pb->ld && st->mg_pad >= pb->mg, "pq_init_state_lr: bad m_ld / mg_pad");
+  const int grid = idx ? nidx : pb->batch;
+  if (grid <= 0) return 0;
+  hipLaunchKernelGGL(pq::k_init_state, dim3(grid), dim3(256), 0, (hipStream_t)stream, *pb, *st, idx, *s,
+                     lr->dg, lr->dg_stride, lr->w_scale);
+  PQ_CHECK_LAUNCH("pq_init_state_lr");
   return 0;
 }
 

@@ -27,8 +27,12 @@ constexpr int GT = 512;      // threads per group workgroup
 constexpr int GNW = GT / 64; // waves
 constexpr int GMAX = 16;     // dates per group (MFMA N)
 constexpr int UMAXG = 320;   // union rows per group
-constexpr int MGG = 8;       // general-row slots in LDS
-constexpr int MGR = 4;       // general constraint rows supported here (register arrays)
+// General constraint rows: the kernel is instantiated with MGG LDS slots per date and
+// either MGR > 0 (rows held in register arrays in the fused passes: mg <= MGR) or MGR == 0
+// (any mg <= MGG: rows re-read from Cg per element and Cg x~ / Cg V as separate half-wave
+// dot products -- group-cap constraints, e.g. 20 sector rows).
+constexpr int MGG_SMALL = 8, MGR_SMALL = 4;
+constexpr int MGG_BIG = 32;
 
 __device__ __forceinline__ double grho(double l, double u, double rho, const pq_settings& s) {
   if (l == u) return rho * s.eq_scale;
@@ -67,7 +71,7 @@ __device__ __forceinline__ int grp_slot(int g, int N) {   // XCD-contiguous grou
 #define GSTAMP(k) do { } while (0)
 #endif
 
-template <int NQK>
+template <int NQK, int MGG, int MGR>
 __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, pq_state st,
                                                  const double* Minv_all, int k_ld, int64_t M_stride,
                                                  const int32_t* gdates, const int32_t* urows_all,
@@ -438,29 +442,45 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       const double dsig = sigma + pd;
       if (hl < mg) g_cw[g * MGG + hl] = sqrt(g_rg[g * MGG + hl]) * g_kug[g * MGG + hl];
       // pass A: x~ = v - D^-1 (X~raw - mu su + Cg' cw), and Cg x~
-      double ztp[MGR];
+      constexpr int MGRA = MGR > 0 ? MGR : 1;
+      double ztp[MGRA];
 #pragma unroll
-      for (int r = 0; r < MGR; ++r) ztp[r] = 0.0;
+      for (int r = 0; r < MGRA; ++r) ztp[r] = 0.0;
 #pragma unroll 2
       for (int i = hl; i < n; i += 32) {
         double corr = X_h[i] - (mu_h ? su * mu_h[i] : 0.0);
         const double rb = has_box ? grho(lo_h[i], up_h[i], rho, s) : 0.0;
-        double cgi[MGR];
+        double cgi[MGRA];
+        if constexpr (MGR > 0) {
 #pragma unroll
-        for (int r = 0; r < MGR; ++r) {
-          cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
-          corr = fma(r < mg ? g_cw[g * MGG + r] : 0.0, cgi[r], corr);
+          for (int r = 0; r < MGR; ++r) {
+            cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
+            corr = fma(r < mg ? g_cw[g * MGG + r] : 0.0, cgi[r], corr);
+          }
+        } else {
+          for (int r = 0; r < mg; ++r) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
         }
         const double xt = V_h[i] - corr / (dsig + rb);
         X_h[i] = xt;
+        if constexpr (MGR > 0) {
 #pragma unroll
-        for (int r = 0; r < MGR; ++r) ztp[r] = fma(cgi[r], xt, ztp[r]);
+          for (int r = 0; r < MGR; ++r) ztp[r] = fma(cgi[r], xt, ztp[r]);
+        }
       }
+      if constexpr (MGR > 0) {
 #pragma unroll
-      for (int r = 0; r < MGR; ++r) {
-        if (r >= mg) break;
-        const double a = hsum(ztp[r]);
-        if (hl == 0) g_zt[g * MGG + r] = a;
+        for (int r = 0; r < MGR; ++r) {
+          if (r >= mg) break;
+          const double a = hsum(ztp[r]);
+          if (hl == 0) g_zt[g * MGG + r] = a;
+        }
+      } else {   // each lane re-reads the x~ entries it wrote
+        for (int r = 0; r < mg; ++r) {
+          double a = 0.0;
+          for (int i = hl; i < n; i += 32) a = fma(Cg_h[(int64_t)r * ld + i], X_h[i], a);
+          a = hsum(a);
+          if (hl == 0) g_zt[g * MGG + r] = a;
+        }
       }
       double mv[7] = {0, 0, 0, 0, 0, 0, 0};   // |Cx-z| |Cx| |z| |dres| |Px| |C'y| |q|
       if (hl < mg) {   // general row hl: z, y, Cx (lane-owned); R z - y for the next rhs
@@ -480,22 +500,31 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
         g_wg[e] = rg * zn - yn;
       }
       // pass B: x, Px, z, y updates, residual terms, next rhs and V = rhs / D, mu.V, Cg.V
-      double muv = 0.0, cvp[MGR];
+      double muv = 0.0, cvp[MGRA];
 #pragma unroll
-      for (int r = 0; r < MGR; ++r) cvp[r] = 0.0;
+      for (int r = 0; r < MGRA; ++r) cvp[r] = 0.0;
 #pragma unroll 2
       for (int i = hl; i < n; i += 32) {
         const double xt = X_h[i];
         const double rb = has_box ? grho(lo_h[i], up_h[i], rho, s) : 0.0;
         double pxt = R_h[i] - sigma * xt - rb * xt;
-        double cgy = 0.0, cgw = 0.0, cgi[MGR];
+        double cgy = 0.0, cgw = 0.0, cgi[MGRA];
+        if constexpr (MGR > 0) {
 #pragma unroll
-        for (int r = 0; r < MGR; ++r) {
-          cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
-          if (r < mg) {
-            pxt -= cgi[r] * g_rgz[g * MGG + r];
-            cgy = fma(cgi[r], g_yg[g * MGG + r], cgy);
-            cgw = fma(cgi[r], g_wg[g * MGG + r], cgw);
+          for (int r = 0; r < MGR; ++r) {
+            cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
+            if (r < mg) {
+              pxt -= cgi[r] * g_rgz[g * MGG + r];
+              cgy = fma(cgi[r], g_yg[g * MGG + r], cgy);
+              cgw = fma(cgi[r], g_wg[g * MGG + r], cgw);
+            }
+          }
+        } else {
+          for (int r = 0; r < mg; ++r) {
+            const double c = Cg_h[(int64_t)r * ld + i];
+            pxt -= c * g_rgz[g * MGG + r];
+            cgy = fma(c, g_yg[g * MGG + r], cgy);
+            cgw = fma(c, g_wg[g * MGG + r], cgw);
           }
         }
         const double xn = alpha * xt + (1.0 - alpha) * x_h[i];
@@ -526,16 +555,27 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
         R_h[i] = rr;
         V_h[i] = v;
         if (mu_h) muv = fma(mu_h[i], v, muv);
+        if constexpr (MGR > 0) {
 #pragma unroll
-        for (int r = 0; r < MGR; ++r) cvp[r] = fma(cgi[r], v, cvp[r]);
+          for (int r = 0; r < MGR; ++r) cvp[r] = fma(cgi[r], v, cvp[r]);
+        }
       }
 #pragma unroll
       for (int e = 0; e < 7; ++e) mv[e] = hmax(mv[e]);
       muv = hsum(muv);
+      if constexpr (MGR > 0) {
 #pragma unroll
-      for (int r = 0; r < MGR; ++r) {
-        if (r >= mg) break;
-        cvp[r] = hsum(cvp[r]);
+        for (int r = 0; r < MGR; ++r) {
+          if (r >= mg) break;
+          cvp[r] = hsum(cvp[r]);
+        }
+      } else {   // Cg V: written straight to the date's slots (read only by the next symv)
+        for (int r = 0; r < mg; ++r) {
+          double a = 0.0;
+          for (int i = hl; i < n; i += 32) a = fma(Cg_h[(int64_t)r * ld + i], V_h[i], a);
+          a = hsum(a);
+          if (hl == 0) g_cgv[g * MGG + r] = a;
+        }
       }
       const int it = g_it[g] + 1;
       int stat = PQ_UNSOLVED;
@@ -562,9 +602,11 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
         g_stat[g] = stat;
         g_act[g] = cont;
         g_muv[g] = muv;
+        if constexpr (MGR > 0) {
 #pragma unroll
-        for (int r = 0; r < MGR; ++r)
-          if (r < mg) g_cgv[g * MGG + r] = cvp[r];
+          for (int r = 0; r < MGR; ++r)
+            if (r < mg) g_cgv[g * MGG + r] = cvp[r];
+        }
       }
     }
     __syncthreads();
@@ -596,9 +638,11 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
     }
   }
 #ifdef PQ_PROFILE
-  if (t < G) {
-    double* dstp = st.work + (int64_t)(d0 + t) * st.work_stride + (int64_t)(4 + st.mg_pad) * ld + 16;
-    for (int k2 = 0; k2 < 4; ++k2) dstp[k2] += (double)pclk[k2] / G;
+  if (t == 0) {   // the timers run on thread 0: share the group's phase times over its dates
+    for (int g = 0; g < G; ++g) {
+      double* dstp = st.work + (int64_t)(d0 + g) * st.work_stride + PQ_WORK_PROF(ld, st.mg_pad) + 16;
+      for (int k2 = 0; k2 < 4; ++k2) dstp[k2] += (double)pclk[k2] / G;
+    }
   }
 #endif
 }
@@ -613,8 +657,8 @@ extern "C" int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq
   PQ_CHECK_ARG(lr && pb && st && s && Minv, "pq_admm_lr_grouped: null argument");
   PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0, "pq_admm_lr_grouped: window missing");
   PQ_CHECK_ARG(gdates && urows && ucnt && uoff && umax > 0, "pq_admm_lr_grouped: group plan missing");
-  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::MGR && (pb->mg == 0 || (pb->Cg && pb->lg && pb->ug)),
-               "pq_admm_lr_grouped: needs 0 <= mg <= %d general rows (mg=%d)", pq::MGR, pb->mg);
+  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::MGG_BIG && (pb->mg == 0 || (pb->Cg && pb->lg && pb->ug)),
+               "pq_admm_lr_grouped: needs 0 <= mg <= %d general rows (mg=%d)", pq::MGG_BIG, pb->mg);
   PQ_CHECK_ARG(pb->n % 2 == 0 && lr->ldp % 2 == 0, "pq_admm_lr_grouped: needs even n and panel stride");
   PQ_CHECK_ARG(st->work && st->work_stride >= 3 * (int64_t)pb->ld, "pq_admm_lr_grouped: work buffer too small");
   const int k = lr->tmax + pb->mg;
@@ -622,15 +666,17 @@ extern "C" int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq
   if (ngroups <= 0) return 0;
   hipStream_t str = (hipStream_t)stream;
   const int nqk = (k_ld + 127) / 128;
-#define PQ_GRP_CASE(NQKV)                                                                                      \
-  case NQKV:                                                                                                   \
-    hipLaunchKernelGGL((pq::k_admm_grp<NQKV>), dim3(ngroups), dim3(pq::GT), 0, str, *lr, *pb, *st, Minv, k_ld, \
-                       M_stride, gdates, urows, ucnt, uoff, umax, *s, iters_this_call);                         \
-    break;
-  switch (nqk) {
-    PQ_GRP_CASE(1)
-    PQ_GRP_CASE(2)
-    PQ_GRP_CASE(3)
+#define PQ_GRP_CASE(NQKV, MGGV, MGRV)                                                                   \
+  hipLaunchKernelGGL((pq::k_admm_grp<NQKV, MGGV, MGRV>), dim3(ngroups), dim3(pq::GT), 0, str, *lr, *pb, *st,   \
+                     Minv, k_ld, M_stride, gdates, urows, ucnt, uoff, umax, *s, iters_this_call)
+  const bool small = pb->mg <= pq::MGR_SMALL;
+  switch (nqk * 2 + (small ? 0 : 1)) {
+    case 2: PQ_GRP_CASE(1, pq::MGG_SMALL, pq::MGR_SMALL); break;
+    case 3: PQ_GRP_CASE(1, pq::MGG_BIG, 0); break;
+    case 4: PQ_GRP_CASE(2, pq::MGG_SMALL, pq::MGR_SMALL); break;
+    case 5: PQ_GRP_CASE(2, pq::MGG_BIG, 0); break;
+    case 6: PQ_GRP_CASE(3, pq::MGG_SMALL, pq::MGR_SMALL); break;
+    case 7: PQ_GRP_CASE(3, pq::MGG_BIG, 0); break;
     default:
       pq::set_error("pq_admm_lr_grouped: unsupported k_ld=%d", k_ld);
       return -1;

@@ -111,7 +111,9 @@ constexpr int CHOL_LDS = 4 * STAGE + TB * LDW;
 // `form(gi, gj)` (read exactly once each) into L stored in K (ld), with the transposed
 // inverses of the diagonal blocks in Dt.  Returns info (0 = success, else first failing
 // column + 1).  All threads of the (256-thread) workgroup must call it.
-template <typename Form>
+// kStoreDiag = false leaves K's diagonal 64x64 blocks untouched (nothing downstream of the
+// polish reads them: the solves use Dt), so they can keep the matrix being factored.
+template <bool kStoreDiag = true, typename Form>
 __device__ int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, int nv, double* Dt, double* smem) {
   double* stg = smem;
   double* sD = smem + 4 * STAGE;
@@ -138,7 +140,7 @@ __device__ int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, int nv,
     for (int q = 0; q < TB * TB / 256; ++q) {
       const int e = threadIdx.x + q * 256;
       const int i = e >> 6, j = e & 63;
-      K[(int64_t)(J * TB + i) * ld + J * TB + j] = (j <= i) ? stg[i * DP + j] : 0.0;
+      if (kStoreDiag) K[(int64_t)(J * TB + i) * ld + J * TB + j] = (j <= i) ? stg[i * DP + j] : 0.0;
       xr[q] = X[i * DP + j];                             // (T^-1)[j][i]
       Dt[(int64_t)J * TB * TB + i * TB + j] = xr[q];     // Dt[c][r] = Dinv[r][c]
     }

@@ -33,6 +33,25 @@ __global__ __launch_bounds__(256) void k_window_mean(const double* panel, int64_
   }
 }
 
+// diag(Xc'Xc): sum_t (X_tj - mu_j)^2 (mu == NULL: sum_t X_tj^2), one thread per column
+__global__ __launch_bounds__(256) void k_window_sumsq(const double* panel, int64_t ldp, int n,
+                                                      const int32_t* rows, const int32_t* tlen,
+                                                      int tmax, const double* mu, int64_t mu_stride,
+                                                      double* out, int64_t out_stride) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int T = tlen[b];
+  const int32_t* rw = rows + (int64_t)b * tmax;
+  const double m = mu ? mu[(int64_t)b * mu_stride + j] : 0.0;
+  double s = 0.0;
+  for (int k = 0; k < T; ++k) {
+    const double d = panel[(int64_t)rw[k] * ldp + j] - m;
+    s = fma(d, d, s);
+  }
+  out[(int64_t)b * out_stride + j] = s;
+}
+
 __device__ __forceinline__ void tri_index(int t, int& I, int& J) {
   // t enumerates lower tiles row by row: (0,0),(1,0),(1,1),(2,0),...
   I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
@@ -291,6 +310,18 @@ extern "C" int pq_window_mean(const double* panel, int64_t ldp, int32_t n, const
   hipLaunchKernelGGL(pq::k_window_mean, dim3((n + 255) / 256, batch), dim3(256), 0,
                      (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mu, mu_stride, 0);
   PQ_CHECK_LAUNCH("pq_window_mean");
+  return 0;
+}
+
+extern "C" int pq_window_sumsq(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                               const int32_t* tlen, int32_t tmax, int32_t batch, const double* mu,
+                               int64_t mu_stride, double* out, int64_t out_stride, void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(out != nullptr, "pq_window_sumsq: out is null");
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(pq::k_window_sumsq, dim3((n + 255) / 256, batch), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mu, mu_stride, out, out_stride);
+  PQ_CHECK_LAUNCH("pq_window_sumsq");
   return 0;
 }
 

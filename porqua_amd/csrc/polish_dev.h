@@ -1,0 +1,246 @@
+// Device helpers of the K4 polish kernels (polish.hip: dense P; polish_w.hip: window form).
+#pragma once
+#include "chol_dev.h"
+#include "../../include/porqua_hip.h"
+
+namespace pq {
+
+constexpr int PT = 256;
+constexpr int PW = PT / 64;
+
+// Optional phase timing (build with -DPQ_PROFILE): wall-clock ticks per phase accumulated
+// into the 16 doubles after the work layout of each problem (tools/prof_polish.py).
+#ifdef PQ_PROFILE
+#define PQ_STAMP(k)                                              \
+  do {                                                           \
+    __syncthreads();                                             \
+    if (threadIdx.x == 0) {                                      \
+      const long long now_ = wall_clock64();                     \
+      prof[k] += (double)(now_ - t_last_);                       \
+      t_last_ = now_;                                            \
+    }                                                            \
+  } while (0)
+#else
+#define PQ_STAMP(k) do { } while (0)
+#endif
+
+
+// y = L^-1 r  (L in K with ld, block inverses in Dt); r, y, t64 in LDS, length nbk*64.
+__device__ void fwd_solve(const double* K, int64_t ld, const double* Dt, int nbk, const double* r,
+                          double* y, double* t64, double* y64p) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  for (int I = 0; I < nbk; ++I) {
+    for (int i = w; i < TB; i += PW) {
+      const double* row = K + (int64_t)(I * TB + i) * ld;
+      double s = 0.0;
+      for (int c = l; c < I * TB; c += 64) s += row[c] * y[c];
+      s = wave_sum(s);
+      if (l == 0) t64[i] = r[I * TB + i] - s;
+    }
+    __syncthreads();
+    {  // y_I = Dinv_I t_I : 4 threads per output row, 16 independent loads each
+      const double* D = Dt + (int64_t)I * TB * TB;
+      const int o = t & 63, part = t >> 6;
+      double s = 0.0;
+#pragma unroll
+      for (int c = part * 16; c < part * 16 + 16; ++c) s += D[c * TB + o] * t64[c];   // Dinv[o][c] = Dt[c][o]
+      y64p[part * TB + o] = s;
+    }
+    __syncthreads();
+    if (t < TB) y[I * TB + t] = (y64p[t] + y64p[TB + t]) + (y64p[2 * TB + t] + y64p[3 * TB + t]);
+    __syncthreads();
+  }
+}
+
+// x = L^-T y ; part[] is 4*64 LDS scratch.
+__device__ void bwd_solve(const double* K, int64_t ld, const double* Dt, int nbk, const double* y,
+                          double* x, double* t64, double* part, double* part_out) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  for (int I = nbk - 1; I >= 0; --I) {
+    // t_I = y_I - sum_{r >= 64(I+1)} L[r][64I + i] x[r]   (lanes over i, waves split r)
+    double s = 0.0;
+    for (int r = (I + 1) * TB + w; r < nbk * TB; r += PW) s += K[(int64_t)r * ld + I * TB + l] * x[r];
+    part[w * TB + l] = s;
+    __syncthreads();
+    if (t < TB) t64[t] = y[I * TB + t] - (part[t] + part[TB + t] + part[2 * TB + t] + part[3 * TB + t]);
+    __syncthreads();
+    {  // x_I = Dinv_I' t_I : (Dinv')[o][c] = Dt[o][c], 4 threads per output
+      const double* D = Dt + (int64_t)I * TB * TB;
+      const int o = t & 63, part = t >> 6;
+      double v = 0.0;
+#pragma unroll
+      for (int c = part * 16; c < part * 16 + 16; ++c) v += D[o * TB + c] * t64[c];
+      part_out[part * TB + o] = v;
+    }
+    __syncthreads();
+    if (t < TB) x[I * TB + t] = (part_out[t] + part_out[TB + t]) + (part_out[2 * TB + t] + part_out[3 * TB + t]);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int block_or(int v, double* red) {
+  return block_max((double)v, red) > 0.5;
+}
+
+// emit(p, P[row(p)] . v) for p < cnt: full rows of the dense symmetric P (n <= 1024
+// columns), v held in registers (lane l owns columns 128 q + 2 l, 2 l + 1; v must be zero
+// from n up to the next even index), 16-B loads, two rows per wave in flight.  Called by
+// every thread; emit runs on lane 0 of the wave that owns the row.
+template <typename RowF, typename EmitF>
+__device__ __forceinline__ void rows_dot_vec(const double* P, int64_t ld, int n, int cnt, RowF row_of,
+                                             const double* v, EmitF emit) {
+  constexpr int NQ = 8;
+  const int w = wave_id(), l = lane_id();
+  double2 vr[NQ];
+#pragma unroll
+  for (int qq = 0; qq < NQ; ++qq) {
+    const int c = 128 * qq + 2 * l;
+    vr[qq] = c < n ? reinterpret_cast<const double2*>(v + c)[0] : double2{0.0, 0.0};
+  }
+  for (int p = w; p < cnt; p += 2 * PW) {
+    const int p1 = p + PW;
+    const bool two = p1 < cnt;
+    const double2* r0 = reinterpret_cast<const double2*>(P + (int64_t)row_of(p) * ld) + l;
+    const double2* r1 = reinterpret_cast<const double2*>(P + (int64_t)row_of(two ? p1 : p) * ld) + l;
+    double2 a[NQ], b[NQ];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const bool ok = 128 * qq + 2 * l < n;
+      a[qq] = ok ? r0[64 * qq] : double2{0.0, 0.0};
+      b[qq] = (ok && two) ? r1[64 * qq] : double2{0.0, 0.0};
+    }
+    double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      d0 = fma(a[qq].x, vr[qq].x, fma(a[qq].y, vr[qq].y, d0));
+      d1 = fma(b[qq].x, vr[qq].x, fma(b[qq].y, vr[qq].y, d1));
+    }
+    d0 = wave_sum(d0);
+    d1 = wave_sum(d1);
+    if (l == 0) {
+      emit(p, d0);
+      if (two) emit(p1, d1);
+    }
+  }
+}
+
+// emit(i, w_scale * (Xc' Xc x)_i) for i < n from the window form of P (pq_lowrank): two
+// passes over the date's window rows (shared by neighbouring dates, so L2-resident)
+// instead of n^2 bytes of P.  Columns go in chunks of 1024 (lane l owns columns
+// c0 + 128 q + 2 l, + 1 of a chunk; 16-B loads), so n is unbounded.  x: global, zero from
+// n to the next even index.  u: LDS >= tmax doubles; tree: LDS >= 2 * 1024 doubles; red:
+// LDS reduction scratch.  Row t of pass 1 is always owned by the same wave, so its
+// partial dot products accumulate across chunks in u[t] without barriers.
+template <typename EmitF>
+__device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* tree,
+                      double* red, EmitF emit) {
+  constexpr int NQ = 8, RU = 4, LM = NQ * 128;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
+  double mux = 0.0;
+  if (mu) {
+    double a = 0.0;
+    for (int i = t; i < n; i += PT) a += mu[i] * x[i];
+    mux = block_sum(a, red);
+  }
+  // pass 1: u_t = X_t . x - mu . x
+  for (int c0 = 0; c0 < n; c0 += LM) {
+    double2 vr[NQ];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+      const int c = c0 + 128 * qq + 2 * l;
+      vr[qq] = c < n ? reinterpret_cast<const double2*>(x + c)[0] : double2{0.0, 0.0};
+    }
+    for (int t0 = w; t0 < T; t0 += RU * PW) {
+      double2 r[RU][NQ];
+#pragma unroll
+      for (int e = 0; e < RU; ++e) {
+        const int tt = t0 + e * PW;
+        const double2* rp =
+            reinterpret_cast<const double2*>(lr.panel + (tt < T ? (int64_t)rws[tt] : 0) * lr.ldp + c0) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq)
+          r[e][qq] = (tt < T && c0 + 128 * qq + 2 * l < n) ? rp[64 * qq] : double2{0.0, 0.0};
+      }
+      double d[RU];
+#pragma unroll
+      for (int e = 0; e < RU; ++e) {
+        double s0 = 0.0;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) s0 = fma(r[e][qq].x, vr[qq].x, fma(r[e][qq].y, vr[qq].y, s0));
+        d[e] = wave_sum(s0);
+      }
+      if (l == 0) {
+#pragma unroll
+        for (int e = 0; e < RU; ++e)
+          if (t0 + e * PW < T) u[t0 + e * PW] = (c0 == 0 ? -mux : u[t0 + e * PW]) + d[e];
+      }
+    }
+  }
+  __syncthreads();
+  double su = 0.0;
+  if (mu) {
+    double a = 0.0;
+    for (int tt = t; tt < T; tt += PT) a += u[tt];
+    su = block_sum(a, red);
+  }
+  // pass 2 per chunk: acc = sum_t u_t X_t (register accumulators), then a fixed-order wave tree
+  for (int c0 = 0; c0 < n; c0 += LM) {
+    double2 acc[NQ];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) acc[qq] = double2{0.0, 0.0};
+    for (int t0 = w; t0 < T; t0 += RU * PW) {
+      double2 r[RU][NQ];
+      double a[RU];
+#pragma unroll
+      for (int e = 0; e < RU; ++e) {
+        const int tt = t0 + e * PW;
+        a[e] = tt < T ? u[tt] : 0.0;
+        const double2* rp =
+            reinterpret_cast<const double2*>(lr.panel + (tt < T ? (int64_t)rws[tt] : 0) * lr.ldp + c0) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq)
+          r[e][qq] = (tt < T && c0 + 128 * qq + 2 * l < n) ? rp[64 * qq] : double2{0.0, 0.0};
+      }
+#pragma unroll
+      for (int e = 0; e < RU; ++e)
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          acc[qq].x = fma(a[e], r[e][qq].x, acc[qq].x);
+          acc[qq].y = fma(a[e], r[e][qq].y, acc[qq].y);
+        }
+    }
+#pragma unroll
+    for (int half = PW / 2; half >= 1; half >>= 1) {
+      if (w >= half && w < 2 * half) {
+        double2* dst = reinterpret_cast<double2*>(tree + (w - half) * LM) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) dst[64 * qq] = acc[qq];
+      }
+      __syncthreads();
+      if (w < half) {
+        const double2* src = reinterpret_cast<const double2*>(tree + w * LM) + l;
+#pragma unroll
+        for (int qq = 0; qq < NQ; ++qq) {
+          const double2 vv = src[64 * qq];
+          acc[qq].x += vv.x;
+          acc[qq].y += vv.y;
+        }
+      }
+      __syncthreads();
+    }
+    if (w == 0) {
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int c = c0 + 128 * qq + 2 * l;
+        if (c < n) emit(c, wsc * (acc[qq].x - (mu ? mu[c] * su : 0.0)));
+        if (c + 1 < n) emit(c + 1, wsc * (acc[qq].y - (mu ? mu[c + 1] * su : 0.0)));
+      }
+    }
+  }
+}
+
+}  // namespace pq

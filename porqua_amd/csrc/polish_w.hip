@@ -1,47 +1,123 @@
-// K4: active-set polish of the ADMM point + exact residuals / objective.
+// K4, window form: the active-set polish of polish.hip for the low-rank (backtest) path,
+// with no n x n matrix anywhere.
 //
-// One 256-thread workgroup per QP.  From the ADMM iterate (x, z, y) the box rows and the
-// general rows (budget / group caps) are classified as active at a bound or free.  Fixed
-// variables are eliminated; the reduced KKT
-//      [P_FF + dI   C_aF'] [x_F]   [-q_F - P_FB x_B]
-//      [C_aF       -dI   ] [lam] = [ d_a - C_aB x_B ]
-// is factored with the same workgroup MFMA Cholesky as K2 (P_FF gathered through the free
-// index list at first touch, never materialised), a Schur complement for the <= 64 active
-// rows, and proximal iterative refinement started at the ADMM point (exact where the
-// system is nonsingular, stays at the ADMM multipliers along degenerate directions, e.g.
-// every weight at a bound).  Primal bound violations / wrong-sign multipliers update the
-// active set for another round.  The accepted point, or the ADMM point when polishing
-// fails, is scored with an exact P x mat-vec: objective 0.5 x'Px + q'x
-// (src/qp_problems.py:219-221, test/tests_quadratic_program.py:72,82) and the qpsolvers
-// residuals of example/compare_solver.ipynb:212-216.
+// P_eff = p_scale w_scale Xc'Xc + p_diag I is only available through the date's window
+// (pq_lowrank).  Each active-set round gathers the free columns of the window (T x k,
+// from the L2-resident panel rows) and forms the reduced matrix P_FF = p_scale w_scale
+// Xc_F'Xc_F + p_diag I with FP64 MFMA tile products (the same SYRK as K1, restricted to
+// the free set) into a compact per-problem scratch of leading dimension ldk >= k:
+//   - the diagonal 64x64 tiles hold P_FF in full,
+//   - the strictly-upper tiles hold P_FF's lower tiles transposed,
+//   - the strictly-lower tiles receive the Cholesky factor L of P_FF + delta I
+//     (wg_cholesky<false>: the diagonal tiles of L are never stored; the solves use Dt),
+// so one k x k buffer serves both the factorisation and the exact residuals of the
+// proximal iterative refinement.  Every n-length quantity (P x_B, the final exact
+// gradient) comes from two passes over the window rows (lr_px); per-variable bookkeeping
+// lives in the work buffer, so n is unbounded and only the free set (k <= min(ldk, 1024))
+// is bounded.  A problem whose free set outgrows ldk is left untouched with
+// out[PQ_OUT_ROUNDS] = -1 so the caller can relaunch it with a larger scratch
+// (final_try = 1: polish fails instead and the ADMM point is scored).
+//
+// Replaces, with polish.hip, the accuracy of qpsolvers' interior-point answer
+// (src/qp_problems.py:211-214); scoring as in polish.hip (src/qp_problems.py:219-221,
+// example/compare_solver.ipynb:212-216).
 #include "polish_dev.h"
 #include "capi_util.h"
 
 namespace pq {
 
-struct PolishForm {
-  const double* P;
+constexpr int KMAX = 1024;   // free variables held in LDS
+
+// P_FF (+ dadd on the diagonal) in the compact polish storage described above
+struct FormW {
+  const double* K;
   int64_t ld;
-  const int* F;
   int k;
-  double ps, dadd;
+  double dadd;
   __device__ __forceinline__ double operator()(int gi, int gj) const {
     if (gi >= k || gj >= k) return gi == gj ? 1.0 : 0.0;
-    double v = ps * P[(int64_t)F[gi] * ld + F[gj]];
+    double v = ((gi >> 6) == (gj >> 6)) ? K[(int64_t)gi * ld + gj] : K[(int64_t)min(gi, gj) * ld + max(gi, gj)];
     if (gi == gj) v += dadd;
     return v;
   }
 };
 
-__global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const int32_t* idx,
-                                               int nidx, pq_settings s, pq_lowrank lr) {
-  constexpr int LDMAX = 1024;
-  __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS + 2 * LDMAX + 14 * 64 + 64 + LDMAX + 256];
-  double* stg = smem;                  // Cholesky stream buffers; S factor during refinement
-  double* vec = smem + 4 * STAGE;      // sD region: 3 LDMAX vectors during refinement
+__device__ __forceinline__ double pc_at(const double* K, int64_t ld, int p, int q) {
+  return ((p >> 6) == (q >> 6)) ? K[(int64_t)p * ld + q] : K[(int64_t)min(p, q) * ld + max(p, q)];
+}
+
+// P_FF = psw Xc_F' Xc_F + pd I into the compact storage (lower tiles computed; diagonal
+// tiles stored in full, off-diagonal tiles transposed into the upper half).  One MFMA
+// tile product per lower tile, contracted over the window in 16-row chunks staged into LDS.
+__device__ void form_pff(const pq_lowrank& lr, int b, const int* Fl, int k, int nbk, double psw,
+                         double pd, double* Ks, int64_t ldk, double* smem) {
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const int t = threadIdx.x;
+  const int kr = t >> 4, i4 = (t & 15) * 4;
+  double* SA = smem;
+  double* SB = smem + STAGE;
+  const int ntile = nbk * (nbk + 1) / 2;
+  for (int tile = 0; tile < ntile; ++tile) {
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    const int J = tile - I * (I + 1) / 2;
+    int ca[4], cb[4];
+    double ma[4], mb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int pa = I * TB + i4 + e, pb_ = J * TB + i4 + e;
+      ca[e] = pa < k ? Fl[pa] : -1;
+      cb[e] = pb_ < k ? Fl[pb_] : -1;
+      ma[e] = (ca[e] >= 0 && mu) ? mu[ca[e]] : 0.0;
+      mb[e] = (cb[e] >= 0 && mu) ? mu[cb[e]] : 0.0;
+    }
+    Acc acc;
+    acc.zero();
+    for (int t0 = 0; t0 < T; t0 += KC) {
+      const int tt = t0 + kr;
+      const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
+      double va[4], vb[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        va[e] = (row && ca[e] >= 0) ? row[ca[e]] - ma[e] : 0.0;
+        vb[e] = (row && cb[e] >= 0) ? row[cb[e]] - mb[e] : 0.0;
+      }
+      __syncthreads();   // the previous chunk's MFMAs are done with SA / SB
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        SA[kr * LDW + i4 + e] = va[e];
+        SB[kr * LDW + i4 + e] = vb[e];
+      }
+      __syncthreads();
+      mma_lds(acc, SA, SB, KC);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = I * TB + acc_row(m, r), gj = J * TB + acc_col(nn);
+          const double v = psw * acc.c[m][nn][r] + (gi == gj ? pd : 0.0);
+          if (I == J) Ks[(int64_t)gi * ldk + gj] = v;
+          else Ks[(int64_t)gj * ldk + gi] = v;
+        }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, pq_state st,
+                                                 const int32_t* idx, int nidx, pq_settings s, int ldk,
+                                                 int final_try) {
+  __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS + 2 * KMAX + 15 * 64 + KMAX / 2 + 256];
+  double* stg = smem;                  // Cholesky / SYRK stream buffers; S factor; lr_px tree
+  double* vec = smem + 4 * STAGE;      // 3 KMAX vectors during refinement; lr_px u
   double* solx = smem + CHOL_LDS;      // compact solution x_F
-  double* rF = solx + LDMAX;           // compact rhs of the F rows
-  double* solL = rF + LDMAX;           // 64: multipliers of the active rows
+  double* rF = solx + KMAX;            // compact rhs of the F rows
+  double* solL = rF + KMAX;            // 64: multipliers of the active rows
   double* dA = solL + 64;              // 64: rhs of the active rows
   double* rl = dA + 64;                // 64
   double* wl = rl + 64;                // 64
@@ -50,12 +126,8 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
   double* red = part + 4 * 64;         // 64
   double* lamF = red + 64;             // 64: multipliers of all general rows (by row)
   double* y64p = lamF + 64;            // 4*64 partial sums of the diagonal-block products
-  // index bookkeeping lives in LDS: these arrays are rewritten every active-set round and
-  // read at wave-uniform addresses, which hipcc serves from the (non-coherent) scalar
-  // cache when they sit in global memory -- stale values in round >= 2.
-  int* fl = reinterpret_cast<int*>(y64p + 4 * 64);   // LDMAX: 0 free, 1 at lower, 2 at upper
-  int* Fl = fl + LDMAX;                               // LDMAX: free-variable list
-  int* act = Fl + LDMAX;                              // 64
+  int* Fl = reinterpret_cast<int*>(y64p + 4 * 64);   // KMAX: free-variable list
+  int* act = Fl + KMAX;                               // 64
   int* Al = act + 64;                                 // 64
   int* cnt = Al + 64;                                 // PT + 8
 
@@ -64,9 +136,9 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
   if (st0 != PQ_SOLVED && st0 != PQ_MAX_ITER) return;
   const int n = pb.n, ld = pb.ld, mg = pb.mg;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
-  const double* P = pb.P + (int64_t)b * pb.P_stride;
   const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
   const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
   const double* q = pb.q + (int64_t)b * pb.q_stride;
   const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
   const double* lg = pb.lg ? pb.lg + (int64_t)b * pb.g_stride : nullptr;
@@ -74,27 +146,30 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
   const bool has_box = pb.lb != nullptr;
   const double* lb = has_box ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
   const double* ub = has_box ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
-  double* K = st.K + (int64_t)b * st.K_stride;
-  double* Dt = st.Dt + (int64_t)b * st.Dt_stride;
+  // compact scratch: one slot per launched workgroup (a relaunch passes a smaller buffer)
+  double* K = st.K + (int64_t)blockIdx.x * st.K_stride;
+  double* Dt = st.Dt + (int64_t)blockIdx.x * st.Dt_stride;
   double* sx = st.x + (int64_t)b * ld;
   double* sz = st.z + (int64_t)b * st.m_ld;
   double* sy = st.y + (int64_t)b * st.m_ld;
-  // work layout (doubles): xs | xb | g | Px | U (mg_pad rows)
+  // work layout (doubles): xs | xb | g | Px | U (mg_pad rows of ldk) | fl (ld ints)
   double* W = st.work + (int64_t)b * st.work_stride;
   double* xs = W;
   double* xb = xs + ld;
   double* g = xb + ld;
   double* Px = g + ld;
   double* U = Px + ld;
+  int* fl = reinterpret_cast<int*>(U + (int64_t)st.mg_pad * ld);   // 0 free, 1 at lower, 2 at upper
 #ifdef PQ_PROFILE
   double* prof = W + PQ_WORK_PROF(ld, st.mg_pad);
   if (t < 16) prof[t] = 0.0;
   long long t_last_ = wall_clock64();
 #endif
 
-  // ---- problem scale -> tolerances ----------------------------------------------------
+  // ---- problem scale -> tolerances (diag P from the window's sums of squares) ----------
+  const double* dgb = lr.dg + (int64_t)b * lr.dg_stride;
   double sc = 0.0;
-  for (int i = t; i < n; i += PT) sc = fmax(sc, fmax(fabs(q[i]), fabs(ps * P[(int64_t)i * ld + i] + pd)));
+  for (int i = t; i < n; i += PT) sc = fmax(sc, fmax(fabs(q[i]), fabs(psw * dgb[i] + pd)));
   sc = block_max(sc, red);
   sc = fmax(sc, 1e-300);
   const double dtol = s.dual_tol * sc;
@@ -125,7 +200,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
   __syncthreads();
   PQ_STAMP(0);
 
-  // exact P x and gradient g = P x + q + Cg' lam of the point in xs (rows_dot_vec emit)
+  // exact P x and gradient g = P x + q + Cg' lam of the point in xs
   auto emit_g = [&](int i, double sum) {
     const double pxi = ps * sum + pd * xs[i];
     double gi = pxi + q[i];
@@ -133,14 +208,9 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     Px[i] = pxi;
     g[i] = gi;
   };
-  // P x of the point in xs: window form when given (vec / stg are free at the call sites:
-  // after refinement and in the final scoring), else the dense rows of P
-  auto full_px = [&]() {
-    if (lr.panel) lr_px(lr, b, n, xs, vec, stg, red, emit_g);
-    else rows_dot_vec(P, ld, n, n, [](int p) { return p; }, xs, emit_g);
-  };
+  auto full_px = [&]() { lr_px(lr, b, n, xs, vec, stg, red, emit_g); };
 
-  int accepted = 0, rounds = 0, nfree = 0;
+  int accepted = 0, rounds = 0, nfree = 0, overflow = 0;
   for (int round = 0; round < s.polish_rounds && !accepted; ++round) {
     rounds = round + 1;
     // ---- free list (stable compaction) ------------------------------------------------
@@ -158,14 +228,18 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
       cnt[PT + 1] = a;
     }
     __syncthreads();
+    const int k = cnt[PT];
+    const int ma = cnt[PT + 1];
+    nfree = k;
+    if (k > ldk || k > KMAX) {   // uniform: the compact scratch cannot hold this free set
+      overflow = 1;
+      break;
+    }
     {
       int p = cnt[t];
       for (int i = t * chunk; i < min(n, (t + 1) * chunk); ++i)
         if (fl[i] == 0) Fl[p++] = i;
     }
-    const int k = cnt[PT];
-    const int ma = cnt[PT + 1];
-    nfree = k;
     const int nbk = (k + TB - 1) / TB;
     int nzb = 0;
     for (int i = t; i < ld; i += PT) {
@@ -176,15 +250,12 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     nzb = block_or(nzb, red);
     PQ_STAMP(1);
     __builtin_amdgcn_s_dcache_inv();
-    // ---- reduced rhs: rF = -q_F - ps P_FB x_B ;  d_a = rhs_a - C_aB x_B -----------------
-    if (nzb && lr.panel) {   // window form (P may hold its lower triangle only): P x_B -> g
+    // ---- reduced rhs: rF = -q_F - P_FB x_B ;  d_a = rhs_a - C_aB x_B --------------------
+    if (nzb) {   // P x_B through the window (pd I does not couple F and B)
       lr_px(lr, b, n, xb, vec, stg, red, [&](int i, double sum) { g[i] = sum; });
       __syncthreads();
       for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]] - ps * g[Fl[p]];
-    } else if (nzb) {   // (long-only: every fixed weight is 0 and P_FB x_B vanishes)
-      rows_dot_vec(P, ld, n, k, [&](int p) { return Fl[p]; }, xb,
-                   [&](int p, double sum) { rF[p] = -q[Fl[p]] - ps * sum; });
-    } else {
+    } else {     // (long-only: every fixed weight is 0 and P_FB x_B vanishes)
       for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]];
     }
     for (int a = w; a < ma; a += PW) {
@@ -200,21 +271,24 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     if (t < ma) solL[t] = lamF[Al[t]];
     __syncthreads();
     PQ_STAMP(2);
-    // ---- factor M = ps P_FF + (pd + delta) I ---------------------------------------------
+    // ---- P_FF from the window, then factor P_FF + delta I --------------------------------
     int info = 0;
-    if (k > 0) info = wg_cholesky(PolishForm{P, ld, Fl, k, ps, pd + delta}, K, ld, nbk, k, Dt, smem);
+    if (k > 0) {
+      form_pff(lr, b, Fl, k, nbk, psw, pd, K, ldk, smem);
+      info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
+    }
     if (info) break;
     PQ_STAMP(3);
-    double* t1 = vec;                 // LDMAX each, inside the sD region
-    double* dx = vec + LDMAX;
-    double* rx = vec + 2 * LDMAX;
+    double* t1 = vec;                 // KMAX each, inside the sD region
+    double* dx = vec + KMAX;
+    double* rx = vec + 2 * KMAX;
     // ---- U = L^-1 C_aF' (columns a), S = U'U + delta I, factor S in stg ---------------
     for (int a = 0; a < ma; ++a) {
       const int r = Al[a];
       for (int p = t; p < nbk * TB; p += PT) rx[p] = p < k ? Cg[(int64_t)r * ld + Fl[p]] : 0.0;
       __syncthreads();
-      fwd_solve(K, ld, Dt, nbk, rx, t1, t64, y64p);
-      for (int p = t; p < nbk * TB; p += PT) U[(int64_t)a * ld + p] = t1[p];
+      fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+      for (int p = t; p < nbk * TB; p += PT) U[(int64_t)a * ldk + p] = t1[p];
       __syncthreads();
     }
     __builtin_amdgcn_s_dcache_inv();   // U is re-read below, partly at uniform addresses
@@ -223,7 +297,7 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
       double v = (i == j) ? 1.0 : 0.0;
       if (i < ma && j < ma) {
         v = (i == j) ? delta : 0.0;
-        if (j <= i) for (int p = 0; p < k; ++p) v += U[(int64_t)i * ld + p] * U[(int64_t)j * ld + p];
+        if (j <= i) for (int p = 0; p < k; ++p) v += U[(int64_t)i * ldk + p] * U[(int64_t)j * ldk + p];
       }
       stg[i * DP + j] = v;
     }
@@ -232,17 +306,13 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     PQ_STAMP(4);
     // ---- proximal iterative refinement -------------------------------------------------
     for (int itr = 0; itr < s.refine_iters; ++itr) {
-      // rx = rF - (ps P_FF + pd I) solx - C_aF' solL ;  rl = dA - C_aF solx
+      // rx = rF - P_FF solx - C_aF' solL ;  rl = dA - C_aF solx
       for (int p = w; p < k; p += PW) {
-        const int fi = Fl[p];
         double sum = 0.0;
-        for (int qq = l; qq < k; qq += 64) {   // lower triangle only: P[max][min]
-          const int fj = Fl[qq];
-          sum += P[(int64_t)max(fi, fj) * ld + min(fi, fj)] * solx[qq];
-        }
+        for (int qq = l; qq < k; qq += 64) sum += pc_at(K, ldk, p, qq) * solx[qq];
         sum = wave_sum(sum);
         if (l == 0) {
-          double v = rF[p] - ps * sum - pd * solx[p];
+          double v = rF[p] - sum;
           for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)Al[a] * ld + Fl[p]] * solL[a];
           rx[p] = v;
         }
@@ -266,11 +336,11 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
         if (t < ma) rm = fmax(rm, fabs(rl[t]));
         if (block_max(rm, red) <= 1e-13 * sc) break;
       }
-      fwd_solve(K, ld, Dt, nbk, rx, t1, t64, y64p);
+      fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
       // wl = U' t1 - rl ; dlam = S^-1 wl (S = Ls Ls', tiny, one thread)
       for (int a = w; a < ma; a += PW) {
         double sum = 0.0;
-        for (int p = l; p < k; p += 64) sum += U[(int64_t)a * ld + p] * t1[p];
+        for (int p = l; p < k; p += 64) sum += U[(int64_t)a * ldk + p] * t1[p];
         sum = wave_sum(sum);
         if (l == 0) wl[a] = sum - rl[a];
       }
@@ -291,11 +361,11 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
       // t1 <- t1 - U dlam ; dx = L^-T t1
       for (int p = t; p < nbk * TB; p += PT) {
         double v = t1[p];
-        for (int a = 0; a < ma; ++a) v -= U[(int64_t)a * ld + p] * wl[a];
+        for (int a = 0; a < ma; ++a) v -= U[(int64_t)a * ldk + p] * wl[a];
         t1[p] = v;
       }
       __syncthreads();
-      bwd_solve(K, ld, Dt, nbk, t1, dx, t64, part, y64p);
+      bwd_solve(K, ldk, Dt, nbk, t1, dx, t64, part, y64p);
       for (int p = t; p < k; p += PT) solx[p] += dx[p];
       if (t < ma) solL[t] += wl[t];
       __syncthreads();
@@ -343,6 +413,14 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
     PQ_STAMP(7);
   }
   __syncthreads();
+  if (overflow && !final_try) {   // leave the problem for a relaunch with a larger ldk
+    if (t == 0) {
+      double* o = st.out + (int64_t)b * PQ_OUT_FIELDS;
+      o[PQ_OUT_NFREE] = (double)nfree;
+      o[PQ_OUT_ROUNDS] = -1.0;
+    }
+    return;
+  }
   // ---- final point: polished or ADMM --------------------------------------------------
   if (!accepted) {
     for (int i = t; i < n; i += PT) xs[i] = sx[i];
@@ -408,35 +486,24 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
 
 }  // namespace pq
 
-static int polish_launch(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const int32_t* idx,
-                         int32_t nidx, const pq_settings* s, void* stream, const char* who) {
-  PQ_CHECK_ARG(pb && st && s, "%s: null argument", who);
-  PQ_CHECK_ARG(pb->ld <= 1024, "%s: ld=%d exceeds the LDS-resident limit 1024", who, pb->ld);
-  PQ_CHECK_ARG(pb->mg <= 64, "%s: mg must be <= 64", who);
+extern "C" int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
+                                   const int32_t* idx, int32_t nidx, const pq_settings* s, int32_t ldk,
+                                   int32_t final_try, void* stream) {
+  PQ_CHECK_ARG(lr && pb && st && s, "pq_polish_w_batched: null argument");
+  PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0 && lr->dg,
+               "pq_polish_w_batched: window (with its diagonal dg) missing");
+  PQ_CHECK_ARG((lr->ldp & 1) == 0, "pq_polish_w_batched: the window form needs an even panel stride");
+  PQ_CHECK_ARG(pb->mg <= 64 && (pb->mg == 0 || (pb->Cg && pb->lg && pb->ug)), "pq_polish_w_batched: bad general rows");
+  PQ_CHECK_ARG(ldk % 64 == 0 && ldk >= 64 && ldk <= pb->ld && ldk <= pq::KMAX,
+               "pq_polish_w_batched: need 64 <= ldk <= min(ld, %d), multiple of 64 (ldk=%d)", pq::KMAX, ldk);
+  PQ_CHECK_ARG(st->K && st->Dt && st->K_stride >= (int64_t)ldk * ldk && st->Dt_stride >= (int64_t)(ldk / 64) * 4096,
+               "pq_polish_w_batched: scratch K / Dt too small for ldk=%d", ldk);
   PQ_CHECK_ARG(st->work && st->work_stride >= PQ_WORK_DOUBLES(pb->ld, st->mg_pad),
-               "%s: work buffer too small", who);
-  pq_lowrank l = {};
-  if (lr) {
-    PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0 && lr->tmax <= 1024,
-                 "%s: window missing or tmax > 1024", who);
-    PQ_CHECK_ARG((lr->ldp & 1) == 0, "%s: the window form needs an even panel stride", who);
-    l = *lr;
-  }
+               "pq_polish_w_batched: work buffer too small");
   const int grid = idx ? nidx : pb->batch;
   if (grid <= 0) return 0;
-  hipLaunchKernelGGL(pq::k_polish, dim3(grid), dim3(pq::PT), 0, (hipStream_t)stream, *pb, *st, idx, nidx, *s, l);
-  PQ_CHECK_LAUNCH(who);
+  hipLaunchKernelGGL(pq::k_polish_w, dim3(grid), dim3(pq::PT), 0, (hipStream_t)stream, *lr, *pb, *st, idx,
+                     nidx, *s, ldk, final_try);
+  PQ_CHECK_LAUNCH("pq_polish_w_batched");
   return 0;
-}
-
-extern "C" int pq_polish_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
-                                 const pq_settings* s, void* stream) {
-  return polish_launch(nullptr, pb, st, idx, nidx, s, stream, "pq_polish_batched");
-}
-
-extern "C" int pq_polish_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
-                                    const int32_t* idx, int32_t nidx, const pq_settings* s,
-                                    void* stream) {
-  PQ_CHECK_ARG(lr != nullptr, "pq_polish_lr_batched: null window description");
-  return polish_launch(lr, pb, st, idx, nidx, s, stream, "pq_polish_lr_batched");
 }

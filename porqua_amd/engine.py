@@ -121,7 +121,8 @@ class QPBatch:
         bs = 0 if (self.shared or not self.has_box) else self.lb.stride(0)
         return _lib.PQProblem(
             n=self.n, ld=ld, batch=self.batch, mg=self.mg,
-            P=self.P.data_ptr(), P_stride=self.P.stride(0),
+            P=None if self.P is None else self.P.data_ptr(),
+            P_stride=0 if self.P is None else self.P.stride(0),
             p_scale=None if self.p_scale is None else self.p_scale.data_ptr(),
             p_diag=None if self.p_diag is None else self.p_diag.data_ptr(),
             q=self.q.data_ptr(), q_stride=self.q.stride(0),
@@ -210,17 +211,25 @@ class QPBatch:
         return self
 
 
-class Workspace:
-    """Solver state for a QPBatch (all device memory; nothing persistent in the library)."""
+LR_POLISH_LDK = 256      # first compact polish scratch of the window path (free set <= 256)
 
-    def __init__(self, qb: QPBatch, dense: bool = True):
+
+class Workspace:
+    """Solver state for a QPBatch (all device memory; nothing persistent in the library).
+
+    ``dense`` (K2/K3/K4 on P itself): K / Dt are the n x n KKT inverse and polish scratch.
+    Otherwise (the window path) they are only the compact ldk x ldk polish scratch of
+    pq_polish_w_batched, ldk = ``kcap`` (default min(ld, LR_POLISH_LDK))."""
+
+    def __init__(self, qb: QPBatch, dense: bool = True, kcap: int | None = None):
         B, ld, dev = qb.batch, qb.ld, qb.device
         self.B, self.device = B, dev
         self.mg_pad = qb.mg_pad
         self.m_ld = qb.mg_pad + ld
-        # K / Dt: the dense KKT inverse (K2 / K3) and the polish scratch (K4)
-        self.K = torch.empty((B, ld, ld), dtype=F64, device=dev)
-        self.Dt = torch.empty((B, ld // 64, 64, 64), dtype=F64, device=dev)
+        self.ldk = ld if dense else min(ld, 1024, round_up(kcap or LR_POLISH_LDK, 64))
+        kd = self.ldk
+        self.K = torch.empty((B, kd, kd), dtype=F64, device=dev)
+        self.Dt = torch.empty((B, kd // 64, 64, 64), dtype=F64, device=dev)
         self._lr = None
         self.x = torch.zeros((B, ld), dtype=F64, device=dev)
         self.Px = torch.zeros((B, ld), dtype=F64, device=dev)
@@ -341,19 +350,27 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
 
 
 class LowRank:
-    """Device description of P_eff = p_scale Xc'Xc + p_diag I through the date windows
-    (pq_lowrank): nothing n x n is formed.  ``mu`` None = uncentred Gram (LeastSquares)."""
+    """Device description of P_eff = p_scale w_scale Xc'Xc + p_diag I through the date
+    windows (pq_lowrank): nothing n x n is formed.  ``mu`` None = uncentred Gram
+    (LeastSquares).  ``dg`` = diag(Xc'Xc) per date (pq_window_sumsq; computed here when
+    not given -- call refresh() after the window means change in place)."""
 
-    def __init__(self, panel, rows, tlen, mu=None, w_scale=None):
+    def __init__(self, panel, rows, tlen, mu=None, w_scale=None, dg=None):
         self.panel, self.rows, self.tlen, self.mu, self.w_scale = panel, rows, tlen, mu, w_scale
         self.tmax = int(rows.shape[1])
+        self.dg = dg if dg is not None else panel.window_sumsq(rows, tlen, mu)
+
+    def refresh(self):
+        self.panel.window_sumsq(self.rows, self.tlen, self.mu, out=self.dg)
+        return self
 
     def c_struct(self) -> _lib.PQLowRank:
         return _lib.PQLowRank(panel=self.panel.R.data_ptr(), ldp=self.panel.R.stride(0),
                               rows=self.rows.data_ptr(), tlen=self.tlen.data_ptr(), tmax=self.tmax,
                               mu=None if self.mu is None else self.mu.data_ptr(),
                               mu_stride=0 if self.mu is None else self.mu.stride(0),
-                              w_scale=None if self.w_scale is None else self.w_scale.data_ptr())
+                              w_scale=None if self.w_scale is None else self.w_scale.data_ptr(),
+                              dg=self.dg.data_ptr(), dg_stride=self.dg.stride(0))
 
 
 def lowrank_shape_ok(n: int, tmax: int, mg: int) -> bool:
@@ -371,7 +388,7 @@ def lowrank_applicable(qb: QPBatch, lr: LowRank) -> bool:
 def grouped_applicable(qb: QPBatch, lr: LowRank, groups: "GroupPlan | None", ws: "Workspace") -> bool:
     k_ld = round_up(lr.tmax + qb.mg, 64)
     return (groups is not None and groups.ok and qb.n % 2 == 0 and lr.panel.R.stride(0) % 2 == 0
-            and qb.mg <= 4 and k_ld <= 384 and ws.work_stride >= 3 * qb.ld)
+            and qb.mg <= 32 and k_ld <= 384 and ws.work_stride >= 3 * qb.ld)
 
 
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
@@ -379,12 +396,14 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
-    windows when a GroupPlan is given), K4 = polish (needs the dense P in qb.P)."""
+    windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
+    may be None): P is the window (lr) throughout."""
     tl = _Timeline(events)
     lib = _lib.load()
     s = (settings or Settings()).to_c()
     ws = ws or Workspace(qb, dense=False)
     B, dev = qb.batch, qb.device
+    ldk = ws.ldk
     k = lr.tmax + qb.mg
     k_ld = round_up(k, 64)
     if not lowrank_applicable(qb, lr):
@@ -408,7 +427,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     strm = _stream()
     P_, S_, SS, L_ = ctypes.byref(pb), ctypes.byref(st), ctypes.byref(s), ctypes.byref(lrs)
     PM_, SM_, SSM = ctypes.byref(pbM), ctypes.byref(stM), ctypes.byref(sM)
-    _lib.check(lib.pq_init_state(P_, S_, None, 0, SS, strm), "pq_init_state")
+    _lib.check(lib.pq_init_state_lr(L_, P_, S_, None, 0, SS, strm), "pq_init_state_lr")
 
     def refactor(idx, nidx):
         _lib.check(lib.pq_lr_capacitance(L_, P_, S_, _ptr(idx), nidx, SS, M["M"].data_ptr(), k_ld,
@@ -440,12 +459,23 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         tl("factor", lambda: refactor(idx, nidx))
         refactors += kk
     if s.polish and polish:
-        if lr.tmax <= 1024 and lr.panel.R.stride(0) % 2 == 0:
-            _lib.check(tl("polish", lambda: lib.pq_polish_lr_batched(L_, P_, S_, None, 0, SS, strm)),
-                       "pq_polish_lr_batched")
-        else:
-            _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, None, 0, SS, strm)),
-                       "pq_polish_batched")
+        kmax = min(qb.ld, 1024)
+        final = ldk >= kmax
+        _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, S_, None, 0, SS, ldk, int(final), strm)),
+                   "pq_polish_w_batched")
+        if not final:   # free sets larger than the compact scratch: relaunch those with ldk = kmax
+            over = torch.nonzero(ws.out[:, _lib.PQ_OUT_ROUNDS] < 0).flatten().to(torch.int32)
+            m = int(over.numel())   # host sync: small vector
+            if m:
+                K2 = torch.empty((m, kmax, kmax), dtype=F64, device=dev)
+                D2 = torch.empty((m, kmax // 64, 64, 64), dtype=F64, device=dev)
+                st2 = ws.c_struct()
+                st2.K, st2.K_stride = K2.data_ptr(), K2.stride(0)
+                st2.Dt, st2.Dt_stride = D2.data_ptr(), D2.stride(0)
+                over = over.contiguous()
+                _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, ctypes.byref(st2), _ptr(over), m,
+                                                                        SS, kmax, 1, strm)),
+                           "pq_polish_w_batched (relaunch)")
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
@@ -607,6 +637,17 @@ class Panel:
         if bm is not None:
             y = bm if isinstance(bm, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(bm, dtype=np.float64).reshape(-1))
             self.bm = y.to(self.device, dtype=F64).contiguous()
+
+    def window_sumsq(self, rows, tlen, mu=None, out=None):
+        """diag(Xc'Xc) of every window (mu None: diag X'X) -> (B, round_up(n, 64))."""
+        lib = _lib.load()
+        B, tmax = rows.shape
+        if out is None:
+            out = torch.zeros((B, round_up(self.n, 64)), dtype=F64, device=self.device)
+        _lib.check(lib.pq_window_sumsq(_ptr(self.R), self.R.stride(0), self.n, _ptr(rows), _ptr(tlen), tmax, B,
+                                       _ptr(mu), 0 if mu is None else mu.stride(0), _ptr(out), out.stride(0),
+                                       _stream()), "pq_window_sumsq")
+        return out
 
     def rows_to_device(self, rows, tlen):
         r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int32)).to(self.device)

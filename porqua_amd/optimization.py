@@ -145,18 +145,18 @@ class MeanVariance(Optimization):
         import torch
         from . import engine
         lowrank = stage.prefer_lowrank and self.covariance.spec["method"] != "duv"
-        S, pdiag, mu_c = self.covariance.estimate_batch_lr(
-            stage.panel, stage.rows, stage.tlen, out=stage.P_buffer(), plan=stage.slide_plan(),
-            lower_only=lowrank)
+        S, pdiag, mu_c, dg = self.covariance.estimate_batch_lr(
+            stage.panel, stage.rows, stage.tlen, out=None if lowrank else stage.P_buffer(),
+            plan=stage.slide_plan(), materialise=not lowrank)
         ra = float(self.params["risk_aversion"])
         B = stage.batch
         dev = stage.device
-        if S is None:  # duv: identity covariance
+        if mu_c is None:  # duv: identity covariance
             S = stage.identity_P()
             pdiag = torch.zeros(B, dtype=torch.float64, device=dev)
-        elif lowrank:   # factored form S = Xc'Xc / (T - 1) for the Woodbury solver
+        elif lowrank:   # factored form S = Xc'Xc / (T - 1) for the Woodbury solver (no n x n S)
             stage.lowrank = engine.LowRank(stage.panel, stage.rows, stage.tlen, mu=mu_c,
-                                           w_scale=1.0 / (stage.tlen.to(torch.float64) - 1.0))
+                                           w_scale=1.0 / (stage.tlen.to(torch.float64) - 1.0), dg=dg)
         me = self.mean_estimator
         if me.spec.get("method") != "geometric":
             return None
@@ -227,10 +227,11 @@ class LeastSquares(Optimization):
             pan = stage.log1p_panel()
         else:
             pan = stage.panel
-        G = pan.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer(), plan=stage.slide_plan(),
-                    lower_only=stage.prefer_lowrank)
-        if stage.prefer_lowrank:   # factored form X'X (uncentred) for the Woodbury solver
+        if stage.prefer_lowrank:   # factored form X'X (uncentred) for the Woodbury solver (no n x n G)
+            G = None
             stage.lowrank = engine.LowRank(pan, stage.rows, stage.tlen, mu=None)
+        else:
+            G = pan.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer(), plan=stage.slide_plan())
         xty, yty = pan.gram_xy(stage.rows, stage.tlen)
         B, dev = stage.batch, stage.device
         l2 = self.params.get("l2_penalty")
