@@ -44,10 +44,10 @@ extern "C" {
 #define PQ_OUT_ROUNDS 6     /* polish active-set rounds                                 */
 #define PQ_OUT_FIELDS 8
 
-/* polish scratch per problem (doubles): xs | xb | g | Px | U (mg_pad rows) | flags (ld
- * int32) | 512 spare (the PQ_PROFILE phase timers sit at PQ_WORK_PROF)                  */
-#define PQ_WORK_DOUBLES(ld, mg_pad) ((int64_t)(5 + (mg_pad)) * (ld) + 512)
-#define PQ_WORK_PROF(ld, mg_pad) ((int64_t)(5 + (mg_pad)) * (ld))
+/* polish scratch per problem (doubles): xs | xb | g | Px | 4 Woodbury-mode vectors |
+ * U (mg_pad rows) | flags (ld int32) | 512 spare (PQ_PROFILE phase timers at PQ_WORK_PROF) */
+#define PQ_WORK_DOUBLES(ld, mg_pad) ((int64_t)(9 + (mg_pad)) * (ld) + 512)
+#define PQ_WORK_PROF(ld, mg_pad) ((int64_t)(9 + (mg_pad)) * (ld))
 
 /* A batch of dense QPs   min 0.5 x'Px + q'x  s.t.  lg <= Cg x <= ug,  lb <= x <= ub
  * (the QuadraticProgram fields P, q, G, h, A, b, lb, ub of src/qp_problems.py:34-38 with

@@ -31,7 +31,7 @@ PQ_OUT_FIELDS = 8
 
 def work_doubles(ld: int, mg_pad: int) -> int:
     """PQ_WORK_DOUBLES of include/porqua_hip.h."""
-    return (5 + mg_pad) * ld + 512
+    return (9 + mg_pad) * ld + 512
 
 
 class PorquaHipError(RuntimeError):

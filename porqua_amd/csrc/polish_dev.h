@@ -124,29 +124,26 @@ __device__ __forceinline__ void rows_dot_vec(const double* P, int64_t ld, int n,
   }
 }
 
-// emit(i, w_scale * (Xc' Xc x)_i) for i < n from the window form of P (pq_lowrank): two
-// passes over the date's window rows (shared by neighbouring dates, so L2-resident)
-// instead of n^2 bytes of P.  Columns go in chunks of 1024 (lane l owns columns
-// c0 + 128 q + 2 l, + 1 of a chunk; 16-B loads), so n is unbounded.  x: global, zero from
-// n to the next even index.  u: LDS >= tmax doubles; tree: LDS >= 2 * 1024 doubles; red:
-// LDS reduction scratch.  Row t of pass 1 is always owned by the same wave, so its
-// partial dot products accumulate across chunks in u[t] without barriers.
-template <typename EmitF>
-__device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* tree,
-                      double* red, EmitF emit) {
+// Window passes of P = w_scale Xc'Xc (pq_lowrank), shared by neighbouring dates, so the
+// rows are L2-resident.  Columns go in chunks of 1024 (lane l owns columns
+// c0 + 128 q + 2 l, + 1 of a chunk; 16-B loads), so n is unbounded.  Vectors in global
+// memory must be zero from n to the next even index.
+//
+// lr_pass1: u_t = Xc_t . x = X_t . x - mu . x for t < T (u in LDS, >= T doubles).  Row t
+// is always owned by the same wave, so its partial dot products accumulate across column
+// chunks in u[t] without barriers.  Ends with a barrier.
+__device__ void lr_pass1(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* red) {
   constexpr int NQ = 8, RU = 4, LM = NQ * 128;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const int T = lr.tlen[b];
   const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
-  const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
   double mux = 0.0;
   if (mu) {
     double a = 0.0;
     for (int i = t; i < n; i += PT) a += mu[i] * x[i];
     mux = block_sum(a, red);
   }
-  // pass 1: u_t = X_t . x - mu . x
   for (int c0 = 0; c0 < n; c0 += LM) {
     double2 vr[NQ];
 #pragma unroll
@@ -181,13 +178,25 @@ __device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, doubl
     }
   }
   __syncthreads();
+}
+
+// lr_pass2: emit(i, (Xc' u)_i) = sum_t u_t X_ti - mu_i sum_t u_t for i < n (u in LDS,
+// T entries).  Register accumulators per chunk, then a fixed-order wave tree in `tree`
+// (LDS >= 2 * 1024 doubles): bit-reproducible.  emit runs on wave 0.
+template <typename EmitF>
+__device__ void lr_pass2(const pq_lowrank& lr, int b, int n, const double* u, double* tree, double* red,
+                         EmitF emit) {
+  constexpr int NQ = 8, RU = 4, LM = NQ * 128;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
   double su = 0.0;
   if (mu) {
     double a = 0.0;
     for (int tt = t; tt < T; tt += PT) a += u[tt];
     su = block_sum(a, red);
   }
-  // pass 2 per chunk: acc = sum_t u_t X_t (register accumulators), then a fixed-order wave tree
   for (int c0 = 0; c0 < n; c0 += LM) {
     double2 acc[NQ];
 #pragma unroll
@@ -236,11 +245,20 @@ __device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, doubl
 #pragma unroll
       for (int qq = 0; qq < NQ; ++qq) {
         const int c = c0 + 128 * qq + 2 * l;
-        if (c < n) emit(c, wsc * (acc[qq].x - (mu ? mu[c] * su : 0.0)));
-        if (c + 1 < n) emit(c + 1, wsc * (acc[qq].y - (mu ? mu[c + 1] * su : 0.0)));
+        if (c < n) emit(c, acc[qq].x - (mu ? mu[c] * su : 0.0));
+        if (c + 1 < n) emit(c + 1, acc[qq].y - (mu ? mu[c + 1] * su : 0.0));
       }
     }
   }
+}
+
+// emit(i, w_scale * (Xc' Xc x)_i) for i < n: both passes (u: LDS >= tmax doubles).
+template <typename EmitF>
+__device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* tree,
+                      double* red, EmitF emit) {
+  const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
+  lr_pass1(lr, b, n, x, u, red);
+  lr_pass2(lr, b, n, u, tree, red, [&](int i, double v) { emit(i, wsc * v); });
 }
 
 }  // namespace pq

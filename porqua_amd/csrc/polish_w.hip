@@ -109,6 +109,66 @@ __device__ void form_pff(const pq_lowrank& lr, int b, const int* Fl, int k, int 
   __syncthreads();
 }
 
+// Woodbury mode: C = cdiag I + Xc diag(free) Xc' (T x T) into the lower tiles (diagonal
+// tiles in full) of Ks; rows / columns >= T are the identity.  Contraction over all n
+// columns (free-masked), 16 at a time through LDS, one MFMA tile product per lower tile.
+__device__ void form_cwood(const pq_lowrank& lr, int b, int n, const int* fl, int nbt, double cdiag,
+                           double* Ks, int64_t ldk, double* smem) {
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const int t = threadIdx.x;
+  const int i = t >> 2, cc = (t & 3) * 4;
+  double* SA = smem;
+  double* SB = smem + STAGE;
+  const int ntile = nbt * (nbt + 1) / 2;
+  for (int tile = 0; tile < ntile; ++tile) {
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    const int J = tile - I * (I + 1) / 2;
+    const double* ra = I * TB + i < T ? lr.panel + (int64_t)rws[I * TB + i] * lr.ldp : nullptr;
+    const double* rb = J * TB + i < T ? lr.panel + (int64_t)rws[J * TB + i] * lr.ldp : nullptr;
+    Acc acc;
+    acc.zero();
+    for (int c0 = 0; c0 < n; c0 += KC) {
+      double va[4], vb[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c0 + cc + e;
+        const bool m = c < n && fl[c] == 0;
+        const double mc = (m && mu) ? mu[c] : 0.0;
+        va[e] = (m && ra) ? ra[c] - mc : 0.0;
+        vb[e] = (m && rb) ? rb[c] - mc : 0.0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        SA[(cc + e) * LDW + i] = va[e];
+        SB[(cc + e) * LDW + i] = vb[e];
+      }
+      __syncthreads();
+      mma_lds(acc, SA, SB, KC);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = I * TB + acc_row(m, r), gj = J * TB + acc_col(nn);
+          Ks[(int64_t)gi * ldk + gj] = acc.c[m][nn][r] + (gi == gj ? (gi < T ? cdiag : 1.0) : 0.0);
+        }
+  }
+  __syncthreads();
+}
+
+struct FormRead {   // the lower tiles (diagonal tiles in full) as written
+  const double* K;
+  int64_t ld;
+  __device__ __forceinline__ double operator()(int gi, int gj) const { return K[(int64_t)gi * ld + gj]; }
+};
+
 __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, pq_state st,
                                                  const int32_t* idx, int nidx, pq_settings s, int ldk,
                                                  int final_try) {
@@ -152,13 +212,14 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
   double* sx = st.x + (int64_t)b * ld;
   double* sz = st.z + (int64_t)b * st.m_ld;
   double* sy = st.y + (int64_t)b * st.m_ld;
-  // work layout (doubles): xs | xb | g | Px | U (mg_pad rows of ldk) | fl (ld ints)
+  // work layout (doubles): xs | xb | g | Px | wr wx wt wd (Woodbury mode) | U (mg_pad rows:
+  // ldk-strided L^-1 C_aF' in compact mode, n-length A^-1 C_aF' in Woodbury mode) | fl (ld ints)
   double* W = st.work + (int64_t)b * st.work_stride;
   double* xs = W;
   double* xb = xs + ld;
   double* g = xb + ld;
   double* Px = g + ld;
-  double* U = Px + ld;
+  double* U = W + 8 * (int64_t)ld;
   int* fl = reinterpret_cast<int*>(U + (int64_t)st.mg_pad * ld);   // 0 free, 1 at lower, 2 at upper
 #ifdef PQ_PROFILE
   double* prof = W + PQ_WORK_PROF(ld, st.mg_pad);
@@ -210,6 +271,8 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
   };
   auto full_px = [&]() { lr_px(lr, b, n, xs, vec, stg, red, emit_g); };
 
+  // Woodbury mode (free set beyond the compact scratch) needs the T x T capacitance to fit
+  const bool wood_ok = ((lr.tmax + TB - 1) / TB) * TB <= ldk && lr.tmax <= KMAX;
   int accepted = 0, rounds = 0, nfree = 0, overflow = 0;
   for (int round = 0; round < s.polish_rounds && !accepted; ++round) {
     rounds = round + 1;
@@ -231,11 +294,12 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
     const int k = cnt[PT];
     const int ma = cnt[PT + 1];
     nfree = k;
-    if (k > ldk || k > KMAX) {   // uniform: the compact scratch cannot hold this free set
+    const bool compact = k <= ldk && k <= KMAX;   // uniform (k from LDS)
+    if (!compact && !wood_ok) {   // neither the compact nor the Woodbury scratch fits
       overflow = 1;
       break;
     }
-    {
+    if (compact) {
       int p = cnt[t];
       for (int i = t * chunk; i < min(n, (t + 1) * chunk); ++i)
         if (fl[i] == 0) Fl[p++] = i;
@@ -250,135 +314,275 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
     nzb = block_or(nzb, red);
     PQ_STAMP(1);
     __builtin_amdgcn_s_dcache_inv();
-    // ---- reduced rhs: rF = -q_F - P_FB x_B ;  d_a = rhs_a - C_aB x_B --------------------
-    if (nzb) {   // P x_B through the window (pd I does not couple F and B)
-      lr_px(lr, b, n, xb, vec, stg, red, [&](int i, double sum) { g[i] = sum; });
-      __syncthreads();
-      for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]] - ps * g[Fl[p]];
-    } else {     // (long-only: every fixed weight is 0 and P_FB x_B vanishes)
-      for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]];
-    }
-    for (int a = w; a < ma; a += PW) {
-      const int r = Al[a];
-      const double* c = Cg + (int64_t)r * ld;
-      double sum = 0.0;
-      for (int j = l; j < n; j += 64) sum += c[j] * xb[j];
-      sum = wave_sum(sum);
-      if (l == 0) dA[a] = (act[r] == 1 ? lg[r] : ug[r]) - sum;
-    }
-    for (int p = k + t; p < nbk * TB; p += PT) rF[p] = 0.0;
-    for (int p = t; p < k; p += PT) solx[p] = xs[Fl[p]];
-    if (t < ma) solL[t] = lamF[Al[t]];
-    __syncthreads();
-    PQ_STAMP(2);
-    // ---- P_FF from the window, then factor P_FF + delta I --------------------------------
-    int info = 0;
-    if (k > 0) {
-      form_pff(lr, b, Fl, k, nbk, psw, pd, K, ldk, smem);
-      info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
-    }
-    if (info) break;
-    PQ_STAMP(3);
-    double* t1 = vec;                 // KMAX each, inside the sD region
-    double* dx = vec + KMAX;
-    double* rx = vec + 2 * KMAX;
-    // ---- U = L^-1 C_aF' (columns a), S = U'U + delta I, factor S in stg ---------------
-    for (int a = 0; a < ma; ++a) {
-      const int r = Al[a];
-      for (int p = t; p < nbk * TB; p += PT) rx[p] = p < k ? Cg[(int64_t)r * ld + Fl[p]] : 0.0;
-      __syncthreads();
-      fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
-      for (int p = t; p < nbk * TB; p += PT) U[(int64_t)a * ldk + p] = t1[p];
-      __syncthreads();
-    }
-    __builtin_amdgcn_s_dcache_inv();   // U is re-read below, partly at uniform addresses
-    for (int e = t; e < TB * TB; e += PT) {
-      const int i = e >> 6, j = e & 63;
-      double v = (i == j) ? 1.0 : 0.0;
-      if (i < ma && j < ma) {
-        v = (i == j) ? delta : 0.0;
-        if (j <= i) for (int p = 0; p < k; ++p) v += U[(int64_t)i * ldk + p] * U[(int64_t)j * ldk + p];
+    if (!compact) {
+      // ---- Woodbury mode: A = P_FF + delta I = psw Xc_F'Xc_F + dl I on F, applied as
+      //      A^-1 v = (v - Xc_F' C^-1 Xc_F v) / dl with C = (dl / psw) I + Xc_F Xc_F' (T x T);
+      //      every vector is n-length in the work buffer (zero outside F) ------------------
+      const int T = lr.tlen[b];
+      const int nbt = (T + TB - 1) / TB;
+      const double dl = pd + delta;
+      double* wr = W + 4 * (int64_t)ld;    // rF on F
+      double* wx = wr + ld;                // x_F
+      double* wt = wx + ld;                // A^-1 rx
+      double* wd = wt + ld;                // rx (also the C_aF' staging)
+      double* u = vec;                     // T (+ padding): Xc v
+      double* y1 = vec + KMAX;
+      double* y2 = vec + 2 * KMAX;
+      double* tree = solx;                 // solx | rF (2 KMAX doubles) are unused in this mode
+      if (nzb) {
+        lr_px(lr, b, n, xb, u, tree, red, [&](int i, double sum) { g[i] = sum; });
+        __syncthreads();
       }
-      stg[i * DP + j] = v;
-    }
-    __syncthreads();
-    if (tile_potrf_lds(stg, ma)) break;
-    PQ_STAMP(4);
-    // ---- proximal iterative refinement -------------------------------------------------
-    for (int itr = 0; itr < s.refine_iters; ++itr) {
-      // rx = rF - P_FF solx - C_aF' solL ;  rl = dA - C_aF solx
-      for (int p = w; p < k; p += PW) {
-        double sum = 0.0;
-        for (int qq = l; qq < k; qq += 64) sum += pc_at(K, ldk, p, qq) * solx[qq];
-        sum = wave_sum(sum);
-        if (l == 0) {
-          double v = rF[p] - sum;
-          for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)Al[a] * ld + Fl[p]] * solL[a];
-          rx[p] = v;
-        }
+      for (int i = t; i < ld; i += PT) {
+        const bool f = i < n && fl[i] == 0;
+        wr[i] = f ? -q[i] - (nzb ? ps * g[i] : 0.0) : 0.0;
+        wx[i] = f ? xs[i] : 0.0;
+        wt[i] = 0.0;
+        wd[i] = 0.0;
       }
-      for (int p = k + t; p < nbk * TB; p += PT) rx[p] = 0.0;
       for (int a = w; a < ma; a += PW) {
+        const int r = Al[a];
+        const double* c = Cg + (int64_t)r * ld;
+        double sum = 0.0;
+        for (int j = l; j < n; j += 64) sum += c[j] * xb[j];
+        sum = wave_sum(sum);
+        if (l == 0) dA[a] = (act[r] == 1 ? lg[r] : ug[r]) - sum;
+      }
+      if (t < ma) solL[t] = lamF[Al[t]];
+      __syncthreads();
+      PQ_STAMP(2);
+      form_cwood(lr, b, n, fl, nbt, dl / psw, K, ldk, smem);
+      const int info = wg_cholesky(FormRead{K, ldk}, K, ldk, nbt, T, Dt, smem);
+      if (info) break;
+      PQ_STAMP(3);
+      auto apply = [&](const double* v, double* out) {   // out = A^-1 v on F, 0 elsewhere
+        lr_pass1(lr, b, n, v, u, red);
+        for (int p = T + t; p < nbt * TB; p += PT) u[p] = 0.0;
+        __syncthreads();
+        fwd_solve(K, ldk, Dt, nbt, u, y1, t64, y64p);
+        bwd_solve(K, ldk, Dt, nbt, y1, y2, t64, part, y64p);
+        lr_pass2(lr, b, n, y2, tree, red,
+                 [&](int i, double sv) { out[i] = fl[i] == 0 ? (v[i] - sv) / dl : 0.0; });
+        for (int i = n + t; i < ld; i += PT) out[i] = 0.0;
+        __syncthreads();
+      };
+      // Z_a = A^-1 C_aF' (rows of U), S = C_aF Z + delta I (lower, in stg)
+      for (int a = 0; a < ma; ++a) {
         const double* c = Cg + (int64_t)Al[a] * ld;
+        for (int i = t; i < n; i += PT) wd[i] = fl[i] == 0 ? c[i] : 0.0;
+        __syncthreads();
+        apply(wd, U + (int64_t)a * ld);
+      }
+      __builtin_amdgcn_s_dcache_inv();
+      for (int e = w; e < ma * ma; e += PW) {
+        const int i = e / ma, j = e % ma;
+        if (j > i) continue;
+        const double* c = Cg + (int64_t)Al[i] * ld;
+        const double* z = U + (int64_t)j * ld;
         double sum = 0.0;
-        for (int p = l; p < k; p += 64) sum += c[Fl[p]] * solx[p];
+        for (int x = l; x < n; x += 64) sum += c[x] * z[x];
         sum = wave_sum(sum);
-        if (l == 0) {
-          const double v = dA[a] - sum;
-          // rounding-level residuals of a row with no free support must not move lam
-          rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dA[a]) + fabs(sum)) ? 0.0 : v;
-        }
+        if (l == 0) stg[i * DP + j] = sum + (i == j ? delta : 0.0);
       }
       __syncthreads();
-      {  // converged to rounding level: further refinement steps change nothing
-        double rm = 0.0;
-        for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
-        if (t < ma) rm = fmax(rm, fabs(rl[t]));
-        if (block_max(rm, red) <= 1e-13 * sc) break;
+      if (tile_potrf_lds(stg, ma)) break;
+      PQ_STAMP(4);
+      for (int itr = 0; itr < s.refine_iters; ++itr) {
+        // wd = rF - P_FF x_F - C_aF' solL on F ;  rl = dA - C_aF x_F
+        lr_px(lr, b, n, wx, u, tree, red, [&](int i, double sum) {
+          double v = 0.0;
+          if (fl[i] == 0) {
+            v = wr[i] - ps * sum - pd * wx[i];
+            for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)Al[a] * ld + i] * solL[a];
+          }
+          wd[i] = v;
+        });
+        for (int a = w; a < ma; a += PW) {
+          const double* c = Cg + (int64_t)Al[a] * ld;
+          double sum = 0.0;
+          for (int x = l; x < n; x += 64) sum += c[x] * wx[x];
+          sum = wave_sum(sum);
+          if (l == 0) {
+            const double v = dA[a] - sum;
+            rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dA[a]) + fabs(sum)) ? 0.0 : v;
+          }
+        }
+        __syncthreads();
+        {
+          double rm = 0.0;
+          for (int i = t; i < n; i += PT) rm = fmax(rm, fabs(wd[i]));
+          if (t < ma) rm = fmax(rm, fabs(rl[t]));
+          if (block_max(rm, red) <= 1e-13 * sc) break;
+        }
+        apply(wd, wt);
+        for (int a = w; a < ma; a += PW) {   // wl = C_aF t1 - rl
+          const double* c = Cg + (int64_t)Al[a] * ld;
+          double sum = 0.0;
+          for (int x = l; x < n; x += 64) sum += c[x] * wt[x];
+          sum = wave_sum(sum);
+          if (l == 0) wl[a] = sum - rl[a];
+        }
+        __syncthreads();
+        if (t == 0) {
+          for (int i = 0; i < ma; ++i) {
+            double v = wl[i];
+            for (int j = 0; j < i; ++j) v -= stg[i * DP + j] * wl[j];
+            wl[i] = v / stg[i * DP + i];
+          }
+          for (int i = ma - 1; i >= 0; --i) {
+            double v = wl[i];
+            for (int j = i + 1; j < ma; ++j) v -= stg[j * DP + i] * wl[j];
+            wl[i] = v / stg[i * DP + i];
+          }
+        }
+        __syncthreads();
+        for (int i = t; i < n; i += PT) {
+          if (fl[i] == 0) {
+            double v = wt[i];
+            for (int a = 0; a < ma; ++a) v -= U[(int64_t)a * ld + i] * wl[a];
+            wx[i] += v;
+          }
+        }
+        if (t < ma) solL[t] += wl[t];
+        __syncthreads();
       }
-      fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
-      // wl = U' t1 - rl ; dlam = S^-1 wl (S = Ls Ls', tiny, one thread)
+      PQ_STAMP(5);
+      for (int i = t; i < n; i += PT) xs[i] = fl[i] == 0 ? wx[i] : xb[i];
+      if (t < 64) lamF[t] = 0.0;
+      __syncthreads();
+      if (t < ma) lamF[Al[t]] = solL[t];
+      __syncthreads();
+    } else {
+      // ---- reduced rhs: rF = -q_F - P_FB x_B ;  d_a = rhs_a - C_aB x_B --------------------
+      if (nzb) {   // P x_B through the window (pd I does not couple F and B)
+        lr_px(lr, b, n, xb, vec, stg, red, [&](int i, double sum) { g[i] = sum; });
+        __syncthreads();
+        for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]] - ps * g[Fl[p]];
+      } else {     // (long-only: every fixed weight is 0 and P_FB x_B vanishes)
+        for (int p = t; p < k; p += PT) rF[p] = -q[Fl[p]];
+      }
       for (int a = w; a < ma; a += PW) {
+        const int r = Al[a];
+        const double* c = Cg + (int64_t)r * ld;
         double sum = 0.0;
-        for (int p = l; p < k; p += 64) sum += U[(int64_t)a * ldk + p] * t1[p];
+        for (int j = l; j < n; j += 64) sum += c[j] * xb[j];
         sum = wave_sum(sum);
-        if (l == 0) wl[a] = sum - rl[a];
+        if (l == 0) dA[a] = (act[r] == 1 ? lg[r] : ug[r]) - sum;
       }
+      for (int p = k + t; p < nbk * TB; p += PT) rF[p] = 0.0;
+      for (int p = t; p < k; p += PT) solx[p] = xs[Fl[p]];
+      if (t < ma) solL[t] = lamF[Al[t]];
       __syncthreads();
-      if (t == 0) {
-        for (int i = 0; i < ma; ++i) {            // forward Ls
-          double v = wl[i];
-          for (int j = 0; j < i; ++j) v -= stg[i * DP + j] * wl[j];
-          wl[i] = v / stg[i * DP + i];
+      PQ_STAMP(2);
+      // ---- P_FF from the window, then factor P_FF + delta I --------------------------------
+      int info = 0;
+      if (k > 0) {
+        form_pff(lr, b, Fl, k, nbk, psw, pd, K, ldk, smem);
+        info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
+      }
+      if (info) break;
+      PQ_STAMP(3);
+      double* t1 = vec;                 // KMAX each, inside the sD region
+      double* dx = vec + KMAX;
+      double* rx = vec + 2 * KMAX;
+      // ---- U = L^-1 C_aF' (columns a), S = U'U + delta I, factor S in stg ---------------
+      for (int a = 0; a < ma; ++a) {
+        const int r = Al[a];
+        for (int p = t; p < nbk * TB; p += PT) rx[p] = p < k ? Cg[(int64_t)r * ld + Fl[p]] : 0.0;
+        __syncthreads();
+        fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+        for (int p = t; p < nbk * TB; p += PT) U[(int64_t)a * ldk + p] = t1[p];
+        __syncthreads();
+      }
+      __builtin_amdgcn_s_dcache_inv();   // U is re-read below, partly at uniform addresses
+      for (int e = t; e < TB * TB; e += PT) {
+        const int i = e >> 6, j = e & 63;
+        double v = (i == j) ? 1.0 : 0.0;
+        if (i < ma && j < ma) {
+          v = (i == j) ? delta : 0.0;
+          if (j <= i) for (int p = 0; p < k; ++p) v += U[(int64_t)i * ldk + p] * U[(int64_t)j * ldk + p];
         }
-        for (int i = ma - 1; i >= 0; --i) {       // backward Ls'
-          double v = wl[i];
-          for (int j = i + 1; j < ma; ++j) v -= stg[j * DP + i] * wl[j];
-          wl[i] = v / stg[i * DP + i];
+        stg[i * DP + j] = v;
+      }
+      __syncthreads();
+      if (tile_potrf_lds(stg, ma)) break;
+      PQ_STAMP(4);
+      // ---- proximal iterative refinement -------------------------------------------------
+      for (int itr = 0; itr < s.refine_iters; ++itr) {
+        // rx = rF - P_FF solx - C_aF' solL ;  rl = dA - C_aF solx
+        for (int p = w; p < k; p += PW) {
+          double sum = 0.0;
+          for (int qq = l; qq < k; qq += 64) sum += pc_at(K, ldk, p, qq) * solx[qq];
+          sum = wave_sum(sum);
+          if (l == 0) {
+            double v = rF[p] - sum;
+            for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)Al[a] * ld + Fl[p]] * solL[a];
+            rx[p] = v;
+          }
         }
+        for (int p = k + t; p < nbk * TB; p += PT) rx[p] = 0.0;
+        for (int a = w; a < ma; a += PW) {
+          const double* c = Cg + (int64_t)Al[a] * ld;
+          double sum = 0.0;
+          for (int p = l; p < k; p += 64) sum += c[Fl[p]] * solx[p];
+          sum = wave_sum(sum);
+          if (l == 0) {
+            const double v = dA[a] - sum;
+            // rounding-level residuals of a row with no free support must not move lam
+            rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dA[a]) + fabs(sum)) ? 0.0 : v;
+          }
+        }
+        __syncthreads();
+        {  // converged to rounding level: further refinement steps change nothing
+          double rm = 0.0;
+          for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
+          if (t < ma) rm = fmax(rm, fabs(rl[t]));
+          if (block_max(rm, red) <= 1e-13 * sc) break;
+        }
+        fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+        // wl = U' t1 - rl ; dlam = S^-1 wl (S = Ls Ls', tiny, one thread)
+        for (int a = w; a < ma; a += PW) {
+          double sum = 0.0;
+          for (int p = l; p < k; p += 64) sum += U[(int64_t)a * ldk + p] * t1[p];
+          sum = wave_sum(sum);
+          if (l == 0) wl[a] = sum - rl[a];
+        }
+        __syncthreads();
+        if (t == 0) {
+          for (int i = 0; i < ma; ++i) {            // forward Ls
+            double v = wl[i];
+            for (int j = 0; j < i; ++j) v -= stg[i * DP + j] * wl[j];
+            wl[i] = v / stg[i * DP + i];
+          }
+          for (int i = ma - 1; i >= 0; --i) {       // backward Ls'
+            double v = wl[i];
+            for (int j = i + 1; j < ma; ++j) v -= stg[j * DP + i] * wl[j];
+            wl[i] = v / stg[i * DP + i];
+          }
+        }
+        __syncthreads();
+        // t1 <- t1 - U dlam ; dx = L^-T t1
+        for (int p = t; p < nbk * TB; p += PT) {
+          double v = t1[p];
+          for (int a = 0; a < ma; ++a) v -= U[(int64_t)a * ldk + p] * wl[a];
+          t1[p] = v;
+        }
+        __syncthreads();
+        bwd_solve(K, ldk, Dt, nbk, t1, dx, t64, part, y64p);
+        for (int p = t; p < k; p += PT) solx[p] += dx[p];
+        if (t < ma) solL[t] += wl[t];
+        __syncthreads();
       }
+      PQ_STAMP(5);
+      // ---- expand, exact gradient, checks -------------------------------------------------
+      for (int i = t; i < n; i += PT) xs[i] = xb[i];
       __syncthreads();
-      // t1 <- t1 - U dlam ; dx = L^-T t1
-      for (int p = t; p < nbk * TB; p += PT) {
-        double v = t1[p];
-        for (int a = 0; a < ma; ++a) v -= U[(int64_t)a * ldk + p] * wl[a];
-        t1[p] = v;
-      }
+      for (int p = t; p < k; p += PT) xs[Fl[p]] = solx[p];
+      if (t < 64) lamF[t] = 0.0;
       __syncthreads();
-      bwd_solve(K, ldk, Dt, nbk, t1, dx, t64, part, y64p);
-      for (int p = t; p < k; p += PT) solx[p] += dx[p];
-      if (t < ma) solL[t] += wl[t];
+      if (t < ma) lamF[Al[t]] = solL[t];  // full-length general multipliers
       __syncthreads();
     }
-    PQ_STAMP(5);
-    // ---- expand, exact gradient, checks -------------------------------------------------
-    for (int i = t; i < n; i += PT) xs[i] = xb[i];
-    __syncthreads();
-    for (int p = t; p < k; p += PT) xs[Fl[p]] = solx[p];
-    if (t < 64) lamF[t] = 0.0;
-    __syncthreads();
-    if (t < ma) lamF[Al[t]] = solL[t];  // full-length general multipliers
-    __syncthreads();
     __builtin_amdgcn_s_dcache_inv();   // xs was rewritten: no stale scalar-cache reads
     full_px();
     __syncthreads();

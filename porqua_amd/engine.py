@@ -528,12 +528,14 @@ def window_rows(dates: np.ndarray, rebdates, width: int):
     return rows, tlen
 
 
-def slide_plan(rows, tlen, group: int = 32, smax: int = 64):
+def slide_plan(rows, tlen, group: int = 32, smax: int = 64, smin: int = 1):
     """Host plan for pq_cov_slide_batched: ``(gstart int32 [G+1], shift int32 [B])``.
 
     Date d joins the group of date d-1 when its window is that window shifted by
-    1 <= s <= smax rows (same length, rows[d][:T-s] == rows[d-1][s:T]) and the group holds
-    fewer than ``group`` dates; otherwise d starts a new group (a full-SYRK anchor)."""
+    smin <= s <= smax rows (same length, rows[d][:T-s] == rows[d-1][s:T]) and the group
+    holds fewer than ``group`` dates; otherwise d starts a new group (a full-SYRK anchor).
+    smin = 0 also joins identical windows (several problems of one date, e.g. a
+    risk-aversion sweep) -- the grouped ADMM accepts that, the sliding K1 does not."""
     rows = np.asarray(rows)
     tlen = np.asarray(tlen)
     B, tmax = rows.shape
@@ -545,12 +547,15 @@ def slide_plan(rows, tlen, group: int = 32, smax: int = 64):
         s = ((prev < cur[:, :1]) & (col < tp[:, None])).sum(1)
         gathered = np.take_along_axis(prev, np.minimum(col + s[:, None], tmax - 1), axis=1)
         match = np.where(col < (tc - s)[:, None], gathered == cur, True).all(1)
-        good = (tp == tc) & (tc > 1) & match & (s >= 1) & (s <= smax)
+        good = (tp == tc) & (tc > 1) & match & (s >= smin) & (s <= smax)
         shift[1:] = np.where(good, s, 0)
+    else:
+        good = np.zeros(0, dtype=bool)
+    joins = np.concatenate([[False], good])
     gstart = []
     cnt = 0
     for d in range(B):
-        if shift[d] == 0 or cnt == group:
+        if not joins[d] or cnt == group:
             gstart.append(d)
             cnt = 0
         cnt += 1
@@ -587,7 +592,7 @@ class GroupPlan:
         rounds = max(1, -(-B // (gmax * cus)))
         gmax = max(1, min(gmax, max(gmin, -(-B // (rounds * cus)))))
         self.ok = B > 0 and int(tlen.min()) >= 2 and int(tlen.max()) <= umax
-        gs, sh = slide_plan(rows, tlen, group=gmax, smax=smax)
+        gs, sh = slide_plan(rows, tlen, group=gmax, smax=smax, smin=0)
         groups = []
         for a, b in zip(gs[:-1], gs[1:]):
             start, U = a, int(tlen[a])

@@ -203,3 +203,40 @@ def test_api_objects_construct_without_gpu():
     bs = BacktestService(data={}, selection_item_builders={"d": SelectionItemBuilder(bibfn=bibfn_selection_data)},
                          optimization_item_builders={}, optimization=mv, rebdates=[])
     Backtest().run(bs)
+
+
+def test_group_plan_joins_identical_windows_of_a_sweep():
+    """A risk-aversion sweep repeats every date's window; the grouped-ADMM plan joins the
+    repeats (shift 0, same union), the sliding-K1 plan does not."""
+    dates, _, _, _ = factor_panel(400, 3)
+    rows, tlen = engine.window_rows(dates, dates[[300, 390]], 120)   # 90-row gap: no slide
+    rep_rows, rep_tlen = np.repeat(rows, 6, axis=0), np.repeat(tlen, 6)
+    gs, sh = engine.slide_plan(rep_rows, rep_tlen, group=16, smin=0)
+    assert list(gs) == [0, 6, 12] and np.all(sh == 0)
+    gs1, _ = engine.slide_plan(rep_rows, rep_tlen, group=16)
+    assert len(gs1) - 1 == 12
+    gp = engine.GroupPlan(rep_rows, rep_tlen, torch.device("cpu"))   # 12 problems: groups of <= 4
+    assert gp.ok and list(gp.gdates.numpy()) == [0, 4, 6, 10, 12]
+    assert np.all(gp.ucnt.numpy() == 120) and np.all(gp.uoff.numpy() == 0)
+
+
+def test_kkt_certificate_accepts_oracle_and_rejects_perturbed():
+    from oracle.qp_ipm import solve_qp
+    from tests.kkt import kkt_residuals
+    rng = np.random.default_rng(3)
+    n = 40
+    X = rng.normal(0, 0.02, (30, n))
+    P = 2 * X.T @ X + 1e-4 * np.eye(n)
+    q = -rng.normal(0, 0.01, n)
+    G = (rng.random((3, n)) < 0.4).astype(float)
+    h = np.full(3, 0.3)
+    o = solve_qp(P, q, G=G, h=h, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.full(n, 0.2))
+    y = np.concatenate([np.atleast_1d(o.y), np.atleast_1d(o.z)])
+    k = kkt_residuals(P, q, o.x, A=np.ones((1, n)), b=np.ones(1), G=G, h=h, lb=np.zeros(n),
+                      ub=np.full(n, 0.2), y=y, z_box=o.z_box)
+    assert max(k.values()) < 1e-9, k
+    xp = o.x.copy()
+    xp[:2] += np.array([1e-4, -1e-4])
+    k2 = kkt_residuals(P, q, xp, A=np.ones((1, n)), b=np.ones(1), G=G, h=h, lb=np.zeros(n),
+                       ub=np.full(n, 0.2), y=y, z_box=o.z_box)
+    assert max(k2.values()) > 1e-7

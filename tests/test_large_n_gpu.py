@@ -1,0 +1,92 @@
+"""BASELINE.json configs[3] and configs[4] beyond the 1024-asset LDS limit of the dense
+kernels, on the window path (grouped low-rank ADMM + window polish):
+
+  * config 4 shape: n = 3000 tracking-error least squares (uncentred Gram, q = -2 X'y,
+    LeastSquares.set_objective, src/optimization.py:206-226) with budget + 20 sector caps
+    (G 20 x n, the group rows of Constraints.to_GhAb, src/constraints.py:114-167) and a
+    long-only box -- 21 general rows;
+  * config 5 shape: n = 5000 mean-variance risk-aversion x date sweep (porqua_amd.sweep).
+
+Rank(P) <= T = 252 < n, so the optimum is a face: the checks are the objective against
+the oracle IPM (n = 3000), feasibility, and the KKT certificate (tests/kkt.py), which is
+size-independent."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.qp_ipm import solve_qp
+from oracle.ref_pipeline import cov_pearson
+from porqua_amd import _lib, engine
+from porqua_amd.sweep import mean_variance_sweep
+from porqua_amd.synthetic import factor_panel
+from tests.kkt import kkt_residuals
+
+pytestmark = pytest.mark.gpu
+
+
+def test_config4_tracking_n3000_sector_caps(device):
+    n, T, ns, cap = 3000, 252, 20, 0.15
+    ends = list(range(260, 266))
+    dates, R, y, sec = factor_panel(max(ends) + 1, n, n_sectors=ns)
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    pan = engine.Panel(R, y, device=device)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    B = len(ends)
+    G = np.stack([(sec == g).astype(float) for g in range(ns)])
+    h = np.full(ns, cap)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=G, h=h, lb=np.zeros(n), ub=np.ones(n), device=device)
+    qb.batch = B
+    qb.P = None
+    xty, _ = pan.gram_xy(r_d, t_d)
+    qb.q = (-2.0 * xty).contiguous()
+    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
+    lr = engine.LowRank(pan, r_d, t_d, mu=None)
+    gp = engine.GroupPlan(rows, tlen, device)
+    ws = engine.Workspace(qb, dense=False)
+    assert qb.mg == 21 and engine.grouped_applicable(qb, lr, gp, ws)
+    res = engine.solve_lowrank(qb, lr, engine.Settings(rho0_rel=0.5), ws=ws, groups=gp)
+    st = res.status.cpu().numpy()
+    x = res.x.cpu().numpy()
+    yv = res.y.cpu().numpy()
+    zb = res.z_box.cpu().numpy()
+    assert np.all(st == _lib.PQ_SOLVED), st
+    for i, e in enumerate(ends):
+        X = R[e - T + 1:e + 1]
+        P, q = 2 * X.T @ X, -2 * X.T @ y[e - T + 1:e + 1]
+        assert abs(x[i].sum() - 1) <= 1e-7 and x[i].min() >= -1e-7 and (G @ x[i]).max() <= cap + 1e-7
+        k = kkt_residuals(P, q, x[i], A=np.ones((1, n)), b=np.ones(1), G=G, h=h, lb=np.zeros(n),
+                          ub=np.ones(n), y=yv[i], z_box=zb[i])
+        assert max(k.values()) <= 1e-7, k
+        if i == 0:
+            o = solve_qp(P, q, G=G, h=h, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n))
+            obj = 0.5 * x[i] @ P @ x[i] + q @ x[i]
+            assert abs(obj - o.obj) <= 1e-6 * abs(o.obj)
+
+
+def test_config5_risk_aversion_sweep_n5000(device):
+    n, T = 5000, 252
+    lambdas = np.logspace(-1, 2, 4)
+    ends = [300, 321]
+    dates, R, y, sec = factor_panel(max(ends) + 1, n)
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    pan = engine.Panel(R, device=device)
+    res, meta = mean_variance_sweep(pan, rows, tlen, lambdas)
+    assert meta["grouped"]
+    st = res.status.cpu().numpy()
+    x = res.x.cpu().numpy()
+    yv = res.y.cpu().numpy()
+    zb = res.z_box.cpu().numpy()
+    assert np.all(st == _lib.PQ_SOLVED), st
+    for d, e in enumerate(ends):
+        W = R[e - T + 1:e + 1]
+        S = cov_pearson(W)
+        mu = np.exp(np.mean(np.log1p(W), axis=0)) - 1.0
+        for j, lam in enumerate(lambdas):
+            p = d * len(lambdas) + j
+            P = 2 * lam * S
+            k = kkt_residuals(P, -mu, x[p], A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n),
+                              y=yv[p], z_box=zb[p])
+            assert max(k.values()) <= 1e-7, (lam, k)
+            obj = 0.5 * x[p] @ P @ x[p] - mu @ x[p]
+            assert abs(res.obj[p].item() - obj) <= 1e-9 * max(1.0, abs(obj))

@@ -35,7 +35,7 @@ def main():
     lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
     ws = engine.Workspace(qb)
     gp = engine.GroupPlan(rows, tlen, qb.P.device) if "--group" in sys.argv else None
-    off = (5 + ws.mg_pad) * qb.ld   # PQ_WORK_PROF
+    off = (9 + ws.mg_pad) * qb.ld   # PQ_WORK_PROF
     for _ in range(2):
         ev = []
         ws.work[:, off + 16:off + 24].zero_()
