@@ -198,7 +198,11 @@ def main():
     cov_t = tk.get("moments+cov") if with_cov else None
     cov_write_gbs = D * ld * ld * 8.0 * args.steps / cov_t / 1e9 if cov_t else None
     kld = ((T + 1 + 63) // 64) * 64
-    factor_flops_per = (2.0 * kld * kld * n + kld ** 3) if use_lr else ld ** 3  # (capacitance SYRK +) potrf+trtri+lauum
+    band = use_lr and res.capacitance == "band"
+    # potrf + trtri + lauum (k^3), plus the per-date capacitance SYRK (2 k^2 n) unless the
+    # band Gram (one row-band SYRK per panel, stage "gram") supplies it
+    factor_flops_per = (kld ** 3 + (0.0 if band else 2.0 * kld * kld * n)) if use_lr else ld ** 3
+    gram_flops = 2.0 * (T - 1 + D) * T * n * args.steps if band else None
     n_factor = D * args.steps + res.refactors * args.steps
     factor_flops = factor_flops_per * n_factor
 
@@ -257,6 +261,8 @@ def main():
                         "full SYRK per date" if plan is None else
                         f"sliding: {plan.ngroups} anchor SYRKs + rank-2 updates",
             "factor_tflops": factor_flops / tk.get("factor", float("nan")) / 1e12,
+            "gram_tflops": gram_flops / tk["gram"] / 1e12 if band and tk.get("gram") else None,
+            "capacitance": res.capacitance or None,
             "fp64_peak_tflops": FP64_PEAK_TFLOPS,
         },
         "solver": {"status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},

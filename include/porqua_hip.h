@@ -187,6 +187,23 @@ int pq_lr_capacitance(const pq_lowrank* lr, const pq_problem* pb, const pq_state
                       const int32_t* idx, int32_t nidx, const pq_settings* s, double* M,
                       int32_t k_ld, int64_t M_stride, void* stream);
 
+/* Low-rank K2, band-Gram form, for a uniform ADMM diagonal D = c I (every box row of a
+ * problem has the same rho: all bounds finite with lb < ub, or all free, or all fixed --
+ * the caller checks) and general rows shared by all problems (Cg_stride == 0):
+ *   pq_lr_band_gram: band[r][j] = x_{r0+r} . x_{r0+r-j} for 0 <= j < W (W >= the widest
+ *     window span in rows) -- an FP64 MFMA SYRK over the assets, once per panel instead
+ *     of T^2 n per date -- and pc[r][g] = x_{r0+r} . Cg_g;
+ *   pq_lr_capacitance_band: the same M as pq_lr_capacitance, assembled per date from the
+ *     band (centring B - r1' - 1r' + s11' by the window's own mean: lr->mu must be the
+ *     pq_window_mean of the same rows, or NULL), pc and cc = Cg Cg' (mg x mg).          */
+int pq_lr_band_gram(const double* panel, int64_t ldp, int32_t n, int32_t r0, int32_t nrows, int32_t W,
+                    double* band, int64_t ldo, const double* Cg, int32_t mg, int32_t ld_cg, double* pc,
+                    int64_t ldpc, void* stream);
+int pq_lr_capacitance_band(const pq_lowrank* lr, const pq_problem* pb, const pq_state* st, const int32_t* idx,
+                           int32_t nidx, const pq_settings* s, const double* band, int64_t ldo, int32_t r0,
+                           const double* pc, int64_t ldpc, const double* cc, double* M, int32_t k_ld,
+                           int64_t M_stride, void* stream);
+
 /* Low-rank K3: the ADMM of pq_admm_batched with x~ = K^-1 rhs applied through the window
  * (two passes over its T rows) and the lower-triangle M^-1 (Minv, k_ld x k_ld).        */
 int pq_admm_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,

@@ -119,6 +119,11 @@ _EXPORTS = {
                               c_dp, c_int32, ctypes.POINTER(PQSettings), c_dp], c_int32),
     "pq_lr_capacitance": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                            c_dp, c_int32, ctypes.POINTER(PQSettings), c_dp, c_int32, c_int64, c_dp], c_int32),
+    "pq_lr_band_gram": ([c_dp, c_int64, c_int32, c_int32, c_int32, c_int32, c_dp, c_int64, c_dp, c_int32, c_int32,
+                         c_dp, c_int64, c_dp], c_int32),
+    "pq_lr_capacitance_band": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                                c_dp, c_int32, ctypes.POINTER(PQSettings), c_dp, c_int64, c_int32, c_dp, c_int64,
+                                c_dp, c_dp, c_int32, c_int64, c_dp], c_int32),
     "pq_admm_lr_batched": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                             c_dp, c_int32, c_int64, c_dp, c_int32, ctypes.POINTER(PQSettings), c_int32,
                             c_dp], c_int32),

@@ -279,6 +279,7 @@ class BatchResult:
     out: torch.Tensor        # (B, PQ_OUT_FIELDS)
     refactors: int = 0
     admm_launches: int = 0
+    capacitance: str = ""    # window path: "band" (pq_lr_capacitance_band) or "direct"
 
     @property
     def obj(self):
@@ -364,6 +365,16 @@ class LowRank:
         self.panel.window_sumsq(self.rows, self.tlen, self.mu, out=self.dg)
         return self
 
+    def span(self):
+        """(r0, nrows, W): the panel rows the windows touch and the widest window span."""
+        if getattr(self, "_span", None) is None:
+            t = self.tlen.to(torch.int64)
+            first = self.rows[:, 0].to(torch.int64)
+            last = self.rows.gather(1, (t - 1).clamp(min=0)[:, None]).flatten().to(torch.int64)
+            v = torch.stack([first.min(), last.max(), (last - first + 1).max()]).cpu().tolist()
+            self._span = (int(v[0]), int(v[1] - v[0] + 1), int(v[2]))
+        return self._span
+
     def c_struct(self) -> _lib.PQLowRank:
         return _lib.PQLowRank(panel=self.panel.R.data_ptr(), ldp=self.panel.R.stride(0),
                               rows=self.rows.data_ptr(), tlen=self.tlen.data_ptr(), tmax=self.tmax,
@@ -391,9 +402,39 @@ def grouped_applicable(qb: QPBatch, lr: LowRank, groups: "GroupPlan | None", ws:
             and qb.mg <= 32 and k_ld <= 384 and ws.work_stride >= 3 * qb.ld)
 
 
+def _uniform_box(qb: QPBatch) -> bool:
+    """Every box row of every problem gets the same ADMM rho (pq_lr_capacitance_band)."""
+    if qb.lb is None:
+        return True
+    n = qb.n
+    lo, up = qb.lb[:, :n], qb.ub[:, :n]
+    cls = torch.where(torch.isinf(lo) & torch.isinf(up), 1, torch.where(lo == up, 2, 0))
+    return bool((cls == cls[:, :1]).all().item()) and (qb.lb.shape[0] == 1 or bool((cls[:, 0] == cls[0, 0]).all().item()))
+
+
+def _band_setup(qb: QPBatch, lr: LowRank, strm):
+    """Band Gram of the panel rows + PC / CC tables for pq_lr_capacitance_band, or None when
+    the band form does not apply (per-problem constraints, non-uniform box rho, tmax > 1024)."""
+    if not qb.shared or lr.tmax > 1024 or not _uniform_box(qb):
+        return None
+    lib = _lib.load()
+    r0, nrows, W = lr.span()
+    dev, n, mg = qb.device, qb.n, qb.mg
+    ldo = round_up(W, 2)
+    band = torch.empty((nrows, ldo), dtype=F64, device=dev)
+    pc = torch.empty((nrows, max(mg, 1)), dtype=F64, device=dev)
+    R = lr.panel.R
+    _lib.check(lib.pq_lr_band_gram(R.data_ptr(), R.stride(0), n, r0, nrows, W, band.data_ptr(), ldo,
+                                   qb.Cg.data_ptr(), mg, qb.ld, pc.data_ptr(), pc.stride(0), strm),
+               "pq_lr_band_gram")
+    C = qb.Cg[0, :mg, :n]
+    cc = (C @ C.T).contiguous() if mg else torch.zeros((1, 1), dtype=F64, device=dev)
+    return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc}
+
+
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
-                  polish: bool = True, groups: "GroupPlan | None" = None) -> BatchResult:
+                  polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -429,11 +470,21 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     PM_, SM_, SSM = ctypes.byref(pbM), ctypes.byref(stM), ctypes.byref(sM)
     _lib.check(lib.pq_init_state_lr(L_, P_, S_, None, 0, SS, strm), "pq_init_state_lr")
 
+    bd = None
+
     def refactor(idx, nidx):
-        _lib.check(lib.pq_lr_capacitance(L_, P_, S_, _ptr(idx), nidx, SS, M["M"].data_ptr(), k_ld,
-                                         k_ld * k_ld, strm), "pq_lr_capacitance")
+        if bd is not None:
+            _lib.check(lib.pq_lr_capacitance_band(L_, P_, S_, _ptr(idx), nidx, SS, bd["band"].data_ptr(), bd["ldo"],
+                                                  bd["r0"], bd["pc"].data_ptr(), bd["pc"].stride(0),
+                                                  bd["cc"].data_ptr(), M["M"].data_ptr(), k_ld, k_ld * k_ld, strm),
+                       "pq_lr_capacitance_band")
+        else:
+            _lib.check(lib.pq_lr_capacitance(L_, P_, S_, _ptr(idx), nidx, SS, M["M"].data_ptr(), k_ld,
+                                             k_ld * k_ld, strm), "pq_lr_capacitance")
         _lib.check(lib.pq_factor_batched(PM_, SM_, _ptr(idx), nidx, SSM, 1, strm), "pq_factor_batched(M)")
 
+    if band:
+        bd = tl("gram", lambda: _band_setup(qb, lr, strm))
     tl("factor", lambda: refactor(None, 0))
     idx, nidx = None, 0
     refactors = launches = 0
@@ -479,7 +530,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
-                       admm_launches=launches)
+                       admm_launches=launches, capacitance="band" if bd is not None else "direct")
 
 
 def factor_only(qb: QPBatch, invert: bool = False, sigma: float = 0.0):

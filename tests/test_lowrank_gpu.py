@@ -133,3 +133,52 @@ def test_grouped_admm_matches_per_date_lowrank(device, n, T, D, stride, groups_r
         o = solve_qp(P, np.zeros(n), G=G, h=h, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n),
                      ub=np.full(n, 0.2))
         assert abs(0.5 * xg[i] @ P @ xg[i] - o.obj) <= 1e-6 * abs(o.obj)
+
+
+@pytest.mark.parametrize("centred,groups_rows,stride", [(True, False, 1), (True, True, 3), (False, True, 1)])
+def test_band_gram_capacitance_matches_direct(device, centred, groups_rows, stride):
+    """pq_lr_capacitance_band (M from the panel's row band Gram, shared by overlapping
+    windows) builds the same capacitance matrices as the per-date MFMA SYRK
+    pq_lr_capacitance, and the solve reaches the same optimum."""
+    n, T, D = 400, 120, 30
+    ends = list(range(T + 5, T + 5 + D * stride, stride))
+    dates, R, y, sec, pan, r_d, t_d, mu = _setup(n, T, ends, centred=centred, D=max(ends) + 1)
+    B = len(ends)
+    G = h = None
+    if groups_rows:
+        G = np.stack([(sec == g).astype(float) for g in range(3)])
+        h = np.full(3, 0.4)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=G, h=h, lb=np.zeros(n), ub=np.full(n, 0.1), device=device)
+    qb.batch = B
+    qb.P = None
+    qb.q = torch.zeros((B, qb.ld), dtype=torch.float64, device=device)
+    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
+    w = 1.0 / (t_d.to(torch.float64) - 1.0) if centred else None
+    lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=w)
+    lib = engine._lib.load()
+    ws = engine.Workspace(qb, dense=False)
+    import ctypes
+    P_, S_ = ctypes.byref(qb.c_struct()), ctypes.byref(ws.c_struct())
+    L_ = ctypes.byref(lr.c_struct())
+    SS = ctypes.byref(engine.Settings().to_c())
+    strm = engine._stream()
+    engine._lib.check(lib.pq_init_state_lr(L_, P_, S_, None, 0, SS, strm), "init")
+    k_ld = engine.round_up(lr.tmax + qb.mg, 64)
+    M1 = torch.zeros((B, k_ld, k_ld), dtype=torch.float64, device=device)
+    M2 = torch.zeros_like(M1)
+    engine._lib.check(lib.pq_lr_capacitance(L_, P_, S_, None, 0, SS, M1.data_ptr(), k_ld, k_ld * k_ld, strm), "direct")
+    bd = engine._band_setup(qb, lr, strm)
+    assert bd is not None
+    engine._lib.check(lib.pq_lr_capacitance_band(L_, P_, S_, None, 0, SS, bd["band"].data_ptr(), bd["ldo"], bd["r0"],
+                                                 bd["pc"].data_ptr(), bd["pc"].stride(0), bd["cc"].data_ptr(),
+                                                 M2.data_ptr(), k_ld, k_ld * k_ld, strm), "band")
+    lower = torch.tril(torch.ones(k_ld, k_ld, dtype=torch.bool, device=device))
+    d = ((M1 - M2).abs() * lower).amax().item()
+    assert d <= 1e-12 * M1.abs().amax().item(), d
+    r1 = engine.solve_lowrank(qb, lr, band=False)
+    x1, i1 = r1.x.cpu().numpy().copy(), r1.iters.cpu().numpy().copy()
+    r2 = engine.solve_lowrank(qb, lr, band=True)
+    assert np.all(r2.status.cpu().numpy() == 1) and np.all(r1.status.cpu().numpy() == 1)
+    assert np.abs(r2.iters.cpu().numpy() - i1).max() <= 2
+    assert np.abs(r2.x.cpu().numpy() - x1).max() < 1e-8
