@@ -215,12 +215,16 @@ int pq_admm_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
  * union rows are urows[g * umax + u] (u < ucnt[g] <= 320) and date b's window is union
  * rows [uoff[b], uoff[b] + tlen[b]).  One workgroup per group runs the dates' iterations
  * in lock step with both window passes as FP64 MFMA GEMMs over the union; results are
- * those of pq_admm_lr_batched up to summation order.  Needs even n and ldp, mg <= 32,
+ * those of pq_admm_lr_batched up to summation order.  Optional pc / cc (the tables of
+ * pq_lr_band_gram: pc[r - r0][g] = x_r . Cg_g, cc = Cg Cg'; NULL = off) select the fused
+ * form for a uniform ADMM diagonal (the pq_lr_capacitance_band condition) and mg <= 4:
+ * Cg x~ from scalars, one pass over each date's vectors per iteration.  Needs even n and ldp, mg <= 32,
  * k_ld <= 384, work_stride >= 3 ld (work holds each date's V / rhs / x~ scratch).      */
 int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const double* Minv,
                        int32_t k_ld, int64_t M_stride, const int32_t* gdates, int32_t ngroups,
                        const int32_t* urows, const int32_t* ucnt, const int32_t* uoff, int32_t umax,
-                       const pq_settings* s, int32_t iters_this_call, void* stream);
+                       const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
+                       int32_t r0, const double* cc, void* stream);
 
 /* K4: active-set polish of the ADMM point (reduced KKT by masked Cholesky + Schur +
  * proximal iterative refinement), then exact residuals / objective of the final point

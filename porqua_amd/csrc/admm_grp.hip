@@ -71,12 +71,19 @@ __device__ __forceinline__ int grp_slot(int g, int N) {   // XCD-contiguous grou
 #define GSTAMP(k) do { } while (0)
 #endif
 
-template <int NQK, int MGG, int MGR>
+// FUSE (uniform ADMM diagonal D_g = c_g I and shared Cg, the band-Gram case): V = rhs / c_g
+// is never stored (pass 1 multiplies the rhs and scales W by 1 / c_g), and Cg x~ is known
+// before the x-update from scalars --
+//   Cg x~ = Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / c_g,   PC[r][g] = x_r . Cg_g,
+// so the x-update, residuals and next rhs run as ONE fused pass over each date's vectors
+// (pass A's x~ round trip and its Cg x~ reductions disappear).
+template <int NQK, int MGG, int MGR, bool FUSE>
 __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, pq_state st,
                                                  const double* Minv_all, int k_ld, int64_t M_stride,
                                                  const int32_t* gdates, const int32_t* urows_all,
                                                  const int32_t* ucnt_all, const int32_t* uoff, int umax,
-                                                 pq_settings s, int iters_call) {
+                                                 pq_settings s, int iters_call, const double* pc,
+                                                 int64_t ldpc, int r0, const double* cc) {
   // pass-1 output W, overwritten in place by the symv with the pass-2 operand Ut (rows outside
   // a date's window zeroed); 2 workgroups fit on a CU
   __shared__ __attribute__((aligned(16))) double WU[(UMAXG + 4) * GMAX];
@@ -88,6 +95,7 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       g_cw[GMAX * MGG], g_zt[GMAX * MGG], g_rgz[GMAX * MGG];
   __shared__ int g_act[GMAX], g_it[GMAX], g_end[GMAX], g_stat[GMAX], g_off[GMAX], g_T[GMAX];
   __shared__ int s_urow[UMAXG];
+  __shared__ double g_dinv[GMAX], g_rb[GMAX], g_cmu[FUSE ? GMAX * MGG : 1];
   __shared__ int s_any;
   __shared__ __attribute__((aligned(16))) double s_part[GNW * NQK * 128];   // symv partial vectors
   __shared__ double s_dot[NQK * 128];                                       // symv dot parts
@@ -125,6 +133,12 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       const double ps = (pb.p_scale ? pb.p_scale[b] : 1.0) * (lr.w_scale ? lr.w_scale[b] : 1.0);
       g_sps[g] = sqrt(fmax(ps, 0.0));
       g_pd[g] = pb.p_diag ? pb.p_diag[b] : 0.0;
+      if (FUSE) {   // uniform box rho (host-checked): D = sigma + p_diag + rho_box
+        const double rb = has_box ? grho(pb.lb[(int64_t)b * pb.box_stride], pb.ub[(int64_t)b * pb.box_stride],
+                                         st.rho[b], s) : 0.0;
+        g_rb[g] = rb;
+        g_dinv[g] = 1.0 / (sigma + g_pd[g] + rb);
+      }
     }
     g_act[g] = act;
   }
@@ -194,6 +208,15 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       if (hl == 0) g_cgv[g * MGG + r] = a;
     }
     if (hl == 0) g_muv[g] = muv;
+    if (FUSE) {   // Cg . mu of the date (constant over the launch)
+      for (int r = 0; r < mg; ++r) {
+        double a = 0.0;
+        if (mu_h)
+          for (int i = hl; i < n; i += 32) a = fma(Cg_h[(int64_t)r * ld + i], mu_h[i], a);
+        a = hsum(a);
+        if (hl == 0) g_cmu[g * MGG + r] = a;
+      }
+    }
   };
 
   // ---- prologue: Cg x and the first rhs -------------------------------------------------
@@ -219,7 +242,9 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
     // ---- pass 1: W = X_union V (MFMA f64 16x16x4; a 16-B load feeds two k-slices) -------
     {
       const int kq = l >> 4, m = l & 15;
-      const double* Vp = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride : nullptr;
+      // V of date m (FUSE: its rhs, W scaled by 1 / c_m below)
+      const double* Vp = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride + (FUSE ? ld : 0) : nullptr;
+      const double wsc1 = (FUSE && m < G) ? g_dinv[m] : 1.0;
       f64x4 c[3];
       const double* arow[3];
       bool tv[3], aval[3];
@@ -271,7 +296,7 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int u = tile * 16 + kq + 4 * r;
-            if (u < UMAXG) W[u * GMAX + m] = c[j][r];
+            if (u < UMAXG) W[u * GMAX + m] = wsc1 * c[j][r];
           }
         }
       }
@@ -441,45 +466,58 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       const double rho = g_rho[g], pd = g_pd[g], su = g_su[g];
       const double dsig = sigma + pd;
       if (hl < mg) g_cw[g * MGG + hl] = sqrt(g_rg[g * MGG + hl]) * g_kug[g * MGG + hl];
-      // pass A: x~ = v - D^-1 (X~raw - mu su + Cg' cw), and Cg x~
       constexpr int MGRA = MGR > 0 ? MGR : 1;
-      double ztp[MGRA];
-#pragma unroll
-      for (int r = 0; r < MGRA; ++r) ztp[r] = 0.0;
-#pragma unroll 2
-      for (int i = hl; i < n; i += 32) {
-        double corr = X_h[i] - (mu_h ? su * mu_h[i] : 0.0);
-        const double rb = has_box ? grho(lo_h[i], up_h[i], rho, s) : 0.0;
-        double cgi[MGRA];
-        if constexpr (MGR > 0) {
-#pragma unroll
-          for (int r = 0; r < MGR; ++r) {
-            cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
-            corr = fma(r < mg ? g_cw[g * MGG + r] : 0.0, cgi[r], corr);
+      if constexpr (!FUSE) {
+        // pass A: x~ = v - D^-1 (X~raw - mu su + Cg' cw), and Cg x~
+        double ztp[MGRA];
+  #pragma unroll
+        for (int r = 0; r < MGRA; ++r) ztp[r] = 0.0;
+  #pragma unroll 2
+        for (int i = hl; i < n; i += 32) {
+          double corr = X_h[i] - (mu_h ? su * mu_h[i] : 0.0);
+          const double rb = has_box ? grho(lo_h[i], up_h[i], rho, s) : 0.0;
+          double cgi[MGRA];
+          if constexpr (MGR > 0) {
+  #pragma unroll
+            for (int r = 0; r < MGR; ++r) {
+              cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
+              corr = fma(r < mg ? g_cw[g * MGG + r] : 0.0, cgi[r], corr);
+            }
+          } else {
+            for (int r = 0; r < mg; ++r) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
           }
-        } else {
-          for (int r = 0; r < mg; ++r) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
+          const double xt = V_h[i] - corr / (dsig + rb);
+          X_h[i] = xt;
+          if constexpr (MGR > 0) {
+  #pragma unroll
+            for (int r = 0; r < MGR; ++r) ztp[r] = fma(cgi[r], xt, ztp[r]);
+          }
         }
-        const double xt = V_h[i] - corr / (dsig + rb);
-        X_h[i] = xt;
         if constexpr (MGR > 0) {
-#pragma unroll
-          for (int r = 0; r < MGR; ++r) ztp[r] = fma(cgi[r], xt, ztp[r]);
+  #pragma unroll
+          for (int r = 0; r < MGR; ++r) {
+            if (r >= mg) break;
+            const double a = hsum(ztp[r]);
+            if (hl == 0) g_zt[g * MGG + r] = a;
+          }
+        } else {   // each lane re-reads the x~ entries it wrote
+          for (int r = 0; r < mg; ++r) {
+            double a = 0.0;
+            for (int i = hl; i < n; i += 32) a = fma(Cg_h[(int64_t)r * ld + i], X_h[i], a);
+            a = hsum(a);
+            if (hl == 0) g_zt[g * MGG + r] = a;
+          }
         }
-      }
-      if constexpr (MGR > 0) {
-#pragma unroll
-        for (int r = 0; r < MGR; ++r) {
-          if (r >= mg) break;
-          const double a = hsum(ztp[r]);
-          if (hl == 0) g_zt[g * MGG + r] = a;
-        }
-      } else {   // each lane re-reads the x~ entries it wrote
+      } else {   // Cg x~ from scalars: Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / c
+        const double dinv = g_dinv[g];
+        const int Ug = ucnt_all[grp];
         for (int r = 0; r < mg; ++r) {
           double a = 0.0;
-          for (int i = hl; i < n; i += 32) a = fma(Cg_h[(int64_t)r * ld + i], X_h[i], a);
+          for (int u = hl; u < Ug; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * GMAX + g], a);
           a = hsum(a);
-          if (hl == 0) g_zt[g * MGG + r] = a;
+          double cw = 0.0;
+          for (int r2 = 0; r2 < mg; ++r2) cw = fma(cc[r * mg + r2], g_cw[g * MGG + r2], cw);
+          if (hl == 0) g_zt[g * MGG + r] = g_cgv[g * MGG + r] - dinv * (a - su * g_cmu[g * MGG + r] + cw);
         }
       }
       double mv[7] = {0, 0, 0, 0, 0, 0, 0};   // |Cx-z| |Cx| |z| |dres| |Px| |C'y| |q|
@@ -505,9 +543,19 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       for (int r = 0; r < MGRA; ++r) cvp[r] = 0.0;
 #pragma unroll 2
       for (int i = hl; i < n; i += 32) {
-        const double xt = X_h[i];
         const double rb = has_box ? grho(lo_h[i], up_h[i], rho, s) : 0.0;
-        double pxt = R_h[i] - sigma * xt - rb * xt;
+        const double rr0 = R_h[i];
+        double xt;
+        if constexpr (FUSE) {   // x~ = (rhs - X~raw + mu su - Cg' cw) / c, fused with the updates
+          double corr = X_h[i] - (mu_h ? su * mu_h[i] : 0.0);
+#pragma unroll
+          for (int r = 0; r < MGRA; ++r)
+            if (r < mg) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
+          xt = (rr0 - corr) * g_dinv[g];
+        } else {
+          xt = X_h[i];
+        }
+        double pxt = rr0 - sigma * xt - rb * xt;
         double cgy = 0.0, cgw = 0.0, cgi[MGRA];
         if constexpr (MGR > 0) {
 #pragma unroll
@@ -551,9 +599,9 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
         const double cy = cty + cgy;
         mv[3] = fmax(mv[3], fabs((pxn + qi + cty) + (cy - cty)));
         mv[5] = fmax(mv[5], fabs(cy));
-        const double v = rr / (dsig + rb);
+        const double v = FUSE ? rr * g_dinv[g] : rr / (dsig + rb);
         R_h[i] = rr;
-        V_h[i] = v;
+        if (!FUSE) V_h[i] = v;
         if (mu_h) muv = fma(mu_h[i], v, muv);
         if constexpr (MGR > 0) {
 #pragma unroll
@@ -653,8 +701,11 @@ extern "C" int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq
                                   const double* Minv, int32_t k_ld, int64_t M_stride,
                                   const int32_t* gdates, int32_t ngroups, const int32_t* urows,
                                   const int32_t* ucnt, const int32_t* uoff, int32_t umax,
-                                  const pq_settings* s, int32_t iters_this_call, void* stream) {
+                                  const pq_settings* s, int32_t iters_this_call, const double* pc,
+                                  int64_t ldpc, int32_t r0, const double* cc, void* stream) {
   PQ_CHECK_ARG(lr && pb && st && s && Minv, "pq_admm_lr_grouped: null argument");
+  PQ_CHECK_ARG((pc == nullptr) == (cc == nullptr), "pq_admm_lr_grouped: pc and cc go together");
+  PQ_CHECK_ARG(pc == nullptr || pb->Cg_stride == 0, "pq_admm_lr_grouped: the fused form needs shared Cg");
   PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0, "pq_admm_lr_grouped: window missing");
   PQ_CHECK_ARG(gdates && urows && ucnt && uoff && umax > 0, "pq_admm_lr_grouped: group plan missing");
   PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::MGG_BIG && (pb->mg == 0 || (pb->Cg && pb->lg && pb->ug)),
@@ -666,17 +717,22 @@ extern "C" int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq
   if (ngroups <= 0) return 0;
   hipStream_t str = (hipStream_t)stream;
   const int nqk = (k_ld + 127) / 128;
-#define PQ_GRP_CASE(NQKV, MGGV, MGRV)                                                                   \
-  hipLaunchKernelGGL((pq::k_admm_grp<NQKV, MGGV, MGRV>), dim3(ngroups), dim3(pq::GT), 0, str, *lr, *pb, *st,   \
-                     Minv, k_ld, M_stride, gdates, urows, ucnt, uoff, umax, *s, iters_this_call)
+#define PQ_GRP_CASE(NQKV, MGGV, MGRV, FUSEV)                                                              \
+  hipLaunchKernelGGL((pq::k_admm_grp<NQKV, MGGV, MGRV, FUSEV>), dim3(ngroups), dim3(pq::GT), 0, str, *lr, *pb,   \
+                     *st, Minv, k_ld, M_stride, gdates, urows, ucnt, uoff, umax, *s, iters_this_call, pc, ldpc,  \
+                     r0, cc)
   const bool small = pb->mg <= pq::MGR_SMALL;
-  switch (nqk * 2 + (small ? 0 : 1)) {
-    case 2: PQ_GRP_CASE(1, pq::MGG_SMALL, pq::MGR_SMALL); break;
-    case 3: PQ_GRP_CASE(1, pq::MGG_BIG, 0); break;
-    case 4: PQ_GRP_CASE(2, pq::MGG_SMALL, pq::MGR_SMALL); break;
-    case 5: PQ_GRP_CASE(2, pq::MGG_BIG, 0); break;
-    case 6: PQ_GRP_CASE(3, pq::MGG_SMALL, pq::MGR_SMALL); break;
-    case 7: PQ_GRP_CASE(3, pq::MGG_BIG, 0); break;
+  const bool fuse = small && pc != nullptr && cc != nullptr;
+  switch (nqk * 4 + (fuse ? 2 : (small ? 0 : 1))) {
+    case 4: PQ_GRP_CASE(1, pq::MGG_SMALL, pq::MGR_SMALL, false); break;
+    case 5: PQ_GRP_CASE(1, pq::MGG_BIG, 0, false); break;
+    case 6: PQ_GRP_CASE(1, pq::MGG_SMALL, pq::MGR_SMALL, true); break;
+    case 8: PQ_GRP_CASE(2, pq::MGG_SMALL, pq::MGR_SMALL, false); break;
+    case 9: PQ_GRP_CASE(2, pq::MGG_BIG, 0, false); break;
+    case 10: PQ_GRP_CASE(2, pq::MGG_SMALL, pq::MGR_SMALL, true); break;
+    case 12: PQ_GRP_CASE(3, pq::MGG_SMALL, pq::MGR_SMALL, false); break;
+    case 13: PQ_GRP_CASE(3, pq::MGG_BIG, 0, false); break;
+    case 14: PQ_GRP_CASE(3, pq::MGG_SMALL, pq::MGR_SMALL, true); break;
     default:
       pq::set_error("pq_admm_lr_grouped: unsupported k_ld=%d", k_ld);
       return -1;

@@ -434,7 +434,8 @@ def _band_setup(qb: QPBatch, lr: LowRank, strm):
 
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
-                  polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True) -> BatchResult:
+                  polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
+                  fuse: bool = True) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -492,10 +493,13 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
 
     def admm(idx, nidx):
         if grouped:   # every group relaunches; solved dates are skipped inside
+            fz = bd is not None and fuse and qb.mg <= 4   # uniform D + shared Cg: the fused form
             return lib.pq_admm_lr_grouped(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
                                           _ptr(groups.gdates), groups.ngroups, _ptr(groups.urows),
                                           _ptr(groups.ucnt), _ptr(groups.uoff), groups.umax, SS,
-                                          int(s.max_iter), strm)
+                                          int(s.max_iter), bd["pc"].data_ptr() if fz else None,
+                                          bd["pc"].stride(0) if fz else 0, bd["r0"] if fz else 0,
+                                          bd["cc"].data_ptr() if fz else None, strm)
         return lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld, _ptr(idx),
                                       nidx, SS, int(s.max_iter), strm)
 

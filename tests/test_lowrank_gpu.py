@@ -182,3 +182,35 @@ def test_band_gram_capacitance_matches_direct(device, centred, groups_rows, stri
     assert np.all(r2.status.cpu().numpy() == 1) and np.all(r1.status.cpu().numpy() == 1)
     assert np.abs(r2.iters.cpu().numpy() - i1).max() <= 2
     assert np.abs(r2.x.cpu().numpy() - x1).max() < 1e-8
+
+
+@pytest.mark.parametrize("n,T,D,stride,groups_rows,centred", [(1000, 252, 40, 1, False, True),
+                                                               (300, 120, 40, 2, True, True),
+                                                               (400, 100, 30, 1, True, False)])
+def test_grouped_fused_matches_unfused(device, n, T, D, stride, groups_rows, centred):
+    """The fused grouped ADMM (uniform D: Cg x~ from the band tables, one pass per date)
+    follows the unfused kernel's iterates and reaches the same polished weights."""
+    ends = list(range(T + 5, T + 5 + D * stride, stride))
+    dates, R, y, sec, pan, r_d, t_d, mu = _setup(n, T, ends, centred=centred, D=max(ends) + 1)
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    B = len(ends)
+    G = h = None
+    if groups_rows:
+        G = np.stack([(sec == g).astype(float) for g in range(3)])
+        h = np.full(3, 0.35)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=G, h=h, lb=np.zeros(n), ub=np.full(n, 0.15), device=device)
+    qb.batch = B
+    qb.P = None
+    qb.q = torch.zeros((B, qb.ld), dtype=torch.float64, device=device)
+    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=device)
+    w = 1.0 / (t_d.to(torch.float64) - 1.0) if centred else None
+    lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=w)
+    gp = engine.GroupPlan(rows, tlen, device)
+    r1 = engine.solve_lowrank(qb, lr, groups=gp, fuse=False)
+    x1, i1 = r1.x.cpu().numpy().copy(), r1.iters.cpu().numpy().copy()
+    assert r1.capacitance == "band"
+    r2 = engine.solve_lowrank(qb, lr, groups=gp, fuse=True)
+    assert np.all(r1.status.cpu().numpy() == 1) and np.all(r2.status.cpu().numpy() == 1)
+    assert np.abs(r2.iters.cpu().numpy() - i1).max() <= 2
+    assert np.abs(r2.x.cpu().numpy() - x1).max() < 1e-8
