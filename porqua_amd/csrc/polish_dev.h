@@ -252,6 +252,45 @@ __device__ void lr_pass2(const pq_lowrank& lr, int b, int n, const double* u, do
   }
 }
 
+// lr_pass1 for an x supported on k listed columns (x_F compact in LDS, index list Fl in
+// LDS): u_t = sum_p X_t,F[p] x_F[p] - mu . x, gathered from the window rows -- k
+// instead of n loads per row.  4 rows per wave in flight.  Ends with a barrier.
+__device__ void lr_pass1_sparse(const pq_lowrank& lr, int b, const int* Fl, int k, const double* xF,
+                                double* u, double* red) {
+  constexpr int RU = 4;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  double mux = 0.0;
+  if (mu) {
+    double a = 0.0;
+    for (int p = t; p < k; p += PT) a += mu[Fl[p]] * xF[p];
+    mux = block_sum(a, red);
+  }
+  for (int t0 = w * RU; t0 < T; t0 += RU * PW) {
+    double a[RU];
+    const double* row[RU];
+#pragma unroll
+    for (int e = 0; e < RU; ++e) {
+      a[e] = 0.0;
+      row[e] = lr.panel + (int64_t)rws[t0 + e < T ? t0 + e : 0] * lr.ldp;
+    }
+    for (int p = l; p < k; p += 64) {
+      const int c = Fl[p];
+      const double xv = xF[p];
+#pragma unroll
+      for (int e = 0; e < RU; ++e) a[e] = fma(row[e][c], xv, a[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < RU; ++e) {
+      const double d = wave_sum(a[e]);
+      if (l == 0 && t0 + e < T) u[t0 + e] = d - mux;
+    }
+  }
+  __syncthreads();
+}
+
 // emit(i, w_scale * (Xc' Xc x)_i) for i < n: both passes (u: LDS >= tmax doubles).
 template <typename EmitF>
 __device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* tree,

@@ -169,6 +169,111 @@ struct FormRead {   // the lower tiles (diagonal tiles in full) as written
   __device__ __forceinline__ double operator()(int gi, int gj) const { return K[(int64_t)gi * ld + gj]; }
 };
 
+// P_FF for k <= 128 (one or two column blocks): each 16-row chunk of the window is
+// gathered ONCE for all (NB (NB + 1) / 2) tiles into one LDS image of pitch NB*64 + 16,
+// double-buffered so the next chunk's gathers are in flight during the MFMAs.
+template <int NB>
+__device__ void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k, double psw, double pd,
+                               double* Ks, int64_t ldk, double* smem) {
+  constexpr int PIT = NB * TB + 16;
+  constexpr int NT = NB * (NB + 1) / 2;
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const int t = threadIdx.x, kr = t >> 4, c4 = (t & 15) * 4;
+  int col[NB][4];
+  double mc[NB][4];
+#pragma unroll
+  for (int h = 0; h < NB; ++h)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int p = h * TB + c4 + e;
+      col[h][e] = p < k ? Fl[p] : -1;
+      mc[h][e] = (col[h][e] >= 0 && mu) ? mu[col[h][e]] : 0.0;
+    }
+  double v[NB][4];
+  auto gather = [&](int t0) {
+    const int tt = t0 + kr;
+    const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
+#pragma unroll
+    for (int h = 0; h < NB; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[h][e] = (row && col[h][e] >= 0) ? row[col[h][e]] - mc[h][e] : 0.0;
+  };
+  auto put = [&](double* S) {
+#pragma unroll
+    for (int h = 0; h < NB; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) S[kr * PIT + h * TB + c4 + e] = v[h][e];
+  };
+  // acc[tile] for tiles (0,0), (1,0), (1,1); mma over an image of pitch PIT
+  Acc acc[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc[q].zero();
+  const int l = lane_id(), w = wave_id();
+  const int i0 = (w >> 1) * 32 + (l & 15), j0 = (w & 1) * 32 + (l & 15), krd = l >> 4;
+  auto mma = [&](const double* S) {
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      const double* r = S + (kk + krd) * PIT;
+      double a[NB][2];
+#pragma unroll
+      for (int h = 0; h < NB; ++h) {
+        a[h][0] = r[h * TB + i0];
+        a[h][1] = r[h * TB + i0 + 16];
+      }
+      double bj[NB][2];
+#pragma unroll
+      for (int h = 0; h < NB; ++h) {
+        bj[h][0] = r[h * TB + j0];
+        bj[h][1] = r[h * TB + j0 + 16];
+      }
+      int q = 0;
+#pragma unroll
+      for (int I = 0; I < NB; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J, ++q)
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int nn = 0; nn < 2; ++nn)
+              acc[q].c[m][nn] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I][m], bj[J][nn], acc[q].c[m][nn], 0, 0, 0);
+    }
+  };
+  double* S0 = smem;
+  double* S1 = smem + KC * PIT;
+  gather(0);
+  __syncthreads();   // the stage buffers' previous users are done
+  put(S0);
+  __syncthreads();
+  int buf = 0;
+  for (int t0 = 0; t0 < T; t0 += KC) {
+    const bool more = t0 + KC < T;
+    if (more) gather(t0 + KC);
+    mma(buf ? S1 : S0);
+    if (more) put(buf ? S0 : S1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  int q = 0;
+#pragma unroll
+  for (int I = 0; I < NB; ++I)
+#pragma unroll
+    for (int J = 0; J <= I; ++J, ++q)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int gi = I * TB + acc_row(m, r), gj = J * TB + acc_col(nn);
+            const double vv = psw * acc[q].c[m][nn][r] + (gi == gj ? pd : 0.0);
+            if (I == J) Ks[(int64_t)gi * ldk + gj] = vv;
+            else Ks[(int64_t)gj * ldk + gi] = vv;
+          }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, pq_state st,
                                                  const int32_t* idx, int nidx, pq_settings s, int ldk,
                                                  int final_try) {
@@ -198,7 +303,8 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
   const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
-  const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
+  const double psw = ps * wsc;
   const double* q = pb.q + (int64_t)b * pb.q_stride;
   const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
   const double* lg = pb.lg ? pb.lg + (int64_t)b * pb.g_stride : nullptr;
@@ -477,7 +583,9 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       // ---- P_FF from the window, then factor P_FF + delta I --------------------------------
       int info = 0;
       if (k > 0) {
-        form_pff(lr, b, Fl, k, nbk, psw, pd, K, ldk, smem);
+        if (nbk == 1) form_pff_small<1>(lr, b, Fl, k, psw, pd, K, ldk, smem);
+        else if (nbk == 2) form_pff_small<2>(lr, b, Fl, k, psw, pd, K, ldk, smem);
+        else form_pff(lr, b, Fl, k, nbk, psw, pd, K, ldk, smem);
         info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
       }
       if (info) break;
@@ -584,7 +692,12 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       __syncthreads();
     }
     __builtin_amdgcn_s_dcache_inv();   // xs was rewritten: no stale scalar-cache reads
-    full_px();
+    if (compact && !nzb) {   // x = x_F exactly: pass 1 gathers the k free columns only
+      lr_pass1_sparse(lr, b, Fl, k, solx, vec, red);
+      lr_pass2(lr, b, n, vec, stg, red, [&](int i, double v) { emit_g(i, wsc * v); });
+    } else {
+      full_px();
+    }
     __syncthreads();
     PQ_STAMP(6);
     int bad = 0;

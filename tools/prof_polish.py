@@ -29,12 +29,13 @@ def main():
                                    lb=np.zeros(n), ub=np.ones(n))
     qb.batch = D
     mu = pan.window_means(r_d, t_d)
-    qb.P = pan.cov(r_d, t_d, mode=0, mu=mu)
-    qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=qb.P.device)
-    qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=qb.P.device)
+    dev = mu.device
+    qb.P = None   # window path: P stays in window form
+    qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=dev)
+    qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)
     lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
-    ws = engine.Workspace(qb)
-    gp = engine.GroupPlan(rows, tlen, qb.P.device) if "--group" in sys.argv else None
+    ws = engine.Workspace(qb, dense=False)
+    gp = engine.GroupPlan(rows, tlen, dev) if "--group" in sys.argv else None
     off = (9 + ws.mg_pad) * qb.ld   # PQ_WORK_PROF
     for _ in range(2):
         ev = []
