@@ -54,8 +54,9 @@ class Settings:
     rho0_rel: float = 4.0      # initial rho = rho0_rel * mean(diag P) (0: use rho0)
     sigma: float = 1e-6
     alpha: float = 1.6
-    eps_abs: float = 1e-5
-    eps_rel: float = 1e-5
+    eps_abs: float = 1e-4      # ADMM stop before the polish (OSQP's default is 1e-3)
+    eps_rel: float = 1e-4
+    eps_retry: float = 1e-7    # problems whose polish is rejected resume ADMM to this eps
     rho_min: float = 1e-6
     rho_max: float = 1e6
     adapt_tol: float = 5.0
@@ -69,7 +70,9 @@ class Settings:
     refine_iters: int = 4
 
     def to_c(self) -> _lib.PQSettings:
-        return _lib.PQSettings(**{f.name: getattr(self, f.name) for f in dataclasses.fields(self)})
+        names = {f[0] for f in _lib.PQSettings._fields_}
+        return _lib.PQSettings(**{f.name: getattr(self, f.name) for f in dataclasses.fields(self)
+                                  if f.name in names})
 
     @classmethod
     def from_params(cls, params) -> "Settings":
@@ -325,29 +328,51 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
     _lib.check(lib.pq_init_state(P_, S_, None, 0, SS, strm), "pq_init_state")
     _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, None, 0, SS, 1, strm)),
                "pq_factor_batched")
-    idx = None
-    nidx = 0
-    refactors = launches = 0
-    for _ in range(max_rounds):
-        _lib.check(tl("admm", lambda: lib.pq_admm_batched(P_, S_, _ptr(idx), nidx, SS,
-                                                          int(s.max_iter), strm)),
-                   "pq_admm_batched")
-        launches += 1
-        need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
-        k = int(need.numel())   # host sync: small status vector
-        if k == 0:
-            break
-        idx, nidx = need.contiguous(), k
-        _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, _ptr(idx), nidx, SS, 1, strm)),
-                   "pq_factor_batched")
-        refactors += k
+    cnt = {"refactors": 0, "launches": 0}
+
+    def admm_rounds(idx, nidx, SSx):
+        for _ in range(max_rounds):
+            _lib.check(tl("admm", lambda: lib.pq_admm_batched(P_, S_, _ptr(idx), nidx, SSx,
+                                                              int(s.max_iter), strm)),
+                       "pq_admm_batched")
+            cnt["launches"] += 1
+            need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
+            k = int(need.numel())   # host sync: small status vector
+            if k == 0:
+                break
+            idx, nidx = need.contiguous(), k
+            _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, _ptr(idx), nidx, SSx, 1, strm)),
+                       "pq_factor_batched")
+            cnt["refactors"] += k
+
+    admm_rounds(None, 0, SS)
     if s.polish:
         _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, None, 0, SS, strm)),
                    "pq_polish_batched")
+        retry = _retry_set(ws, settings or Settings())
+        if retry is not None:   # polish rejected: resume ADMM to eps_retry, polish again
+            idx, nidx, s2 = retry
+            admm_rounds(idx, nidx, ctypes.byref(s2))
+            _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, _ptr(idx), nidx, SS, strm)),
+                       "pq_polish_batched (retry)")
+    refactors, launches = cnt["refactors"], cnt["launches"]
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
                        admm_launches=launches)
+
+
+def _retry_set(ws: "Workspace", settings: Settings):
+    """Problems whose polish was rejected at the loose ADMM eps: reset them to UNSOLVED
+    and return (idx, n, settings with eps = eps_retry), or None (host sync: status)."""
+    bad = torch.nonzero(ws.status == _lib.PQ_SOLVED_INACCURATE).flatten().to(torch.int32)
+    m = int(bad.numel())
+    if m == 0 or settings.eps_retry <= 0 or settings.eps_retry >= min(settings.eps_abs, settings.eps_rel):
+        return None
+    ws.status[bad.long()] = _lib.PQ_UNSOLVED
+    s2 = settings.to_c()
+    s2.eps_abs = s2.eps_rel = settings.eps_retry
+    return bad.contiguous(), m, s2
 
 
 class LowRank:
@@ -487,8 +512,6 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     if band:
         bd = tl("gram", lambda: _band_setup(qb, lr, strm))
     tl("factor", lambda: refactor(None, 0))
-    idx, nidx = None, 0
-    refactors = launches = 0
     grouped = grouped_applicable(qb, lr, groups, ws)
 
     def admm(idx, nidx):
@@ -503,21 +526,28 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         return lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld, _ptr(idx),
                                       nidx, SS, int(s.max_iter), strm)
 
-    for _ in range(max_rounds):
-        _lib.check(tl("admm", lambda: admm(idx, nidx)), "pq_admm_lr")
-        launches += 1
-        need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
-        kk = int(need.numel())
-        if kk == 0:
-            break
-        idx, nidx = need.contiguous(), kk
-        tl("factor", lambda: refactor(idx, nidx))
-        refactors += kk
-    if s.polish and polish:
+    cnt = {"refactors": 0, "launches": 0}
+
+    def admm_rounds(idx, nidx, SSx):
+        nonlocal SS
+        SS0, SS = SS, SSx   # admm() reads SS
+        for _ in range(max_rounds):
+            _lib.check(tl("admm", lambda: admm(idx, nidx)), "pq_admm_lr")
+            cnt["launches"] += 1
+            need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
+            kk = int(need.numel())
+            if kk == 0:
+                break
+            idx, nidx = need.contiguous(), kk
+            tl("factor", lambda: refactor(idx, nidx))
+            cnt["refactors"] += kk
+        SS = SS0
+
+    def polish_w(idx, nidx):
         kmax = min(qb.ld, 1024)
         final = ldk >= kmax
-        _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, S_, None, 0, SS, ldk, int(final), strm)),
-                   "pq_polish_w_batched")
+        _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, S_, _ptr(idx), nidx, SS, ldk, int(final),
+                                                                strm)), "pq_polish_w_batched")
         if not final:   # free sets larger than the compact scratch: relaunch those with ldk = kmax
             over = torch.nonzero(ws.out[:, _lib.PQ_OUT_ROUNDS] < 0).flatten().to(torch.int32)
             m = int(over.numel())   # host sync: small vector
@@ -531,6 +561,16 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                 _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, ctypes.byref(st2), _ptr(over), m,
                                                                         SS, kmax, 1, strm)),
                            "pq_polish_w_batched (relaunch)")
+
+    admm_rounds(None, 0, SS)
+    if s.polish and polish:
+        polish_w(None, 0)
+        retry = _retry_set(ws, settings or Settings())
+        if retry is not None:   # polish rejected: resume ADMM to eps_retry, polish again
+            ridx, rn, s2 = retry
+            admm_rounds(ridx, rn, ctypes.byref(s2))
+            polish_w(ridx, rn)
+    refactors, launches = cnt["refactors"], cnt["launches"]
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,

@@ -214,3 +214,35 @@ def test_grouped_fused_matches_unfused(device, n, T, D, stride, groups_rows, cen
     assert np.all(r1.status.cpu().numpy() == 1) and np.all(r2.status.cpu().numpy() == 1)
     assert np.abs(r2.iters.cpu().numpy() - i1).max() <= 2
     assert np.abs(r2.x.cpu().numpy() - x1).max() < 1e-8
+
+
+@pytest.mark.parametrize("path", ["window", "dense"])
+def test_polish_rejection_resumes_admm_to_tight_eps(device, path):
+    """ADMM stops at eps 1e-4 for the polish; a problem whose polish is rejected (forced
+    here with a single active-set round) resumes ADMM to eps_retry from its iterate and is
+    polished again -- it ends SOLVED at the same optimum as the default settings."""
+    n, T, D = 300, 100, 12
+    ends = list(range(T + 5, T + 5 + D))
+    dates, R, y, sec, pan, r_d, t_d, mu = _setup(n, T, ends, D=max(ends) + 1)
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   lb=np.zeros(n), ub=np.full(n, 0.1), device=device)
+    qb.batch = D
+    qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=device)
+    qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=device)
+    if path == "dense":
+        qb.P = pan.cov(r_d, t_d, mode=0, mu=mu)
+        run = lambda st: engine.solve(qb, st)
+    else:
+        qb.P = None
+        lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+        gp = engine.GroupPlan(rows, tlen, device)
+        run = lambda st: engine.solve_lowrank(qb, lr, st, groups=gp)
+    ref = run(engine.Settings())
+    x0 = ref.x.cpu().numpy().copy()
+    assert np.all(ref.status.cpu().numpy() == 1)
+    one = run(engine.Settings(polish_rounds=1))
+    st = one.status.cpu().numpy()
+    assert np.all(st == 1), st
+    assert one.iters.cpu().numpy().max() > ref.iters.cpu().numpy().max()   # the retry ran
+    assert np.abs(one.x.cpu().numpy() - x0).max() < 1e-8
