@@ -533,7 +533,7 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
   }
   if (status == PQ_UNSOLVED && it >= s.max_iter) status = PQ_MAX_ITER;
   __syncthreads();
-  pc.flush(st.work + (int64_t)b * st.work_stride + (int64_t)(4 + st.mg_pad) * ld + 16);
+  pc.flush(st.work + (int64_t)b * st.work_stride + PQ_WORK_PROF(ld, st.mg_pad) + 16);
   // ---- save state --------------------------------------------------------------------
   {
     double* gx = st.x + (int64_t)b * ld;

@@ -335,6 +335,8 @@ __global__ __launch_bounds__(PT) void k_polish(pq_problem pb, pq_state st, const
         else if (a == 0 && sum < lg[r] - ptol * (1.0 + fabs(lg[r]))) { act[r] = 1; bad = 1; }
         else if (a == 2 && lam < -dtol) { act[r] = 0; bad = 1; }
         else if (a == 1 && lam > dtol) { act[r] = 0; bad = 1; }
+      } else if (l == 0 && fabs(sum - ug[r]) > 1e-10 * (1.0 + fabs(ug[r]))) {
+        bad = 1;   // an equality row the reduced system could not satisfy (no free support)
       }
     }
     bad = block_or(bad, red);

@@ -352,6 +352,9 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
         retry = _retry_set(ws, settings or Settings())
         if retry is not None:   # polish rejected: resume ADMM to eps_retry, polish again
             idx, nidx, s2 = retry
+            # the polish used K as scratch: restore K^-1 (current rho) before resuming
+            _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, _ptr(idx), nidx, SS, 1, strm)),
+                       "pq_factor_batched (retry)")
             admm_rounds(idx, nidx, ctypes.byref(s2))
             _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, _ptr(idx), nidx, SS, strm)),
                        "pq_polish_batched (retry)")

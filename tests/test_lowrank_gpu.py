@@ -230,6 +230,7 @@ def test_polish_rejection_resumes_admm_to_tight_eps(device, path):
     qb.batch = D
     qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=device)
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=device)
+    qb.p_diag = torch.full((D,), 1e-4, dtype=torch.float64, device=device)   # P > 0: a unique optimum
     if path == "dense":
         qb.P = pan.cov(r_d, t_d, mode=0, mu=mu)
         run = lambda st: engine.solve(qb, st)
