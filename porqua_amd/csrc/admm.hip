@@ -345,11 +345,6 @@ __device__ void lr_apply(const pq_lowrank& lr, int b, const pq_problem& pb, cons
 // Grid position -> problem slot so that the blocks sharing an XCD (g = x mod 8) take a
 // contiguous range of dates: neighbouring windows overlap in T-1 rows, so the low-rank
 // kernels then find the panel rows in that XCD's L2 (speed only, bijective for any N).
-__device__ __forceinline__ int xcd_slot(int g, int N) {
-  const int x = g & 7, q = N >> 3, r = N & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (g >> 3);
-}
-
 template <int NQ, int NQK, int MODE>
 __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const int32_t* idx,
                                              int nidx, pq_settings s, int iters_call, pq_lowrank lr,

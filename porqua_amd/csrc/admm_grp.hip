@@ -52,11 +52,6 @@ __device__ __forceinline__ double hmax(double v) {
   return v;
 }
 
-__device__ __forceinline__ int grp_slot(int g, int N) {   // XCD-contiguous group order
-  const int x = g & 7, q = N >> 3, r = N & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (g >> 3);
-}
-
 #ifdef PQ_PROFILE
 #define GSTAMP(k)                                                 \
   do {                                                            \
@@ -101,7 +96,7 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
   __shared__ double s_dot[NQK * 128];                                       // symv dot parts
   __shared__ double s_red[GNW];
 
-  const int grp = grp_slot(blockIdx.x, gridDim.x);
+  const int grp = xcd_slot(blockIdx.x, gridDim.x);
   const int d0 = gdates[grp];
   const int G = gdates[grp + 1] - d0;
   const int U = ucnt_all[grp];

@@ -185,6 +185,14 @@ __device__ __forceinline__ void acc_store_T(const Acc& acc, double* G, int64_t l
         G[(int64_t)(row0 + acc_col(n)) * ld + col0 + acc_row(m, r)] = acc.c[m][n][r];
 }
 
+// XCD-contiguous block order: the hardware deals workgroups round-robin over the 8 XCDs
+// (each with its own L2); slot g' = xcd_slot(blockIdx.x) gives XCD x a contiguous range of
+// slots, so neighbouring problems (overlapping windows) share one L2.
+__device__ __forceinline__ int xcd_slot(int g, int N) {
+  const int x = g & 7, q = N >> 3, r = N & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (g >> 3);
+}
+
 // ---- workgroup reductions (any block size that is a multiple of 64, <= 1024) ----------
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -219,11 +219,6 @@ __global__ __launch_bounds__(64) void k_panel_cg(const double* panel, int64_t ld
   }
 }
 
-__device__ __forceinline__ int xcd_slot(int g, int N) {   // XCD-contiguous block order
-  const int x = g & 7, q = N >> 3, r = N & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (g >> 3);
-}
-
 // M (lower 64x64 tiles, diagonal tiles in full) of one date per 256-thread workgroup
 __global__ __launch_bounds__(256) void k_lr_cap_band(pq_lowrank lr, pq_problem pb, const double* rho_all,
                                                      const int32_t* idx, pq_settings s, const double* band,
