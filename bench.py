@@ -274,6 +274,29 @@ def main():
                    "settings_overrides": args.set},
         "cpu_baseline": None,
     }
+    # ---- next row, outside the timed region: Strategy.simulate of
+    # the solved weights, one holding period per rebalance date (float, level, turnover) ----
+    wx = res.x[:, :n]
+    row0 = ends_local.copy()
+    nrows = np.full(D, 2, dtype=np.int64)
+    nrows[-1] = 1                                       # the last period ends at the panel end
+    sim_args = (pan.R, wx, engine.PeriodPlan(row0, nrows, device=dev, panel_rows=pan.D))
+    engine.simulate_periods(*sim_args, want_end=True)
+    s_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    reps = 20
+    s_ev[0].record()
+    for _ in range(reps):
+        engine.simulate_periods(*sim_args, want_end=True)
+    s_ev[1].record()
+    torch.cuda.synchronize()
+    sim_s = s_ev[0].elapsed_time(s_ev[1]) * 1e-3 / reps
+    sim_bytes = 8.0 * n * (int((nrows - 1).sum()) + 2 * D) + 16.0 * D   # panel rows + W in + wend out
+    out["next_rows"] = {"simulate": {
+        "kernel": "k_float_periods (pq_simulate_periods)", "periods": D,
+        "us_per_launch": sim_s * 1e6, "algorithmic_bytes": int(sim_bytes),
+        "achieved_gbs": sim_bytes / sim_s / 1e9, "frac_hbm": sim_bytes / sim_s / 1e9 / HBM_PEAK_GBS,
+        "note": "daily periods: 1 panel row + weights in, floated weights out, per period; "
+                "period tables staged once (engine.PeriodPlan)"}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.cpu_baseline import blas_threads, time_reference
         sample = np.linspace(T - 1, T - 1 + D - 1, 8).astype(int)

@@ -249,6 +249,23 @@ int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st
                         int32_t nidx, const pq_settings* s, int32_t ldk, int32_t final_try,
                         void* stream);
 
+/* Strategy simulation: one holding period per rebalance date.
+ * Replaces Strategy.simulate (src/portfolio.py:209-248) with floating_weights
+ * (src/portfolio.py:259-296) and the end-weight part of Portfolio.turnover
+ * (src/portfolio.py:111-123).  Period p floats W[p] (n weights, stride ldw) over panel rows
+ * row0[p] .. row0[p] + nrows[p] - 1 (row 0 of the period is the weights themselves; NaN
+ * returns count as 0) and writes its nrows[p] - 1 level returns (loan + cash + margin +
+ * floated weights, pct_change) to ret[ret_off[p] ...].  fc != 0 subtracts the fixed cost
+ * (1 + fc)^((ret_day[q] - ret_day[q-1]) / days_per_year) - 1 from every return q > 0 of
+ * the flattened series (ret_day = calendar day of each return).  Optional outputs: wend
+ * (floated end weights, rescaled to unit long / short books when rescale != 0, stride
+ * ldwe) and turnover[p] = sum_j |wend[p][j] - W[p][j]|.  n <= 8192.                   */
+int pq_simulate_periods(const double* panel, int64_t ldp, int32_t n, const double* W, int64_t ldw,
+                        const int32_t* row0, const int32_t* nrows, int32_t nper,
+                        const int64_t* ret_off, const int32_t* ret_day, double fc,
+                        double days_per_year, double* ret, double* wend, int64_t ldwe,
+                        double* turnover, int32_t rescale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

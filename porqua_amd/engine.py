@@ -803,3 +803,67 @@ class Panel:
                                           _ptr(tlen), tmax, B, _ptr(xty), xty.stride(0), _ptr(yty),
                                           _stream()), "pq_gram_xy_batched")
         return xty, yty
+
+
+
+class PeriodPlan:
+    """Device tables of one simulation launch: first panel row and row count of every
+    holding period, the offset of its returns in the flattened series and (for the fixed
+    cost) the calendar day of every return.  Built once, reusable across launches."""
+
+    def __init__(self, row0, nrows, ret_day=None, device=None, panel_rows=None):
+        row0 = np.asarray(row0, dtype=np.int64)
+        nrows = np.asarray(nrows, dtype=np.int64)
+        if len(row0) != len(nrows):
+            raise ValueError("PeriodPlan: one (row0, nrows) per period")
+        if len(row0) and (row0.min() < 0 or nrows.min() < 1 or
+                          (panel_rows is not None and (row0 + nrows).max() > panel_rows)):
+            raise ValueError("PeriodPlan: period rows outside the panel")
+        self.nper = len(row0)
+        self.rows_end = int((row0 + nrows).max()) if self.nper else 0
+        nret = np.maximum(nrows - 1, 0)
+        off = np.concatenate([[0], np.cumsum(nret)[:-1]]) if self.nper else np.zeros(0, np.int64)
+        self.total = int(nret.sum())
+        dev = device or default_device()
+        self.row0 = torch.as_tensor(row0.astype(np.int32), device=dev)
+        self.nrows = torch.as_tensor(nrows.astype(np.int32), device=dev)
+        self.off = torch.as_tensor(off.astype(np.int64), device=dev)
+        self.ret_day = None
+        if ret_day is not None:
+            if len(ret_day) != self.total:
+                raise ValueError("PeriodPlan: one calendar day per return")
+            self.ret_day = torch.as_tensor(np.asarray(ret_day, dtype=np.int32), device=dev)
+
+
+def simulate_periods(panel: torch.Tensor, W: torch.Tensor, plan, nrows=None, ret_day=None,
+                     fc: float = 0.0, days_per_year: float = 252.0, rescale: bool = False,
+                     want_end: bool = False):
+    """Float each period's weights over its panel rows on the device (pq_simulate_periods;
+    Strategy.simulate / floating_weights / Portfolio.turnover, src/portfolio.py:111-123,
+    209-296).  ``panel`` (rows x n) and ``W`` (periods x n) are FP64 device tensors;
+    ``plan`` is a PeriodPlan (or the row0 array, with ``nrows`` / ``ret_day`` given).
+    Returns (ret [sum(nrows - 1)], wend [periods x n] or None, turnover [periods] or None),
+    all on the device."""
+    dev = panel.device
+    nper, n = int(W.shape[0]), int(W.shape[1])
+    if panel.dtype != F64 or W.dtype != F64 or panel.dim() != 2 or panel.shape[1] != n:
+        raise ValueError("simulate_periods: FP64 panel (rows x n) and W (periods x n) expected")
+    if not isinstance(plan, PeriodPlan):
+        plan = PeriodPlan(plan, nrows, ret_day, dev, panel_rows=panel.shape[0])
+    if plan.nper != nper or plan.rows_end > panel.shape[0]:
+        raise ValueError("simulate_periods: plan does not match the weights / panel")
+    if fc != 0.0 and plan.ret_day is None:
+        raise ValueError("simulate_periods: fc needs one calendar day per return")
+    if panel.stride(1) != 1:
+        panel = panel.contiguous()
+    if W.stride(1) != 1:
+        W = W.contiguous()
+    total = plan.total
+    ret = torch.empty(max(total, 1), dtype=F64, device=dev)
+    wend = torch.empty((nper, n), dtype=F64, device=dev) if want_end else None
+    to = torch.empty(max(nper, 1), dtype=F64, device=dev) if want_end else None
+    _lib.check(_lib.load().pq_simulate_periods(
+        _ptr(panel), panel.stride(0), n, _ptr(W), W.stride(0), _ptr(plan.row0), _ptr(plan.nrows), nper,
+        _ptr(plan.off), _ptr(plan.ret_day), float(fc), float(days_per_year), _ptr(ret), _ptr(wend),
+        n, _ptr(to), int(bool(rescale)), _stream()), "pq_simulate_periods")
+    return ret[:total], wend, (to[:nper] if to is not None else None)
