@@ -69,12 +69,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("PQ_BENCH_SHARE_DEVICE"):   # rehearsal: every rank on cuda:0 (1-GPU box)
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("PQ_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     n, T, D = args.n, args.window, args.dates
     d_total = T - 1 + D * world
@@ -105,8 +108,17 @@ def main():
     if with_cov:   # K1 writes Sigma every step (dense path: P = 2 Sigma is what K2 factors)
         qb.P = torch.empty((D, ld, ld), dtype=torch.float64, device=dev)
     ws = engine.Workspace(qb, dense=not use_lr)
-    w_host = torch.empty((D * world, n), dtype=torch.float64).pin_memory() if rank == 0 else None
-    gather_buf = torch.empty((world, D, n), dtype=torch.float64, device=dev) if world > 1 else None
+    # weights leave the device on a side stream: step k's all-gather (RCCL) and D2H copy to
+    # rank 0's pinned host panel overlap step k + 1's kernels (double-buffered staging)
+    nbuf = 2
+    w_host = [torch.empty((D * world, n), dtype=torch.float64).pin_memory() for _ in range(nbuf)] \
+        if rank == 0 else None
+    x_stage = [torch.empty((D, n), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    gather_buf = [torch.empty((world * D, n), dtype=torch.float64, device=dev) for _ in range(nbuf)] \
+        if world > 1 else None
+    side = torch.cuda.Stream(device=dev)
+    side_done = [None] * nbuf
+    nstep = [0]
 
     def step(events=None):
         if events is not None:
@@ -123,13 +135,24 @@ def main():
             res = engine.solve_lowrank(qb, lr, settings, ws, events=events, groups=gplan)
         else:
             res = engine.solve(qb, settings, ws, events=events)
-        x = res.x.contiguous()
-        if world > 1:
-            dist.all_gather_into_tensor(gather_buf, x)
-            if rank == 0:
-                w_host.copy_(gather_buf.view(-1, n), non_blocking=True)
-        else:
-            w_host.copy_(x, non_blocking=True)
+        k = nstep[0] % nbuf
+        nstep[0] += 1
+        main = torch.cuda.current_stream()
+        if side_done[k] is not None:
+            main.wait_event(side_done[k])      # staging buffer k is free again
+        x_stage[k].copy_(res.x[:, :n])
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            if world > 1:
+                dist.all_gather_into_tensor(gather_buf[k], x_stage[k])
+                if rank == 0:
+                    w_host[k].copy_(gather_buf[k], non_blocking=True)
+            else:
+                w_host[k].copy_(x_stage[k], non_blocking=True)
+            side_done[k] = torch.cuda.Event()
+            side_done[k].record(side)
         return res
 
     for _ in range(args.warmup):
