@@ -169,14 +169,18 @@ struct FormRead {   // the lower tiles (diagonal tiles in full) as written
   __device__ __forceinline__ double operator()(int gi, int gj) const { return K[(int64_t)gi * ld + gj]; }
 };
 
-// P_FF for k <= 128 (one or two column blocks): each 16-row chunk of the window is
+// P_FF for k <= 128 (one or two column blocks): each 32-row chunk of the window is
 // gathered ONCE for all (NB (NB + 1) / 2) tiles into one LDS image of pitch NB*64 + 16,
-// double-buffered so the next chunk's gathers are in flight during the MFMAs.
+// double-buffered so the next chunk's gathers (2 rows x 4 NB columns per thread, all in
+// flight together) overlap the MFMAs: 8 dependent gather round trips for T = 252.
 template <int NB>
 __device__ void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k, double psw, double pd,
                                double* Ks, int64_t ldk, double* smem) {
   constexpr int PIT = NB * TB + 16;
   constexpr int NT = NB * (NB + 1) / 2;
+  constexpr int KCH = 32;             // window rows per chunk (2 x 32 x PIT <= CHOL_LDS)
+  constexpr int RS = KCH / 16;        // rows per thread and chunk
+  static_assert(2 * KCH * PIT <= CHOL_LDS, "form_pff_small: stage buffers exceed the LDS region");
   const int T = lr.tlen[b];
   const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
@@ -191,20 +195,25 @@ __device__ void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k
       col[h][e] = p < k ? Fl[p] : -1;
       mc[h][e] = (col[h][e] >= 0 && mu) ? mu[col[h][e]] : 0.0;
     }
-  double v[NB][4];
+  double v[RS][NB][4];
   auto gather = [&](int t0) {
-    const int tt = t0 + kr;
-    const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
 #pragma unroll
-    for (int h = 0; h < NB; ++h)
+    for (int s = 0; s < RS; ++s) {
+      const int tt = t0 + kr + 16 * s;
+      const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[h][e] = (row && col[h][e] >= 0) ? row[col[h][e]] - mc[h][e] : 0.0;
+      for (int h = 0; h < NB; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[s][h][e] = (row && col[h][e] >= 0) ? row[col[h][e]] - mc[h][e] : 0.0;
+    }
   };
   auto put = [&](double* S) {
 #pragma unroll
-    for (int h = 0; h < NB; ++h)
+    for (int s = 0; s < RS; ++s)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) S[kr * PIT + h * TB + c4 + e] = v[h][e];
+      for (int h = 0; h < NB; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) S[(kr + 16 * s) * PIT + h * TB + c4 + e] = v[s][h][e];
   };
   // acc[tile] for tiles (0,0), (1,0), (1,1); mma over an image of pitch PIT
   Acc acc[NT];
@@ -214,7 +223,7 @@ __device__ void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k
   const int i0 = (w >> 1) * 32 + (l & 15), j0 = (w & 1) * 32 + (l & 15), krd = l >> 4;
   auto mma = [&](const double* S) {
 #pragma unroll
-    for (int kk = 0; kk < KC; kk += 4) {
+    for (int kk = 0; kk < KCH; kk += 4) {
       const double* r = S + (kk + krd) * PIT;
       double a[NB][2];
 #pragma unroll
@@ -241,15 +250,15 @@ __device__ void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k
     }
   };
   double* S0 = smem;
-  double* S1 = smem + KC * PIT;
+  double* S1 = smem + KCH * PIT;
   gather(0);
   __syncthreads();   // the stage buffers' previous users are done
   put(S0);
   __syncthreads();
   int buf = 0;
-  for (int t0 = 0; t0 < T; t0 += KC) {
-    const bool more = t0 + KC < T;
-    if (more) gather(t0 + KC);
+  for (int t0 = 0; t0 < T; t0 += KCH) {
+    const bool more = t0 + KCH < T;
+    if (more) gather(t0 + KCH);
     mma(buf ? S1 : S0);
     if (more) put(buf ? S0 : S1);
     __syncthreads();
@@ -586,6 +595,7 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
         if (nbk == 1) form_pff_small<1>(lr, b, Fl, k, psw, pd, K, ldk, smem);
         else if (nbk == 2) form_pff_small<2>(lr, b, Fl, k, psw, pd, K, ldk, smem);
         else form_pff(lr, b, Fl, k, nbk, psw, pd, K, ldk, smem);
+        PQ_STAMP(9);
         info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
       }
       if (info) break;
@@ -692,6 +702,7 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       __syncthreads();
     }
     __builtin_amdgcn_s_dcache_inv();   // xs was rewritten: no stale scalar-cache reads
+    PQ_STAMP(6);
     if (compact && !nzb) {   // x = x_F exactly: pass 1 gathers the k free columns only
       lr_pass1_sparse(lr, b, Fl, k, solx, vec, red);
       lr_pass2(lr, b, n, vec, stg, red, [&](int i, double v) { emit_g(i, wsc * v); });
@@ -699,7 +710,7 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       full_px();
     }
     __syncthreads();
-    PQ_STAMP(6);
+    PQ_STAMP(10);
     int bad = 0;
     for (int i = t; i < n; i += PT) {
       const int f = fl[i];

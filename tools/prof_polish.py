@@ -14,8 +14,8 @@ sys.path.insert(0, ROOT)
 from porqua_amd import engine  # noqa: E402
 from porqua_amd.synthetic import factor_panel  # noqa: E402
 
-PHASES = ["setup+classify", "free list", "rF/dA", "cholesky", "U+S", "refine", "expand+Px",
-          "checks", "final", "form P_FF"]
+PHASES = ["setup+classify", "free list", "rF/dA", "cholesky", "U+S", "refine", "expand",
+          "checks", "final", "form P_FF", "exact Px"]
 
 
 def main():
@@ -55,7 +55,7 @@ def main():
     for i, p in enumerate(["rhs", "v, mu.v", "w = U v", "M^-1 symv", "U'u + tree + corr", "updates+resid"]):
         print("  %-18s %8.2f us/iter (%4.1f %%)" % (p, (ad[:, i] / its).mean(), 100 * ad[:, i].mean() / atot.mean()))
     prof = ws.work[:, off:off + 16].cpu().numpy() * 10e-3   # ticks (10 ns) -> us
-    tot = prof[:, :10].sum(1)
+    tot = prof[:, :11].sum(1)
     print("polish us per problem: mean %.1f  p50 %.1f  p90 %.1f" % (tot.mean(), np.median(tot), np.percentile(tot, 90)))
     for i, p in enumerate(PHASES):
         print("  %-16s %8.1f us  (%4.1f %%)" % (p, prof[:, i].mean(), 100 * prof[:, i].mean() / tot.mean()))
