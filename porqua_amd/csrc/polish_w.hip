@@ -305,7 +305,8 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
   int* Al = act + 64;                                 // 64
   int* cnt = Al + 64;                                 // PT + 8
 
-  const int b = idx ? idx[blockIdx.x] : (int)blockIdx.x;
+  const int slot = xcd_slot(blockIdx.x, gridDim.x);   // neighbouring dates share an XCD L2
+  const int b = idx ? idx[slot] : slot;
   const int st0 = st.status[b];
   if (st0 != PQ_SOLVED && st0 != PQ_MAX_ITER) return;
   const int n = pb.n, ld = pb.ld, mg = pb.mg;

@@ -37,11 +37,23 @@ class QuadraticProgram(dict):
     def __init__(self, *args, **kwargs):
         super().__init__(*args, **kwargs)
         self.solver = self["params"]["solver_name"]
+        self._l1 = None         # recorded l1 term (l1split.L1Split) + the problem before it
+
+    def _record_l1(self, kind, x0, value):
+        """Keep the problem as it was before the (first) l1 linearisation: the engine solves
+        the signed split of it (porqua_amd/l1split.py) instead of the 2n linearised rows."""
+        from .l1split import L1Split
+        if self._l1 is None:
+            base = {k: self.get(k) for k in ("P", "q", "G", "h", "A", "b", "lb", "ub")}
+            self._l1 = (L1Split(kind, x0, value), base)
+        else:
+            self._l1 = "unsupported"   # several l1 terms: solved in the linearised form
 
     # -- l1 linearisations (src/qp_problems.py:40-157): auxiliary variables d >= |x - x0| ----
     def linearize_turnover_constraint(self, x_init, to_budget=float("inf")) -> None:
         """Turnover budget sum|x - x0| <= to_budget via d: [x; d], x - d <= x0, -x - d <= -x0."""
         x0 = np.asarray(x_init, dtype=np.float64).reshape(-1)
+        self._record_l1("budget", x0, to_budget)
         n = len(self["q"])
         eye = np.eye(n)
         rows = [np.hstack([eye, -eye]), np.hstack([-eye, -eye]),
@@ -52,6 +64,7 @@ class QuadraticProgram(dict):
     def linearize_turnover_objective(self, x_init, transaction_cost=0.002) -> None:
         """Proportional cost transaction_cost * sum|x - x0| in the objective via d."""
         x0 = np.asarray(x_init, dtype=np.float64).reshape(-1)
+        self._record_l1("cost", x0, transaction_cost)
         n = len(self["q"])
         eye = np.eye(n)
         rows = [np.hstack([eye, -eye]), np.hstack([-eye, -eye])]
@@ -61,6 +74,7 @@ class QuadraticProgram(dict):
         """sum|x| <= leverage_budget via x = x+ - x-, x+, x- >= 0 (src/qp_problems.py:79-118)."""
         n = len(self["q"])
         N = n if N is None else int(N)
+        self._l1 = "unsupported"   # leverage: solved in the linearised form (DESIGN.md §7)
         P = self.get("P")
         if P is not None:
             P = np.pad(P, (0, 2 * N))
@@ -120,9 +134,32 @@ class QuadraticProgram(dict):
 
     def solve(self) -> None:
         if self.solver in ENGINE_SOLVERS:
-            self["solution"] = solve_batch([self])[0]
+            if isinstance(self._l1, tuple):
+                self["solution"] = self._solve_l1_split()
+            else:
+                self["solution"] = solve_batch([self])[0]
             return None
         return self._solve_qpsolvers()
+
+    def _solve_l1_split(self):
+        """The engine solve of a problem with one turnover term: the signed split
+        (l1split.split_problem), mapped back to the reference's [x; d] variables and
+        objective (0.5 x'Px + q'x + c 1'd, src/qp_problems.py:219-221)."""
+        from .l1split import merge_solution, split_problem
+        term, base = self._l1
+        sp = split_problem(base, term)
+        sub = {k: sp[k] for k in ("P", "q", "G", "h", "A", "b", "lb", "ub")}
+        sub["params"] = self["params"]
+        sol = solve_batch([sub])[0]
+        if sol.x is not None:
+            x, d = merge_solution(sol.x, term)
+            sol.x = np.concatenate([x, d])
+            if sol.found:
+                sol.obj = self.objective_value(sol.x, with_const=False)
+        sol.z = None      # multipliers of the split rows, not of the 2n linearised rows
+        sol.z_box = None
+        sol.extras = dict(sol.extras or {}, l1_split=term.kind)
+        return sol
 
     def _solve_qpsolvers(self) -> None:
         """Non-engine solver names keep the reference behaviour (third-party qpsolvers)."""
