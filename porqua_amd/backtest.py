@@ -274,9 +274,11 @@ class Backtest:
         # ---- phase A: static selection / constraints, window row lists ------------------
         bs.prepare_rebalancing(rebalancing_date=rebdates[0])
         cons = opt.constraints
-        if cons.l1:
-            return False                      # l1 linearisations: serial path
         universe = bs.selection.selected
+        from .l1split import merge_batch, split_batch, term_from_model
+        l1term = term_from_model(cons, opt.params, universe)   # src/optimization.py:125-142
+        if l1term == "unsupported":
+            return False                      # leverage: linearised rows, serial path
         X = bs.data.get("return_series")
         if X is None:
             raise ValueError("Return series data is missing.")
@@ -322,6 +324,12 @@ class Backtest:
         ST = np.zeros(hi - lo, dtype=np.int32)
         OBJ = np.zeros(hi - lo)
         mg = sum(0 if GhAb[k] is None else np.atleast_2d(GhAb[k]).shape[0] for k in ("A", "G"))
+        split_panel = None
+        if l1term is not None:
+            if lb is None or ub is None:
+                return False                  # the split needs a box (serial path raises)
+            split_panel = engine.Panel(torch.cat([panel.R, -panel.R], 1).contiguous(), None, device=dev)
+            mg += 1 if l1term.kind == "budget" else 0
         for s in range(lo, hi, chunk):
             e = min(hi, s + chunk)
             stage = BatchStage(panel, rows[s:e], tlen[s:e], dev)
@@ -342,13 +350,23 @@ class Backtest:
             qq = torch.zeros((e - s, qb.ld), dtype=torch.float64, device=dev)
             qq[:, :n] = q[:, :n]
             qb.q = qq
-            if stage.lowrank is not None:
-                res = engine.solve_lowrank(qb, stage.lowrank, settings, groups=stage.group_plan())
+            if l1term is not None:   # one turnover term: the signed split (porqua_amd/l1split.py)
+                qb2, lr2, const = split_batch(qb, stage.lowrank, l1term, split_panel, GhAb["A"], GhAb["b"],
+                                              GhAb["G"], GhAb["h"], lb, ub)
+                if lr2 is not None:
+                    res = engine.solve_lowrank(qb2, lr2, settings, groups=stage.group_plan())
+                else:
+                    res = engine.solve(qb2, settings)
+                W[s - lo:e - lo] = merge_batch(res.x, l1term).cpu().numpy()
+                OBJ[s - lo:e - lo] = (res.obj + const).cpu().numpy()
             else:
-                res = engine.solve(qb, settings)
-            W[s - lo:e - lo] = res.x.cpu().numpy()
+                if stage.lowrank is not None:
+                    res = engine.solve_lowrank(qb, stage.lowrank, settings, groups=stage.group_plan())
+                else:
+                    res = engine.solve(qb, settings)
+                W[s - lo:e - lo] = res.x[:, :n].cpu().numpy()
+                OBJ[s - lo:e - lo] = res.obj.cpu().numpy()
             ST[s - lo:e - lo] = res.status.cpu().numpy()
-            OBJ[s - lo:e - lo] = res.obj.cpu().numpy()
         if dist is not None:
             W, ST, OBJ = gather_shards(W, ST, OBJ, len(rebdates), world, dist, dev)
         # ---- phase C: portfolios -----------------------------------------------------------

@@ -84,3 +84,103 @@ def merge_solution(w: np.ndarray, term: L1Split) -> tuple[np.ndarray, np.ndarray
     n = term.x0.size
     x = term.x0 + w[:n] - w[n:2 * n]
     return x, np.abs(x - term.x0)
+
+
+def term_from_model(constraints, params, universe):
+    """The l1 term model_qpsolvers would linearise (src/optimization.py:125-142): None,
+    an L1Split, or "unsupported" (leverage, which the split does not cover)."""
+    if constraints.l1.get("leverage") is not None:
+        return "unsupported"
+    tocon = constraints.l1.get("turnover")
+    x0 = tocon["x0"] if tocon is not None and tocon.get("x0") is not None else params.get("x0")
+    if x0 is None:
+        return None
+    x_init = np.array([x0.get(a, 0) for a in universe], dtype=np.float64)
+    tc = params.get("transaction_cost")
+    if tc is not None:
+        return L1Split("cost", x_init, tc)
+    if tocon:
+        return L1Split("budget", x_init, tocon["rhs"])
+    return None
+
+
+def split_batch(qb, lowrank, term: L1Split, split_panel, A, b, G, h, lb, ub):
+    """Device form of split_problem for a batch of dates sharing the constraints (the
+    batched backtest).  ``qb`` holds the original problems (dense P in qb.P when
+    ``lowrank`` is None, else P_eff = p_scale w_scale Xc'Xc + p_diag I in window form);
+    ``split_panel`` is the panel [R, -R].  Returns (qb2, lowrank2 or None, const[B]) with
+    the original objective = split objective + const.
+
+    Window form: [P -P; -P P] = p_scale w_scale [Xc, -Xc]'[Xc, -Xc] + p_diag [I -I; -I I];
+    the p_diag block is replaced by p_diag I_2n, which only adds p_diag (u'u + v'v -
+    (u - v)'(u - v)) = 2 p_diag u'v >= 0 -- zero at every complementary point, and every
+    optimum is complementary (lowering u_i and v_i together keeps x and every constraint
+    and lowers the objective), so the optimum is unchanged."""
+    import torch
+    from . import engine
+    F64 = torch.float64
+    B, n, dev = qb.batch, qb.n, qb.device
+    x0 = torch.as_tensor(term.x0, dtype=F64, device=dev)
+    ps = qb.p_scale if qb.p_scale is not None else torch.ones(B, dtype=F64, device=dev)
+    pd = qb.p_diag if qb.p_diag is not None else torch.zeros(B, dtype=F64, device=dev)
+    q = qb.q[:, :n]
+    if lowrank is not None:
+        R = lowrank.panel.R
+        rows = lowrank.rows.to(torch.int64)
+        T = rows.shape[1]
+        mask = torch.arange(T, device=dev)[None, :] < lowrank.tlen.to(torch.int64)[:, None]
+        u = torch.where(mask, (R @ x0)[rows.clamp(min=0)], torch.zeros((), dtype=F64, device=dev))
+        if lowrank.mu is not None:
+            u = torch.where(mask, u - (lowrank.mu[:, :n] @ x0)[:, None], torch.zeros((), dtype=F64, device=dev))
+        xtu = torch.empty((B, n), dtype=F64, device=dev)
+        ch = max(1, int(2e8 // (8 * R.shape[0])))        # S chunk <= 200 MB
+        for s in range(0, B, ch):
+            e = min(B, s + ch)
+            S = torch.zeros((e - s, R.shape[0]), dtype=F64, device=dev)
+            S.scatter_add_(1, rows[s:e].clamp(min=0), u[s:e])
+            xtu[s:e] = S @ R
+        if lowrank.mu is not None:
+            xtu -= lowrank.mu[:, :n] * u.sum(1)[:, None]
+        ws = lowrank.w_scale if lowrank.w_scale is not None else torch.ones(B, dtype=F64, device=dev)
+        px0 = (ps * ws)[:, None] * xtu + pd[:, None] * x0[None, :]
+        xpx = ps * ws * (u * u).sum(1) + pd * (x0 @ x0)
+    else:
+        P = ps[:, None, None] * qb.P[:, :n, :n] + pd[:, None, None] * torch.eye(n, dtype=F64, device=dev)
+        px0 = P @ x0
+        xpx = px0 @ x0
+    g0 = px0 + q
+    const = 0.5 * xpx + q @ x0
+    base = dict(P=np.zeros((n, n)), q=np.zeros(n), A=A, b=b, G=G, h=h, lb=lb, ub=ub)
+    sp = split_problem(base, term)
+    qb2 = engine.QPBatch.from_dense(np.zeros((1, 2 * n, 2 * n)), np.zeros((1, 2 * n)), A=sp["A"], b=sp["b"],
+                                    G=sp["G"], h=sp["h"], lb=sp["lb"], ub=sp["ub"], device=dev)
+    qb2.batch = B
+    c = term.value if term.kind == "cost" else 0.0
+    q2 = torch.zeros((B, qb2.ld), dtype=F64, device=dev)
+    q2[:, :n] = g0 + c
+    q2[:, n:2 * n] = -g0 + c
+    qb2.q = q2
+    lr2 = None
+    if lowrank is not None:
+        qb2.P = None
+        qb2.p_scale = ps
+        qb2.p_diag = pd
+        mu2 = None if lowrank.mu is None else torch.cat([lowrank.mu[:, :n], -lowrank.mu[:, :n]], 1).contiguous()
+        lr2 = engine.LowRank(split_panel, lowrank.rows, lowrank.tlen, mu=mu2, w_scale=lowrank.w_scale)
+    else:
+        P2 = torch.zeros((B, qb2.ld, qb2.ld), dtype=F64, device=dev)
+        P2[:, :n, :n] = P
+        P2[:, :n, n:2 * n] = -P
+        P2[:, n:2 * n, :n] = -P
+        P2[:, n:2 * n, n:2 * n] = P
+        qb2.P = P2
+        qb2.p_scale = qb2.p_diag = None
+    return qb2, lr2, const
+
+
+def merge_batch(x2, term: L1Split):
+    """x = x0 + u - v for every date (x2: B x >= 2n device tensor)."""
+    import torch
+    n = term.x0.size
+    x0 = torch.as_tensor(term.x0, dtype=x2.dtype, device=x2.device)
+    return x0[None, :] + x2[:, :n] - x2[:, n:2 * n]

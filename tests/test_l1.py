@@ -91,3 +91,118 @@ def test_device_l1_matches_golden(tag):
         viol = max(abs(x.sum() - 1.0), float(np.maximum(-x, 0).max()),
                    (np.abs(x - term.x0).sum() - term.value) if term.kind == "budget" else 0.0)
         assert viol <= 1e-7
+
+
+def _msci():
+    import pandas as pd
+    p = np.load(os.path.join(GOLD, "msci_panel.npz"))
+    idx = pd.DatetimeIndex(p["dates"].astype("datetime64[D]"))
+    cols = [str(c) for c in p["columns"]]
+    return pd.DataFrame(p["returns"], index=idx, columns=cols), pd.DataFrame({"bm": p["bm"]}, index=idx)
+
+
+def _service(opt, X, y, rebdates, extra=None, width=252, box_kw=None):
+    from porqua_amd.backtest import BacktestService
+    from porqua_amd.builders import (OptimizationItemBuilder, SelectionItemBuilder, bibfn_bm_series,
+                                     bibfn_box_constraints, bibfn_budget_constraint, bibfn_return_series,
+                                     bibfn_selection_data)
+    blds = {"return_series": OptimizationItemBuilder(bibfn=bibfn_return_series, width=width),
+            "bm_series": OptimizationItemBuilder(bibfn=bibfn_bm_series, width=width),
+            "budget_constraint": OptimizationItemBuilder(bibfn=bibfn_budget_constraint, budget=1),
+            "box_constraints": OptimizationItemBuilder(bibfn=bibfn_box_constraints, **(box_kw or {}))}
+    if extra is not None:
+        blds["l1"] = extra
+    return BacktestService(data={"return_series": X, "bm_series": y},
+                           selection_item_builders={"data": SelectionItemBuilder(bibfn=bibfn_selection_data)},
+                           optimization_item_builders=blds, optimization=opt, rebdates=rebdates, quiet=True)
+
+
+@pytest.mark.gpu
+def test_device_backtest_transaction_cost_matches_reference():
+    """The reference's own msci backtest with transaction_cost around params['x0']
+    (tools/capture_l1.py), batched on the device through the split."""
+    from porqua_amd.backtest import Backtest
+    from porqua_amd.covariance import Covariance
+    from porqua_amd.optimization import MeanVariance
+    g = np.load(os.path.join(GOLD, "msci_l1_tc.npz"))
+    X, y = _msci()
+    n = X.shape[1]
+    x0 = dict(zip(X.columns, g["x0"]))
+    opt = MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1),
+                       solver_name="mi355x", transaction_cost=0.002, x0=x0)
+    bt = Backtest()
+    bt.run(_service(opt, X, y, [str(d) for d in g["rebdates"]]))
+    assert bt.stats["solved"] == len(g["rebdates"])         # batched path, all solved
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    assert np.abs(W - g["x"][:, :n]).max() < 1e-5
+    obj = bt.stats["objective"]
+    assert np.max(np.abs(obj - g["obj"]) / np.maximum(np.abs(g["obj"]), 1e-12)) < 1e-6
+
+
+@pytest.mark.gpu
+def test_device_backtest_turnover_budget_matches_reference():
+    """A custom l1 builder (serial loop, one split QP per date) against the reference."""
+    from porqua_amd.backtest import Backtest
+    from porqua_amd.builders import OptimizationItemBuilder
+    from porqua_amd.optimization import LeastSquares
+    g = np.load(os.path.join(GOLD, "msci_l1_to.npz"))
+    X, y = _msci()
+    n = X.shape[1]
+    x0 = dict(zip(X.columns, g["x0"]))
+
+    def add_turnover(bs, rebdate, **kw):
+        bs.optimization.constraints.add_l1("turnover", rhs=kw["rhs"], x0=kw["x0"])
+
+    opt = LeastSquares(l2_penalty=1e-3, solver_name="mi355x")
+    bt = Backtest()
+    bt.run(_service(opt, X, y, [str(d) for d in g["rebdates"]],
+                    extra=OptimizationItemBuilder(bibfn=add_turnover, rhs=0.3, x0=x0)))
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    assert np.abs(W - g["x"][:, :n]).max() < 1e-5
+    assert np.all(np.abs(W - g["x0"][None, :]).sum(1) <= 0.3 + 1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shrink", [True, False])
+def test_device_backtest_window_path_transaction_cost(shrink):
+    """n > window: the split runs on the Woodbury (window) path with the panel [R, -R];
+    checked against the oracle IPM on the split problem per date."""
+    import pandas as pd
+    from porqua_amd.backtest import Backtest
+    from porqua_amd.covariance import Covariance
+    from porqua_amd.optimization import MeanVariance
+    from porqua_amd.synthetic import factor_panel
+    from oracle import ref_pipeline as rp
+    n, D, width = 200, 120, 60
+    dates, R, yv, _ = factor_panel(D, n, seed=3)
+    idx = pd.DatetimeIndex(dates)
+    X = pd.DataFrame(R, index=idx, columns=[f"a{i}" for i in range(n)])
+    y = pd.DataFrame({"bm": yv}, index=idx)
+    rebdates = [str(d.date()) for d in X.index[width + 2:width + 2 + 16]]
+    w0 = np.random.default_rng(9).dirichlet(np.ones(n))
+    cov = Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1) if shrink else Covariance()
+    opt = MeanVariance(covariance=cov, solver_name="mi355x", transaction_cost=0.001,
+                       x0=dict(zip(X.columns, w0)))
+    bt = Backtest()
+    bt.run(_service(opt, X, y, rebdates, width=width, box_kw={"upper": 0.1}))
+    assert bt.stats["solved"] == len(rebdates) and bt.stats["path"] == "lowrank"
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    for i in (0, 7, len(rebdates) - 1):
+        e = X.index.get_loc(pd.Timestamp(rebdates[i]))
+        Xw = R[e - width + 1:e + 1]
+        S = rp.cov_pearson(Xw)
+        if shrink:
+            S = S + 0.1 * np.mean(np.diag(S)) * np.eye(n)
+        P, q = 2 * S, -rp.mean_geometric(Xw, None, None, None)
+        base = dict(P=P, q=q, A=np.ones((1, n)), b=np.ones(1), G=None, h=None, lb=np.zeros(n),
+                    ub=np.full(n, 0.1))
+        term = L1Split("cost", w0, 0.001)
+        sp = split_problem(base, term)
+        o = solve_qp(sp["P"], sp["q"], sp["G"], sp["h"], sp["A"], sp["b"], sp["lb"], sp["ub"])
+        xo, do = merge_solution(o.x, term)
+        f = lambda x: 0.5 * x @ P @ x + q @ x + 0.001 * np.abs(x - w0).sum()   # noqa: E731
+        assert abs(f(W[i]) - f(xo)) <= 1e-6 * max(abs(f(xo)), 1e-12), (i, f(W[i]), f(xo))
+        assert abs(bt.stats["objective"][i] - f(W[i])) <= 1e-6 * max(abs(f(xo)), 1e-12)
+        if shrink:
+            assert np.abs(W[i] - xo).max() < 1e-5
+        assert abs(W[i].sum() - 1) < 1e-7 and W[i].min() > -1e-7 and W[i].max() < 0.1 + 1e-7
