@@ -25,14 +25,19 @@ import numpy as np
 
 class L1Split:
     """One recorded l1 term: kind 'cost' (transaction_cost * sum|x - x0| in the objective)
-    or 'budget' (sum|x - x0| <= tau)."""
+    or 'budget' (sum|x - x0| <= tau).  The leverage constraint sum|x| <= L is the budget
+    form around x0 = 0.  ``layout`` is the reference's variable vector: 'd' = [x; d]
+    (turnover, src/qp_problems.py:40-77, 120-157), 'pm' = [x; x+; x-] (leverage, :79-118)."""
 
-    def __init__(self, kind: str, x0, value: float):
+    def __init__(self, kind: str, x0, value: float, layout: str = "d"):
         if kind not in ("cost", "budget"):
             raise ValueError("L1Split: kind must be 'cost' or 'budget'")
+        if layout not in ("d", "pm"):
+            raise ValueError("L1Split: layout must be 'd' or 'pm'")
         self.kind = kind
         self.x0 = np.asarray(x0, dtype=np.float64).reshape(-1)
         self.value = float(value)
+        self.layout = layout
 
 
 def split_problem(base: dict, term: L1Split) -> dict:
@@ -80,28 +85,34 @@ def split_problem(base: dict, term: L1Split) -> dict:
 
 
 def merge_solution(w: np.ndarray, term: L1Split) -> tuple[np.ndarray, np.ndarray]:
-    """(x, d) of the reference's variable vector [x; d] from the split solution w."""
+    """(x, aux) of the reference's variable vector from the split solution w: aux = d =
+    |x - x0| (layout 'd') or [x+; x-] (layout 'pm')."""
     n = term.x0.size
     x = term.x0 + w[:n] - w[n:2 * n]
+    if term.layout == "pm":
+        return x, np.concatenate([np.maximum(x, 0.0), np.maximum(-x, 0.0)])
     return x, np.abs(x - term.x0)
 
 
 def term_from_model(constraints, params, universe):
     """The l1 term model_qpsolvers would linearise (src/optimization.py:125-142): None,
     an L1Split, or "unsupported" (leverage, which the split does not cover)."""
-    if constraints.l1.get("leverage") is not None:
-        return "unsupported"
+    term = None
     tocon = constraints.l1.get("turnover")
     x0 = tocon["x0"] if tocon is not None and tocon.get("x0") is not None else params.get("x0")
-    if x0 is None:
-        return None
-    x_init = np.array([x0.get(a, 0) for a in universe], dtype=np.float64)
-    tc = params.get("transaction_cost")
-    if tc is not None:
-        return L1Split("cost", x_init, tc)
-    if tocon:
-        return L1Split("budget", x_init, tocon["rhs"])
-    return None
+    if x0 is not None:
+        x_init = np.array([x0.get(a, 0) for a in universe], dtype=np.float64)
+        tc = params.get("transaction_cost")
+        if tc is not None:
+            term = L1Split("cost", x_init, tc)
+        elif tocon:
+            term = L1Split("budget", x_init, tocon["rhs"])
+    levcon = constraints.l1.get("leverage")
+    if levcon is not None:
+        if term is not None:
+            return "unsupported"      # turnover and leverage together: linearised rows
+        term = L1Split("budget", np.zeros(len(universe)), levcon["rhs"], layout="pm")
+    return term
 
 
 def split_batch(qb, lowrank, term: L1Split, split_panel, A, b, G, h, lb, ub):

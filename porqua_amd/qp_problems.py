@@ -39,13 +39,13 @@ class QuadraticProgram(dict):
         self.solver = self["params"]["solver_name"]
         self._l1 = None         # recorded l1 term (l1split.L1Split) + the problem before it
 
-    def _record_l1(self, kind, x0, value):
+    def _record_l1(self, kind, x0, value, layout="d"):
         """Keep the problem as it was before the (first) l1 linearisation: the engine solves
         the signed split of it (porqua_amd/l1split.py) instead of the 2n linearised rows."""
         from .l1split import L1Split
         if self._l1 is None:
             base = {k: self.get(k) for k in ("P", "q", "G", "h", "A", "b", "lb", "ub")}
-            self._l1 = (L1Split(kind, x0, value), base)
+            self._l1 = (L1Split(kind, x0, value, layout), base)
         else:
             self._l1 = "unsupported"   # several l1 terms: solved in the linearised form
 
@@ -74,7 +74,10 @@ class QuadraticProgram(dict):
         """sum|x| <= leverage_budget via x = x+ - x-, x+, x- >= 0 (src/qp_problems.py:79-118)."""
         n = len(self["q"])
         N = n if N is None else int(N)
-        self._l1 = "unsupported"   # leverage: solved in the linearised form (DESIGN.md §7)
+        if N == n:
+            self._record_l1("budget", np.zeros(n), leverage_budget, layout="pm")
+        else:
+            self._l1 = "unsupported"
         P = self.get("P")
         if P is not None:
             P = np.pad(P, (0, 2 * N))
@@ -152,8 +155,8 @@ class QuadraticProgram(dict):
         sub["params"] = self["params"]
         sol = solve_batch([sub])[0]
         if sol.x is not None:
-            x, d = merge_solution(sol.x, term)
-            sol.x = np.concatenate([x, d])
+            x, aux = merge_solution(sol.x, term)
+            sol.x = np.concatenate([x, aux])
             if sol.found:
                 sol.obj = self.objective_value(sol.x, with_const=False)
         sol.z = None      # multipliers of the split rows, not of the 2n linearised rows

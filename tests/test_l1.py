@@ -19,15 +19,19 @@ from porqua_amd.l1split import L1Split, merge_solution, split_problem
 from porqua_amd.qp_problems import QuadraticProgram
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-KINDS = {"tc": "cost", "to": "budget"}
+KINDS = {"tc": "cost", "to": "budget", "lev": "budget"}
+TAGS = ["tc", "to", "lev"]
 
 
 def _case(tag, i):
     g = np.load(os.path.join(GOLD, f"msci_l1_{tag}.npz"))
-    n = g["P"].shape[-1] // 2
-    base = dict(P=g["P"][i][:n, :n], q=g["q"][i][:n], A=g["A"][i][:, :n], b=np.atleast_1d(g["b"][i]),
+    n = g["P"].shape[-1] // (3 if tag == "lev" else 2)
+    b0 = np.atleast_1d(g["b"][i])[:1]
+    base = dict(P=g["P"][i][:n, :n], q=g["q"][i][:n], A=g["A"][i][:1, :n], b=b0,
                 lb=g["lb"][i][:n], ub=g["ub"][i][:n], G=None, h=None)
     value = 0.002 if tag == "tc" else float(g["h"][i][-1])
+    if tag == "lev":
+        return g, n, base, L1Split("budget", np.zeros(n), value, layout="pm")
     return g, n, base, L1Split(KINDS[tag], g["x0"], value)
 
 
@@ -35,14 +39,16 @@ def _qp(base, term, solver):
     qp = QuadraticProgram(P=base["P"].copy(), q=base["q"].copy(), A=base["A"].copy(), b=base["b"].copy(),
                           lb=base["lb"].copy(), ub=base["ub"].copy(), G=None, h=None,
                           params={"solver_name": solver})
-    if term.kind == "cost":
+    if term.layout == "pm":
+        qp.linearize_leverage_constraint(N=term.x0.size, leverage_budget=term.value)
+    elif term.kind == "cost":
         qp.linearize_turnover_objective(term.x0, transaction_cost=term.value)
     else:
         qp.linearize_turnover_constraint(term.x0, to_budget=term.value)
     return qp
 
 
-@pytest.mark.parametrize("tag", ["tc", "to"])
+@pytest.mark.parametrize("tag", TAGS)
 def test_linearisation_matches_reference(tag):
     for i in (0, 7, 23):
         g, n, base, term = _case(tag, i)
@@ -51,11 +57,14 @@ def test_linearisation_matches_reference(tag):
         # which adds ~1e-19 to the zero auxiliary block
         assert np.allclose(qp["P"], g["P"][i], rtol=0, atol=1e-15 * np.abs(g["P"][i]).max())
         for k in ("q", "G", "h", "lb", "ub"):
-            assert np.array_equal(np.asarray(qp[k], dtype=float), g[k][i]), k
+            assert np.array_equal(np.asarray(qp[k], dtype=float).reshape(g[k][i].shape), g[k][i]), k
         assert np.array_equal(qp["A"].reshape(g["A"][i].shape), g["A"][i])
+        # leverage: the reference leaves b 0-d (a defect, see tools/capture_l1.py); the
+        # fixture and this package hold the intended [b; 0]
+        assert np.array_equal(np.asarray(qp["b"], dtype=float).reshape(-1), np.atleast_1d(g["b"][i]))
 
 
-@pytest.mark.parametrize("tag", ["tc", "to"])
+@pytest.mark.parametrize("tag", TAGS)
 def test_split_solved_by_oracle_matches_golden(tag):
     for i in range(0, 24, 3):
         g, n, base, term = _case(tag, i)
@@ -76,7 +85,7 @@ def test_split_rejects_x0_outside_box():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", ["tc", "to"])
+@pytest.mark.parametrize("tag", TAGS)
 def test_device_l1_matches_golden(tag):
     for i in range(24):
         g, n, base, term = _case(tag, i)
@@ -88,7 +97,8 @@ def test_device_l1_matches_golden(tag):
         assert np.abs(x - g["x"][i][:n]).max() < 1e-5, (i, np.abs(x - g["x"][i][:n]).max())
         obj_ref = float(g["obj"][i])
         assert abs(s.obj - obj_ref) <= 1e-6 * max(1.0, abs(obj_ref))
-        viol = max(abs(x.sum() - 1.0), float(np.maximum(-x, 0).max()),
+        viol = max(abs(x.sum() - 1.0), float(np.maximum(base["lb"] - x, 0).max()),
+                   float(np.maximum(x - base["ub"], 0).max()),
                    (np.abs(x - term.x0).sum() - term.value) if term.kind == "budget" else 0.0)
         assert viol <= 1e-7
 

@@ -11,7 +11,9 @@ that adds an l1 term, so the captured problems are exactly what
 
 * ``msci_l1_tc``: MeanVariance (linear shrinkage 0.1) with ``transaction_cost = 0.002``
   around ``params['x0']`` = a fixed non-uniform portfolio;
-* ``msci_l1_to``: LeastSquares (l2_penalty 1e-3) with ``add_l1('turnover', rhs=0.3, x0)``.
+* ``msci_l1_to``: LeastSquares (l2_penalty 1e-3) with ``add_l1('turnover', rhs=0.3, x0)``;
+* ``msci_l1_lev``: MeanVariance (risk aversion 5) on a long/short box [-0.1, 0.3] with
+  ``add_l1('leverage', rhs=1.5)`` (``linearize_leverage_constraint``, src/qp_problems.py:79-118).
 
 Golden optima of the linearised problems come from ``oracle.qp_ipm`` (KKT-certified).
 Usage:  python tools/capture_l1.py
@@ -44,12 +46,20 @@ def main():
     def add_turnover(bs, rebdate, **kw):
         bs.optimization.constraints.add_l1("turnover", rhs=kw["rhs"], x0=kw["x0"])
 
+    def add_leverage(bs, rebdate, **kw):
+        bs.optimization.constraints.add_l1("leverage", rhs=kw["rhs"])
+
     cases = {
         "tc": (MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1),
                             solver_name="cvxopt", transaction_cost=0.002, x0=x0), None),
         "to": (LeastSquares(l2_penalty=1e-3, solver_name="cvxopt"),
                cg.OptimizationItemBuilder(bibfn=add_turnover, rhs=0.3, x0=x0)),
+        "lev": (MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1),
+                             solver_name="cvxopt", risk_aversion=5.0),
+                cg.OptimizationItemBuilder(bibfn=add_leverage, rhs=1.5)),
     }
+    box = {"tc": {"box_type": "LongOnly"}, "to": {"box_type": "LongOnly"},
+           "lev": {"box_type": "LongShort", "lower": -0.1, "upper": 0.3}}
     orig_run = cg.run_backtest
     for tag, (opt, extra) in cases.items():
         if extra is not None:
@@ -70,9 +80,15 @@ def main():
                                         optimization=optimization, rebdates=reb, quiet=True)
                 cg.Backtest().run(bs)
                 return list(cg.CAPTURED), None, None
-            probs, _, _ = run_backtest(opt, X, y, rebdates, width, {"box_type": "LongOnly"})
+            probs, _, _ = run_backtest(opt, X, y, rebdates, width, box[tag])
         else:
-            probs, _, _ = orig_run(opt, X, y, rebdates, width, {"box_type": "LongOnly"})
+            probs, _, _ = orig_run(opt, X, y, rebdates, width, box[tag])
+        if tag == "lev":
+            # reference defect: linearize_leverage_constraint pads a 0-d b (np.pad returns it
+            # unchanged), so A has 1 + N rows and b one entry and qpsolvers rejects the
+            # problem; the intended right-hand side [b; 0] is used for the golden optimum
+            for p in probs:
+                p.b = np.concatenate([np.atleast_1d(p.b), np.zeros(p.A.shape[0] - np.atleast_1d(p.b).size)])
         xs, objs, kp, kd = cg.golden_solutions(probs)
         rec = {k: cg.stack(probs, k) for k in ("P", "q", "G", "h", "A", "b", "lb", "ub")}
         rec = {k: v for k, v in rec.items() if v is not None}
