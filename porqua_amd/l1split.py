@@ -77,8 +77,11 @@ def split_problem(base: dict, term: L1Split) -> dict:
         rows.append(np.hstack([G, -G]))
         rhs.append(np.asarray(h, dtype=np.float64).reshape(-1) - G @ x0)
     if term.kind == "budget" and np.isfinite(term.value):
-        rows.append(np.ones((1, 2 * n)))
-        rhs.append(np.array([term.value]))
+        # 1'u + 1'v <= tau, scaled to a unit-norm row (the same constraint; ADMM's rho for a
+        # row of 2n ones would be off by sqrt(2n) against the unit box rows)
+        r = 1.0 / np.sqrt(2 * n)
+        rows.append(np.full((1, 2 * n), r))
+        rhs.append(np.array([term.value * r]))
     out["G"] = np.vstack(rows) if rows else None
     out["h"] = np.concatenate(rhs) if rows else None
     return out
