@@ -71,6 +71,12 @@ class Settings:
     polish: int = 1
     polish_rounds: int = 8
     refine_iters: int = 1      # proximal refinement steps per polish round (then KKT-checked)
+    # problems whose polish is rejected are polished again with this many refinement steps
+    # (nearly singular P_FF, e.g. small risk aversions) before the ADMM retry (host-side)
+    refine_retry: int = 4
+    # window path: initial rho >= rho0_qrel * max|q| (host-side, not in pq_settings): for
+    # nearly linear objectives (small risk aversion) 4 mean(diag P) is far too small a rho
+    rho0_qrel: float = 10.0
 
     def to_c(self) -> _lib.PQSettings:
         names = {f[0] for f in _lib.PQSettings._fields_}
@@ -329,6 +335,7 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
     strm = _stream()
     P_, S_, SS = ctypes.byref(pb), ctypes.byref(st), ctypes.byref(s)
     _lib.check(lib.pq_init_state(P_, S_, None, 0, SS, strm), "pq_init_state")
+    _rho_floor_q(qb, ws, settings or Settings())
     _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, None, 0, SS, 1, strm)),
                "pq_factor_batched")
     cnt = {"refactors": 0, "launches": 0}
@@ -352,6 +359,11 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
     if s.polish:
         _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, None, 0, SS, strm)),
                    "pq_polish_batched")
+        rp = _repolish_set(ws, settings or Settings())
+        if rp is not None:      # polish rejected: polish again with more refinement steps
+            pidx, pn, s3 = rp
+            _lib.check(tl("polish", lambda: lib.pq_polish_batched(P_, S_, _ptr(pidx), pn, ctypes.byref(s3), strm)),
+                       "pq_polish_batched (refine)")
         retry = _retry_set(ws, settings or Settings())
         if retry is not None:   # polish rejected: resume ADMM to eps_retry, polish again
             idx, nidx, s2 = retry
@@ -366,6 +378,30 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
                        admm_launches=launches)
+
+
+def _rho_floor_q(qb: "QPBatch", ws: "Workspace", settings: Settings):
+    """Initial rho >= rho0_qrel * max|q| per problem (both paths, before the first factor)."""
+    if settings.rho0_qrel > 0:
+        qinf = qb.q[:, :qb.n].abs().amax(1)
+        torch.clamp(torch.maximum(ws.rho, settings.rho0_qrel * qinf), settings.rho_min, settings.rho_max,
+                    out=ws.rho)
+
+
+def _repolish_set(ws: "Workspace", settings: Settings):
+    """Problems whose polish was rejected: set them back to SOLVED (their ADMM point is
+    untouched by a rejected polish) and return (idx, n, settings with refine_iters =
+    refine_retry) for a second polish, or None (host sync: status)."""
+    if settings.refine_retry <= settings.refine_iters:
+        return None
+    bad = torch.nonzero(ws.status == _lib.PQ_SOLVED_INACCURATE).flatten().to(torch.int32)
+    m = int(bad.numel())
+    if m == 0:
+        return None
+    ws.status[bad.long()] = _lib.PQ_SOLVED
+    s3 = settings.to_c()
+    s3.refine_iters = settings.refine_retry
+    return bad.contiguous(), m, s3
 
 
 def _retry_set(ws: "Workspace", settings: Settings):
@@ -501,6 +537,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     P_, S_, SS, L_ = ctypes.byref(pb), ctypes.byref(st), ctypes.byref(s), ctypes.byref(lrs)
     PM_, SM_, SSM = ctypes.byref(pbM), ctypes.byref(stM), ctypes.byref(sM)
     _lib.check(lib.pq_init_state_lr(L_, P_, S_, None, 0, SS, strm), "pq_init_state_lr")
+    _rho_floor_q(qb, ws, settings or Settings())
 
     bd = None
 
@@ -549,7 +586,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             cnt["refactors"] += kk
         SS = SS0
 
-    def polish_w(idx, nidx):
+    def polish_w(idx, nidx, SSp=None):
+        SS = SSp if SSp is not None else SS_main
         kmax = min(qb.ld, 1024)
         final = ldk >= kmax
         _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, S_, _ptr(idx), nidx, SS, ldk, int(final),
@@ -569,13 +607,20 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                            "pq_polish_w_batched (relaunch)")
 
     admm_rounds(None, 0, SS)
+    SS_main = SS
     if s.polish and polish:
         polish_w(None, 0)
+        rp = _repolish_set(ws, settings or Settings())
+        if rp is not None:      # polish rejected: polish again with more refinement steps
+            pidx, pn, s3 = rp
+            polish_w(pidx, pn, ctypes.byref(s3))
         retry = _retry_set(ws, settings or Settings())
         if retry is not None:   # polish rejected: resume ADMM to eps_retry, polish again
             ridx, rn, s2 = retry
             admm_rounds(ridx, rn, ctypes.byref(s2))
-            polish_w(ridx, rn)
+            s4 = (settings or Settings()).to_c()
+            s4.refine_iters = max(s4.refine_iters, (settings or Settings()).refine_retry)
+            polish_w(ridx, rn, ctypes.byref(s4))
     refactors, launches = cnt["refactors"], cnt["launches"]
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],

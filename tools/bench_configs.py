@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Throughput of BASELINE.json configs 4 and 5 on one MI355X (the bench line is config 3).
+
+* config 4: synthetic 3000 assets x 10000 dates, 252-day windows, daily rebalance
+  (9749 QPs), tracking-error least squares (P = 2 X'X uncentred, q = -2 X'y) with budget,
+  long-only box and 20 sector caps <= 0.15 (G 20 x n) -- the window path with 21 general
+  rows.  --dates limits the number of rebalance dates (memory / time).
+* config 5: synthetic 5000 assets, 64 rebalance dates x 64 risk aversions log-spaced in
+  [0.1, 100] = 4096 mean-variance QPs (porqua_amd.sweep).
+
+Prints one JSON line per config: QPs/s over --steps timed solves after one warmup, status
+counts and ADMM iterations.  Experiment tooling; numbers are quoted in DESIGN.md §9."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from porqua_amd import engine  # noqa: E402
+from porqua_amd.sweep import mean_variance_sweep  # noqa: E402
+from porqua_amd.synthetic import factor_panel  # noqa: E402
+
+
+def timed(fn, steps):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = fn()
+    torch.cuda.synchronize()
+    return res, (time.perf_counter() - t0) / steps
+
+
+def summary(res):
+    st = res.status.cpu().numpy()
+    return {"status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+            "mean_iters": float(res.iters.float().mean().item()), "max_iters": int(res.iters.max().item())}
+
+
+def config4(dates_limit, steps, dev):
+    n, T, ns, cap = 3000, 252, 20, 0.15
+    dates, R, y, sec = factor_panel(10000, n, n_sectors=ns)
+    ends = np.arange(T - 1, 10000)[:dates_limit]
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    pan = engine.Panel(R, y, device=dev)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    B = len(ends)
+    G = np.stack([(sec == g).astype(float) for g in range(ns)])
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=G, h=np.full(ns, cap), lb=np.zeros(n), ub=np.ones(n), device=dev)
+    qb.batch, qb.P = B, None
+    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=dev)
+    lr = engine.LowRank(pan, r_d, t_d, mu=None)
+    gp = engine.GroupPlan(rows, tlen, dev)
+    ws = engine.Workspace(qb, dense=False)
+    settings = engine.Settings(rho0_rel=0.5)
+
+    def run():
+        xty, _ = pan.gram_xy(r_d, t_d)                 # q = -2 X'y per date, inside the step
+        qb.q = (-2.0 * xty).contiguous()
+        lr.refresh()
+        return engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp)
+
+    res, dt = timed(run, steps)
+    return dict({"config": "config4: n=3000 tracking LS, budget + box + 20 sector caps, daily",
+                 "qps": B / dt, "ms_per_step": dt * 1e3, "dates": B}, **summary(res))
+
+
+def config5(steps, dev, settings=None):
+    n, T, nd, L = 5000, 252, 64, 64
+    dates, R, _, _ = factor_panel(T - 1 + 21 * nd, n)
+    ends = np.arange(T - 1, T - 1 + 21 * nd, 21)
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    pan = engine.Panel(R, device=dev)
+    lambdas = np.logspace(-1, 2, L)
+    res, dt = timed(lambda: mean_variance_sweep(pan, rows, tlen, lambdas, settings=settings)[0], steps)
+    return dict({"config": "config5: n=5000 mean-variance, 64 monthly dates x 64 risk aversions",
+                 "qps": nd * L / dt, "ms_per_step": dt * 1e3, "qps_per_step": nd * L}, **summary(res))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--dates", type=int, default=9749, help="config 4 rebalance dates")
+    ap.add_argument("--only", choices=["4", "5"], default=None)
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="engine.Settings override for config 5 (experiments)")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if args.only in (None, "4"):
+        print(json.dumps(config4(args.dates, args.steps, dev)), flush=True)
+    if args.only in (None, "5"):
+        st = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set)) if args.set else None
+        print(json.dumps(dict(config5(args.steps, dev, st), settings_overrides=args.set)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
