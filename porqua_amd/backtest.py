@@ -275,7 +275,7 @@ class Backtest:
         bs.prepare_rebalancing(rebalancing_date=rebdates[0])
         cons = opt.constraints
         universe = bs.selection.selected
-        from .l1split import merge_batch, split_batch, term_from_model
+        from .l1split import merge_batch, split_batch, split_settings, term_from_model
         l1term = term_from_model(cons, opt.params, universe)   # src/optimization.py:125-142
         if l1term == "unsupported":
             return False                      # leverage: linearised rows, serial path
@@ -353,10 +353,11 @@ class Backtest:
             if l1term is not None:   # one turnover term: the signed split (porqua_amd/l1split.py)
                 qb2, lr2, const = split_batch(qb, stage.lowrank, l1term, split_panel, GhAb["A"], GhAb["b"],
                                               GhAb["G"], GhAb["h"], lb, ub)
+                s_split = split_settings(settings, opt.params)
                 if lr2 is not None:
-                    res = engine.solve_lowrank(qb2, lr2, settings, groups=stage.group_plan())
+                    res = engine.solve_lowrank(qb2, lr2, s_split, groups=stage.group_plan())
                 else:
-                    res = engine.solve(qb2, settings)
+                    res = engine.solve(qb2, s_split)
                 W[s - lo:e - lo] = merge_batch(res.x, l1term).cpu().numpy()
                 OBJ[s - lo:e - lo] = (res.obj + const).cpu().numpy()
             else:

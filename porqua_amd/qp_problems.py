@@ -153,7 +153,10 @@ class QuadraticProgram(dict):
         sp = split_problem(base, term)
         sub = {k: sp[k] for k in ("P", "q", "G", "h", "A", "b", "lb", "ub")}
         sub["params"] = self["params"]
-        sol = solve_batch([sub])[0]
+        from . import engine
+        from .l1split import split_settings
+        sol = solve_batch([sub], settings=split_settings(engine.Settings.from_params(self["params"]),
+                                                         self["params"]))[0]
         if sol.x is not None:
             x, aux = merge_solution(sol.x, term)
             sol.x = np.concatenate([x, aux])

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--budget", type=float, default=None)
     ap.add_argument("--cost", type=float, default=1e-5)
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
     args = ap.parse_args()
     n, T, D = 1000, 252, 4749
     dev = torch.device("cuda", 0)
@@ -43,7 +44,9 @@ def main():
     x0 = np.random.default_rng(1).dirichlet(np.ones(n))
     term = L1Split("budget", x0, args.budget) if args.budget else L1Split("cost", x0, args.cost)
     split_panel = engine.Panel(torch.cat([pan.R, -pan.R], 1).contiguous(), None, device=dev)
-    settings = engine.Settings()
+    from porqua_amd.l1split import split_settings
+    ov = dict(kv.split("=", 1) for kv in args.set)
+    settings = split_settings(engine.Settings.from_params(ov), ov)
 
     def step():
         qb2, lr2, const = split_batch(qb, lr, term, split_panel, np.ones((1, n)), np.ones(1), None, None,
@@ -66,7 +69,8 @@ def main():
                                                                                 zip(*np.unique(st, return_counts=True))},
                       "mean_iters": float(res.iters.float().mean().item()),
                       "max_budget_violation": float(np.abs(xh.sum(1) - 1).max()),
-                      "mean_turnover": float(np.abs(xh - x0[None, :]).sum(1).mean())}))
+                      "mean_turnover": float(np.abs(xh - x0[None, :]).sum(1).mean()),
+                      "settings_overrides": args.set}))
 
 
 if __name__ == "__main__":
