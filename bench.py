@@ -230,6 +230,7 @@ def main():
     factor_flops = factor_flops_per * n_factor
 
     traffic, traffic_src = None, None
+    mfma_busy, mfma_src = None, None
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
         try:
@@ -237,6 +238,10 @@ def main():
             k = pm["kernels"][kern]
             if int(round(k["algorithmic_bytes_per_admm_iteration"])) == int(it_bytes):
                 traffic, traffic_src = k["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
+                if "mfma_busy_fraction" in pm:
+                    mfma_busy = {kk: pm["mfma_busy_fraction"][kk] for kk in
+                                 ("k_band_gram", "k_factor", "k_admm_grp", "k_polish_w") if kk in pm["mfma_busy_fraction"]}
+                    mfma_src = os.path.relpath(f, ROOT)
         except Exception:
             pass
 
@@ -287,6 +292,9 @@ def main():
             "gram_tflops": gram_flops / tk["gram"] / 1e12 if band and tk.get("gram") else None,
             "capacitance": res.capacitance or None,
             "fp64_peak_tflops": FP64_PEAK_TFLOPS,
+            "mfma_busy_fraction_pmc": mfma_busy,
+            "mfma_busy_source": (mfma_src + " (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))")
+            if mfma_src else None,
         },
         "solver": {"status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
                    "mean_iters": float(iters.float().mean().item()),

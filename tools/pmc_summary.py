@@ -59,6 +59,16 @@ def main():
         adm["hbm_bytes_per_admm_iteration"] = adm["hbm_bytes_per_step"] / iters
         adm["algorithmic_bytes_per_admm_iteration"] = float(bench_pmc["roofline"]["algorithmic_bytes_per_iteration"])
     out["admm_kernel"] = kern
+    # optional MFMA pass (SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-busy cycles summed over every
+    # SIMD; GRBM_GUI_ACTIVE counts the dispatch's cycles summed over the 8 XCDs): busy
+    # fraction = MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 * 256 CUs * 4 SIMDs) -- the fraction of the
+    # chip's FP64-matrix issue capacity the kernel kept busy (1.0 = 78.6 TF/s of FP64 MFMA)
+    mf = os.path.join(src, "pmc_mfma", "run_counter_collection.csv")
+    if os.path.exists(mf):
+        busy, _ = per_kernel(mf, "SQ_VALU_MFMA_BUSY_CYCLES")
+        act, _ = per_kernel(mf, "GRBM_GUI_ACTIVE")
+        out["mfma_busy_fraction"] = {k: busy[k] / (act[k] / 8.0 * 256 * 4) for k in busy if act.get(k)}
+        out["mfma_source"] = "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE (own pass)"
     with open(os.path.join(dst, f"{rnd}_pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     full = os.path.join(src, "bench_full.log")
