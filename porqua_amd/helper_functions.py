@@ -1,12 +1,13 @@
 """PD test / repair and small helpers (mirror of src/helper_functions.py:29-83).
 
-``isPD`` is the batched device Cholesky (K2) info flag.  ``nearestPD`` repairs on the
-device by the reference's own fall-back step -- a diagonal shift grown until the Cholesky
-succeeds (src/helper_functions.py:50-56) -- starting from a shift of
-spacing(||A||_F) and multiplying it by 4 per attempt.  The reference first projects onto
-the PSD cone with an SVD (:41-45); for the symmetric covariance / Gram inputs on this path
-that projection only zeroes eigen-components at rounding level (measured: |lambda_min|
-~1e-18 at n = 1000), so the two repairs agree to ~1e-15 relative.
+``isPD`` is the batched device Cholesky (K2) info flag.  ``nearestPD`` is the reference's
+Higham / D'Errico repair (src/helper_functions.py:29-58) on the device for a whole batch:
+symmetrise, SVD polar projection onto the PSD cone, and -- while the K2 Cholesky still
+fails -- the shift A3 += I (-lambda_min k^2 + spacing(||A||_F)), k = 1, 2, ...  The SVD and
+the eigenvalues run on the GPU through rocSOLVER (torch.linalg; the repair is a library
+factorisation, not a hot-path kernel), the PD tests on K2.  ``nearestPD_shift`` is the
+cheaper repair used before (a spacing-scaled diagonal shift grown x4 until K2 succeeds);
+for the covariance / Gram inputs on this path both agree to ~1e-15 relative.
 """
 from __future__ import annotations
 
@@ -40,6 +41,33 @@ def isPD(B, device=None) -> bool:
 
 
 def nearestPD(A, device=None, max_attempts: int = 60):
+    """src/helper_functions.py:29-58 on the device, for one matrix or a batch."""
+    from . import engine
+    Ab, single = _as_batch(A)
+    dev = device or engine.default_device()
+    At = torch.from_numpy(np.ascontiguousarray(Ab)).to(dev)
+    B = 0.5 * (At + At.transpose(1, 2))
+    _, s, Vh = torch.linalg.svd(B)                                   # :42
+    H = Vh.transpose(1, 2) @ (s[:, :, None] * Vh)                      # :43  V' diag(s) V
+    A2 = 0.5 * (B + H)                                                 # :44
+    A3 = 0.5 * (A2 + A2.transpose(1, 2))                               # :45
+    n = Ab.shape[-1]
+    eye = torch.eye(n, dtype=torch.float64, device=dev)
+    spacing = torch.from_numpy(np.array([np.spacing(np.linalg.norm(Ab[i])) for i in range(len(Ab))])).to(dev)
+    todo = np.flatnonzero(pd_info(A3.cpu().numpy(), dev) != 0)         # :47 isPD
+    k = 1
+    while todo.size and k <= max_attempts:                             # :51-56
+        t = torch.from_numpy(todo).to(dev)
+        mineig = torch.linalg.eigvalsh(A3[t]).amin(1)                  # symmetric: eigvals are real
+        A3[t] += eye[None] * (-mineig * k ** 2 + spacing[t])[:, None, None]
+        k += 1
+        ok = pd_info(A3[t].cpu().numpy(), dev) == 0
+        todo = todo[~ok]
+    out = A3.cpu().numpy()
+    return out[0] if single else out
+
+
+def nearestPD_shift(A, device=None, max_attempts: int = 60):
     """Symmetrise, then add the smallest spacing-scaled diagonal shift (x4 per attempt)
     that lets the device Cholesky succeed.  Works on one matrix or a batch."""
     from . import engine
