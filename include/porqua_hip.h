@@ -266,6 +266,15 @@ int pq_simulate_periods(const double* panel, int64_t ldp, int32_t n, const doubl
                         double days_per_year, double* ret, double* wend, int64_t ldwe,
                         double* turnover, int32_t rescale, void* stream);
 
+/* Device bytes of the per-batch buffers a caller allocates before the solve entry points
+ * (the pq_state arrays, the polish scratch and, for the window path, the capacitance
+ * matrices M, M^-1 and their factor scratch), so a non-Python host can size one arena.
+ * path 0 = dense (K, Dt: ld x ld per problem), 1 = window (compact polish scratch ldk x ldk,
+ * ldk = min(ld, 1024, round_up(ldk, 64)); k_ld = round_up(tmax + mg, 64)).  ld =
+ * round_up(n, 64), mg_pad = round_up(max(mg, 1), 8).  Returns -1 on invalid arguments.
+ * Replaces nothing in the reference (qpsolvers allocates internally); SURVEY.md §8(b).   */
+int64_t pq_workspace_bytes(int32_t n, int32_t batch, int32_t mg, int32_t path, int32_t tmax, int32_t ldk);
+
 #ifdef __cplusplus
 }
 #endif

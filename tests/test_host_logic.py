@@ -151,11 +151,21 @@ def test_constraints_values_match_reference_golden():
 def test_library_loads_and_exports_every_header_symbol():
     lib = _lib.load()
     header = open(os.path.join(ROOT, "include", "porqua_hip.h")).read()
-    declared = set(re.findall(r"^(?:int|const char\*)\s+(pq_\w+)\(", header, flags=re.M))
+    declared = set(re.findall(r"^(?:int|int64_t|const char\*)\s+(pq_\w+)\(", header, flags=re.M))
     assert declared and declared == set(_lib.exported_symbols())
     for name in declared:
         assert hasattr(lib, name)
     assert lib.pq_version() == 100
+    # size query (host-only arithmetic, no GPU): dense and window layouts, bad arguments
+    n, B, mg = 1000, 7, 1
+    ld, mgp = 1024, 8
+    dense = B * (8 * (ld * ld + (ld // 64) * 4096) + 16 * ld + 16 * (mgp + ld) + 8 + 12 + 64
+                 + 8 * ((9 + mgp) * ld + 512))
+    assert lib.pq_workspace_bytes(n, B, mg, 0, 0, 0) == dense
+    win = lib.pq_workspace_bytes(n, B, mg, 1, 252, 256)
+    assert win == dense - B * 8 * (ld * ld - 256 * 256 + (ld // 64 - 4) * 4096) + \
+        B * (8 * (2 * 256 * 256 + 4 * 4096) + 12)
+    assert lib.pq_workspace_bytes(0, B, mg, 0, 0, 0) == -1
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     for name in declared:
         assert re.search(rf"\bT {name}\b", nm), name

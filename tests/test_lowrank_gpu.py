@@ -247,3 +247,22 @@ def test_polish_rejection_resumes_admm_to_tight_eps(device, path):
     assert np.all(st == 1), st
     assert one.iters.cpu().numpy().max() > ref.iters.cpu().numpy().max()   # the retry ran
     assert np.abs(one.x.cpu().numpy() - x0).max() < 1e-8
+
+
+@pytest.mark.gpu
+def test_workspace_bytes_matches_the_allocation(device):
+    """pq_workspace_bytes (the C-ABI size query) equals what engine.Workspace allocates."""
+    from porqua_amd import _lib
+    n, B, T = 1000, 5, 252
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   lb=np.zeros(n), ub=np.ones(n), device=device)
+    qb.batch = B
+    lib = _lib.load()
+    for dense in (True, False):
+        ws = engine.Workspace(qb, dense=dense)
+        ts = [ws.K, ws.Dt, ws.x, ws.Px, ws.z, ws.y, ws.rho, ws.iters, ws.status, ws.info, ws.out, ws.work]
+        if not dense:
+            lrb = ws.lr_buffers(engine.round_up(T + qb.mg, 64))
+            ts += [lrb[k] for k in ("M", "Minv", "Dt", "iters", "status", "info")]
+        got = sum(t.numel() * t.element_size() for t in ts)
+        assert lib.pq_workspace_bytes(n, B, qb.mg, 0 if dense else 1, T, ws.ldk) == got
