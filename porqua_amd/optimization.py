@@ -259,3 +259,50 @@ class WeightedLeastSquares(Optimization):
         sw = np.sqrt(self._weights(Xv.shape[0]))
         G, xty, yty = _device_gram(Xv * sw[:, None], yv * sw)
         self.objective = Objective(P=2 * G, q=-2 * xty, constant=yty)
+
+    def objective_batch(self, stage):
+        """Every date's WLS objective from one row-scaled panel.
+
+        The reference's weights (src/optimization.py:242-246) are exponential in the row's
+        age: the row r of the window ending at panel row e gets lam^(e - r) T / S_T, with
+        S_T = sum_{i<T} lam^i.  Writing lam^(e - r) = lam^(a - r) lam^(e - a) for one anchor
+        row a >= e of the whole chunk, the panel is scaled ONCE by sqrt(lam^(a - r)) and
+        each date keeps a scalar c_e = lam^(e - a) T / S_T: X'WX = c_e Xs'Xs, X'Wy = c_e Xs'ys.
+        K1 (Gram mode, sliding) or the window form then runs on the scaled panel unchanged,
+        with c_e folded into p_scale (dense) or w_scale (window path)."""
+        import torch
+        from . import engine
+        if stage.panel.bm is None:
+            return None
+        pan = stage.log1p_panel() if self.params.get("log_transform") else stage.panel
+        lam = float(np.exp(-np.log(2) / self.params["tau"]))
+        B, dev = stage.batch, stage.device
+        t = stage.tlen_host.astype(np.int64)
+        if np.any(t <= 0):
+            return None
+        # age counts window positions, not panel rows: rank every row the windows use
+        # (weekend rows the builders drop are skipped) and require each window to be a run
+        used = np.unique(np.concatenate([stage.rows_host[b, :t[b]] for b in range(B)]))
+        pos = np.full(pan.D, -1, dtype=np.int64)
+        pos[used] = np.arange(used.size)
+        first = pos[stage.rows_host[:, 0]]
+        last = pos[stage.rows_host[np.arange(B), t - 1]]
+        if np.any(last - first != t - 1):
+            return None
+        a = int(last.max())
+        if (a - int(first.min())) * -np.log2(lam) > 600:     # keep lam^(a - r) far from underflow
+            return None
+        age = np.where(pos >= 0, a - pos, 0)
+        sw = torch.from_numpy(np.sqrt(lam ** age.astype(np.float64))).to(dev)
+        span = engine.Panel(pan.R * sw[:, None], pan.bm * sw, device=dev)
+        s_T = (1.0 - lam ** t) / (1.0 - lam) if lam < 1.0 else t.astype(np.float64)
+        c = torch.from_numpy(lam ** (last - a).astype(np.float64) * t / s_T).to(dev)
+        if stage.prefer_lowrank:
+            G = None
+            stage.lowrank = engine.LowRank(span, stage.rows, stage.tlen, mu=None, w_scale=c)
+            scale = torch.full((B,), 2.0, dtype=torch.float64, device=dev)
+        else:
+            G = span.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer(), plan=stage.slide_plan())
+            scale = 2.0 * c
+        xty, yty = span.gram_xy(stage.rows, stage.tlen)
+        return G, scale, None, -2.0 * c[:, None] * xty, c * yty

@@ -14,7 +14,7 @@ from porqua_amd.constraints import Constraints
 from porqua_amd.covariance import Covariance
 from porqua_amd.helper_functions import isPD, nearestPD
 from porqua_amd.mean_estimation import MeanEstimator
-from porqua_amd.optimization import LeastSquares, MeanVariance, QEQW
+from porqua_amd.optimization import LeastSquares, MeanVariance, QEQW, WeightedLeastSquares
 from porqua_amd.optimization_data import OptimizationData
 from tests.conftest import load_golden
 
@@ -100,6 +100,9 @@ def _service(opt, X, y, rebdates, box_kw, width=252):
     ("msci_mv_shrink", lambda: MeanVariance(covariance=Covariance(method="linear_shrinkage",
                                                                   lambda_covmat_regularization=0.1),
                                             solver_name="mi355x", risk_aversion=3.0), {"upper": 0.25}),
+    ("msci_wls", lambda: WeightedLeastSquares(solver_name="mi355x", tau=252), {}),
+    ("msci_wls_log", lambda: WeightedLeastSquares(solver_name="mi355x", tau=21, log_transform=True),
+     {"upper": 0.3}),
 ])
 def test_backtest_batched_matches_golden(device, tag, make, box):
     X, y = msci()
@@ -111,7 +114,7 @@ def test_backtest_batched_matches_golden(device, tag, make, box):
     W = bt.strategy.get_weights_df().to_numpy(dtype=float)
     assert W.shape == g["x"].shape
     assert np.abs(W - g["x"]).max() < 1e-5
-    obj = np.array([0.5 * w @ P @ w + q @ w for w, P, q in zip(W, g["P"], g["q"])])
+    obj = np.array([0.5 * w @ P @ w + q.reshape(-1) @ w for w, P, q in zip(W, g["P"], g["q"])])
     assert np.max(np.abs(obj - g["obj"]) / np.maximum(np.abs(g["obj"]), 1e-12)) < 1e-6
 
 
@@ -148,7 +151,25 @@ def _synthetic(n, D, seed):
             pd.DataFrame({"bm": y}, index=idx))
 
 
-@pytest.mark.parametrize("kind", ["mv", "mv_shrink", "ls"])
+def test_wls_serial_equals_batched(device):
+    """WeightedLeastSquares: the per-date set_objective (weighted Gram on the device) and the
+    batched row-scaled panel (one scaled panel + a per-date scalar) give the same weights."""
+    X, y = msci()
+    g = load_golden("msci_wls_log")
+    rebdates = [str(d) for d in g["rebdates"][:10]]
+    W = []
+    for batched in (True, False):
+        bs = _service(WeightedLeastSquares(solver_name="mi355x", tau=21, log_transform=True), X, y,
+                      rebdates, {"upper": 0.3})
+        bs.settings["batched"] = batched
+        bt = Backtest()
+        bt.run(bs)
+        W.append(bt.strategy.get_weights_df().to_numpy(dtype=float))
+    assert np.abs(W[0] - W[1]).max() < 1e-7
+    assert np.abs(W[0] - g["x"][:10]).max() < 1e-5
+
+
+@pytest.mark.parametrize("kind", ["mv", "mv_shrink", "ls", "wls"])
 def test_backtest_lowrank_path_matches_oracle(device, kind):
     """Backtest.run with n > width: sliding K1 (lower triangle), Woodbury factor, grouped
     ADMM and window-form polish; weights checked against the oracle IPM per date."""
@@ -160,7 +181,8 @@ def test_backtest_lowrank_path_matches_oracle(device, kind):
             "mv_shrink": lambda: MeanVariance(covariance=Covariance(method="linear_shrinkage",
                                                                     lambda_covmat_regularization=0.1),
                                               solver_name="mi355x", risk_aversion=2.0),
-            "ls": lambda: LeastSquares(solver_name="mi355x")}[kind]
+            "ls": lambda: LeastSquares(solver_name="mi355x"),
+            "wls": lambda: WeightedLeastSquares(solver_name="mi355x", tau=30)}[kind]
     bt = Backtest()
     bt.run(_service(make(), X, y, rebdates, {"upper": 0.1}, width=width))
     assert bt.stats["solved"] == len(rebdates) and bt.stats["path"] == "lowrank"
@@ -171,6 +193,8 @@ def test_backtest_lowrank_path_matches_oracle(device, kind):
         Xw, yw = Xv[e - width + 1:e + 1], yv[e - width + 1:e + 1]
         if kind == "ls":
             P, q = 2 * Xw.T @ Xw, -2 * Xw.T @ yw
+        elif kind == "wls":
+            P, q, _ = rp.objective_wls(Xw, yw, 30)
         else:
             S = rp.cov_pearson(Xw)
             ra = 2.0 if kind == "mv_shrink" else 1.0
@@ -180,7 +204,7 @@ def test_backtest_lowrank_path_matches_oracle(device, kind):
         o = solve_qp(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.full(n, 0.1))
         obj = 0.5 * W[i] @ P @ W[i] + q @ W[i]
         assert abs(obj - o.obj) <= 1e-6 * max(abs(o.obj), 1e-12), (kind, i, obj, o.obj)
-        if kind != "ls":   # LS: rank(X'X) <= width < n, the optimum is a face (compare value)
+        if kind not in ("ls", "wls"):   # LS: rank(X'X) <= width < n, the optimum is a face (compare value)
             assert np.abs(W[i] - o.x).max() < 1e-5, (kind, i, np.abs(W[i] - o.x).max())
         assert abs(W[i].sum() - 1) < 1e-7 and W[i].min() > -1e-7 and W[i].max() < 0.1 + 1e-7
 

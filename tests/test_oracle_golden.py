@@ -53,6 +53,23 @@ def test_least_squares_objective_matches_reference(tag):
         assert abs(c - g["const"][i]) <= 1e-12 * abs(c)
 
 
+@pytest.mark.parametrize("tag", ["msci_wls", "msci_wls_log"])
+def test_weighted_least_squares_objective_matches_reference(tag):
+    """src/optimization.py:232-256 (tools/capture_wls.py): P, q, constant of every 7th date."""
+    dates, R, y = _panel()
+    g = load_golden(tag)
+    params = eval(str(g["params"]))
+    for i in range(0, len(g["rebdates"]), 7):
+        rows = rp.window_rows(dates, g["rebdates"][i], int(g["width"]))
+        assert len(rows) == g["win_len"][i]
+        P, q, c = rp.objective_wls(R[rows], y[rows], params["tau"], params.get("log_transform", False))
+        assert np.allclose(P, g["P"][i], rtol=1e-12, atol=1e-15)
+        # the reference's q is an (n, 1) column here (X' W y with y a DataFrame)
+        assert np.allclose(q, g["q"][i].reshape(-1), rtol=1e-12, atol=1e-15)
+        assert abs(c - g["const"][i]) <= 1e-12 * abs(c)
+    assert g["kkt_primal"].max() < 1e-9 and g["kkt_dual"].max() < 1e-9
+
+
 @pytest.mark.parametrize("tag", ["msci_mv", "msci_mv_shrink"])
 def test_mean_variance_objective_matches_reference(tag):
     dates, R, _ = _panel()
