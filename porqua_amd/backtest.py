@@ -377,9 +377,12 @@ class Backtest:
                       "path": "lowrank" if stage.lowrank is not None else "dense"}
         if not bs.settings.get("quiet"):
             print(f"Rebalanced {len(rebdates)} dates on the device ({int(solved.sum())} solved)")
+        keys = list(universe)
+        none = [None] * n
         for i, d in enumerate(rebdates):
-            w = W[i] if solved[i] else [None] * n
-            opt.results = {"weights": pd.Series(w, index=universe).to_dict(), "status": bool(solved[i])}
+            # == pd.Series(w, index=universe).to_dict() (Python floats), without 4749 Series
+            w = W[i].tolist() if solved[i] else none
+            opt.results = {"weights": dict(zip(keys, w)), "status": bool(solved[i])}
             self._after_solve(bs, d)
         return True
 

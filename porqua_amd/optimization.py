@@ -10,7 +10,8 @@ Deliberate differences from the reference ("Reference defects"):
   package) and lets ``verbose=False`` stick (src/optimization.py:45-46).
 * ``MeanVariance`` uses the mean estimator that is passed in; the reference stores the
   class instead of the instance (src/optimization.py:165).
-LAD and PercentilePortfolios (LP / ranking, not the QP path) are out of scope.
+LAD (an LP with T equality rows) and PercentilePortfolios (ranking, not
+the QP path) are not built.
 """
 from __future__ import annotations
 
