@@ -330,8 +330,20 @@ class Backtest:
                 return False                  # the split needs a box (serial path raises)
             split_panel = engine.Panel(torch.cat([panel.R, -panel.R], 1).contiguous(), None, device=dev)
             mg += 1 if l1term.kind == "budget" else 0
+        lad = hasattr(opt, "lad_batch")       # LAD: the LP on the device IPM (porqua_amd/lad.py)
+        if lad:
+            if l1term is not None:
+                return False
+            chunk = min(chunk, max(1, (1 << 34) // (8 * (n + 64) ** 2 + 64 * n * int(tlen.max()))))
+        path = "lp-ipm" if lad else "dense"
         for s in range(lo, hi, chunk):
             e = min(hi, s + chunk)
+            if lad:
+                r = opt.lad_batch(panel, rows[s:e], tlen[s:e], GhAb, lb, ub)
+                if r is None:
+                    return False
+                W[s - lo:e - lo], ST[s - lo:e - lo], OBJ[s - lo:e - lo] = r
+                continue
             stage = BatchStage(panel, rows[s:e], tlen[s:e], dev)
             # T + mg < n: the Woodbury (window-form) solver; its consumers read P's lower
             # triangle only (engine.lowrank_shape_ok: same test as solve_lowrank's)
@@ -341,6 +353,8 @@ class Backtest:
             if obj is None:
                 return False
             Pm, scale, pdiag, q, _const = obj
+            if stage.lowrank is not None:
+                path = "lowrank"
             qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=GhAb["A"], b=GhAb["b"],
                                            G=GhAb["G"], h=GhAb["h"], lb=lb, ub=ub, device=dev)
             qb.batch = e - s
@@ -374,7 +388,7 @@ class Backtest:
         from . import _lib
         solved = (ST == _lib.PQ_SOLVED) | (ST == _lib.PQ_SOLVED_INACCURATE)
         self.stats = {"dates": len(rebdates), "solved": int(solved.sum()), "status": ST, "objective": OBJ,
-                      "path": "lowrank" if stage.lowrank is not None else "dense"}
+                      "path": path}
         if not bs.settings.get("quiet"):
             print(f"Rebalanced {len(rebdates)} dates on the device ({int(solved.sum())} solved)")
         keys = list(universe)

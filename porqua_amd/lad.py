@@ -1,0 +1,252 @@
+"""LAD (least absolute deviation) tracking as a batched LP on the device.
+
+The reference's ``LAD.model_qpsolvers`` (src/optimization.py:296-345) hands qpsolvers a QP
+with P = 0: variables [w; u; v] (n + 2T), equality rows [budget; X I -I] = [b; y], box on w,
+u, v >= 0, objective 1'u + 1'v.  That LP has T + 1 general rows, beyond what the ADMM
+engine keeps in LDS, and ADMM converges slowly on LPs anyway, so it is solved here by a
+batched Mehrotra predictor-corrector interior-point method for
+
+    min c'x   s.t.  A x = b,  l <= x <= h   (infinite bounds allowed)
+
+Each iteration forms the normal matrix M = A diag(theta) A' (m x m, m = T + 1 + rows of G)
+for every date at once (one batched GEMM), factors and inverts it on K2
+(``pq_factor_batched``, the engine's FP64-MFMA blocked Cholesky, invert = 2) and reuses
+M^-1 for the predictor and the corrector (each with one refinement step against M).
+Inequality rows G x <= h become equality rows with slack columns s >= 0.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib, engine
+
+F64 = torch.float64
+_REFINE = 1
+
+
+class LPResult:
+    def __init__(self, x, lam, status, iters, obj):
+        self.x, self.lam, self.status, self.iters, self.obj = x, lam, status, iters, obj
+
+    @property
+    def found(self):
+        return self.status == _lib.PQ_SOLVED
+
+
+class LADProblem:
+    """The reference's LP (src/optimization.py:301-336) for a batch of windows, kept in
+    structured form: variables x = [w (n); u (T); v (T); s (mi)], rows
+    [C w + [0; s] = d  (C = [A; G], the budget / equality rows first);  X w + u - v = y].
+    The reference's dense A_tilde = [[A, 0, 0], [X, I, -I]] and G_tilde = [G, 0, 0] are the
+    same rows (G written with slacks).  X (B, T, n) and y (B, T) are device tensors."""
+
+    def __init__(self, X, y, A=None, b=None, G=None, h=None, lb=None, ub=None):
+        B, T, n = X.shape
+        dev = X.device
+        self.X, self.y, self.B, self.T, self.n, self.dev = X, y, B, T, n, dev
+        rows, rhs = [], []
+        self.me = 0 if A is None else np.atleast_2d(A).shape[0]
+        self.mi = 0 if G is None else np.atleast_2d(G).shape[0]
+        if self.me:
+            rows.append(np.atleast_2d(np.asarray(A, dtype=np.float64)))
+            rhs.append(np.asarray(b, dtype=np.float64).reshape(-1))
+        if self.mi:
+            rows.append(np.atleast_2d(np.asarray(G, dtype=np.float64)))
+            rhs.append(np.asarray(h, dtype=np.float64).reshape(-1))
+        self.mc = self.me + self.mi
+        self.C = torch.as_tensor(np.vstack(rows) if rows else np.zeros((0, n)), dtype=F64, device=dev)
+        d = torch.as_tensor(np.concatenate(rhs) if rhs else np.zeros(0), dtype=F64, device=dev)
+        self.b = torch.cat([d.expand(B, self.mc), y], 1)          # (B, mc + T)
+        N = n + 2 * T + self.mi
+        self.N, self.m = N, self.mc + T
+        self.c = torch.zeros(N, dtype=F64, device=dev)
+        self.c[n:n + 2 * T] = 1.0
+        self.lo = torch.zeros(N, dtype=F64, device=dev)
+        self.hi = torch.full((N,), np.inf, dtype=F64, device=dev)
+        self.lo[:n] = -np.inf if lb is None else torch.as_tensor(np.asarray(lb, dtype=np.float64), device=dev)
+        self.hi[:n] = np.inf if ub is None else torch.as_tensor(np.asarray(ub, dtype=np.float64), device=dev)
+
+    def split(self, x):
+        n, T = self.n, self.T
+        return x[:, :n], x[:, n:n + T], x[:, n + T:n + 2 * T], x[:, n + 2 * T:]
+
+    def A(self, x):
+        w, u, v, s = self.split(x)
+        rc = w @ self.C.T
+        if self.mi:
+            rc = rc + torch.cat([torch.zeros_like(rc[:, :self.me]), s], 1)
+        rt = torch.bmm(self.X, w.unsqueeze(2)).squeeze(2) + u - v
+        return torch.cat([rc, rt], 1)
+
+    def At(self, lam):
+        lc, lt = lam[:, :self.mc], lam[:, self.mc:]
+        gw = lc @ self.C + torch.bmm(lt.unsqueeze(1), self.X).squeeze(1)
+        return torch.cat([gw, lt, -lt, lc[:, self.me:]], 1)
+
+
+class _NormalFactor:
+    """H = diag(1/theta_w) + X' diag(1/(theta_u + theta_v)) X per window (n x n), factored
+    on K2 (pq_factor_batched: H = L L')."""
+
+    def __init__(self, B, m, dev):
+        self.m = m
+        self.qb = engine.QPBatch(m, B, 0, device=dev, has_box=False)
+        self.ws = engine.Workspace(self.qb)
+        self.s = engine.Settings(sigma=0.0).to_c()
+        self.pb = self.qb.c_struct()
+        self.st = self.ws.c_struct()
+        lib = _lib.load()
+        _lib.check(lib.pq_init_state(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
+                                     ctypes.byref(self.s), engine._stream()), "pq_init_state (LP)")
+
+    def factor(self, M):
+        m, lib = self.m, _lib.load()
+        self.qb.P[:, :m, :m] = M
+        _lib.check(lib.pq_factor_batched(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
+                                         ctypes.byref(self.s), 0, engine._stream()), "pq_factor_batched (LP)")
+        self.L = self.ws.K[:, :m, :m]
+        return self.ws.info
+
+    def solve_mat(self, R):
+        """H^-1 R (B x n x k) by the two triangular solves against the K2 factor."""
+        t = torch.linalg.solve_triangular(self.L, R, upper=False)
+        return torch.linalg.solve_triangular(self.L.transpose(1, 2), t, upper=True)
+
+
+def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace=None) -> LPResult:
+    """Mehrotra predictor-corrector IPM for min c'x, A x = b, lo <= x <= hi on the LAD
+    structure, batched over windows; converged problems are frozen.
+
+    Newton directions come from the w-space normal equations (the Koenker / Portnoy form of
+    LAD interior-point methods): u, v, s and the T window rows are eliminated exactly, which
+    leaves H dw - C' dlam_C = f (n x n, K2 Cholesky) bordered by the few rows of C."""
+    B, m, N, n, T = pr.B, pr.m, pr.N, pr.n, pr.T
+    dev = pr.dev
+    c, lo, hi, b = pr.c, pr.lo, pr.hi, pr.b
+    FL = torch.isfinite(lo).to(F64).expand(B, N)
+    FH = torch.isfinite(hi).to(F64).expand(B, N)
+    lo_ = torch.where(torch.isfinite(lo), lo, torch.zeros_like(lo))
+    hi_ = torch.where(torch.isfinite(hi), hi, torch.zeros_like(hi))
+    span = (hi_ - lo_).clamp(min=0)
+    x0 = torch.full((N,), 1.0, dtype=F64, device=dev)
+    both = torch.isfinite(lo) & torch.isfinite(hi)
+    x0 = torch.where(both, lo_ + 0.5 * span, x0)
+    x0 = torch.where(torch.isfinite(lo) & ~torch.isfinite(hi), lo_ + 1.0, x0)
+    x0 = torch.where(~torch.isfinite(lo) & torch.isfinite(hi), hi_ - 1.0, x0)
+    x = x0.expand(B, N).clone()
+    lam = torch.zeros((B, m), dtype=F64, device=dev)
+    zl = FL.clone()
+    zh = FH.clone()
+    nfac = _NormalFactor(B, n, dev)
+    ncomp = (FL + FH).sum(1).clamp(min=1)
+    bn = 1.0 + b.abs().amax(1)
+    cn = 1.0 + c.abs().amax()
+    done = torch.zeros(B, dtype=torch.bool, device=dev)
+    iters = torch.zeros(B, dtype=torch.int32, device=dev)
+    mc, me, X, C = pr.mc, pr.me, pr.X, pr.C
+
+    for it in range(max_iter):
+        sl = torch.where(FL > 0, (x - lo_).clamp(min=1e-200), torch.ones_like(x))
+        sh = torch.where(FH > 0, (hi_ - x).clamp(min=1e-200), torch.ones_like(x))
+        rp = b - pr.A(x)
+        rd = c - pr.At(lam) - zl + zh
+        pobj = (c * x).sum(1)
+        dobj = (b * lam).sum(1) + (lo_ * zl * FL).sum(1) - (hi_ * zh * FH).sum(1)
+        mu = ((sl * zl * FL).sum(1) + (sh * zh * FH).sum(1)) / ncomp
+        conv = ((rp.abs().amax(1) / bn < tol) & (rd.abs().amax(1) / cn < tol)
+                & ((pobj - dobj).abs() / (1.0 + pobj.abs()) < tol))
+        done = done | conv
+        if trace is not None:
+            trace.append((it, float(mu.max()), float((rp.abs().amax(1) / bn).max()),
+                          float((rd.abs().amax(1) / cn).max()), float(((pobj - dobj).abs() / (1.0 + pobj.abs())).max())))
+        if bool(done.all()):
+            break
+        iters += (~done).to(torch.int32)
+        Dg = (FL * zl / sl + FH * zh / sh).clamp(1e-12, 1e24)
+        Dg = torch.where(done[:, None], torch.ones_like(Dg), Dg)     # frozen: any PD system
+        th = 1.0 / Dg
+        th_w, th_u, th_v, th_s = pr.split(th)
+        e_inv = 1.0 / (th_u + th_v)
+        H = torch.bmm(X.transpose(1, 2) * e_inv.unsqueeze(1), X)
+        H.diagonal(dim1=1, dim2=2).add_(Dg[:, :n])
+        # factor a slightly shifted H (rank-deficient X'E^-1 X at degenerate vertices); the
+        # refinement step in hsolve is taken against the unshifted H
+        Hd = H.diagonal(dim1=1, dim2=2)
+        nfac.factor(H + torch.diag_embed(1e-12 * Hd))
+
+        def hsolve(R):                       # H^-1 R (R: B x n x k), refined against H
+            Y = nfac.solve_mat(R)
+            for _ in range(_REFINE):
+                Y = Y + nfac.solve_mat(R - torch.bmm(H, Y))
+            return Y
+
+        if mc:
+            HiC = hsolve(C.T.expand(B, n, mc).contiguous())          # H^-1 C'
+            S = C @ HiC                                              # C H^-1 C' (B, mc, mc)
+            theta_S = torch.cat([torch.zeros((B, me), dtype=F64, device=dev), th_s], 1)
+            S = S + torch.diag_embed(theta_S)
+            S = S + torch.diag_embed(1e-14 * S.diagonal(dim1=1, dim2=2).abs())
+
+        def bordered(f, g):                  # [H -C'; C Theta_S] [dw; dlc] = [f; g]
+            Hf = hsolve(f.unsqueeze(2)).squeeze(2)
+            dlc = torch.linalg.solve(S, g - Hf @ C.T)
+            return Hf + torch.bmm(HiC, dlc.unsqueeze(2)).squeeze(2), dlc
+
+        def direction(rl, rh):
+            rx = rd - rl / sl + rh / sh              # D dx - A' dlam = -rx,  A dx = rp
+            rx_w, rx_u, rx_v, rx_s = pr.split(rx)
+            r_c, r_t = rp[:, :mc], rp[:, mc:]
+            g_t = r_t + th_u * rx_u - th_v * rx_v
+            f = -rx_w + torch.bmm((g_t * e_inv).unsqueeze(1), X).squeeze(1)
+            if mc:
+                g_c = r_c.clone()
+                if pr.mi:
+                    g_c[:, me:] += th_s * rx_s
+                dw, dlc = bordered(f, g_c)
+                for _ in range(2):     # refine against [H -C'; C Theta_S]
+                    e1 = f - (torch.bmm(H, dw.unsqueeze(2)).squeeze(2) - dlc @ C)
+                    e2 = g_c - (dw @ C.T + theta_S * dlc)
+                    cw, cl = bordered(e1, e2)
+                    dw, dlc = dw + cw, dlc + cl
+            else:
+                dlc = torch.zeros((B, 0), dtype=F64, device=dev)
+                dw = hsolve(f.unsqueeze(2)).squeeze(2)
+            dlt = (g_t - torch.bmm(X, dw.unsqueeze(2)).squeeze(2)) * e_inv
+            du = th_u * (dlt - rx_u)
+            dv = th_v * (-dlt - rx_v)
+            ds = th_s * (dlc[:, me:] - rx_s)
+            dx = torch.cat([dw, du, dv, ds], 1)
+            dl = torch.cat([dlc, dlt], 1)
+            dzl = FL * (rl - zl * dx) / sl
+            dzh = FH * (rh + zh * dx) / sh
+            return dx, dl, dzl, dzh
+
+        def steps(dx, dzl, dzh):
+            inf = torch.full_like(dx, np.inf)
+            ap = torch.minimum(torch.where((FL > 0) & (dx < 0), -sl / dx, inf),
+                               torch.where((FH > 0) & (dx > 0), sh / dx, inf)).amin(1)
+            ad = torch.minimum(torch.where(dzl < 0, -zl / dzl, inf), torch.where(dzh < 0, -zh / dzh, inf)).amin(1)
+            return ap.clamp(max=1.0), ad.clamp(max=1.0)
+
+        dx, dl, dzl, dzh = direction(-sl * zl * FL, -sh * zh * FH)
+        ap, ad = steps(dx, dzl, dzh)
+        mu_aff = (((sl + ap[:, None] * dx) * (zl + ad[:, None] * dzl) * FL).sum(1)
+                  + ((sh - ap[:, None] * dx) * (zh + ad[:, None] * dzh) * FH).sum(1)) / ncomp
+        sig = (mu_aff / mu).clamp(0, 1) ** 3
+        smu = (sig * mu)[:, None]
+        rl = FL * (smu - sl * zl - dx * dzl)
+        rh = FH * (smu - sh * zh + dx * dzh)
+        dx, dl, dzl, dzh = direction(rl, rh)
+        ap, ad = steps(dx, dzl, dzh)
+        act = ~done[:, None]
+        ap = (0.995 * ap)[:, None]
+        ad = (0.995 * ad)[:, None]
+        x = torch.where(act, x + ap * dx, x)
+        lam = torch.where(act, lam + ad * dl, lam)
+        zl = torch.where(act, zl + ad * dzl, zl)
+        zh = torch.where(act, zh + ad * dzh, zh)
+    status = torch.where(done, torch.full_like(iters, _lib.PQ_SOLVED), torch.full_like(iters, _lib.PQ_MAX_ITER))
+    return LPResult(x, lam, status, iters, (c * x).sum(1))

@@ -307,3 +307,104 @@ class WeightedLeastSquares(Optimization):
             scale = 2.0 * c
         xty, yty = span.gram_xy(stage.rows, stage.tlen)
         return G, scale, None, -2.0 * c[:, None] * xty, c * yty
+
+
+class LAD(Optimization):
+    """Least absolute deviation tracking (src/optimization.py:263-345): min sum |y - X w| as
+    the reference's LP over [w; u; v].  solver_name 'mi355x' solves it with the batched
+    device IPM of porqua_amd/lad.py; other names build the reference's dense LP for
+    qpsolvers exactly as src/optimization.py:296-345 does."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self.params["use_level"] = self.params.get("use_level", True)
+        self.params["use_log"] = self.params.get("use_log", True)
+
+    def set_objective(self, optimization_data: OptimizationData) -> None:
+        X = optimization_data["return_series"]
+        y = optimization_data["bm_series"]
+        if self.params.get("use_level"):
+            X = (1 + X).cumprod()
+            y = (1 + y).cumprod()
+            if self.params.get("use_log"):
+                X = np.log(X)
+                y = np.log(y)
+        self.objective = Objective(X=X, y=y)
+
+    def _bounds(self):
+        boxed = self.constraints.box["box_type"] != "NA"
+        lb = self.constraints.box["lower"].to_numpy(dtype=np.float64) if boxed else None
+        ub = self.constraints.box["upper"].to_numpy(dtype=np.float64) if boxed else None
+        return lb, ub
+
+    def solve(self) -> bool:
+        """src/optimization.py:286-294 (results hold the weights only, as there)."""
+        universe = self.constraints.selection
+        if self.params.get("solver_name") not in qp_problems.ENGINE_SOLVERS:
+            self.model_qpsolvers()
+            self.model.solve()
+            x = self.model["solution"].x
+        else:
+            import torch
+            from . import engine
+            from . import lad as _lad
+            if "leverage" in self.constraints.l1:
+                raise TypeError("LAD with a leverage constraint: the reference's np.zeros() call "
+                                "raises here (src/optimization.py:333)")
+            X = np.ascontiguousarray(to_numpy(self.objective["X"]), dtype=np.float64)
+            y = np.ascontiguousarray(to_numpy(self.objective["y"]), dtype=np.float64).reshape(-1)
+            dev = engine.default_device()
+            GhAb = self.constraints.to_GhAb()
+            lb, ub = self._bounds()
+            pr = _lad.LADProblem(torch.from_numpy(X)[None].to(dev), torch.from_numpy(y)[None].to(dev),
+                                 A=GhAb["A"], b=GhAb["b"], G=GhAb["G"], h=GhAb["h"], lb=lb, ub=ub)
+            res = _lad.lad_ipm_batched(pr)
+            x = res.x[0].cpu().numpy() if bool(res.found[0]) else None
+        w = x[:len(universe)] if x is not None else [None] * len(universe)
+        self.results = {"weights": pd.Series(w, index=universe).to_dict()}
+        return True
+
+    def lad_batch(self, panel, rows, tlen, GhAb, lb, ub):
+        """Every window of a backtest chunk in one device IPM: (W, status, obj) or None."""
+        import torch
+        from . import lad as _lad
+        if panel.bm is None or len(tlen) == 0 or np.any(tlen != tlen[0]) or tlen[0] < 1:
+            return None
+        if "leverage" in self.constraints.l1:
+            return None
+        idx = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int64)).to(panel.device)
+        X, y = panel.R[idx], panel.bm[idx]
+        if self.params.get("use_level"):
+            X, y = torch.cumprod(1 + X, 1), torch.cumprod(1 + y, 1)
+            if self.params.get("use_log"):
+                X, y = torch.log(X), torch.log(y)
+        pr = _lad.LADProblem(X.contiguous(), y.contiguous(), A=GhAb["A"], b=GhAb["b"], G=GhAb["G"],
+                             h=GhAb["h"], lb=lb, ub=ub)
+        res = _lad.lad_ipm_batched(pr)
+        n = panel.n
+        return res.x[:, :n].cpu().numpy(), res.status.cpu().numpy(), res.obj.cpu().numpy()
+
+    def model_qpsolvers(self) -> None:
+        """The reference's dense LP for a non-engine solver (src/optimization.py:296-345)."""
+        X = to_numpy(self.objective["X"])
+        y = to_numpy(self.objective["y"]).reshape(-1)
+        GhAb = self.constraints.to_GhAb()
+        N, T = X.shape[1], X.shape[0]
+        G_t = np.pad(GhAb["G"], [(0, 0), (0, 2 * T)]) if GhAb["G"] is not None else None
+        A = GhAb["A"]
+        meq = 0 if A is None else 1 if A.ndim == 1 else A.shape[0]
+        A_t = np.zeros((T, N + 2 * T)) if A is None else np.pad(np.atleast_2d(A), [(0, T), (0, 2 * T)])
+        A_t[meq:T + meq, :N] = X
+        A_t[meq:T + meq, N:N + T] = np.eye(T)
+        A_t[meq:T + meq, N + T:] = -np.eye(T)
+        b_t = y if GhAb["b"] is None else np.append(GhAb["b"], y)
+        lb, ub = self._bounds()
+        lb = np.pad(np.full(N, -np.inf) if lb is None else lb, (0, 2 * T))
+        ub = np.pad(np.full(N, np.inf) if ub is None else ub, (0, 2 * T), constant_values=np.inf)
+        if "leverage" in self.constraints.l1:
+            raise TypeError("LAD with a leverage constraint: the reference's np.zeros() call raises "
+                            "(src/optimization.py:333)")
+        self.model = qp_problems.QuadraticProgram(P=np.zeros((N + 2 * T, N + 2 * T)),
+                                                  q=np.append(np.zeros(N), np.ones(2 * T)),
+                                                  G=G_t, h=GhAb["h"], A=A_t, b=b_t, lb=lb, ub=ub,
+                                                  params=self.params)

@@ -1,0 +1,89 @@
+"""LAD (src/optimization.py:263-345) on the device: the reference's LP solved by the batched
+IPM of porqua_amd/lad.py (w-space normal equations factored on K2), checked against the
+golden LPs captured from the reference's own backtest (tools/capture_lad.py) and HiGHS
+(oracle/lad.py).  An LP's optimal value is unique; weights are compared only through it."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import lad as olad
+from porqua_amd.backtest import Backtest
+from porqua_amd.constraints import Constraints
+from porqua_amd.optimization import LAD
+from porqua_amd.optimization_data import OptimizationData
+from tests.conftest import load_golden
+from tests.test_api_gpu import _service, msci
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_weights(W, g, X, y, box_ub, use_level, use_log, tol=1e-7):
+    dates = X.index.values.astype("datetime64[D]")
+    R, yv = X.to_numpy(), y.to_numpy()[:, 0]
+    for i, rb in enumerate(g["rebdates"]):
+        e = np.searchsorted(dates, np.datetime64(str(rb)), side="right")
+        rows = np.arange(e - int(g["width"]), e)
+        Xl = olad.levels(R[rows], use_level, use_log)
+        yl = olad.levels(yv[rows], use_level, use_log)
+        w = W[i]
+        f = np.abs(yl - Xl @ w).sum()
+        assert abs(f - g["obj"][i]) <= tol * g["obj"][i], (i, f, g["obj"][i])
+        assert abs(w.sum() - 1) < 1e-9 and w.min() > -1e-9 and w.max() < box_ub + 1e-9
+
+
+@pytest.mark.parametrize("tag,kw,box", [("msci_lad", {}, {}),
+                                        ("msci_lad_ret", {"use_level": False}, {"upper": 0.3})])
+def test_lad_backtest_batched_matches_golden(device, tag, kw, box):
+    X, y = msci()
+    g = load_golden(tag)
+    rebdates = [str(d) for d in g["rebdates"]]
+    bt = Backtest()
+    bt.run(_service(LAD(solver_name="mi355x", **kw), X, y, rebdates, box))
+    assert bt.stats["path"] == "lp-ipm" and bt.stats["solved"] == len(rebdates)
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    _check_weights(W, g, X, y, box.get("upper", 1.0), kw.get("use_level", True), True)
+
+
+def test_lad_serial_equals_batched_value(device):
+    X, y = msci()
+    g = load_golden("msci_lad_ret")
+    rebdates = [str(d) for d in g["rebdates"][:6]]
+    bs = _service(LAD(solver_name="mi355x", use_level=False), X, y, rebdates, {"upper": 0.3})
+    bs.settings["batched"] = False
+    bt = Backtest()
+    bt.run(bs)
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    sub = {k: g[k][:6] if k in ("rebdates", "obj") else g[k] for k in ("rebdates", "obj", "width")}
+    _check_weights(W, sub, X, y, 0.3, False, True)
+
+
+def test_lad_solve_with_group_caps_matches_highs(device):
+    """LAD.solve (the reference API) with budget, box and two '<=' group rows, on windows
+    with and without a box; value vs HiGHS on the reference's LP."""
+    X, y = msci()
+    n = X.shape[1]
+    rng = np.random.default_rng(3)
+    groups = [(rng.random(n) < 0.4).astype(float) for _ in range(2)]
+    for end, boxed in [(900, True), (1700, True), (2500, False)]:
+        Xw, yw = X.iloc[end - 252:end], y.iloc[end - 252:end]
+        cons = Constraints(selection=X.columns)
+        cons.add_budget()
+        if boxed:
+            cons.add_box("LongOnly", upper=0.25)
+        for gv in groups:
+            cons.add_linear(None, pd.Series(gv, index=X.columns), "<=", 0.3)
+        opt = LAD(solver_name="mi355x", constraints=cons)
+        opt.set_objective(OptimizationData(return_series=Xw, bm_series=yw))
+        assert opt.solve() is True
+        w = pd.Series(opt.results["weights"]).to_numpy(dtype=float)
+        Xl = olad.levels(Xw.to_numpy())
+        yl = olad.levels(yw.to_numpy()[:, 0])
+        GhAb = cons.to_GhAb()
+        lb = cons.box["lower"].to_numpy(dtype=float) if boxed else None
+        ub = cons.box["upper"].to_numpy(dtype=float) if boxed else None
+        q, A, b, G, h, lbt, ubt = olad.lad_lp(Xl, yl, A=GhAb["A"], b=GhAb["b"], G=GhAb["G"], h=GhAb["h"],
+                                              lb=lb, ub=ub)
+        ref = olad.solve_lp(q, A, b, lbt, ubt, G, h)
+        f = np.abs(yl - Xl @ w).sum()
+        assert abs(f - ref.fun) <= 1e-7 * ref.fun, (end, f, ref.fun)
+        assert abs(w.sum() - 1) < 1e-9 and (GhAb["G"] @ w <= GhAb["h"] + 1e-9).all()

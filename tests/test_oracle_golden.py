@@ -111,3 +111,29 @@ def test_ipm_oracle_is_kkt_certified(tag):
         assert s.primal_residual() < 1e-12 and s.dual_residual() < 1e-12
         assert np.abs(s.x - g["x"][i]).max() < 1e-9
         assert abs(s.obj - g["obj"][i]) <= 1e-12 * max(1.0, abs(g["obj"][i]))
+
+
+@pytest.mark.parametrize("tag", ["msci_lad", "msci_lad_ret"])
+def test_lad_lp_matches_reference(tag):
+    """oracle/lad.py restates LAD.set_objective / model_qpsolvers (src/optimization.py:271-336):
+    the LP the reference hands to qpsolvers (tools/capture_lad.py) is reproduced entry for
+    entry, and HiGHS reproduces the golden optimal value."""
+    from oracle import lad as olad
+    dates, R, y = _panel()
+    g = load_golden(tag)
+    params = eval(str(g["params"]))
+    box = eval(str(g["box"]))
+    # P = 0 reaches qpsolvers as nearestPD(0) = spacing(0) I = 5e-324 I (src/qp_problems.py:189-191)
+    assert (g["P_absmax"] <= 1e-300).all()
+    n = R.shape[1]
+    for i in range(0, len(g["rebdates"]), 5):
+        rows = rp.window_rows(dates, g["rebdates"][i], int(g["width"]))
+        X = olad.levels(R[rows], params.get("use_level", True), params.get("use_log", True))
+        yl = olad.levels(y[rows], params.get("use_level", True), params.get("use_log", True))
+        q, A, b, G, h, lb, ub = olad.lad_lp(X, yl, A=np.ones(n), b=np.array(1.0), lb=np.zeros(n),
+                                            ub=np.full(n, box.get("upper", 1.0)))
+        assert np.array_equal(q, g["q"][i]) and np.allclose(A, g["A"][i], rtol=1e-13, atol=0)
+        assert np.allclose(b, g["b"][i], rtol=1e-13, atol=0)
+        assert np.array_equal(lb, g["lb"][i]) and np.array_equal(ub, g["ub"][i])
+        s = olad.solve_lp(q, A, b, lb, ub)
+        assert abs(s.fun - g["obj"][i]) <= 1e-9 * g["obj"][i]
