@@ -25,15 +25,19 @@ from . import _lib, engine
 
 F64 = torch.float64
 _REFINE = 1
+_INACCURATE = 1e-6
 
 
 class LPResult:
-    def __init__(self, x, lam, status, iters, obj):
-        self.x, self.lam, self.status, self.iters, self.obj = x, lam, status, iters, obj
+    """x: the best iterate by the merit max(rel. primal residual, rel. dual residual, rel.
+    gap); status PQ_SOLVED (merit < tol), PQ_SOLVED_INACCURATE (< 1e-6) or PQ_MAX_ITER."""
+
+    def __init__(self, x, lam, status, iters, obj, merit):
+        self.x, self.lam, self.status, self.iters, self.obj, self.merit = x, lam, status, iters, obj, merit
 
     @property
     def found(self):
-        return self.status == _lib.PQ_SOLVED
+        return (self.status == _lib.PQ_SOLVED) | (self.status == _lib.PQ_SOLVED_INACCURATE)
 
 
 class LADProblem:
@@ -146,6 +150,9 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
     cn = 1.0 + c.abs().amax()
     done = torch.zeros(B, dtype=torch.bool, device=dev)
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
+    best_x = x.clone()
+    best_merit = torch.full((B,), np.inf, dtype=F64, device=dev)
+    best_it = torch.zeros(B, dtype=torch.int64, device=dev)
     mc, me, X, C = pr.mc, pr.me, pr.X, pr.C
 
     for it in range(max_iter):
@@ -156,9 +163,15 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         pobj = (c * x).sum(1)
         dobj = (b * lam).sum(1) + (lo_ * zl * FL).sum(1) - (hi_ * zh * FH).sum(1)
         mu = ((sl * zl * FL).sum(1) + (sh * zh * FH).sum(1)) / ncomp
-        conv = ((rp.abs().amax(1) / bn < tol) & (rd.abs().amax(1) / cn < tol)
-                & ((pobj - dobj).abs() / (1.0 + pobj.abs()) < tol))
-        done = done | conv
+        merit = torch.maximum(torch.maximum(rp.abs().amax(1) / bn, rd.abs().amax(1) / cn),
+                              (pobj - dobj).abs() / (1.0 + pobj.abs()))
+        merit = torch.where(torch.isnan(merit), torch.full_like(merit, np.inf), merit)
+        better = (merit < best_merit) & ~done
+        best_x = torch.where(better[:, None], x, best_x)
+        best_it = torch.where(better, torch.full_like(best_it, it), best_it)
+        best_merit = torch.where(better, merit, best_merit)
+        # converged, or stalled (the normal matrix has run out of accuracy): keep the best iterate
+        done = done | (merit < tol) | ((it - best_it > 6) & (best_merit < _INACCURATE))
         if trace is not None:
             trace.append((it, float(mu.max()), float((rp.abs().amax(1) / bn).max()),
                           float((rd.abs().amax(1) / cn).max()), float(((pobj - dobj).abs() / (1.0 + pobj.abs())).max())))
@@ -248,5 +261,7 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         lam = torch.where(act, lam + ad * dl, lam)
         zl = torch.where(act, zl + ad * dzl, zl)
         zh = torch.where(act, zh + ad * dzh, zh)
-    status = torch.where(done, torch.full_like(iters, _lib.PQ_SOLVED), torch.full_like(iters, _lib.PQ_MAX_ITER))
-    return LPResult(x, lam, status, iters, (c * x).sum(1))
+    status = torch.full_like(iters, _lib.PQ_MAX_ITER)
+    status = torch.where(best_merit < _INACCURATE, torch.full_like(iters, _lib.PQ_SOLVED_INACCURATE), status)
+    status = torch.where(best_merit < tol, torch.full_like(iters, _lib.PQ_SOLVED), status)
+    return LPResult(best_x, lam, status, iters, (c * best_x).sum(1), best_merit)

@@ -10,8 +10,8 @@ Deliberate differences from the reference ("Reference defects"):
   package) and lets ``verbose=False`` stick (src/optimization.py:45-46).
 * ``MeanVariance`` uses the mean estimator that is passed in; the reference stores the
   class instead of the instance (src/optimization.py:165).
-LAD (an LP with T equality rows) and PercentilePortfolios (ranking, not
-the QP path) are not built.
+LAD runs on the batched device IPM of porqua_amd/lad.py; PercentilePortfolios (ranking,
+not the QP path) is not built.
 """
 from __future__ import annotations
 

@@ -87,3 +87,27 @@ def test_lad_solve_with_group_caps_matches_highs(device):
         f = np.abs(yl - Xl @ w).sum()
         assert abs(f - ref.fun) <= 1e-7 * ref.fun, (end, f, ref.fun)
         assert abs(w.sum() - 1) < 1e-9 and (GhAb["G"] @ w <= GhAb["h"] + 1e-9).all()
+
+
+def test_lad_backtest_n300_matches_highs(device):
+    """n = 300 > window: 24 daily windows of the synthetic factor panel in one batch."""
+    from porqua_amd.synthetic import factor_panel
+    n, D, width = 300, 320, 252
+    dates, R, yv, _ = factor_panel(D, n, seed=5)
+    idx = pd.DatetimeIndex(dates)
+    X = pd.DataFrame(R, index=idx, columns=[f"a{i}" for i in range(n)])
+    y = pd.DataFrame({"bm": yv}, index=idx)
+    rebdates = [str(d.date()) for d in idx[width + 10:width + 34]]
+    bt = Backtest()
+    bt.run(_service(LAD(solver_name="mi355x"), X, y, rebdates, {"upper": 0.05}, width=width))
+    assert bt.stats["path"] == "lp-ipm" and bt.stats["solved"] == len(rebdates)
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    for i in (0, 13, 23):
+        e = idx.get_loc(pd.Timestamp(rebdates[i])) + 1
+        Xl, yl = olad.levels(R[e - width:e]), olad.levels(yv[e - width:e])
+        q, A, b, G, h, lb, ub = olad.lad_lp(Xl, yl, A=np.ones(n), b=np.array(1.0), lb=np.zeros(n),
+                                            ub=np.full(n, 0.05))
+        ref = olad.solve_lp(q, A, b, lb, ub)
+        f = np.abs(yl - Xl @ W[i]).sum()
+        assert abs(f - ref.fun) <= 1e-7 * ref.fun, (i, f, ref.fun)
+        assert abs(W[i].sum() - 1) < 1e-9 and W[i].min() > -1e-9 and W[i].max() < 0.05 + 1e-9
