@@ -8,11 +8,12 @@ batched Mehrotra predictor-corrector interior-point method for
 
     min c'x   s.t.  A x = b,  l <= x <= h   (infinite bounds allowed)
 
-Each iteration forms the normal matrix M = A diag(theta) A' (m x m, m = T + 1 + rows of G)
-for every date at once (one batched GEMM), factors and inverts it on K2
-(``pq_factor_batched``, the engine's FP64-MFMA blocked Cholesky, invert = 2) and reuses
-M^-1 for the predictor and the corrector (each with one refinement step against M).
-Inequality rows G x <= h become equality rows with slack columns s >= 0.
+Each iteration eliminates u, v, the slacks and the T window rows exactly and forms the
+w-space normal matrix H = diag(z/s) + X' diag(1/(theta_u + theta_v)) X (n x n) for every
+window at once (one batched GEMM).  K2 (``pq_factor_batched``, the engine's FP64-MFMA
+blocked Cholesky, invert = 2) factors and inverts it; the predictor and the corrector
+reuse the inverse, refined against the unshifted H, and the few budget / group rows
+border it through a small Schur system.  Inequality rows G x <= h get slack columns.
 """
 from __future__ import annotations
 
@@ -24,7 +25,7 @@ import torch
 from . import _lib, engine
 
 F64 = torch.float64
-_REFINE = 1
+_REFINE = 2
 _INACCURATE = 1e-6
 
 
@@ -93,7 +94,7 @@ class LADProblem:
 
 class _NormalFactor:
     """H = diag(1/theta_w) + X' diag(1/(theta_u + theta_v)) X per window (n x n), factored
-    on K2 (pq_factor_batched: H = L L')."""
+    and inverted on K2 (pq_factor_batched, invert = 2: Cholesky, trtri, lauum)."""
 
     def __init__(self, B, m, dev):
         self.m = m
@@ -106,18 +107,20 @@ class _NormalFactor:
         _lib.check(lib.pq_init_state(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
                                      ctypes.byref(self.s), engine._stream()), "pq_init_state (LP)")
 
-    def factor(self, M):
+    def factor(self, H, shift):
+        """Factor H + diag(shift) and overwrite the K2 scratch with its inverse (invert = 2)."""
         m, lib = self.m, _lib.load()
-        self.qb.P[:, :m, :m] = M
+        P = self.qb.P
+        P[:, :m, :m].copy_(H)
+        P.diagonal(dim1=1, dim2=2)[:, :m].add_(shift)
         _lib.check(lib.pq_factor_batched(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
-                                         ctypes.byref(self.s), 0, engine._stream()), "pq_factor_batched (LP)")
-        self.L = self.ws.K[:, :m, :m]
+                                         ctypes.byref(self.s), 2, engine._stream()), "pq_factor_batched (LP)")
+        self.Hinv = self.ws.K[:, :m, :m]
         return self.ws.info
 
     def solve_mat(self, R):
-        """H^-1 R (B x n x k) by the two triangular solves against the K2 factor."""
-        t = torch.linalg.solve_triangular(self.L, R, upper=False)
-        return torch.linalg.solve_triangular(self.L.transpose(1, 2), t, upper=True)
+        """(H + diag(shift))^-1 R for R (B x n x k)."""
+        return torch.bmm(self.Hinv, R)
 
 
 def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace=None) -> LPResult:
@@ -183,12 +186,11 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         th = 1.0 / Dg
         th_w, th_u, th_v, th_s = pr.split(th)
         e_inv = 1.0 / (th_u + th_v)
-        H = torch.bmm(X.transpose(1, 2) * e_inv.unsqueeze(1), X)
+        H = torch.bmm(X.transpose(1, 2), X * e_inv.unsqueeze(2))
         H.diagonal(dim1=1, dim2=2).add_(Dg[:, :n])
         # factor a slightly shifted H (rank-deficient X'E^-1 X at degenerate vertices); the
         # refinement step in hsolve is taken against the unshifted H
-        Hd = H.diagonal(dim1=1, dim2=2)
-        nfac.factor(H + torch.diag_embed(1e-12 * Hd))
+        nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2))
 
         def hsolve(R):                       # H^-1 R (R: B x n x k), refined against H
             Y = nfac.solve_mat(R)
