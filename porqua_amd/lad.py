@@ -175,6 +175,7 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         best_merit = torch.where(better, merit, best_merit)
         # converged, or stalled (the normal matrix has run out of accuracy): keep the best iterate
         done = done | (merit < tol) | ((it - best_it > 6) & (best_merit < _INACCURATE))
+        done = done | ~torch.isfinite(x).all(1)             # broke down: keep the best iterate
         if trace is not None:
             trace.append((it, float(mu.max()), float((rp.abs().amax(1) / bn).max()),
                           float((rd.abs().amax(1) / cn).max()), float(((pobj - dobj).abs() / (1.0 + pobj.abs())).max())))
@@ -185,16 +186,16 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         Dg = torch.where(done[:, None], torch.ones_like(Dg), Dg)     # frozen: any PD system
         th = 1.0 / Dg
         th_w, th_u, th_v, th_s = pr.split(th)
-        e_inv = 1.0 / (th_u + th_v)
+        e_inv = torch.where(done[:, None], torch.ones_like(th_u), 1.0 / (th_u + th_v))
         H = torch.bmm(X.transpose(1, 2), X * e_inv.unsqueeze(2))
         H.diagonal(dim1=1, dim2=2).add_(Dg[:, :n])
         # factor a slightly shifted H (rank-deficient X'E^-1 X at degenerate vertices); the
         # refinement step in hsolve is taken against the unshifted H
         nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2))
 
-        def hsolve(R):                       # H^-1 R (R: B x n x k), refined against H
+        def hsolve(R, refine=_REFINE):       # H^-1 R (R: B x n x k), refined against H
             Y = nfac.solve_mat(R)
-            for _ in range(_REFINE):
+            for _ in range(refine):
                 Y = Y + nfac.solve_mat(R - torch.bmm(H, Y))
             return Y
 
