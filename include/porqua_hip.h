@@ -266,6 +266,15 @@ int pq_simulate_periods(const double* panel, int64_t ldp, int32_t n, const doubl
                         double days_per_year, double* ret, double* wend, int64_t ldwe,
                         double* turnover, int32_t rescale, void* stream);
 
+/* LAD interior-point method (porqua_amd/lad.py; replaces the LP solve behind
+ * LAD.model_qpsolvers, src/optimization.py:296-345): out[b] = M[b] V[b], or
+ * out[b] = S[b] - M[b] V[b] when S != NULL, for M[b] n x n (row stride ldm, batch stride
+ * sm) and V, S, out n x k row-major (batch strides sv, ss, so).  n <= 1024, 1 <= k <= 4.
+ * Applies the K2-inverted normal matrix H^-1 and H itself to the IPM right-hand sides.   */
+int pq_lad_mv_batched(const double* M, int64_t ldm, int64_t sm, int32_t n, int32_t batch,
+                      const double* V, int64_t sv, int32_t k, const double* S, int64_t ss,
+                      double* out, int64_t so, void* stream);
+
 /* Device bytes of the per-batch buffers a caller allocates before the solve entry points
  * (the pq_state arrays, the polish scratch and, for the window path, the capacitance
  * matrices M, M^-1 and their factor scratch), so a non-Python host can size one arena.

@@ -130,6 +130,8 @@ _EXPORTS = {
     "pq_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_int64),
     "pq_simulate_periods": ([c_dp, c_int64, c_int32, c_dp, c_int64, c_dp, c_dp, c_int32, c_dp, c_dp,
                              ctypes.c_double, ctypes.c_double, c_dp, c_dp, c_int64, c_dp, c_int32, c_dp], c_int32),
+    "pq_lad_mv_batched": ([c_dp, c_int64, c_int64, c_int32, c_int32, c_dp, c_int64, c_int32, c_dp, c_int64,
+                           c_dp, c_int64, c_dp], c_int32),
 }
 
 _lib = None

@@ -92,6 +92,23 @@ class LADProblem:
         return torch.cat([gw, lt, -lt, lc[:, self.me:]], 1)
 
 
+def _mv(M, V, S=None):
+    """M V, or S - M V, for M (B, n, n) with unit column stride and V (B, n, k): the HIP
+    kernel pq_lad_mv_batched for k <= 4 (one pass over M), a batched GEMM otherwise."""
+    B, n, k = V.shape
+    if k > 4 or n > 1024:
+        return torch.bmm(M, V) if S is None else S - torch.bmm(M, V)
+    assert M.stride(2) == 1 and M.shape[1] == n and M.shape[2] == n
+    V = V.contiguous()
+    S = None if S is None else S.contiguous()
+    out = torch.empty_like(V)
+    lib = _lib.load()
+    _lib.check(lib.pq_lad_mv_batched(M.data_ptr(), M.stride(1), M.stride(0), n, B, V.data_ptr(), V.stride(0), k,
+                                     None if S is None else S.data_ptr(), 0 if S is None else S.stride(0),
+                                     out.data_ptr(), out.stride(0), engine._stream()), "pq_lad_mv_batched")
+    return out
+
+
 class _NormalFactor:
     """H = diag(1/theta_w) + X' diag(1/(theta_u + theta_v)) X per window (n x n), factored
     and inverted on K2 (pq_factor_batched, invert = 2: Cholesky, trtri, lauum)."""
@@ -120,7 +137,7 @@ class _NormalFactor:
 
     def solve_mat(self, R):
         """(H + diag(shift))^-1 R for R (B x n x k)."""
-        return torch.bmm(self.Hinv, R)
+        return _mv(self.Hinv, R)
 
 
 def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace=None) -> LPResult:
@@ -196,7 +213,7 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         def hsolve(R, refine=_REFINE):       # H^-1 R (R: B x n x k), refined against H
             Y = nfac.solve_mat(R)
             for _ in range(refine):
-                Y = Y + nfac.solve_mat(R - torch.bmm(H, Y))
+                Y = Y + nfac.solve_mat(_mv(H, Y, R))
             return Y
 
         if mc:
@@ -223,7 +240,7 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
                     g_c[:, me:] += th_s * rx_s
                 dw, dlc = bordered(f, g_c)
                 for _ in range(2):     # refine against [H -C'; C Theta_S]
-                    e1 = f - (torch.bmm(H, dw.unsqueeze(2)).squeeze(2) - dlc @ C)
+                    e1 = f - (_mv(H, dw.unsqueeze(2)).squeeze(2) - dlc @ C)
                     e2 = g_c - (dw @ C.T + theta_S * dlc)
                     cw, cl = bordered(e1, e2)
                     dw, dlc = dw + cw, dlc + cl
