@@ -239,9 +239,58 @@ def solve_batch(qps, settings=None, device=None):
         b = np.broadcast_to(b, (len(qps), b.size)).copy()
     if G is not None and G.ndim == 3 and h is not None and h.ndim == 1:
         h = np.broadcast_to(h, (len(qps), h.size)).copy()
+    me = 0 if A is None else A.shape[-2]
+    mi = 0 if G is None else G.shape[-2]
+    if me + mi > IPM_ROWS:
+        return _solve_batch_ipm(P, q, A, b, G, h, lb, ub, device)
     qb = engine.QPBatch.from_dense(P, q, A=A, b=b, G=G, h=h, lb=lb, ub=ub, device=device)
     res = engine.solve(qb, settings)
     return batch_result_to_solutions(res, qb)
+
+
+IPM_ROWS = 64    # general rows the ADMM engine keeps in LDS; beyond: the device IPM
+
+
+def _solve_batch_ipm(P, q, A, b, G, h, lb, ub, device=None):
+    """More than IPM_ROWS general rows (e.g. the reference's linearised turnover + leverage
+    rows together, src/qp_problems.py:40-118): porqua_amd.ipm.qp_ipm_batched (K2-factored
+    normal equations, N <= 1024, constraint matrices shared by the batch)."""
+    import torch
+    from . import _lib, engine
+    from .ipm import qp_ipm_batched
+    if (A is not None and A.ndim == 3) or (G is not None and G.ndim == 3):
+        raise NotImplementedError("more than 64 general rows with per-problem constraint matrices")
+    if P.shape[-1] > 1024:
+        raise NotImplementedError("more than 64 general rows with n > 1024")
+    dev = device or engine.default_device()
+    B, n = q.shape
+    T = lambda v: None if v is None else torch.from_numpy(np.array(v, dtype=np.float64)).to(dev)
+    def rows(v, m):
+        v = np.asarray(v, dtype=np.float64)
+        return np.broadcast_to(v.reshape(1, -1) if v.ndim < 2 else v, (B, m))
+
+    bb = None if A is None else rows(b, A.shape[0])
+    hh = None if G is None else rows(h, G.shape[0])
+    res = qp_ipm_batched(T(P), T(q), T(A), T(bb), T(G), T(hh), T(lb), T(ub))
+    x = res.x.cpu().numpy()
+    st = res.status.cpu().numpy()
+    it = res.iters.cpu().numpy()
+    obj = res.obj.cpu().numpy()
+    merit = res.merit.cpu().numpy()
+    ya = res.lam.cpu().numpy()
+    sols = []
+    for i in range(B):
+        s = Solution(x=x[i].copy(), status=int(st[i]), iterations=int(it[i]))
+        s.found = int(st[i]) in (_lib.PQ_SOLVED, _lib.PQ_SOLVED_INACCURATE)
+        s.y = -ya[i].copy() if A is not None else None      # qpsolvers sign: Px + q + A'y + ... = 0
+        s.z = s.z_box = None
+        s.obj = float(obj[i]) if s.found else None
+        s._prim = s._dual = s._gap = float(merit[i])
+        s.extras = {"solver": "device IPM (more than 64 general rows)"}
+        if not s.found:
+            s.x = None
+        sols.append(s)
+    return sols
 
 
 def batch_result_to_solutions(res, qb):
