@@ -196,6 +196,53 @@ def test_product_path_fails_loudly_without_gpu():
                           ub=np.ones(n), params={"solver_name": "mi355x"})
     with pytest.raises(_lib.PorquaHipError):
         qp.solve()
+    # more than 64 general rows (device IPM) and LAD (device LP IPM): no CPU fallback either
+    big = QuadraticProgram(P=np.eye(n), q=np.zeros(n), G=np.ones((70, n)), h=np.ones(70),
+                           params={"solver_name": "mi355x"})
+    with pytest.raises(_lib.PorquaHipError):
+        big.solve()
+    import pandas as pd
+    from porqua_amd.constraints import Constraints
+    from porqua_amd.optimization import LAD
+    from porqua_amd.optimization_data import OptimizationData
+    idx = pd.bdate_range("2020-01-01", periods=30)
+    X = pd.DataFrame(np.random.default_rng(0).normal(0, 0.01, (30, n)), index=idx, columns=list("abcd"))
+    y = pd.DataFrame({"bm": X.mean(1)}, index=idx)
+    cons = Constraints(selection=X.columns)
+    cons.add_budget()
+    lad = LAD(solver_name="mi355x", constraints=cons)
+    lad.set_objective(OptimizationData(return_series=X, bm_series=y))
+    with pytest.raises(_lib.PorquaHipError):
+        lad.solve()
+
+
+def test_lad_model_qpsolvers_matches_reference_lp():
+    """LAD.model_qpsolvers (the non-engine route) builds the reference's LP
+    (src/optimization.py:296-336) entry for entry: golden problems from tools/capture_lad.py."""
+    import pandas as pd
+    from porqua_amd.constraints import Constraints
+    from porqua_amd.optimization import LAD
+    from porqua_amd.optimization_data import OptimizationData
+    from tests.conftest import load_golden
+    p = load_golden("msci_panel")
+    g = load_golden("msci_lad_ret")
+    idx = pd.DatetimeIndex(p["dates"].astype("datetime64[D]"))
+    cols = [str(c) for c in p["columns"]]
+    X = pd.DataFrame(p["returns"], index=idx, columns=cols)
+    y = pd.DataFrame({"bm": p["bm"]}, index=idx)
+    for i in (0, 11):
+        e = idx.searchsorted(pd.Timestamp(str(g["rebdates"][i])), side="right")
+        cons = Constraints(selection=cols)
+        cons.add_budget()
+        cons.add_box("LongOnly", upper=0.3)
+        lad = LAD(solver_name="cvxopt", use_level=False, constraints=cons)
+        lad.set_objective(OptimizationData(return_series=X.iloc[e - 252:e], bm_series=y.iloc[e - 252:e]))
+        lad.model_qpsolvers()
+        m = lad.model
+        assert np.array_equal(m["q"], g["q"][i]) and np.allclose(m["A"], g["A"][i], rtol=1e-13, atol=0)
+        assert np.allclose(m["b"], g["b"][i], rtol=1e-13, atol=0)
+        assert np.array_equal(m["lb"], g["lb"][i]) and np.array_equal(m["ub"], g["ub"][i])
+        assert not np.any(m["P"]) and m["G"] is None
 
 
 def test_api_objects_construct_without_gpu():
