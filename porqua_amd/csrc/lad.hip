@@ -2,7 +2,7 @@
 // out[b] = M[b] V[b]  or  out[b] = S[b] - M[b] V[b],  M n x n (row stride ldm), V / S / out
 // n x k row-major (k <= 4).  Each LAD iteration applies H^-1 (from K2) and H to a handful of
 // right-hand sides; the product is HBM-bound on M (8 n^2 bytes per date), so one wave
-// streams whole rows of M with coalesced loads while V sits in LDS, and the k dot products
+// streams whole rows of M with coalesced (16-B when aligned) loads while V sits in LDS, and the k dot products
 // of a row share every load of M.
 #include "capi_util.h"
 
@@ -13,7 +13,7 @@ constexpr int kRowsPerWG = 16;    // 4 rows per wave
 constexpr int kMaxN = 1024;
 constexpr int kMaxK = 4;
 
-template <int K>
+template <int K, bool VEC>
 __global__ __launch_bounds__(kWG) void k_lad_mv(const double* __restrict__ M, int64_t ldm, int64_t sm,
                                                 int n, const double* __restrict__ V, int64_t sv,
                                                 const double* __restrict__ S, int64_t ss,
@@ -32,10 +32,18 @@ __global__ __launch_bounds__(kWG) void k_lad_mv(const double* __restrict__ M, in
     double acc[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) acc[j] = 0.0;
-    for (int c = lane; c < n; c += 64) {
-      const double m = row[c];
+    if (VEC) {                               // 16-B loads: rows 16-B aligned, n even
+      for (int c = 2 * lane; c < n; c += 128) {
+        const double2 m = *reinterpret_cast<const double2*>(row + c);
 #pragma unroll
-      for (int j = 0; j < K; ++j) acc[j] = fma(m, v[c * K + j], acc[j]);
+        for (int j = 0; j < K; ++j) acc[j] = fma(m.y, v[(c + 1) * K + j], fma(m.x, v[c * K + j], acc[j]));
+      }
+    } else {
+      for (int c = lane; c < n; c += 64) {
+        const double m = row[c];
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc[j] = fma(m, v[c * K + j], acc[j]);
+      }
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -58,7 +66,11 @@ template <int K>
 void launch(const double* M, int64_t ldm, int64_t sm, int n, int batch, const double* V, int64_t sv,
             const double* S, int64_t ss, double* out, int64_t so, hipStream_t st) {
   dim3 grid((n + kRowsPerWG - 1) / kRowsPerWG, batch);
-  hipLaunchKernelGGL(k_lad_mv<K>, grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
+  const bool vec = (n % 2 == 0) && (ldm % 2 == 0) && (sm % 2 == 0) && ((uintptr_t)M % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL((k_lad_mv<K, true>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
+  else
+    hipLaunchKernelGGL((k_lad_mv<K, false>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
 }
 
 }  // namespace
