@@ -216,3 +216,47 @@ def test_device_backtest_window_path_transaction_cost(shrink):
         if shrink:
             assert np.abs(W[i] - xo).max() < 1e-5
         assert abs(W[i].sum() - 1) < 1e-7 and W[i].min() > -1e-7 and W[i].max() < 0.1 + 1e-7
+
+
+@pytest.mark.gpu
+def test_device_backtest_turnover_and_leverage_together():
+    """A turnover budget and a leverage constraint together (two l1 terms: the reference's
+    linearised rows, 2n + 2 inequality and n + 1 equality rows) run through the device IPM
+    (porqua_amd/ipm.py) date by date; each date's QP is checked against the oracle IPM."""
+    from oracle.qp_ipm import solve_qp
+    from porqua_amd.backtest import Backtest
+    from porqua_amd.builders import OptimizationItemBuilder
+    from porqua_amd.covariance import Covariance
+    from porqua_amd.optimization import MeanVariance
+    X, y = _msci()
+    n = X.shape[1]
+    rng = np.random.default_rng(9)
+    x0 = dict(zip(X.columns, rng.dirichlet(np.ones(n))))
+
+    def add_l1(bs, rebdate, **kw):
+        bs.optimization.constraints.add_l1("turnover", rhs=0.4, x0=x0)
+        bs.optimization.constraints.add_l1("leverage", rhs=1.3)
+
+    seen = []
+
+    def keep(backtest, bs, rebalancing_date, what):
+        m = bs.optimization.model
+        seen.append(({k: m.get(k) for k in ("P", "q", "G", "h", "A", "b", "lb", "ub")}, m["solution"]))
+
+    opt = MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1),
+                       solver_name="mi355x", risk_aversion=3.0)
+    rebdates = [str(d.date()) for d in X.index[1000:2600:200]]
+    bs = _service(opt, X, y, rebdates, extra=OptimizationItemBuilder(bibfn=add_l1),
+                  box_kw={"box_type": "LongShort", "lower": -0.1, "upper": 0.3})
+    bs.settings["append_fun"] = keep
+    bt = Backtest()
+    bt.run(bs)
+    assert len(seen) == len(rebdates)
+    for prob, sol in seen:
+        assert sol.found and sol.extras.get("solver", "").startswith("device IPM")
+        o = solve_qp(prob["P"], prob["q"], G=prob["G"], h=prob["h"], A=prob["A"], b=prob["b"],
+                     lb=prob["lb"], ub=prob["ub"])
+        assert abs(sol.obj - o.obj) <= 1e-6 * max(abs(o.obj), 1e-3), (sol.obj, o.obj)
+        w = sol.x[:n]
+        assert np.abs(w).sum() <= 1.3 + 1e-7 and abs(w.sum() - 1) < 1e-8
+        assert np.abs(w - np.array(list(x0.values()))).sum() <= 0.4 + 1e-7
