@@ -328,6 +328,26 @@ def main():
         "achieved_gbs": sim_bytes / sim_s / 1e9, "frac_hbm": sim_bytes / sim_s / 1e9 / HBM_PEAK_GBS,
         "note": "daily periods: 1 panel row + weights in, floated weights out, per period; "
                 "period tables staged once (engine.PeriodPlan)"}}
+    # ---- next row, outside the timed region: LAD (the reference's LP,
+    # levels + log, budget + long-only box) on the device IPM for the first 256 windows ----
+    from porqua_amd import lad as _lad
+    nl = min(256, D)
+    idx = torch.from_numpy(ends_local[:nl, None] - T + 1 + np.arange(T)[None, :]).to(dev)
+    y_d = torch.from_numpy(np.ascontiguousarray(y[lo:lo + T - 1 + D], dtype=np.float64)).to(dev)
+    Xl = torch.log(torch.cumprod(1 + pan.R[idx], 1)).contiguous()
+    yl = torch.log(torch.cumprod(1 + y_d[idx], 1)).contiguous()
+    lad_pr = _lad.LADProblem(Xl, yl, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n))
+    _lad.lad_ipm_batched(lad_pr)
+    torch.cuda.synchronize()
+    t_l = time.perf_counter()
+    lad_res = _lad.lad_ipm_batched(lad_pr)
+    torch.cuda.synchronize()
+    lad_s = time.perf_counter() - t_l
+    out["next_rows"]["lad"] = {
+        "solver": "batched Mehrotra IPM, H^-1 from K2 (pq_factor_batched) applied by k_lad_mv",
+        "lps": nl, "lps_per_s": nl / lad_s, "ipm_iterations_max": int(lad_res.iters.max().item()),
+        "status_counts": {str(k): int(v) for k, v in
+                          zip(*np.unique(lad_res.status.cpu().numpy(), return_counts=True))}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.cpu_baseline import blas_threads, time_reference
         sample = np.linspace(T - 1, T - 1 + D - 1, 8).astype(int)
