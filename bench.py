@@ -34,7 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from porqua_amd import engine  # noqa: E402
-from porqua_amd.synthetic import factor_panel  # noqa: E402
+from porqua_amd.workloads import MinVarianceBacktest  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 matrix spec
@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--with-cov", action="store_true",
                     help="low-rank path: also materialise every date's n x n covariance with K1 "
                          "(nothing on that path reads it)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --dates rebalance dates in total, split over the ranks "
+                         "(default: weak scaling, --dates per rank)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="override an engine.Settings field (experiments)")
@@ -79,68 +82,37 @@ def main():
         backend = os.environ.get("PQ_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
-    n, T, D = args.n, args.window, args.dates
-    d_total = T - 1 + D * world
-    dates, R, y, _ = factor_panel(d_total, n)           # deterministic, identical on every rank
-    lo = rank * D                                       # this rank's rows: [lo, lo + T - 1 + D)
-    R_rank = R[lo:lo + T - 1 + D]
-    ends_local = np.arange(T - 1, T - 1 + D)            # rebalance row within the rank slice
-    rebdates = dates[lo:lo + T - 1 + D][ends_local]
-    rows, tlen = engine.window_rows(dates[lo:lo + T - 1 + D], rebdates, T)
-
-    pan = engine.Panel(R_rank, device=dev)
-    rows_d, tlen_d = pan.rows_to_device(rows, tlen)
-    plan = None if args.no_slide else engine.SlidePlan(rows, tlen, dev)
-    gplan = None if args.no_group else engine.GroupPlan(rows, tlen, dev)
-    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)),
-                                   b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), device=dev)
-    # re-shape the batch to D problems sharing constraints
-    ld = qb.ld
-    qb.batch = D
-    qb.P = None
-    qb.q = torch.zeros((D, ld), dtype=torch.float64, device=dev)
-    qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)   # P = 2 * Sigma
+    n, T = args.n, args.window
     settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))
-    mu_lr = pan.window_means(rows_d, tlen_d)
-    lr = engine.LowRank(pan, rows_d, tlen_d, mu=mu_lr, w_scale=1.0 / (tlen_d.to(torch.float64) - 1.0))
-    use_lr = args.path == "lowrank" or (args.path == "auto" and engine.lowrank_applicable(qb, lr))
-    with_cov = (not use_lr) or args.with_cov
-    if with_cov:   # K1 writes Sigma every step (dense path: P = 2 Sigma is what K2 factors)
-        qb.P = torch.empty((D, ld, ld), dtype=torch.float64, device=dev)
-    ws = engine.Workspace(qb, dense=not use_lr)
+    wl = MinVarianceBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
+                             path=args.path, group=not args.no_group, slide=not args.no_slide,
+                             with_cov=args.with_cov, strong=args.strong)
+    D = wl.D                                            # dates of this rank
+    D_all = wl.global_dates                             # dates of the whole job
+    R_rank, y_rank, ends_local, pan = wl.R_rank, wl.y_rank, wl.ends_local, wl.pan
+    qb, lr, plan, gplan, ws = wl.qb, wl.lr, wl.plan, wl.gplan, wl.ws
+    use_lr, with_cov = wl.use_lr, wl.with_cov
     # weights leave the device on a side stream: step k's all-gather (RCCL) and D2H copy to
     # rank 0's pinned host panel overlap step k + 1's kernels (double-buffered staging)
     nbuf = 2
-    w_host = [torch.empty((D * world, n), dtype=torch.float64).pin_memory() for _ in range(nbuf)] \
+    Dpad = -(-D_all // world)                           # equal all-gather blocks (strong: last rank padded)
+    w_host = [torch.empty((Dpad * world, n), dtype=torch.float64).pin_memory() for _ in range(nbuf)] \
         if rank == 0 else None
-    x_stage = [torch.empty((D, n), dtype=torch.float64, device=dev) for _ in range(nbuf)]
-    gather_buf = [torch.empty((world * D, n), dtype=torch.float64, device=dev) for _ in range(nbuf)] \
+    x_stage = [torch.zeros((Dpad if world > 1 else D, n), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    gather_buf = [torch.empty((world * Dpad, n), dtype=torch.float64, device=dev) for _ in range(nbuf)] \
         if world > 1 else None
     side = torch.cuda.Stream(device=dev)
     side_done = [None] * nbuf
     nstep = [0]
 
     def step(events=None):
-        if events is not None:
-            e0 = torch.cuda.Event(enable_timing=True); e0.record()
-        mu = pan.window_means(rows_d, tlen_d, out=mu_lr)
-        if use_lr:
-            lr.refresh()   # diag(Xc'Xc) of the windows: the only O(n) per-date moment besides mu
-        if with_cov:
-            pan.cov(rows_d, tlen_d, mode=0, out=qb.P, mu=mu, plan=plan, lower_only=use_lr)
-        if events is not None:
-            e1 = torch.cuda.Event(enable_timing=True); e1.record()
-            events.append(("moments+cov" if with_cov else "moments", e0, e1))
-        if use_lr:
-            res = engine.solve_lowrank(qb, lr, settings, ws, events=events, groups=gplan)
-        else:
-            res = engine.solve(qb, settings, ws, events=events)
+        res = wl.step(events)
         k = nstep[0] % nbuf
         nstep[0] += 1
         main = torch.cuda.current_stream()
         if side_done[k] is not None:
             main.wait_event(side_done[k])      # staging buffer k is free again
-        x_stage[k].copy_(res.x[:, :n])
+        x_stage[k][:D].copy_(res.x[:, :n])
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(side):
@@ -176,6 +148,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    # ---- accuracy of every solution of the last step (outside the timed region): primal
+    # violation and relative stationarity recomputed from the panel rows with torch -------
+    cert = wl.certificate(res)
+    if dist:
+        cv = torch.tensor([cert["max_violation"], cert["max_rel_stationarity"],
+                           cert["max_rel_complementarity"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(cv, op=dist.ReduceOp.MAX)
+        cert["max_violation"], cert["max_rel_stationarity"], cert["max_rel_complementarity"] = cv.tolist()
+        st_all = torch.bincount((res.status.long() + 8).clamp(0, 15), minlength=16).to(dev)
+        dist.all_reduce(st_all)
+        cert["status_counts"] = {str(i - 8): int(v) for i, v in enumerate(st_all.tolist()) if v}
     # ---- per-kernel timing (HIP events on the launch stream) ------------------------------
     tk = {}
     cnt = {}
@@ -245,7 +228,7 @@ def main():
         except Exception:
             pass
 
-    qps = D * world * args.steps / dt
+    qps = D_all * args.steps / dt
     out = {
         "metric": "QPs solved/sec (rebalance dates) at N=1000 assets, 1-8 GPU; x vs host CPU",
         "value": qps,
@@ -255,13 +238,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (factor-model panel, seed 20240314; usa_returns absent)",
         "config": {"workload": "config3: long-only min-variance (P=2*Pearson cov, budget + box [0,1]), "
                                "daily rebalance", "n_assets": n, "window": T,
-                   "dates_per_gpu": D, "global_batch": D * world, "parallelism": f"dates-sharded x{world}"},
+                   "dates_per_gpu": D, "global_batch": D_all, "parallelism": f"dates-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": kern + (" (K3, grouped low-rank)" if grouped else " (K3)"),
                      "achieved": admm_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": admm_gbs / HBM_PEAK_GBS,
@@ -302,7 +285,9 @@ def main():
                    "refactors_per_step": res.refactors, "admm_launches_per_step": res.admm_launches,
                    "polish_nfree_mean": float(nfree.mean()), "polish_nfree_max": int(nfree.max()),
                    "polish_rounds_mean": float(prounds.mean()), "polish_rounds_max": int(prounds.max()),
-                   "settings_overrides": args.set},
+                   "settings_overrides": args.set,
+                   "certificate": dict(cert, note="all solutions of the last timed step; P x recomputed "
+                                                   "from the panel rows (torch), not by the engine")},
         "cpu_baseline": None,
     }
     # ---- next row, outside the timed region: Strategy.simulate of
@@ -333,7 +318,7 @@ def main():
     from porqua_amd import lad as _lad
     nl = min(256, D)
     idx = torch.from_numpy(ends_local[:nl, None] - T + 1 + np.arange(T)[None, :]).to(dev)
-    y_d = torch.from_numpy(np.ascontiguousarray(y[lo:lo + T - 1 + D], dtype=np.float64)).to(dev)
+    y_d = torch.from_numpy(np.ascontiguousarray(y_rank, dtype=np.float64)).to(dev)
     Xl = torch.log(torch.cumprod(1 + pan.R[idx], 1)).contiguous()
     yl = torch.log(torch.cumprod(1 + y_d[idx], 1)).contiguous()
     lad_pr = _lad.LADProblem(Xl, yl, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n))

@@ -336,12 +336,17 @@ class Backtest:
                 return False
             chunk = min(chunk, max(1, (1 << 34) // (8 * (n + 64) ** 2 + 64 * n * int(tlen.max()))))
         path = "lp-ipm" if lad else "dense"
+        # batchability of a chunk depends on its own windows (window lengths, WLS runs): a
+        # rank that cannot batch must not return while the others block in the all-gather,
+        # so every rank finishes its loop and the verdict is agreed collectively below
+        ok = True
         for s in range(lo, hi, chunk):
             e = min(hi, s + chunk)
             if lad:
                 r = opt.lad_batch(panel, rows[s:e], tlen[s:e], GhAb, lb, ub)
                 if r is None:
-                    return False
+                    ok = False
+                    break
                 W[s - lo:e - lo], ST[s - lo:e - lo], OBJ[s - lo:e - lo] = r
                 continue
             stage = BatchStage(panel, rows[s:e], tlen[s:e], dev)
@@ -351,7 +356,8 @@ class Backtest:
                                     and engine.lowrank_shape_ok(n, int(stage.rows_host.shape[1]), mg))
             obj = opt.objective_batch(stage)
             if obj is None:
-                return False
+                ok = False
+                break
             Pm, scale, pdiag, q, _const = obj
             if stage.lowrank is not None:
                 path = "lowrank"
@@ -382,6 +388,10 @@ class Backtest:
                 W[s - lo:e - lo] = res.x[:, :n].cpu().numpy()
                 OBJ[s - lo:e - lo] = res.obj.cpu().numpy()
             ST[s - lo:e - lo] = res.status.cpu().numpy()
+        if dist is not None:
+            ok = agree_all(ok, dist, dev)
+        if not ok:
+            return False                      # some rank cannot batch: serial path everywhere
         if dist is not None:
             W, ST, OBJ = gather_shards(W, ST, OBJ, len(rebdates), world, dist, dev)
         # ---- phase C: portfolios -----------------------------------------------------------
@@ -415,6 +425,15 @@ def _auto_chunk(n: int) -> int:
     ld = ((n + 63) // 64) * 64
     per = 2 * 8 * ld * ld + 64 * ld * 8
     return max(1, int((96 << 30) // per))
+
+
+def agree_all(ok: bool, dist, device) -> bool:
+    """True iff ``ok`` holds on every rank (one MIN all-reduce)."""
+    import torch
+    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
 
 
 def gather_shards(W, ST, OBJ, total, world, dist, device):

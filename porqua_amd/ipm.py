@@ -97,7 +97,11 @@ def qp_ipm_batched(P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, tol: 
         if mi:
             H = H + torch.matmul(G.T * eg.unsqueeze(1), G)
         H.diagonal(dim1=1, dim2=2).add_(Dg)
-        nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2).abs() + 1e-300)
+        failed = nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2).abs() + 1e-300)
+        if bool(failed.any()):               # K2 broke down even shifted: freeze at the best iterate
+            done = done | failed
+            if bool(done.all()):
+                break
 
         def hsolve(R, refine=2):
             Y = nfac.solve_mat(R)

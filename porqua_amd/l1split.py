@@ -89,11 +89,14 @@ def split_problem(base: dict, term: L1Split) -> dict:
 
 def merge_solution(w: np.ndarray, term: L1Split) -> tuple[np.ndarray, np.ndarray]:
     """(x, aux) of the reference's variable vector from the split solution w: aux = d =
-    |x - x0| (layout 'd') or [x+; x-] (layout 'pm')."""
+    |x - x0| (layout 'd') or the reference's [x+; x-] blocks (layout 'pm'), ordered so that
+    the linearised rows x + x+ - x- = 0 hold."""
     n = term.x0.size
     x = term.x0 + w[:n] - w[n:2 * n]
     if term.layout == "pm":
-        return x, np.concatenate([np.maximum(x, 0.0), np.maximum(-x, 0.0)])
+        # linearize_leverage_constraint writes x + x+ - x- = 0 (src/qp_problems.py:79-118),
+        # i.e. x = x- - x+: its first auxiliary block holds the negative part
+        return x, np.concatenate([np.maximum(-x, 0.0), np.maximum(x, 0.0)])
     return x, np.abs(x - term.x0)
 
 
@@ -122,7 +125,12 @@ def term_from_model(constraints, params, universe):
     if x0 is not None:
         x_init = np.array([x0.get(a, 0) for a in universe], dtype=np.float64)
         tc = params.get("transaction_cost")
-        if tc is not None:
+        if tc is not None and tocon and not tc:
+            # the reference applies BOTH linearisations here (tc is not None, and `not 0` is
+            # True, src/optimization.py:131-137): a zero-cost term plus the budget -- the
+            # budget form's optimum
+            term = L1Split("budget", x_init, tocon["rhs"])
+        elif tc is not None:
             term = L1Split("cost", x_init, tc)
         elif tocon:
             term = L1Split("budget", x_init, tocon["rhs"])

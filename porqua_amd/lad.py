@@ -124,16 +124,28 @@ class _NormalFactor:
         _lib.check(lib.pq_init_state(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
                                      ctypes.byref(self.s), engine._stream()), "pq_init_state (LP)")
 
-    def factor(self, H, shift):
-        """Factor H + diag(shift) and overwrite the K2 scratch with its inverse (invert = 2)."""
+    def factor(self, H, shift, retries: int = 3):
+        """Factor H + diag(shift) and overwrite the K2 scratch with its inverse (invert = 2).
+        A problem whose Cholesky breaks down (K2 ``info`` != 0: its inverse is NOT formed)
+        is refactored with a 1e4x larger shift, up to ``retries`` times.  Returns a bool
+        tensor of the problems that still failed -- the caller must freeze those (their
+        Hinv is garbage but finite)."""
         m, lib = self.m, _lib.load()
         P = self.qb.P
-        P[:, :m, :m].copy_(H)
-        P.diagonal(dim1=1, dim2=2)[:, :m].add_(shift)
-        _lib.check(lib.pq_factor_batched(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
-                                         ctypes.byref(self.s), 2, engine._stream()), "pq_factor_batched (LP)")
+        shift = shift.clone() if torch.is_tensor(shift) else torch.full(H.shape[:2], float(shift), dtype=F64,
+                                                                           device=H.device)
+        for attempt in range(retries + 1):
+            P[:, :m, :m].copy_(H)
+            P.diagonal(dim1=1, dim2=2)[:, :m].add_(shift)
+            _lib.check(lib.pq_factor_batched(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
+                                             ctypes.byref(self.s), 2, engine._stream()), "pq_factor_batched (LP)")
+            bad = self.ws.info != 0
+            if attempt == retries or not bool(bad.any()):     # host sync: one small flag
+                break
+            scale = H.diagonal(dim1=1, dim2=2).abs().amax(1, keepdim=True).clamp(min=1e-300)
+            shift = torch.where(bad[:, None], shift * 1e4 + 1e-12 * scale, shift)
         self.Hinv = self.ws.K[:, :m, :m]
-        return self.ws.info
+        return bad
 
     def solve_mat(self, R):
         """(H + diag(shift))^-1 R for R (B x n x k)."""
@@ -208,7 +220,11 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         H.diagonal(dim1=1, dim2=2).add_(Dg[:, :n])
         # factor a slightly shifted H (rank-deficient X'E^-1 X at degenerate vertices); the
         # refinement step in hsolve is taken against the unshifted H
-        nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2))
+        failed = nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2))
+        if bool(failed.any()):               # K2 broke down even shifted: freeze at the best iterate
+            done = done | failed
+            if bool(done.all()):
+                break
 
         def hsolve(R, refine=_REFINE):       # H^-1 R (R: B x n x k), refined against H
             Y = nfac.solve_mat(R)

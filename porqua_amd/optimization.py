@@ -372,6 +372,9 @@ class LAD(Optimization):
             return None
         if "leverage" in self.constraints.l1:
             return None
+        # the row table is padded to the longest window of the whole backtest: slice it to
+        # this chunk's (uniform) window length, or the padding rows would join the LP
+        rows = np.asarray(rows)[:, :int(tlen[0])]
         idx = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int64)).to(panel.device)
         X, y = panel.R[idx], panel.bm[idx]
         if self.params.get("use_level"):

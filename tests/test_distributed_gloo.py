@@ -37,3 +37,30 @@ def test_gather_shards_world2():
     for p in procs:
         p.join(timeout=60)
     assert sorted(res) == [(0, True), (1, True)]
+
+
+def _agree_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from porqua_amd.backtest import agree_all
+    # only rank 1's shard cannot batch (e.g. unequal window lengths in one of its chunks):
+    # every rank must fall back together instead of rank 0 blocking in the all-gather
+    a = agree_all(rank != 1, dist, torch.device("cpu"))
+    b = agree_all(True, dist, torch.device("cpu"))
+    q.put((rank, a, b))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_batchability_is_agreed_by_all_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31500 + os.getpid() % 2000
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == [(0, False, True), (1, False, True)]

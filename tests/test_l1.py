@@ -77,6 +77,40 @@ def test_split_solved_by_oracle_matches_golden(tag):
         assert abs(obj - obj_ref) <= 1e-8 * max(1.0, abs(obj_ref))
 
 
+def test_merged_vector_satisfies_linearised_rows():
+    """merge_solution's full vector [x; aux] satisfies the reference's linearised equality
+    rows (leverage: x + x+ - x- = 0, src/qp_problems.py:79-118) and the turnover rows
+    (d >= |x - x0|)."""
+    for tag in TAGS:
+        g, n, base, term = _case(tag, 3)
+        qp = _qp(base, term, "mi355x")
+        sp = split_problem(base, term)
+        s = solve_qp(sp["P"], sp["q"], sp["G"], sp["h"], sp["A"], sp["b"], sp["lb"], sp["ub"])
+        x, aux = merge_solution(s.x, term)
+        full = np.concatenate([x, aux])
+        A = np.atleast_2d(qp["A"])
+        assert np.abs(A @ full - np.asarray(qp["b"], dtype=float).reshape(-1)).max() < 1e-9, tag
+        if qp.get("G") is not None:
+            assert (np.atleast_2d(qp["G"]) @ full - np.asarray(qp["h"]).reshape(-1)).max() < 1e-9, tag
+
+
+def test_zero_transaction_cost_keeps_the_turnover_budget():
+    """transaction_cost = 0 with a turnover constraint: the reference applies both
+    linearisations (src/optimization.py:131-137: 0 is not None, and `not 0`), so the
+    budget binds; the batched backtest's term must be the budget, not a zero cost."""
+    from porqua_amd.l1split import term_from_model
+
+    class C:
+        l1 = {"turnover": {"x0": {"a": 0.5, "b": 0.5}, "rhs": 0.3}}
+
+    t = term_from_model(C(), {"transaction_cost": 0.0}, ["a", "b", "c"])
+    assert t.kind == "budget" and t.value == 0.3 and np.array_equal(t.x0, [0.5, 0.5, 0.0])
+    t = term_from_model(C(), {"transaction_cost": 0.01}, ["a", "b", "c"])
+    assert t.kind == "cost" and t.value == 0.01
+    t = term_from_model(C(), {}, ["a", "b", "c"])
+    assert t.kind == "budget"
+
+
 def test_split_rejects_x0_outside_box():
     g, n, base, term = _case("tc", 0)
     bad = L1Split("cost", np.full(n, 2.0), 0.002)
