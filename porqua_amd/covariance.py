@@ -1,3 +1,8 @@
+# Host-side API restatement of PorQua (part of the GeomScale project; reference tree
+# amolrpatil21/PorQua): src/covariance.py.  PorQua is Copyright (c) 2024 Cyril Bachelard and
+# Minh Ha Ho and licensed under the GNU LGPL v3; this module keeps that API and its
+# behaviour (quirks included) so that the MI355X engine is a drop-in, and is distributed
+# under the same licence terms.
 """Covariance estimation on the device (mirror of src/covariance.py:21-84).
 
 ``Covariance.estimate(X)`` keeps the reference signature (T x n DataFrame in, n x n

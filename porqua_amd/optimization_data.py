@@ -1,3 +1,8 @@
+# Host-side API restatement of PorQua (part of the GeomScale project; reference tree
+# amolrpatil21/PorQua): src/optimization_data.py.  PorQua is Copyright (c) 2024 Cyril Bachelard and
+# Minh Ha Ho and licensed under the GNU LGPL v3; this module keeps that API and its
+# behaviour (quirks included) so that the MI355X engine is a drop-in, and is distributed
+# under the same licence terms.
 """Per-date data container (mirror of src/optimization_data.py:19-49)."""
 from __future__ import annotations
 

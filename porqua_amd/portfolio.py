@@ -1,3 +1,8 @@
+# Host-side API restatement of PorQua (part of the GeomScale project; reference tree
+# amolrpatil21/PorQua): src/portfolio.py.  PorQua is Copyright (c) 2024 Cyril Bachelard and
+# Minh Ha Ho and licensed under the GNU LGPL v3; this module keeps that API and its
+# behaviour (quirks included) so that the MI355X engine is a drop-in, and is distributed
+# under the same licence terms.
 """Portfolio / Strategy containers (mirror of src/portfolio.py:20-296).
 
 The rebalance loop fills these; ``Strategy.simulate`` and ``Strategy.turnover_pairs`` float
