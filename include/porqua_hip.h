@@ -249,6 +249,31 @@ int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st
                         int32_t nidx, const pq_settings* s, int32_t ldk, int32_t final_try,
                         void* stream);
 
+/* K4, grouped pipeline (polish_g.hip): the active-set polish of pq_polish_w_batched as a
+ * few throughput kernels per round over every date of a window-path batch -- per-date
+ * setup, an LDS-resident packed Cholesky of P_FF (free sets 1..128) with the same
+ * regularised reduced KKT and refinement, and the exact P x / gradient / acceptance
+ * checks as FP64 MFMA passes over the union rows of each slide group (the group plan of
+ * pq_admm_lr_grouped).  rec holds PQ_PG_RECORD doubles per problem (field 3 = state:
+ * PQ_PG_PENDING / DONE / FALLBACK / SKIP).  pq_polish_grouped_init classifies the ADMM
+ * point; each pq_polish_grouped_round call runs one active-set round for the pending
+ * problems.  Accepted problems are scored exactly as pq_polish_w_batched scores them
+ * (status PQ_SOLVED, out[]); FALLBACK problems (free set outside 1..min(128, ldk), more
+ * than 32 active rows, a failed factorisation, or not accepted within polish_rounds) are
+ * left at their ADMM point for pq_polish_w_batched.  K scratch: ldk x ldk per problem
+ * (indexed by problem id).  Needs even n and ldp, mg <= 32, umax <= 320, lr->dg.
+ * Replaces, with pq_polish_w_batched, the accuracy of qpsolvers (src/qp_problems.py:211-214). */
+#define PQ_PG_RECORD 320
+#define PQ_PG_PENDING 0
+#define PQ_PG_DONE 1
+#define PQ_PG_FALLBACK 2
+#define PQ_PG_SKIP 3
+int pq_polish_grouped_init(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
+                           const pq_settings* s, void* stream);
+int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec, int32_t ldk,
+                            const int32_t* gdates, int32_t ngroups, const int32_t* urows, const int32_t* ucnt,
+                            const int32_t* uoff, int32_t umax, const pq_settings* s, void* stream);
+
 /* Strategy simulation: one holding period per rebalance date.
  * Replaces Strategy.simulate (src/portfolio.py:209-248) with floating_weights
  * (src/portfolio.py:259-296) and the end-weight part of Portfolio.turnover

@@ -25,6 +25,10 @@ PQ_PRIMAL_INFEASIBLE = -3
 PQ_DUAL_INFEASIBLE = -4
 PQ_NON_CONVEX = -5
 
+PQ_PG_RECORD = 320                   # doubles per problem of the grouped polish record
+PQ_PG_PENDING, PQ_PG_DONE, PQ_PG_FALLBACK, PQ_PG_SKIP = range(4)
+PQ_PG_STATE = 3                      # record field holding the state
+
 PQ_OUT_OBJ, PQ_OUT_PRIM, PQ_OUT_DUAL, PQ_OUT_GAP, PQ_OUT_RHO, PQ_OUT_NFREE, PQ_OUT_ROUNDS = range(7)
 PQ_OUT_FIELDS = 8
 
@@ -127,6 +131,11 @@ _EXPORTS = {
     "pq_admm_lr_batched": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                             c_dp, c_int32, c_int64, c_dp, c_int32, ctypes.POINTER(PQSettings), c_int32,
                             c_dp], c_int32),
+    "pq_polish_grouped_init": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                                c_dp, ctypes.POINTER(PQSettings), c_dp], c_int32),
+    "pq_polish_grouped_round": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                                 c_dp, c_int32, c_dp, c_int32, c_dp, c_dp, c_dp, c_int32,
+                                 ctypes.POINTER(PQSettings), c_dp], c_int32),
     "pq_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_int64),
     "pq_simulate_periods": ([c_dp, c_int64, c_int32, c_dp, c_int64, c_dp, c_dp, c_int32, c_dp, c_dp,
                              ctypes.c_double, ctypes.c_double, c_dp, c_dp, c_int64, c_dp, c_int32, c_dp], c_int32),

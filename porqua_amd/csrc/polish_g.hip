@@ -1,0 +1,953 @@
+// K4, grouped pipeline: the window-form active-set polish of polish_w.hip restructured as
+// a few throughput kernels per active-set round over ALL dates of a backtest, instead of
+// one latency-bound workgroup per date that runs every round's phases back to back.
+//
+// Per round (pq_polish_grouped_round), for every date still pending:
+//   setup   (one workgroup per date)   free list F (stable order), active general rows,
+//                                       fixed values x_B, reduced rhs pieces;
+//   pass 0  (one workgroup per GROUP)  P x_B through the window for dates with x_B != 0,
+//                                       both window passes as FP64 MFMA GEMMs over the union
+//                                       rows of a slide group (as in the grouped ADMM);
+//   form    (one workgroup per date)   P_FF = p_scale w_scale Xc_F'Xc_F + p_diag I, MFMA tile
+//                                       products over the window gathered 16 rows at a time;
+//   solve   (one workgroup per date)   LDS-resident packed Cholesky of P_FF + delta I
+//                                       (16-column panels: one wave factors the diagonal
+//                                       block, all waves the panel and the MFMA trailing
+//                                       update), the Schur complement of the active rows,
+//                                       proximal iterative refinement;
+//   pass 1  (one workgroup per GROUP)  exact P x and gradient of the new point through the
+//                                       window (MFMA over the union), the active-set checks,
+//                                       and for accepted dates the final scoring.
+// The arithmetic of every step is polish_w.hip's (same classification, same regularised
+// reduced KKT, same refinement, same acceptance tests), so results agree with it to
+// rounding.  Dates the pipeline does not take (free set outside 1..128, more than 32
+// active rows, a failed factorisation, not accepted within polish_rounds) are marked
+// FALLBACK and left untouched for pq_polish_w_batched, which restarts them from the ADMM
+// point.
+//
+// Replaces, with polish_w.hip, the accuracy of qpsolvers' interior-point answer
+// (src/qp_problems.py:211-214); scoring as src/qp_problems.py:219-221 and
+// example/compare_solver.ipynb:212-216.
+#include "polish_dev.h"
+#include "capi_util.h"
+
+namespace pq {
+
+// per-date polish record (doubles), PQ_PG_RECORD in include/porqua_hip.h
+constexpr int PGR = PQ_PG_RECORD;
+enum : int {
+  R_K = 0, R_MA = 1, R_NZB = 2, R_STATE = 3, R_ROUNDS = 4, R_SC = 5,
+  R_ACT = 64, R_LAM = 128, R_DA = 192, R_SOL = 256, R_AL = 288
+};
+constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
+constexpr int PG_MGMAX = 32;   // general rows
+
+struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
+  double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;
+  int *Fl, *fl;
+  __device__ __forceinline__ PGWork(const pq_state& st, int b, int ld) {
+    double* W = st.work + (int64_t)b * st.work_stride;
+    xs = W;
+    xb = W + ld;
+    g = W + 2 * (int64_t)ld;
+    Px = W + 3 * (int64_t)ld;
+    Fl = reinterpret_cast<int*>(W + 4 * (int64_t)ld);
+    rF = W + 5 * (int64_t)ld;
+    solx = W + 6 * (int64_t)ld;
+    pxb = W + 7 * (int64_t)ld;
+    U = W + 8 * (int64_t)ld;
+    fl = reinterpret_cast<int*>(U + (int64_t)st.mg_pad * ld);
+  }
+};
+
+__device__ __forceinline__ int pk(int r, int c) { return ((r * (r + 1)) >> 1) + c; }
+
+// ---------------------------------------------------------------------------------------
+// init: classification from the ADMM point (polish_w.hip's, verbatim) + problem scale
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                pq_settings s) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  double* R = rec + (int64_t)b * PGR;
+  const int st0 = st.status[b];
+  if (st0 != PQ_SOLVED && st0 != PQ_MAX_ITER) {
+    if (t == 0) R[R_STATE] = PQ_PG_SKIP;
+    return;
+  }
+  const int n = pb.n, ld = pb.ld, mg = pb.mg;
+  const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  const double* q = pb.q + (int64_t)b * pb.q_stride;
+  const double* lg = pb.lg ? pb.lg + (int64_t)b * pb.g_stride : nullptr;
+  const double* ug = pb.ug ? pb.ug + (int64_t)b * pb.g_stride : nullptr;
+  const bool has_box = pb.lb != nullptr;
+  const double* lb = has_box ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
+  const double* ub = has_box ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
+  const double* sz = st.z + (int64_t)b * st.m_ld;
+  const double* sy = st.y + (int64_t)b * st.m_ld;
+  const double* sx = st.x + (int64_t)b * ld;
+  PGWork wk(st, b, ld);
+  const double* dgb = lr.dg + (int64_t)b * lr.dg_stride;
+  double sc = 0.0;
+  for (int i = t; i < n; i += PT) sc = fmax(sc, fmax(fabs(q[i]), fabs(psw * dgb[i] + pd)));
+  sc = block_max(sc, red);
+  sc = fmax(sc, 1e-300);
+  for (int i = t; i < ld; i += PT) {
+    int f = 0;
+    if (i < n && has_box) {
+      const double zi = sz[st.mg_pad + i], yi = sy[st.mg_pad + i];
+      if (!isinf(lb[i]) && zi - lb[i] < -yi) f = 1;
+      else if (!isinf(ub[i]) && ub[i] - zi < yi) f = 2;
+      if (lb[i] == ub[i]) f = 1;
+    }
+    wk.fl[i] = (i < n) ? f : 1;
+    wk.xs[i] = (i < n) ? sx[i] : 0.0;
+  }
+  if (t < 64) {
+    int a = 0;
+    double lam = 0.0;
+    if (t < mg) {
+      const double zr = sz[t], yr = sy[t];
+      if (lg[t] == ug[t]) a = 2;
+      else if (!isinf(lg[t]) && zr - lg[t] < -yr) a = 1;
+      else if (!isinf(ug[t]) && ug[t] - zr < yr) a = 2;
+      lam = yr;
+    }
+    R[R_ACT + t] = a;
+    R[R_LAM + t] = lam;
+  }
+  if (t == 0) {
+    R[R_STATE] = PQ_PG_PENDING;
+    R[R_ROUNDS] = 0;
+    R[R_SC] = sc;
+    R[R_K] = 0;
+    R[R_NZB] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// setup: free list, active rows, x_B, dA, the starting point of the refinement
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, double* rec, int kmax) {
+  __shared__ int wcnt[PW];
+  __shared__ int s_al[PG_MGMAX + 1];
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  double* R = rec + (int64_t)b * PGR;
+  if (R[R_STATE] != PQ_PG_PENDING) return;   // uniform
+  const int n = pb.n, ld = pb.ld, mg = pb.mg;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const double* q = pb.q + (int64_t)b * pb.q_stride;
+  const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
+  const double* lg = pb.lg ? pb.lg + (int64_t)b * pb.g_stride : nullptr;
+  const double* ug = pb.ug ? pb.ug + (int64_t)b * pb.g_stride : nullptr;
+  const bool has_box = pb.lb != nullptr;
+  const double* lb = has_box ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
+  const double* ub = has_box ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
+  PGWork wk(st, b, ld);
+  // ---- stable compaction of the free variables: wave w owns a contiguous index range ----
+  const int seg = ((n + PW * 64 - 1) / (PW * 64)) * 64;
+  const int lo = w * seg, hi = min(n, lo + seg);
+  int c = 0;
+  for (int i0 = lo; i0 < hi; i0 += 64) {
+    const int i = i0 + l;
+    c += __popcll(__ballot(i < hi && wk.fl[i] == 0));
+  }
+  if (l == 0) wcnt[w] = c;
+  if (t == 0) {
+    int a = 0;
+    for (int r = 0; r < mg && a <= PG_MGMAX; ++r)
+      if (R[R_ACT + r] != 0.0) s_al[a++] = r;
+    s_al[PG_MGMAX] = a;
+  }
+  __syncthreads();
+  int base = 0, k = 0;
+  for (int ww = 0; ww < PW; ++ww) {
+    if (ww < w) base += wcnt[ww];
+    k += wcnt[ww];
+  }
+  const int ma = s_al[PG_MGMAX];
+  if (k == 0 || k > kmax || ma > PG_MGMAX) {   // uniform: the per-date kernel takes it
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  for (int i0 = lo; i0 < hi; i0 += 64) {
+    const int i = i0 + l;
+    const bool f = i < hi && wk.fl[i] == 0;
+    const unsigned long long m = __ballot(f);
+    if (f) wk.Fl[base + __popcll(m & ((1ull << l) - 1ull))] = i;
+    base += __popcll(m);
+  }
+  // ---- fixed values, nzb -------------------------------------------------------------------
+  int nzb = 0;
+  for (int i = t; i < ld; i += PT) {
+    const int f = wk.fl[i];
+    const double v = i < n ? (f == 1 ? lb[i] : (f == 2 ? ub[i] : 0.0)) : 0.0;
+    wk.xb[i] = v;
+    nzb |= (v != 0.0);
+  }
+  nzb = block_or(nzb, red);   // barrier: Fl complete below
+  // ---- d_a = rhs_a - C_aB x_B ----------------------------------------------------------------
+  for (int a = w; a < ma; a += PW) {
+    const int r = s_al[a];
+    const double* cr = Cg + (int64_t)r * ld;
+    double sum = 0.0;
+    for (int j = l; j < n; j += 64) sum += cr[j] * wk.xb[j];
+    sum = wave_sum(sum);
+    if (l == 0) R[R_DA + a] = (R[R_ACT + r] == 1.0 ? lg[r] : ug[r]) - sum;
+  }
+  const int kp = (k + 15) & ~15;
+  for (int p = t; p < kp; p += PT) {
+    const int i = p < k ? wk.Fl[p] : 0;
+    wk.solx[p] = p < k ? wk.xs[i] : 0.0;
+    wk.rF[p] = p < k ? -q[i] : 0.0;
+  }
+  if (t < ma) {
+    R[R_AL + t] = s_al[t];
+    R[R_SOL + t] = R[R_LAM + s_al[t]];
+  }
+  if (t == 0) {
+    R[R_K] = k;
+    R[R_MA] = ma;
+    R[R_NZB] = nzb;
+    R[R_ROUNDS] += 1.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// form: P_FF (lower tiles, diagonal tiles in full) into the date's K scratch (pitch ldk)
+// ---------------------------------------------------------------------------------------
+template <int NB>
+__global__ __launch_bounds__(PT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, const double* rec,
+                                                int ldk) {
+  constexpr int PIT = NB * TB + 16;
+  constexpr int KCH = 16;   // window rows per staged chunk (one per 16-thread row group)
+  __shared__ __attribute__((aligned(16))) double S[2 * KCH * PIT];
+  const int b = blockIdx.x;
+  const double* R = rec + (int64_t)b * PGR;
+  if (R[R_STATE] != PQ_PG_PENDING) return;
+  const int k = (int)R[R_K];
+  if (k <= (NB - 1) * TB || k > NB * TB) return;   // another instantiation's range
+  const int ld = pb.ld;
+  const int t = threadIdx.x, kr = t >> 4, c4 = (t & 15) * 4;
+  PGWork wk(st, b, ld);
+  const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  if (R[R_NZB] != 0.0)   // rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F  (pass 0 left it in pxb)
+    for (int p = t; p < k; p += PT) wk.rF[p] -= ps * wk.pxb[wk.Fl[p]];
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  int col[NB][4];
+  double mc[NB][4];
+#pragma unroll
+  for (int h = 0; h < NB; ++h)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int p = h * TB + c4 + e;
+      col[h][e] = p < k ? wk.Fl[p] : -1;
+      mc[h][e] = (col[h][e] >= 0 && mu) ? mu[col[h][e]] : 0.0;
+    }
+  double v[NB][4];
+  auto gather = [&](int t0) {
+    const int tt = t0 + kr;
+    const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
+#pragma unroll
+    for (int h = 0; h < NB; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[h][e] = (row && col[h][e] >= 0) ? row[col[h][e]] - mc[h][e] : 0.0;
+  };
+  auto put = [&](double* Sb) {
+#pragma unroll
+    for (int h = 0; h < NB; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Sb[kr * PIT + h * TB + c4 + e] = v[h][e];
+  };
+  constexpr int NT = NB * (NB + 1) / 2;
+  Acc acc[NT];
+#pragma unroll
+  for (int qq = 0; qq < NT; ++qq) acc[qq].zero();
+  const int l = lane_id(), w = wave_id();
+  const int i0 = (w >> 1) * 32 + (l & 15), j0 = (w & 1) * 32 + (l & 15), krd = l >> 4;
+  auto mma = [&](const double* Sb) {
+#pragma unroll
+    for (int kk = 0; kk < KCH; kk += 4) {
+      const double* r = Sb + (kk + krd) * PIT;
+      double a[NB][2], bj[NB][2];
+#pragma unroll
+      for (int h = 0; h < NB; ++h) {
+        a[h][0] = r[h * TB + i0];
+        a[h][1] = r[h * TB + i0 + 16];
+        bj[h][0] = r[h * TB + j0];
+        bj[h][1] = r[h * TB + j0 + 16];
+      }
+      int qq = 0;
+#pragma unroll
+      for (int I = 0; I < NB; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J, ++qq)
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int nn = 0; nn < 2; ++nn)
+              acc[qq].c[m][nn] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I][m], bj[J][nn], acc[qq].c[m][nn], 0, 0, 0);
+    }
+  };
+  double* S0 = S;
+  double* S1 = S + KCH * PIT;
+  gather(0);
+  put(S0);
+  __syncthreads();
+  int buf = 0;
+  for (int t0 = 0; t0 < T; t0 += KCH) {
+    const bool more = t0 + KCH < T;
+    if (more) gather(t0 + KCH);
+    mma(buf ? S1 : S0);
+    if (more) put(buf ? S0 : S1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  double* K = st.K + (int64_t)b * st.K_stride;
+  int qq = 0;
+#pragma unroll
+  for (int I = 0; I < NB; ++I)
+#pragma unroll
+    for (int J = 0; J <= I; ++J, ++qq)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int gi = I * TB + acc_row(m, r), gj = J * TB + acc_col(nn);
+            K[(int64_t)gi * ldk + gj] = psw * acc[qq].c[m][nn][r] + (gi == gj ? pd : 0.0);
+          }
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-resident packed Cholesky and triangular solves (k <= KS, 256 threads)
+// ---------------------------------------------------------------------------------------
+// Lp holds the lower triangle row by row (element (r, c) at r (r + 1) / 2 + c).  16-column
+// panels: wave 0 factors the 16 x 16 diagonal block in registers (lane i = row i, pivot
+// values exchanged by shuffles), every thread solves one row of the panel below it, and
+// the trailing lower triangle is updated with 16x16x4 FP64 MFMA tiles spread over the
+// waves.  Returns 0 or the failing column + 1 (uniform).
+__device__ int lds_potrf(double* Lp, int k, int* flag) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  for (int p0 = 0; p0 < k; p0 += 16) {
+    const int nb = min(16, k - p0);
+    __syncthreads();
+    if (w == 0) {
+      const int i = l;
+      double r[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) r[j] = (i < nb && j <= i) ? Lp[pk(p0 + i, p0 + j)] : 0.0;
+      int bad = 0;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        if (kk < nb && !bad) {
+          const double d = __shfl(r[kk], kk, 64);
+          if (!(d > 0.0) || !isfinite(d)) {
+            bad = p0 + kk + 1;
+          } else {
+            const double sd = sqrt(d);
+            const double lik = (i > kk) ? r[kk] / sd : (i == kk ? sd : 0.0);
+            r[kk] = lik;
+#pragma unroll
+            for (int j = kk + 1; j < 16; ++j) {
+              const double ljk = __shfl(lik, j, 64);
+              if (j <= i) r[j] = fma(-lik, ljk, r[j]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (i < nb && j <= i) Lp[pk(p0 + i, p0 + j)] = r[j];
+      if (l == 0) *flag = bad;
+    }
+    __syncthreads();
+    const int bad = *flag;
+    if (bad) return bad;
+    for (int r = p0 + nb + t; r < k; r += PT) {   // panel rows below the diagonal block
+      double* lr_ = Lp + pk(r, p0);                   // row r, panel columns (no register arrays)
+#pragma unroll 1
+      for (int j = 0; j < nb; ++j) {
+        const double* lj = Lp + pk(p0 + j, p0);
+        double v = lr_[j];
+#pragma unroll 4
+        for (int m = 0; m < j; ++m) v = fma(-lr_[m], lj[m], v);
+        lr_[j] = v / lj[j];
+      }
+    }
+    __syncthreads();
+    const int q0 = p0 + 16;
+    if (q0 < k) {   // trailing update A22 -= L21 L21' (lower 16x16 tiles)
+      const int nt = (k - q0 + 15) >> 4;
+      const int ntile = nt * (nt + 1) / 2;
+      for (int tile = w; tile < ntile; tile += PW) {
+        int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+        while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+        while (I * (I + 1) / 2 > tile) --I;
+        const int J = tile - I * (I + 1) / 2;
+        const int ri = q0 + 16 * I + (l & 15), cj = q0 + 16 * J + (l & 15);
+        f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int kc = p0 + 4 * s4 + (l >> 4);
+          const double av = ri < k ? Lp[pk(ri, kc)] : 0.0;
+          const double bv = cj < k ? Lp[pk(cj, kc)] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int gr = q0 + 16 * I + (l >> 4) + 4 * rr, gc = q0 + 16 * J + (l & 15);
+          if (gr < k && gc <= gr) Lp[pk(gr, gc)] -= acc[rr];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  return 0;
+}
+
+// y <- L^-1 y (in place, k entries in LDS)
+__device__ void lds_fwd(const double* Lp, int k, double* y) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  for (int p0 = 0; p0 < k; p0 += 16) {
+    const int nb = min(16, k - p0);
+    __syncthreads();
+    if (w == 0) {
+      const int i = l;
+      double v = i < nb ? y[p0 + i] : 0.0;
+      const double dii = i < nb ? Lp[pk(p0 + i, p0 + i)] : 1.0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (j < nb) {
+          const double yj = __shfl(v / dii, j, 64);
+          if (i > j && i < nb) v = fma(-Lp[pk(p0 + i, p0 + j)], yj, v);
+        }
+      }
+      if (i < nb) y[p0 + i] = v / dii;
+    }
+    __syncthreads();
+    for (int r = p0 + nb + t; r < k; r += PT) {
+      double v = y[r];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < nb) v = fma(-Lp[pk(r, p0 + j)], y[p0 + j], v);
+      y[r] = v;
+    }
+  }
+  __syncthreads();
+}
+
+// y <- L^-T y (in place)
+__device__ void lds_bwd(const double* Lp, int k, double* y) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int nblk = (k + 15) >> 4;
+  for (int B = nblk - 1; B >= 0; --B) {
+    const int p0 = 16 * B, nb = min(16, k - p0);
+    __syncthreads();
+    if (w == 0) {
+      const int i = l;
+      double v = i < nb ? y[p0 + i] : 0.0;
+      const double dii = i < nb ? Lp[pk(p0 + i, p0 + i)] : 1.0;
+#pragma unroll
+      for (int j = 15; j >= 0; --j) {
+        if (j < nb) {
+          const double xj = __shfl(v / dii, j, 64);
+          if (i < j) v = fma(-Lp[pk(p0 + j, p0 + i)], xj, v);
+        }
+      }
+      if (i < nb) y[p0 + i] = v / dii;
+    }
+    __syncthreads();
+    for (int c = t; c < p0; c += PT) {
+      double v = y[c];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < nb) v = fma(-Lp[pk(p0 + j, c)], y[p0 + j], v);
+      y[c] = v;
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------
+// solve: factor P_FF + delta I in LDS, Schur complement of the active rows, refinement
+// ---------------------------------------------------------------------------------------
+template <int KS>
+__global__ __launch_bounds__(PT) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
+                                                 int klo) {
+  constexpr int NP = KS * (KS + 1) / 2;
+  __shared__ double Lp[NP];
+  __shared__ double xF[KS], t1[KS], rx[KS];
+  __shared__ double Sm[PG_MGMAX * PG_MGMAX];
+  __shared__ double lamv[PG_MGMAX], wl[PG_MGMAX], rl[PG_MGMAX], dAv[PG_MGMAX];
+  __shared__ int s_al[PG_MGMAX];
+  __shared__ int flag;
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  double* R = rec + (int64_t)b * PGR;
+  if (R[R_STATE] != PQ_PG_PENDING) return;
+  const int k = (int)R[R_K];
+  if (k <= klo || k > KS) return;
+  const int ma = (int)R[R_MA];
+  const int n = pb.n, ld = pb.ld, mg = pb.mg;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
+  PGWork wk(st, b, ld);
+  const double sc = R[R_SC];
+  const double delta = s.delta * sc;
+  const double* K = st.K + (int64_t)b * st.K_stride;   // P_FF (lower), kept for the residuals
+  for (int r = w; r < k; r += PW)
+    for (int c = l; c <= r; c += 64) Lp[pk(r, c)] = K[(int64_t)r * ldk + c] + (r == c ? delta : 0.0);
+  for (int p = t; p < k; p += PT) xF[p] = wk.solx[p];
+  if (t < ma) {
+    s_al[t] = (int)R[R_AL + t];
+    lamv[t] = R[R_SOL + t];
+    dAv[t] = R[R_DA + t];
+  }
+  if (lds_potrf(Lp, k, &flag)) {
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  // U = L^-1 C_aF' (column a -> row a of the global U scratch), S = U'U + delta I
+  for (int a = 0; a < ma; ++a) {
+    const double* cr = Cg + (int64_t)s_al[a] * ld;
+    for (int p = t; p < k; p += PT) t1[p] = cr[wk.Fl[p]];
+    lds_fwd(Lp, k, t1);
+    for (int p = t; p < k; p += PT) wk.U[(int64_t)a * ld + p] = t1[p];
+  }
+  __syncthreads();
+  for (int e = w; e < ma * ma; e += PW) {
+    const int i = e / ma, j = e % ma;
+    if (j > i) continue;
+    const double* ui = wk.U + (int64_t)i * ld;
+    const double* uj = wk.U + (int64_t)j * ld;
+    double sum = 0.0;
+    for (int p = l; p < k; p += 64) sum += ui[p] * uj[p];
+    sum = wave_sum(sum);
+    if (l == 0) Sm[i * PG_MGMAX + j] = sum + (i == j ? delta : 0.0);
+  }
+  __syncthreads();
+  if (t == 0) {   // tiny Cholesky of S (ma <= 32), one thread
+    int bad = 0;
+    for (int c = 0; c < ma && !bad; ++c) {
+      double d = Sm[c * PG_MGMAX + c];
+      for (int m = 0; m < c; ++m) d -= Sm[c * PG_MGMAX + m] * Sm[c * PG_MGMAX + m];
+      if (!(d > 0.0) || !isfinite(d)) { bad = 1; break; }
+      d = sqrt(d);
+      Sm[c * PG_MGMAX + c] = d;
+      for (int r = c + 1; r < ma; ++r) {
+        double v = Sm[r * PG_MGMAX + c];
+        for (int m = 0; m < c; ++m) v -= Sm[r * PG_MGMAX + m] * Sm[c * PG_MGMAX + m];
+        Sm[r * PG_MGMAX + c] = v / d;
+      }
+    }
+    flag = bad;
+  }
+  __syncthreads();
+  if (flag) {
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------
+  for (int itr = 0; itr < s.refine_iters; ++itr) {
+    // rx = rF - P_FF x - C_aF' lam ;  rl = dA - C_aF x
+    for (int p = w; p < k; p += PW) {
+      double sum = 0.0;
+      for (int qq = l; qq < k; qq += 64)
+        sum += (qq <= p ? K[(int64_t)p * ldk + qq] : K[(int64_t)qq * ldk + p]) * xF[qq];
+      sum = wave_sum(sum);
+      if (l == 0) {
+        double v = wk.rF[p] - sum;
+        for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + wk.Fl[p]] * lamv[a];
+        rx[p] = v;
+      }
+    }
+    for (int a = w; a < ma; a += PW) {
+      const double* cr = Cg + (int64_t)s_al[a] * ld;
+      double sum = 0.0;
+      for (int p = l; p < k; p += 64) sum += cr[wk.Fl[p]] * xF[p];
+      sum = wave_sum(sum);
+      if (l == 0) {
+        const double v = dAv[a] - sum;
+        rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dAv[a]) + fabs(sum)) ? 0.0 : v;
+      }
+    }
+    __syncthreads();
+    {
+      double rm = 0.0;
+      for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
+      if (t < ma) rm = fmax(rm, fabs(rl[t]));
+      if (block_max(rm, red) <= 1e-13 * sc) break;
+    }
+    for (int p = t; p < k; p += PT) t1[p] = rx[p];
+    lds_fwd(Lp, k, t1);
+    for (int a = w; a < ma; a += PW) {   // wl = U' t1 - rl
+      const double* ua = wk.U + (int64_t)a * ld;
+      double sum = 0.0;
+      for (int p = l; p < k; p += 64) sum += ua[p] * t1[p];
+      sum = wave_sum(sum);
+      if (l == 0) wl[a] = sum - rl[a];
+    }
+    __syncthreads();
+    if (t == 0) {   // dlam = S^-1 wl
+      for (int i = 0; i < ma; ++i) {
+        double v = wl[i];
+        for (int j = 0; j < i; ++j) v -= Sm[i * PG_MGMAX + j] * wl[j];
+        wl[i] = v / Sm[i * PG_MGMAX + i];
+      }
+      for (int i = ma - 1; i >= 0; --i) {
+        double v = wl[i];
+        for (int j = i + 1; j < ma; ++j) v -= Sm[j * PG_MGMAX + i] * wl[j];
+        wl[i] = v / Sm[i * PG_MGMAX + i];
+      }
+    }
+    __syncthreads();
+    for (int p = t; p < k; p += PT) {
+      double v = t1[p];
+      for (int a = 0; a < ma; ++a) v -= wk.U[(int64_t)a * ld + p] * wl[a];
+      t1[p] = v;
+    }
+    lds_bwd(Lp, k, t1);
+    for (int p = t; p < k; p += PT) xF[p] += t1[p];
+    if (t < ma) lamv[t] += wl[t];
+    __syncthreads();
+  }
+  // ---- expand: xs = x_B off F, x_F on F; general multipliers by row ------------------------
+  for (int i = t; i < n; i += PT) wk.xs[i] = wk.xb[i];
+  __syncthreads();
+  for (int p = t; p < k; p += PT) {
+    wk.xs[wk.Fl[p]] = xF[p];
+    wk.solx[p] = xF[p];
+  }
+  if (t < 64) R[R_LAM + t] = 0.0;
+  __syncthreads();
+  if (t < ma) {
+    R[R_LAM + s_al[t]] = lamv[t];
+    R[R_SOL + t] = lamv[t];
+  }
+  (void)mg;
+}
+
+// ---------------------------------------------------------------------------------------
+// grouped window passes: MODE 0 -> pxb = w_scale Xc'Xc x_B (dates with x_B != 0);
+// MODE 1 -> exact P x, gradient, active-set checks, final scoring of accepted dates
+// ---------------------------------------------------------------------------------------
+constexpr int QT = 512;
+constexpr int QNW = QT / 64;
+constexpr int QG = 16;     // dates per group (MFMA N)
+constexpr int QU = 320;    // union rows per group
+
+__device__ __forceinline__ double hsum32(double v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double hmax32(double v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                pq_settings s, const int32_t* gdates, const int32_t* urows_all,
+                                                const int32_t* ucnt_all, const int32_t* uoff, int umax) {
+  __shared__ __attribute__((aligned(16))) double WU[(QU + 4) * QG];
+  __shared__ int s_urow[QU];
+  __shared__ int g_on[QG], g_T[QG], g_off[QG];
+  __shared__ double g_mux[QG];
+  __shared__ int s_any;
+  const int grp = xcd_slot(blockIdx.x, gridDim.x);
+  const int d0 = gdates[grp];
+  const int G = gdates[grp + 1] - d0;
+  const int U = ucnt_all[grp];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int n = pb.n, ld = pb.ld, mg = pb.mg;
+  if (t < QG) {
+    int on = 0;
+    if (t < G) {
+      const double* R = rec + (int64_t)(d0 + t) * PGR;
+      on = R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || R[R_NZB] != 0.0);
+      g_T[t] = lr.tlen[d0 + t];
+      g_off[t] = uoff[d0 + t];
+    }
+    g_on[t] = on;
+  }
+  for (int u = t; u < QU; u += QT) s_urow[u] = u < U ? urows_all[(int64_t)grp * umax + u] : 0;
+  for (int e = t; e < (QU + 4) * QG; e += QT) WU[e] = 0.0;
+  __syncthreads();
+  if (t == 0) {
+    int any = 0;
+    for (int g = 0; g < G; ++g) any |= g_on[g];
+    s_any = any;
+  }
+  __syncthreads();
+  if (!s_any) return;
+  const int hg = t >> 5, hl = t & 31;
+  const bool hmine = hg < G && g_on[hg];
+  const int hb = d0 + (hg < G ? hg : 0);
+  // mu . v of every participating date (half-wave per date)
+  if (hmine) {
+    PGWork wk(st, hb, ld);
+    const double* v = MODE == 0 ? wk.xb : wk.xs;
+    const double* mu = lr.mu ? lr.mu + (int64_t)hb * lr.mu_stride : nullptr;
+    double a = 0.0;
+    if (mu)
+      for (int i = hl; i < n; i += 32) a = fma(mu[i], v[i], a);
+    a = hsum32(a);
+    if (hl == 0) g_mux[hg] = a;
+  }
+  // ---- pass 1: W (U x 16) = X_union V ---------------------------------------------------
+  const int ntile = (U + 15) >> 4;
+  {
+    const int kq = l >> 4, m = l & 15;
+    const double* Vp = nullptr;
+    if (m < G && g_on[m]) {
+      PGWork wk(st, d0 + m, ld);
+      Vp = MODE == 0 ? wk.xb : wk.xs;
+    }
+    f64x4 c[3];
+    const double* arow[3];
+    bool tv[3], aval[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      c[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+      const int u = (w + QNW * j) * 16 + m;
+      tv[j] = w + QNW * j < ntile;
+      aval[j] = u < U;
+      arow[j] = lr.panel + (int64_t)s_urow[u < QU ? u : 0] * lr.ldp;
+    }
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      const int kk = k0 + 2 * kq;
+      const bool kin = kk + 1 < n;   // n even (host check)
+      const double2 bv = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (tv[j]) {
+          const double2 av = (aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c[j], 0, 0, 0);
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c[j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();   // g_mux visible
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int tile = w + QNW * j;
+      if (tv[j]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int u = tile * 16 + kq + 4 * r;
+          // u_t = X_t . v - mu . v on the date's own window rows, 0 elsewhere
+          const bool inw = m < G && g_on[m] && u >= g_off[m] && u < g_off[m] + g_T[m];
+          if (u < QU) WU[u * QG + m] = inw ? c[j][r] - g_mux[m] : 0.0;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- pass 2: X~ (n x 16) = X_union' Ut -> raw into the date's target vector ----------
+  {
+    const int kq = l >> 4, m = l & 15;
+    const int Uk = (U + 3) & ~3;
+    double* dst = nullptr;
+    if (m < G && g_on[m]) {
+      PGWork wk(st, d0 + m, ld);
+      dst = MODE == 0 ? wk.pxb : wk.g;
+    }
+    for (int p = w; p * 32 < n; p += QNW) {
+      const int col = p * 32 + 2 * m;
+      const bool cin = col < n;
+      f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
+      for (int u0 = 0; u0 < Uk; u0 += 4) {
+        const int u = u0 + kq;
+        const double2 a = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + col)
+                                         : double2{0.0, 0.0};
+        const double bv = WU[u * QG + m];
+        ce = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, bv, ce, 0, 0, 0);
+        co = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, bv, co, 0, 0, 0);
+      }
+      if (dst) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = p * 32 + 2 * (kq + 4 * r);
+          if (i < n) dst[i] = ce[r];
+          if (i + 1 < n) dst[i + 1] = co[r];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (!hmine) return;
+  // ---- per-date post (half-wave) ---------------------------------------------------------
+  const int b = hb;
+  double* R = rec + (int64_t)b * PGR;
+  PGWork wk(st, b, ld);
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  double su = 0.0;
+  for (int u = hl; u < U; u += 32) su += WU[u * QG + hg];
+  su = hsum32(su);
+  const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
+  if (MODE == 0) {
+    for (int i = hl; i < n; i += 32) wk.pxb[i] = wsc * (wk.pxb[i] - (mu ? mu[i] * su : 0.0));
+    return;
+  }
+  const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double* q = pb.q + (int64_t)b * pb.q_stride;
+  const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
+  const double* lg = pb.lg ? pb.lg + (int64_t)b * pb.g_stride : nullptr;
+  const double* ug = pb.ug ? pb.ug + (int64_t)b * pb.g_stride : nullptr;
+  const bool has_box = pb.lb != nullptr;
+  const double* lb = has_box ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
+  const double* ub = has_box ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
+  const double sc = R[R_SC];
+  const double dtol = s.dual_tol * sc;
+  const double ptol = 1e-12;
+  // exact P x and gradient g = P x + q + Cg' lam; box checks
+  int bad = 0;
+  for (int i = hl; i < n; i += 32) {
+    const double xi = wk.xs[i];
+    const double pxi = ps * (wsc * (wk.g[i] - (mu ? mu[i] * su : 0.0))) + pd * xi;
+    double gi = pxi + q[i];
+    for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * R[R_LAM + r];
+    wk.Px[i] = pxi;
+    wk.g[i] = gi;
+    const int f = wk.fl[i];
+    if (f == 0 && has_box) {
+      if (!isinf(lb[i]) && xi < lb[i] - ptol * (1.0 + fabs(lb[i]))) { wk.fl[i] = 1; bad = 1; }
+      else if (!isinf(ub[i]) && xi > ub[i] + ptol * (1.0 + fabs(ub[i]))) { wk.fl[i] = 2; bad = 1; }
+    } else if (f == 1 && lb[i] != ub[i] && -gi > dtol) { wk.fl[i] = 0; bad = 1; }
+    else if (f == 2 && -gi < -dtol) { wk.fl[i] = 0; bad = 1; }
+  }
+  // general rows: Cg x, activity checks (lane 0 decides, as the reference kernel's lane 0)
+  for (int r = 0; r < mg; ++r) {
+    const double* cr = Cg + (int64_t)r * ld;
+    double sum = 0.0;
+    for (int j = hl; j < n; j += 32) sum += cr[j] * wk.xs[j];
+    sum = hsum32(sum);
+    if (hl == 0) {
+      if (lg[r] != ug[r]) {
+        const int a = (int)R[R_ACT + r];
+        const double lam = R[R_LAM + r];
+        if (a == 0 && sum > ug[r] + ptol * (1.0 + fabs(ug[r]))) { R[R_ACT + r] = 2; bad = 1; }
+        else if (a == 0 && sum < lg[r] - ptol * (1.0 + fabs(lg[r]))) { R[R_ACT + r] = 1; bad = 1; }
+        else if (a == 2 && lam < -dtol) { R[R_ACT + r] = 0; bad = 1; }
+        else if (a == 1 && lam > dtol) { R[R_ACT + r] = 0; bad = 1; }
+      } else if (fabs(sum - ug[r]) > 1e-10 * (1.0 + fabs(ug[r]))) {
+        bad = 1;
+      }
+    }
+  }
+  bad = hmax32((double)bad) > 0.5;
+  if (bad) {
+    if (hl == 0 && R[R_ROUNDS] >= s.polish_rounds) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  // ---- accepted: score the polished point (polish_w.hip's final block) ------------------
+  double* sx = st.x + (int64_t)b * ld;
+  double* sz = st.z + (int64_t)b * st.m_ld;
+  double* sy = st.y + (int64_t)b * st.m_ld;
+  double xpx = 0.0, qx = 0.0, pres = 0.0, dres = 0.0, gapb = 0.0;
+  for (int i = hl; i < n; i += 32) {
+    const double xi = wk.xs[i];
+    double zb = 0.0;
+    if (has_box) zb = wk.fl[i] ? -wk.g[i] : 0.0;
+    xpx += xi * wk.Px[i];
+    qx += q[i] * xi;
+    dres = fmax(dres, fabs(wk.g[i] + zb));
+    if (has_box) {
+      if (!isinf(lb[i])) { pres = fmax(pres, lb[i] - xi); gapb += lb[i] * fmin(zb, 0.0); }
+      if (!isinf(ub[i])) { pres = fmax(pres, xi - ub[i]); gapb += ub[i] * fmax(zb, 0.0); }
+      sy[st.mg_pad + i] = zb;
+    }
+    sx[i] = xi;
+  }
+  for (int r = 0; r < mg; ++r) {
+    const double* cr = Cg + (int64_t)r * ld;
+    double sum = 0.0;
+    for (int j = hl; j < n; j += 32) sum += cr[j] * wk.xs[j];
+    sum = hsum32(sum);
+    const double lam = R[R_LAM + r];
+    double v;
+    if (lg[r] == ug[r]) v = fabs(sum - ug[r]);
+    else v = fmax(isinf(ug[r]) ? 0.0 : sum - ug[r], isinf(lg[r]) ? 0.0 : lg[r] - sum);
+    if (hl == 0) {
+      pres = fmax(pres, v);
+      gapb += (lam > 0.0 ? ug[r] : (isinf(lg[r]) ? 0.0 : lg[r])) * lam;
+      sy[r] = lam;
+      sz[r] = sum;
+    }
+  }
+  xpx = hsum32(xpx);
+  qx = hsum32(qx);
+  gapb = hsum32(gapb);
+  pres = hmax32(pres);
+  dres = hmax32(dres);
+  if (hl == 0) {
+    double* o = st.out + (int64_t)b * PQ_OUT_FIELDS;
+    o[PQ_OUT_OBJ] = 0.5 * xpx + qx;
+    o[PQ_OUT_PRIM] = fmax(pres, 0.0);
+    o[PQ_OUT_DUAL] = dres;
+    o[PQ_OUT_GAP] = fabs(xpx + qx + gapb);
+    o[PQ_OUT_RHO] = st.rho[b];
+    o[PQ_OUT_NFREE] = R[R_K];
+    o[PQ_OUT_ROUNDS] = R[R_ROUNDS];
+    st.status[b] = PQ_SOLVED;
+    R[R_STATE] = PQ_PG_DONE;
+  }
+}
+
+}  // namespace pq
+
+extern "C" int pq_polish_grouped_init(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
+                                      const pq_settings* s, void* stream) {
+  PQ_CHECK_ARG(lr && pb && st && s && rec, "pq_polish_grouped_init: null argument");
+  PQ_CHECK_ARG(lr->dg && lr->panel && lr->rows && lr->tlen, "pq_polish_grouped_init: window (with dg) missing");
+  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::PG_MGMAX && (pb->mg == 0 || (pb->Cg && pb->lg && pb->ug)),
+               "pq_polish_grouped_init: needs 0 <= mg <= %d general rows", pq::PG_MGMAX);
+  PQ_CHECK_ARG(st->work && st->work_stride >= PQ_WORK_DOUBLES(pb->ld, st->mg_pad),
+               "pq_polish_grouped_init: work buffer too small");
+  if (pb->batch <= 0) return 0;
+  hipLaunchKernelGGL(pq::k_pg_init, dim3(pb->batch), dim3(pq::PT), 0, (hipStream_t)stream, *lr, *pb, *st, rec, *s);
+  PQ_CHECK_LAUNCH("pq_polish_grouped_init");
+  return 0;
+}
+
+extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
+                                       int32_t ldk, const int32_t* gdates, int32_t ngroups, const int32_t* urows,
+                                       const int32_t* ucnt, const int32_t* uoff, int32_t umax, const pq_settings* s,
+                                       void* stream) {
+  PQ_CHECK_ARG(lr && pb && st && s && rec, "pq_polish_grouped_round: null argument");
+  PQ_CHECK_ARG(gdates && urows && ucnt && uoff && umax > 0 && umax <= pq::QU,
+               "pq_polish_grouped_round: group plan missing (umax <= %d)", pq::QU);
+  PQ_CHECK_ARG(pb->n % 2 == 0 && lr->ldp % 2 == 0, "pq_polish_grouped_round: needs even n and panel stride");
+  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::PG_MGMAX, "pq_polish_grouped_round: mg <= %d", pq::PG_MGMAX);
+  PQ_CHECK_ARG(st->K && ldk >= 64 && st->K_stride >= (int64_t)ldk * ldk,
+               "pq_polish_grouped_round: K scratch (ldk x ldk per problem) too small");
+  if (pb->batch <= 0 || ngroups <= 0) return 0;
+  hipStream_t str = (hipStream_t)stream;
+  const int B = pb->batch;
+  const int kmax = ldk < pq::PG_KMAX ? ldk : pq::PG_KMAX;
+  hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax);
+  hipLaunchKernelGGL(pq::k_pg_pass<0>, dim3(ngroups), dim3(pq::QT), 0, str, *lr, *pb, *st, rec, *s, gdates, urows,
+                     ucnt, uoff, umax);
+  hipLaunchKernelGGL(pq::k_pg_form<1>, dim3(B), dim3(pq::PT), 0, str, *lr, *pb, *st, rec, ldk);
+  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_form<2>, dim3(B), dim3(pq::PT), 0, str, *lr, *pb, *st, rec, ldk);
+  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 0);
+  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 64);
+  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 96);
+  hipLaunchKernelGGL(pq::k_pg_pass<1>, dim3(ngroups), dim3(pq::QT), 0, str, *lr, *pb, *st, rec, *s, gdates, urows,
+                     ucnt, uoff, umax);
+  PQ_CHECK_LAUNCH("pq_polish_grouped_round");
+  return 0;
+}

@@ -255,6 +255,12 @@ class Workspace:
         self.work_stride = _lib.work_doubles(ld, qb.mg_pad)
         self.work = torch.zeros((B, self.work_stride), dtype=F64, device=dev)
 
+    def pg_record(self):
+        """Per-problem record of the grouped polish pipeline (PQ_PG_RECORD doubles each)."""
+        if getattr(self, "_pg_rec", None) is None:
+            self._pg_rec = torch.zeros((self.B, _lib.PQ_PG_RECORD), dtype=F64, device=self.device)
+        return self._pg_rec
+
     def lr_buffers(self, k_ld: int):
         """Capacitance matrices M, their inverses and factor scratch (low-rank path)."""
         if self._lr is None or self._lr["k_ld"] != k_ld:
@@ -502,7 +508,7 @@ def _band_setup(qb: QPBatch, lr: LowRank, strm):
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
-                  fuse: bool = True) -> BatchResult:
+                  fuse: bool = True, grouped_polish: bool = True) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -586,11 +592,11 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             cnt["refactors"] += kk
         SS = SS0
 
-    def polish_w(idx, nidx, SSp=None):
+    def polish_w(idx, nidx, SSp=None, name="polish"):
         SS = SSp if SSp is not None else SS_main
         kmax = min(qb.ld, 1024)
         final = ldk >= kmax
-        _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, S_, _ptr(idx), nidx, SS, ldk, int(final),
+        _lib.check(tl(name, lambda: lib.pq_polish_w_batched(L_, P_, S_, _ptr(idx), nidx, SS, ldk, int(final),
                                                                 strm)), "pq_polish_w_batched")
         if not final:   # free sets larger than the compact scratch: relaunch those with ldk = kmax
             over = torch.nonzero(ws.out[:, _lib.PQ_OUT_ROUNDS] < 0).flatten().to(torch.int32)
@@ -602,14 +608,35 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                 st2.K, st2.K_stride = K2.data_ptr(), K2.stride(0)
                 st2.Dt, st2.Dt_stride = D2.data_ptr(), D2.stride(0)
                 over = over.contiguous()
-                _lib.check(tl("polish", lambda: lib.pq_polish_w_batched(L_, P_, ctypes.byref(st2), _ptr(over), m,
+                _lib.check(tl(name, lambda: lib.pq_polish_w_batched(L_, P_, ctypes.byref(st2), _ptr(over), m,
                                                                         SS, kmax, 1, strm)),
                            "pq_polish_w_batched (relaunch)")
+
+    def polish_grouped():
+        """Grouped polish pipeline (polish_g.hip) for every date; the dates it hands back
+        (FALLBACK) go through pq_polish_w_batched from their ADMM point."""
+        rec = ws.pg_record()
+        rp = rec.data_ptr()
+        g = groups
+        _lib.check(lib.pq_polish_grouped_init(L_, P_, S_, rp, SS_main, strm), "pq_polish_grouped_init")
+        for r in range(int(s.polish_rounds)):
+            _lib.check(lib.pq_polish_grouped_round(L_, P_, S_, rp, ldk, _ptr(g.gdates), g.ngroups, _ptr(g.urows),
+                                                   _ptr(g.ucnt), _ptr(g.uoff), g.umax, SS_main, strm),
+                       "pq_polish_grouped_round")
+            if r >= 1 and not bool((rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_PENDING).any()):   # host sync
+                break
+        fb = torch.nonzero(rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_FALLBACK).flatten().to(torch.int32)
+        m = int(fb.numel())
+        if m:
+            polish_w(fb.contiguous(), m, name="polish (fallback, inside polish)")
 
     admm_rounds(None, 0, SS)
     SS_main = SS
     if s.polish and polish:
-        polish_w(None, 0)
+        if grouped and grouped_polish and ldk >= 64:
+            tl("polish", polish_grouped)
+        else:
+            polish_w(None, 0)
         rp = _repolish_set(ws, settings or Settings())
         if rp is not None:      # polish rejected: polish again with more refinement steps
             pidx, pn, s3 = rp

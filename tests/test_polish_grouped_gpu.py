@@ -1,0 +1,102 @@
+"""The grouped polish pipeline (polish_g.hip: per-round setup / form / LDS solve kernels and
+MFMA window passes over each slide group's union rows) against the per-date window polish
+it restructures (polish_w.hip, pq_polish_w_batched): same ADMM point in, the same polished
+weights, statuses, objective and multipliers out (to rounding), on the shapes the
+backtests use -- long-only min-variance at n = 1000 (bench), capped boxes (fixed weights at
+an upper bound: the P x_B pass), sector caps (active general rows), uncentred least
+squares, and a free set beyond the LDS solve (handed to the per-date kernel)."""
+import numpy as np
+import pytest
+import torch
+
+from porqua_amd import _lib, engine
+from porqua_amd.synthetic import factor_panel
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(device, n, T, D, ub, ngroups_rows=0, cap=0.3, centred=True, stride=1, seed=None):
+    ends = list(range(T + 5, T + 5 + D * stride, stride))
+    dates, R, y, sec = factor_panel(max(ends) + 1, n, **({} if seed is None else {"seed": seed}))
+    rows, tlen = engine.window_rows(dates, dates[ends], T)
+    pan = engine.Panel(R, y, device=device)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    G = h = None
+    if ngroups_rows:
+        G = np.stack([(sec == g).astype(float) for g in range(ngroups_rows)])
+        h = np.full(ngroups_rows, cap)
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+                                   G=G, h=h, lb=np.zeros(n), ub=np.full(n, ub), device=device)
+    qb.batch = D
+    qb.P = None
+    qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=device)
+    if centred:
+        mu = pan.window_means(r_d, t_d)
+        qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=device)
+        lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+    else:
+        xty, _ = pan.gram_xy(r_d, t_d)
+        qb.q = (-2.0 * xty).contiguous()
+        lr = engine.LowRank(pan, r_d, t_d, mu=None)
+    gp = engine.GroupPlan(rows, tlen, device)
+    return qb, lr, gp
+
+
+def _solve(qb, lr, gp, grouped_polish, settings=None):
+    ws = engine.Workspace(qb, dense=False)
+    assert engine.grouped_applicable(qb, lr, gp, ws)
+    res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, grouped_polish=grouped_polish)
+    torch.cuda.synchronize()
+    rec = ws.pg_record()[:, _lib.PQ_PG_STATE].cpu().numpy().copy() if grouped_polish else None
+    return (res.x.cpu().numpy().copy(), res.status.cpu().numpy().copy(), res.obj.cpu().numpy().copy(),
+            res.y.cpu().numpy().copy(), res.z_box.cpu().numpy().copy(), res.out.cpu().numpy().copy(), rec)
+
+
+@pytest.mark.parametrize("case", ["bench", "capped", "sectors", "lsq", "small_T"])
+def test_grouped_polish_matches_per_date_polish(device, case):
+    if case == "bench":
+        qb, lr, gp = _problem(device, 1000, 252, 48, 1.0)
+        settings = None
+    elif case == "capped":
+        qb, lr, gp = _problem(device, 400, 120, 40, 0.05)
+        settings = None
+    elif case == "sectors":
+        qb, lr, gp = _problem(device, 600, 150, 36, 0.2, ngroups_rows=5, cap=0.25, stride=2)
+        settings = None
+    elif case == "lsq":
+        qb, lr, gp = _problem(device, 500, 120, 30, 0.1, centred=False)
+        settings = engine.Settings(rho0_rel=0.5)
+    else:
+        qb, lr, gp = _problem(device, 300, 60, 40, 1.0)
+        settings = None
+    xa, sa, oa, ya, za, outa, _ = _solve(qb, lr, gp, False, settings)
+    xb, sb, ob, yb, zb, outb, rec = _solve(qb, lr, gp, True, settings)
+    assert np.array_equal(sa, sb), (sa, sb)
+    assert np.all(sb == _lib.PQ_SOLVED)
+    # most dates go through the pipeline (the rest fall back to the per-date kernel); the
+    # tracking problem's free sets exceed the LDS solve (k > 128), so it all falls back
+    if case != "lsq":
+        assert (rec == _lib.PQ_PG_DONE).mean() >= 0.8, np.unique(rec, return_counts=True)
+    assert np.all((rec == _lib.PQ_PG_DONE) | (rec == _lib.PQ_PG_FALLBACK))
+    assert np.abs(xa - xb).max() <= 1e-10, np.abs(xa - xb).max()
+    assert np.abs(oa - ob).max() <= 1e-12 * max(1.0, np.abs(oa).max()) + 1e-15
+    sc = max(np.abs(ya).max(), np.abs(za).max(), 1e-30)
+    assert np.abs(ya - yb).max() <= 1e-8 * sc and np.abs(za - zb).max() <= 1e-8 * sc
+    # the same free sets and rounds as the per-date kernel
+    assert np.array_equal(outa[:, _lib.PQ_OUT_NFREE], outb[:, _lib.PQ_OUT_NFREE])
+    assert np.abs(outa[:, _lib.PQ_OUT_PRIM] - outb[:, _lib.PQ_OUT_PRIM]).max() <= 1e-12
+
+
+def test_grouped_polish_hands_large_free_sets_to_the_per_date_kernel(device):
+    """Free sets beyond the LDS solve (k > 128: the tracking problem holds most assets
+    strictly inside the box) are FALLBACK problems and still end SOLVED with the per-date
+    kernel's answer."""
+    qb, lr, gp = _problem(device, 500, 120, 30, 0.1, centred=False)
+    st_ = engine.Settings(rho0_rel=0.5)
+    xa, sa, oa, *_ = _solve(qb, lr, gp, False, st_)
+    xb, sb, ob, _, _, outb, rec = _solve(qb, lr, gp, True, st_)
+    assert np.array_equal(sa, sb)
+    assert np.abs(xa - xb).max() <= 1e-10
+    big = outb[:, _lib.PQ_OUT_NFREE] > 128
+    assert big.any()
+    assert np.all(rec[big] == _lib.PQ_PG_FALLBACK)
