@@ -226,6 +226,41 @@ int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
                        const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
                        int32_t r0, const double* cc, void* stream);
 
+/* Group capacitance (admm_gcap.hip): the dates of each slide group (same T, same
+ * c = p_scale w_scale, same p_diag, one shared rho grho[g]) share ONE capacitance matrix of
+ * the union of their windows, M_U = I + W_U W_U' / d with W_U = [sqrt(c) X_U; sqrt(R) Cg]
+ * (raw union rows; (U + mg) x (U + mg), general rows after the U union rows, identity
+ * padding to k_ld), and each date applies its own K_b^-1 through a rank-(U - T + 1)
+ * Woodbury correction (the union rows outside its window and its mean):
+ *   pq_gcap_assemble   M_U per group from the band Gram (W >= the widest union span), pc, cc;
+ *   (pq_factor_batched on {n = k, ld = k_ld, P = M, batch = ngroups}, invert = 2 -> Minv)
+ *   pq_gcap_prepare    per date a_b = W_U mu_b, q_b = M_U^-1 a_b (aq: a | q, 2 k_ld each)
+ *                      and H_b^-1 (ldh x ldh, ldh >= U - T + 1 <= 64);
+ *   pq_admm_lr_gcap    the fused grouped ADMM (pq_admm_lr_grouped with pc / cc) with the
+ *                      per-date M_b^-1 symv replaced by one MFMA GEMM with M_U^-1 per
+ *                      group plus the small per-date correction.  Adaptive rho is decided
+ *                      per group (NEED_REFACTOR for all its running dates, grho updated).
+ * Centred windows (lr->mu != NULL), shared general rows (mg <= 4), uniform ADMM diagonal.
+ * Replaces qpsolvers.solve_problem (src/qp_problems.py:211-214) for the batched backtest. */
+typedef struct pq_gcap {
+  const int32_t* gdates; int32_t ngroups;
+  const int32_t* urows; const int32_t* ucnt; const int32_t* uoff; int32_t umax;
+  const int32_t* gidx;          /* group of each date                                    */
+  double* grho;                 /* rho of each group                                     */
+  double* M; double* Minv; int32_t k_ld; int64_t M_stride;    /* per group                */
+  double* aq; int64_t aq_stride;                               /* per date: a | q          */
+  double* hinv; int32_t ldh;                                   /* per date: ldh x ldh      */
+} pq_gcap;
+int pq_gcap_assemble(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap* gc, const pq_settings* s,
+                     const double* band, int64_t ldo, int32_t r0, const double* pc, int64_t ldpc,
+                     const double* cc, void* stream);
+int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
+                    const pq_settings* s, const int32_t* idx, int32_t nidx, const double* band, int64_t ldo,
+                    int32_t r0, const double* pc, int64_t ldpc, void* stream);
+int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
+                    const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc, int32_t r0,
+                    const double* cc, void* stream);
+
 /* K4: active-set polish of the ADMM point (reduced KKT by masked Cholesky + Schur +
  * proximal iterative refinement), then exact residuals / objective of the final point
  * into out[] (Solution.obj / primal_residual / dual_residual / duality_gap).            */

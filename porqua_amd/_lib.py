@@ -91,6 +91,17 @@ class PQLowRank(ctypes.Structure):
     ]
 
 
+class PQGcap(ctypes.Structure):
+    _fields_ = [
+        ("gdates", c_dp), ("ngroups", c_int32),
+        ("urows", c_dp), ("ucnt", c_dp), ("uoff", c_dp), ("umax", c_int32),
+        ("gidx", c_dp), ("grho", c_dp),
+        ("M", c_dp), ("Minv", c_dp), ("k_ld", c_int32), ("M_stride", c_int64),
+        ("aq", c_dp), ("aq_stride", c_int64),
+        ("hinv", c_dp), ("ldh", c_int32),
+    ]
+
+
 _EXPORTS = {
     "pq_version": ([], c_int32),
     "pq_last_error": ([], ctypes.c_char_p),
@@ -136,6 +147,14 @@ _EXPORTS = {
     "pq_polish_grouped_round": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                                  c_dp, c_int32, c_dp, c_int32, c_dp, c_dp, c_dp, c_int32,
                                  ctypes.POINTER(PQSettings), c_dp], c_int32),
+    "pq_gcap_assemble": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQGcap),
+                          ctypes.POINTER(PQSettings), c_dp, c_int64, c_int32, c_dp, c_int64, c_dp, c_dp], c_int32),
+    "pq_gcap_prepare": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                         ctypes.POINTER(PQGcap), ctypes.POINTER(PQSettings), c_dp, c_int32, c_dp, c_int64, c_int32,
+                         c_dp, c_int64, c_dp], c_int32),
+    "pq_admm_lr_gcap": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                         ctypes.POINTER(PQGcap), ctypes.POINTER(PQSettings), c_int32, c_dp, c_int64, c_int32, c_dp,
+                         c_dp], c_int32),
     "pq_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_int64),
     "pq_simulate_periods": ([c_dp, c_int64, c_int32, c_dp, c_int64, c_dp, c_dp, c_int32, c_dp, c_dp,
                              ctypes.c_double, ctypes.c_double, c_dp, c_dp, c_int64, c_dp, c_int32, c_dp], c_int32),

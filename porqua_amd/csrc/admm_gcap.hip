@@ -1,0 +1,794 @@
+// K2 + K3 with ONE capacitance matrix per slide group ("group capacitance").
+//
+// The grouped ADMM of admm_grp.hip applies every date's own k x k capacitance inverse
+// M_b^-1 (k = T + mg) each iteration: 4749 factorisations per config-3 backtest, and a
+// 512 KB per-date stream that dominates the kernel's HBM traffic.  Neighbouring windows
+// share all but a few rows, so here the dates of a group (same T, same c = p_scale w_scale,
+// same p_diag, one rho) share the capacitance of the UNION of their windows,
+//     K_U = d I + W_U' W_U,   W_U = [sqrt(c) X_U ; sqrt(R) Cg]   (raw union rows),
+//     M_U = I + W_U W_U' / d   ((U + mg) x (U + mg): one factorisation per group),
+// and each date's own system differs from K_U by a low-rank term:
+//     K_b = K_U - V_b V_b',   V_b = sqrt(c) [X_Cb' , sqrt(T) mu_b]
+// (C_b = the union rows outside the date's window, m = U - T of them; the mean column is
+// the centring).  Woodbury on that difference needs only the small SPD matrix
+//     H_b = I - V_b' K_U^-1 V_b = [[ (M_U^-1)_CC , -(sqrt(cT)/d) q_C ],
+//                                  [ .           , 1 - (cT/d)(mu'mu - a'q/d) ]]
+// with a_b = W_U mu_b and q_b = M_U^-1 a_b, so per date the preparation is O(U T + U^2 +
+// m^3) (pq_gcap_prepare).  Per ADMM iteration the group does
+//     z' = M_U^-1 [sqrt(c) X_U V ; sqrt(R) Cg V]                (one MFMA GEMM, G columns)
+//     s_b = [z'_C ; sqrt(cT)(mu_b.V - a_b.z'/d)],  y_b = H_b^-1 s_b
+//     Ut_b = sqrt(c) (z' - (M_U^-1)_{:,C} y_C + (sqrt(cT)/d) y_mu q_b)_X,
+//     cw_b = sqrt(R) (same)_G,  su_b = sqrt(cT) y_mu,
+// after which pass 2 and the fused per-date updates of admm_grp.hip run unchanged
+// (x~ = V - D^-1 (X_U' Ut - su mu + Cg' cw)).  Exact algebra: the iterates are those of
+// the per-date kernel with the group's rho, to rounding (checked against a dense solve in
+// tests).  Adaptive rho is decided per group (geometric mean of the dates' requests), so
+// a refactorisation rebuilds one M_U per group.
+//
+// Replaces qpsolvers.solve_problem (src/qp_problems.py:211-214) for the batched backtest,
+// like pq_admm_lr_grouped.
+#include "common.h"
+#include "capi_util.h"
+
+namespace pq {
+
+constexpr int CT = 512;        // threads per group workgroup
+constexpr int CNW = CT / 64;
+constexpr int CG_MAX = 16;     // dates per group (MFMA N)
+constexpr int CU_MAX = 320;    // union rows per group
+constexpr int CMG = 4;         // general rows (register-resident, fused form)
+constexpr int CK_MAX = CU_MAX + CMG;   // capacitance rows
+constexpr int CH_MAX = 64;     // m + 1 = U - T + 1 <= 64
+
+__device__ __forceinline__ double crho(double l, double u, double rho, const pq_settings& s) {
+  if (l == u) return rho * s.eq_scale;
+  if (isinf(l) && isinf(u)) return s.rho_min;
+  return rho;
+}
+__device__ __forceinline__ double csum32(double v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double cmax32(double v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// uniform ADMM diagonal d and the group constants of date b (rho = the group's)
+struct GConst {
+  double c, sqc, d, rho;
+};
+__device__ __forceinline__ GConst gconst(const pq_lowrank& lr, const pq_problem& pb, const pq_settings& s, int b,
+                                         double rho) {
+  GConst g;
+  g.c = (pb.p_scale ? pb.p_scale[b] : 1.0) * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  g.sqc = sqrt(fmax(g.c, 0.0));
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double rb = pb.lb ? crho(pb.lb[(int64_t)b * pb.box_stride], pb.ub[(int64_t)b * pb.box_stride], rho, s) : 0.0;
+  g.d = s.sigma + pd + rb;
+  g.rho = rho;
+  return g;
+}
+
+// G_U[u][v] = x_u . x_v from the row band (rows relative to r0)
+__device__ __forceinline__ double band_at(const double* band, int64_t ldo, int ru, int rv) {
+  if (ru < rv) { const int z = ru; ru = rv; rv = z; }
+  return band[(int64_t)ru * ldo + (ru - rv)];
+}
+
+// ---- assemble M_U (lower 64-tiles, diagonal tiles in full; identity padding) -----------
+__global__ __launch_bounds__(256) void k_gcap_assemble(pq_lowrank lr, pq_problem pb, pq_gcap gc, pq_settings s,
+                                                       const double* band, int64_t ldo, int r0, const double* pc,
+                                                       int64_t ldpc, const double* cc) {
+  __shared__ int s_w[CU_MAX];
+  __shared__ double s_sr[CMG];
+  const int grp = blockIdx.x;
+  const int d0 = gc.gdates[grp];
+  const int U = gc.ucnt[grp], mg = pb.mg, k_ld = gc.k_ld;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  for (int u = t; u < U; u += 256) s_w[u] = gc.urows[(int64_t)grp * gc.umax + u] - r0;
+  const GConst g = gconst(lr, pb, s, d0, gc.grho[grp]);
+  if (t < mg) s_sr[t] = sqrt(crho(pb.lg[t], pb.ug[t], g.rho, s));
+  __syncthreads();
+  const double a1 = g.c / g.d, a2 = g.sqc / g.d;
+  double* M = gc.M + (int64_t)grp * gc.M_stride;
+  for (int i = w; i < k_ld; i += 4) {
+    const int jend = (i / TB + 1) * TB;
+    const bool icg = i >= U && i < U + mg;
+    for (int j = l; j < jend; j += 64) {
+      double v = (i == j) ? 1.0 : 0.0;
+      const bool jcg = j >= U && j < U + mg;
+      if (i < U && j < U) v += a1 * band_at(band, ldo, s_w[i], s_w[j]);
+      else if (icg && j < U) v += a2 * s_sr[i - U] * pc[(int64_t)s_w[j] * ldpc + (i - U)];
+      else if (i < U && jcg) v += a2 * s_sr[j - U] * pc[(int64_t)s_w[i] * ldpc + (j - U)];
+      else if (icg && jcg) v += s_sr[i - U] * s_sr[j - U] / g.d * cc[(i - U) * mg + (j - U)];
+      M[(int64_t)i * k_ld + j] = v;
+    }
+  }
+}
+
+// ---- per-date preparation: a_b, q_b = M_U^-1 a_b, H_b^-1 ---------------------------------
+__global__ __launch_bounds__(256) void k_gcap_prep(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
+                                                   pq_settings s, const int32_t* idx, const double* band,
+                                                   int64_t ldo, int r0, const double* pc, int64_t ldpc) {
+  __shared__ int s_w[CU_MAX];
+  __shared__ double s_a[CK_MAX], s_q[CK_MAX];
+  __shared__ double H[CH_MAX * (CH_MAX + 1)];
+  __shared__ double red[16];
+  __shared__ int s_bad;
+  const int slot = xcd_slot(blockIdx.x, gridDim.x);
+  const int b = idx ? idx[slot] : slot;
+  const int grp = gc.gidx[b];
+  const int U = gc.ucnt[grp], mg = pb.mg, n = pb.n;
+  const int T = lr.tlen[b], off = gc.uoff[b];
+  const int m = U - T, kU = U + mg, k_ld = gc.k_ld;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  constexpr int HP = CH_MAX + 1;
+  for (int u = t; u < U; u += 256) s_w[u] = gc.urows[(int64_t)grp * gc.umax + u] - r0;
+  __syncthreads();
+  const GConst g = gconst(lr, pb, s, b, gc.grho[grp]);
+  // a = [sqrt(c) X_U mu ; sqrt(R) Cg mu],  X_U mu = (1/T) G_U[:, window] 1
+  for (int u = w; u < U; u += 4) {
+    double sum = 0.0;
+    for (int tt = l; tt < T; tt += 64) sum += band_at(band, ldo, s_w[u], s_w[off + tt]);
+    sum = wave_sum(sum);
+    if (l == 0) s_a[u] = g.sqc * sum / T;
+  }
+  for (int r = w; r < mg; r += 4) {
+    double sum = 0.0;
+    for (int tt = l; tt < T; tt += 64) sum += pc[(int64_t)s_w[off + tt] * ldpc + r];
+    sum = wave_sum(sum);
+    if (l == 0) s_a[U + r] = sqrt(crho(pb.lg[r], pb.ug[r], g.rho, s)) * sum / T;
+  }
+  double mm = 0.0;
+  const double* mu = lr.mu + (int64_t)b * lr.mu_stride;
+  for (int i = t; i < n; i += 256) mm = fma(mu[i], mu[i], mm);
+  mm = block_sum(mm, red);   // (barrier: s_a complete)
+  const double* Mi = gc.Minv + (int64_t)grp * gc.M_stride;   // full symmetric M_U^-1
+  for (int u = w; u < kU; u += 4) {
+    double sum = 0.0;
+    for (int v = l; v < kU; v += 64) sum += Mi[(int64_t)u * k_ld + v] * s_a[v];
+    sum = wave_sum(sum);
+    if (l == 0) s_q[u] = sum;
+  }
+  __syncthreads();
+  double aq = 0.0;
+  for (int u = t; u < kU; u += 256) aq += s_a[u] * s_q[u];
+  aq = block_sum(aq, red);
+  double* A = gc.aq + (int64_t)b * gc.aq_stride;
+  for (int u = t; u < k_ld; u += 256) {
+    A[u] = u < kU ? s_a[u] : 0.0;
+    A[k_ld + u] = u < kU ? s_q[u] : 0.0;
+  }
+  // H (m + 1) x (m + 1): C = union rows outside [off, off + T)
+  const int mh = m + 1;
+  const double sct = sqrt(g.c * T);
+  for (int e = t; e < mh * mh; e += 256) {
+    const int i = e / mh, j = e % mh;
+    double v;
+    if (i < m && j < m) {
+      const int ci = i < off ? i : i + T, cj = j < off ? j : j + T;
+      v = Mi[(int64_t)ci * k_ld + cj];
+    } else if (i < m) {
+      const int ci = i < off ? i : i + T;
+      v = -(sct / g.d) * s_q[ci];
+    } else if (j < m) {
+      const int cj = j < off ? j : j + T;
+      v = -(sct / g.d) * s_q[cj];
+    } else {
+      v = 1.0 - (g.c * T / g.d) * (mm - aq / g.d);
+    }
+    H[i * HP + j] = v;
+  }
+  __syncthreads();
+  // Cholesky of H (LDS, one column per step), then H^-1 = L^-T L^-1 column by column
+  for (int k = 0; k < mh; ++k) {
+    const double dk = H[k * HP + k];
+    __syncthreads();
+    if (t == 0) s_bad = !(dk > 0.0) || !isfinite(dk);
+    __syncthreads();
+    if (s_bad) break;
+    const double sd = sqrt(dk);
+    if (t > k && t < mh) H[t * HP + k] /= sd;
+    __syncthreads();
+    if (t == 0) H[k * HP + k] = sd;
+    const int rem = mh - 1 - k;
+    for (int e = t; e < rem * rem; e += 256) {
+      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
+      if (j <= i) H[i * HP + j] -= H[i * HP + k] * H[j * HP + k];
+    }
+    __syncthreads();
+  }
+  double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
+  if (s_bad) {   // not SPD to rounding: the date cannot use the group form
+    if (t == 0) st.status[b] = PQ_NON_CONVEX;
+    return;
+  }
+  if (t < mh) {   // column t of H^-1: solve L L' x = e_t (forward then backward, one thread)
+    double x[CH_MAX];
+    for (int i = 0; i < mh; ++i) {
+      double v = (i == t) ? 1.0 : 0.0;
+      for (int j = 0; j < i; ++j) v -= H[i * HP + j] * x[j];
+      x[i] = v / H[i * HP + i];
+    }
+    for (int i = mh - 1; i >= 0; --i) {
+      double v = x[i];
+      for (int j = i + 1; j < mh; ++j) v -= H[j * HP + i] * x[j];
+      x[i] = v / H[i * HP + i];
+    }
+    for (int i = 0; i < gc.ldh; ++i) Hi[(int64_t)i * gc.ldh + t] = i < mh ? x[i] : 0.0;
+  }
+}
+
+// ---- the ADMM iterations -------------------------------------------------------------------
+__global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
+                                                  pq_settings s, int iters_call, const double* pc, int64_t ldpc,
+                                                  int r0, const double* cc) {
+  constexpr int MGG = 8;
+  __shared__ __attribute__((aligned(16))) double WU[(CU_MAX + 4) * CG_MAX];
+  double* const UT = WU;
+  __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX];
+  __shared__ double g_y[CG_MAX * CH_MAX];   // y_b = H_b^-1 s_b of every date
+  __shared__ double g_zg[CG_MAX * MGG], g_yg[CG_MAX * MGG], g_rg[CG_MAX * MGG], g_lg[CG_MAX * MGG],
+      g_ug[CG_MAX * MGG], g_cgv[CG_MAX * MGG], g_cgx[CG_MAX * MGG], g_wg[CG_MAX * MGG],
+      g_cw[CG_MAX * MGG], g_zt[CG_MAX * MGG], g_rgz[CG_MAX * MGG], g_cmu[CG_MAX * MGG];
+  __shared__ int g_act[CG_MAX], g_it[CG_MAX], g_end[CG_MAX], g_stat[CG_MAX], g_off[CG_MAX], g_T[CG_MAX];
+  __shared__ int s_urow[CU_MAX];
+  __shared__ double s_sr[CMG];
+  __shared__ double s_rho;
+  __shared__ int s_any;
+
+  const int grp = xcd_slot(blockIdx.x, gridDim.x);
+  const int d0 = gc.gdates[grp];
+  const int G = gc.gdates[grp + 1] - d0;
+  const int U = gc.ucnt[grp];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int n = pb.n, ld = pb.ld, mg = pb.mg, k_ld = gc.k_ld;
+  const int kU = U + mg;
+  const bool has_box = pb.lb != nullptr;
+  const double sigma = s.sigma, alpha = s.alpha;
+  const double* Mi = gc.Minv + (int64_t)grp * gc.M_stride;
+
+  // ---- setup -------------------------------------------------------------------------------
+  for (int u = t; u < CU_MAX; u += CT) s_urow[u] = u < U ? gc.urows[(int64_t)grp * gc.umax + u] : 0;
+  for (int e = t; e < (CU_MAX + 4) * CG_MAX; e += CT) UT[e] = 0.0;
+  if (t == 0) s_rho = gc.grho[grp];
+  __syncthreads();
+  const double rho = s_rho;
+  const GConst gk = gconst(lr, pb, s, d0, rho);
+  if (t < mg) s_sr[t] = sqrt(crho(pb.lg[t], pb.ug[t], rho, s));
+  if (t < CG_MAX) {
+    const int g = t;
+    int act = 0;
+    if (g < G) {
+      const int b = d0 + g;
+      const int stt = st.status[b];
+      act = (stt == PQ_UNSOLVED || stt == PQ_NEED_REFACTOR);
+      g_it[g] = st.iters[b];
+      g_end[g] = min(s.max_iter, st.iters[b] + iters_call);
+      g_stat[g] = stt;
+      g_T[g] = lr.tlen[b];
+      g_off[g] = gc.uoff[b];
+      g_dinv[g] = 1.0 / gk.d;
+    }
+    g_act[g] = act;
+  }
+  for (int e = t; e < CG_MAX * MGG; e += CT) {
+    const int g = e / MGG, r = e % MGG;
+    double zg = 0, yg = 0, lgv = 0, ugv = 0, rg = 0;
+    if (g < G && r < mg) {
+      const int b = d0 + g;
+      zg = st.z[(int64_t)b * st.m_ld + r];
+      yg = st.y[(int64_t)b * st.m_ld + r];
+      lgv = pb.lg[r];
+      ugv = pb.ug[r];
+      rg = crho(lgv, ugv, rho, s);
+    }
+    g_zg[e] = zg;
+    g_yg[e] = yg;
+    g_lg[e] = lgv;
+    g_ug[e] = ugv;
+    g_rg[e] = rg;
+  }
+  __syncthreads();
+
+  const int hg = t >> 5, hl = t & 31;
+  const bool hmine = hg < G;
+  const int hb = d0 + (hmine ? hg : 0);
+#define GC_HPTRS                                                                              \
+  const double* __restrict__ q_h = pb.q + (int64_t)hb * pb.q_stride;                          \
+  const double* __restrict__ lo_h = has_box ? pb.lb + (int64_t)hb * pb.box_stride : nullptr;  \
+  const double* __restrict__ up_h = has_box ? pb.ub + (int64_t)hb * pb.box_stride : nullptr;  \
+  const double* __restrict__ Cg_h = mg ? pb.Cg : nullptr;                                     \
+  const double* __restrict__ mu_h = lr.mu + (int64_t)hb * lr.mu_stride;                       \
+  double* __restrict__ x_h = st.x + (int64_t)hb * ld;                                         \
+  double* __restrict__ Px_h = st.Px + (int64_t)hb * ld;                                       \
+  double* __restrict__ zb_h = st.z + (int64_t)hb * st.m_ld + st.mg_pad;                       \
+  double* __restrict__ yb_h = st.y + (int64_t)hb * st.m_ld + st.mg_pad;                       \
+  double* __restrict__ R_h = st.work + (int64_t)hb * st.work_stride + ld;                     \
+  double* __restrict__ X_h = R_h + ld;                                                        \
+  (void)q_h; (void)lo_h; (void)up_h; (void)Cg_h; (void)mu_h; (void)x_h; (void)Px_h;           \
+  (void)zb_h; (void)yb_h; (void)R_h; (void)X_h
+
+  // ---- prologue: Cg x, the first rhs, mu.V, Cg.V, Cg.mu (admm_grp.hip's next_rhs, fused) --
+  if (hmine && g_act[hg]) {
+    GC_HPTRS;
+    const int g = hg;
+    const double dinv = g_dinv[g];
+    for (int r = 0; r < mg; ++r) {
+      double a = 0.0, am = 0.0;
+      for (int i = hl; i < n; i += 32) {
+        a = fma(Cg_h[(int64_t)r * ld + i], x_h[i], a);
+        am = fma(Cg_h[(int64_t)r * ld + i], mu_h[i], am);
+      }
+      a = csum32(a);
+      am = csum32(am);
+      if (hl == 0) {
+        g_cgx[g * MGG + r] = a;
+        g_cmu[g * MGG + r] = am;
+      }
+    }
+    if (hl < mg) g_wg[g * MGG + hl] = g_rg[g * MGG + hl] * g_zg[g * MGG + hl] - g_yg[g * MGG + hl];
+    double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = hl; i < n; i += 32) {
+      const double rb = has_box ? crho(lo_h[i], up_h[i], rho, s) : 0.0;
+      double rr = sigma * x_h[i] - q_h[i];
+      if (has_box) rr += rb * zb_h[i] - yb_h[i];
+#pragma unroll
+      for (int r = 0; r < CMG; ++r)
+        if (r < mg) rr += Cg_h[(int64_t)r * ld + i] * g_wg[g * MGG + r];
+      const double v = rr * dinv;
+      R_h[i] = rr;
+      muv = fma(mu_h[i], v, muv);
+#pragma unroll
+      for (int r = 0; r < CMG; ++r)
+        if (r < mg) cvp[r] = fma(Cg_h[(int64_t)r * ld + i], v, cvp[r]);
+    }
+    muv = csum32(muv);
+#pragma unroll
+    for (int r = 0; r < CMG; ++r) cvp[r] = csum32(cvp[r]);
+    if (hl == 0) {
+      g_muv[g] = muv;
+      for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
+    }
+  }
+  if (t == 0) {
+    int any = 0;
+    for (int g = 0; g < G; ++g) any |= g_act[g];
+    s_any = any;
+  }
+  __syncthreads();
+
+  const int ntile = (U + 15) >> 4;
+  const int ktile = (kU + 15) >> 4;
+  while (s_any) {
+    // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs) ----------------------
+    {
+      const int kq = l >> 4, m = l & 15;
+      const double* Vp = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride + ld : nullptr;
+      const double wsc1 = m < G ? g_dinv[m] : 1.0;
+      f64x4 c[3];
+      const double* arow[3];
+      bool tv[3], aval[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        c[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+        const int u = (w + CNW * j) * 16 + m;
+        tv[j] = w + CNW * j < ntile;
+        aval[j] = u < U;
+        arow[j] = lr.panel + (int64_t)s_urow[u < CU_MAX ? u : 0] * lr.ldp;
+      }
+      struct Buf { double2 b; double2 a[3]; };
+      auto load = [&](Buf& f, int k0) {
+        const int kk = k0 + 2 * kq;
+        const bool kin = kk + 1 < n;
+        f.b = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          f.a[j] = (tv[j] && aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
+      };
+      auto mma = [&](const Buf& f) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          if (tv[j]) {
+            c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].x, f.b.x, c[j], 0, 0, 0);
+            c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].y, f.b.y, c[j], 0, 0, 0);
+          }
+      };
+      Buf f0, f1;
+      load(f0, 0);
+      for (int k0 = 0; k0 < n; k0 += 16) {
+        load(f1, k0 + 8);
+        mma(f0);
+        load(f0, k0 + 16);
+        mma(f1);
+      }
+      // B operand of the group GEMM in place: rows < U = sqrt(c) W, rows U + r = sqrt(R_r) Cg_r V
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int tile = w + CNW * j;
+        if (tv[j]) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = tile * 16 + kq + 4 * r;
+            if (u < U) WU[u * CG_MAX + m] = gk.sqc * wsc1 * c[j][r];
+          }
+        }
+      }
+      if (t < CG_MAX * CMG) {
+        const int g = t / CMG, r = t % CMG;
+        if (r < mg) WU[(U + r) * CG_MAX + g] = (g < G) ? s_sr[r] * g_cgv[g * MGG + r] : 0.0;
+      }
+    }
+    __syncthreads();
+    // ---- z' = M_U^-1 B (MFMA, A from the full symmetric M_U^-1 rows, B from LDS) -------------
+    {
+      const int kq = l >> 4, m = l & 15;
+      f64x4 z[3];
+      const double* mrow[3];
+      bool zv[3], rv[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        z[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+        const int row = (w + CNW * j) * 16 + m;
+        zv[j] = w + CNW * j < ktile;
+        rv[j] = row < kU;
+        mrow[j] = Mi + (int64_t)(rv[j] ? row : 0) * k_ld;
+      }
+      const int kU4 = (kU + 7) & ~7;
+      for (int k0 = 0; k0 < kU4; k0 += 8) {
+        const int kk = k0 + 2 * kq;   // k_ld padding: rows / columns >= kU of M^-1 are never read
+        const bool kin = kk < kU;
+        const bool kin1 = kk + 1 < kU;
+        const double b0 = kin ? WU[kk * CG_MAX + m] : 0.0;
+        const double b1 = kin1 ? WU[(kk + 1) * CG_MAX + m] : 0.0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (zv[j]) {
+            double2 a = double2{0.0, 0.0};
+            if (rv[j] && kin1) a = *reinterpret_cast<const double2*>(mrow[j] + kk);
+            else if (rv[j] && kin) a.x = mrow[j][kk];
+            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b0, z[j], 0, 0, 0);
+            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b1, z[j], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();   // every wave is done reading B
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int tile = w + CNW * j;
+        if (zv[j]) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = tile * 16 + kq + 4 * r;
+            if (u < kU) WU[u * CG_MAX + m] = z[j][r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- per date: s, y = H^-1 s, Ut / cw / su (half-wave per date) ---------------------------
+    if (hmine && g_act[hg]) {
+      const int g = hg, b = hb;
+      const int T = g_T[g], off = g_off[g];
+      const int m = U - T, mh = m + 1;
+      const double d = gk.d, sct = sqrt(gk.c * T);
+      const double* A = gc.aq + (int64_t)b * gc.aq_stride;
+      const double* Q = A + k_ld;
+      const double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
+      double az = 0.0;
+      for (int u = hl; u < kU; u += 32) az = fma(A[u], WU[u * CG_MAX + g], az);
+      az = csum32(az);
+      // s: lane j < m holds s_j = z'_{C_j}; lane m (or the last) holds s_mu
+      double sj[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = hl + 32 * h;
+        double v = 0.0;
+        if (j < m) {
+          const int cj = j < off ? j : j + T;
+          v = WU[cj * CG_MAX + g];
+        } else if (j == m) {
+          v = sct * (g_muv[g] - az / d);
+        }
+        sj[h] = v;
+      }
+      // y = H^-1 s (H^-1 row i . s): lane i computes y_i for i = hl, hl + 32
+      double yi[2] = {0.0, 0.0};
+      for (int j = 0; j < mh; ++j) {
+        const double sv = __shfl(j < 32 ? sj[0] : sj[1], (hg & 1) * 32 + (j & 31), 64);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = hl + 32 * h;
+          if (i < mh) yi[h] = fma(Hi[(int64_t)i * gc.ldh + j], sv, yi[h]);
+        }
+      }
+      const double ymu = __shfl(m < 32 ? yi[0] : yi[1], (hg & 1) * 32 + (m & 31), 64);
+      const double coef = sct / d * ymu;
+      // y to LDS: the loop below has a lane-dependent trip count, so no shuffles inside it
+      // (an inactive source lane would read as garbage)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (hl + 32 * h < mh) g_y[g * CH_MAX + hl + 32 * h] = yi[h];
+      // base = z' - M^-1[:, C] y_C + coef q ; Ut = sqrt(c) base on X rows, cw = sqrt(R) base on G rows
+      for (int u = hl; u < kU; u += 32) {
+        double v = WU[u * CG_MAX + g] + coef * Q[u];
+        for (int j = 0; j < m; ++j) {
+          const int cj = j < off ? j : j + T;
+          v = fma(-Mi[(int64_t)cj * k_ld + u], g_y[g * CH_MAX + j], v);
+        }
+        if (u < U) UT[u * CG_MAX + g] = gk.sqc * v;
+        else g_cw[g * MGG + (u - U)] = s_sr[u - U] * v;
+      }
+      if (hl == 0) g_su[g] = sct * ymu;
+    }
+    __syncthreads();
+    // ---- pass 2: X~raw (n x G) = X_union' Ut ---------------------------------------------------
+    {
+      const int kq = l >> 4, m = l & 15;
+      const int Uk = (U + 3) & ~3;
+      constexpr int PS = 4;
+      for (int p = w; p * 32 < n; p += CNW) {
+        const int col = p * 32 + 2 * m;
+        const bool cin = col < n;
+        f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
+        struct ABuf { double2 a[PS]; };
+        auto load = [&](ABuf& f, int u0) {
+#pragma unroll
+          for (int h = 0; h < PS; ++h) {
+            const int u = u0 + 4 * h + kq;
+            f.a[h] = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + col)
+                                    : double2{0.0, 0.0};
+          }
+        };
+        auto mma = [&](const ABuf& f, int u0) {
+#pragma unroll
+          for (int h = 0; h < PS; ++h) {
+            const int u = u0 + 4 * h + kq;
+            const double bv = u < Uk ? UT[u * CG_MAX + m] : 0.0;
+            ce = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[h].x, bv, ce, 0, 0, 0);
+            co = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[h].y, bv, co, 0, 0, 0);
+          }
+        };
+        ABuf f0, f1;
+        load(f0, 0);
+        for (int u0 = 0; u0 < Uk; u0 += 8 * PS) {
+          load(f1, u0 + 4 * PS);
+          mma(f0, u0);
+          load(f0, u0 + 8 * PS);
+          mma(f1, u0 + 4 * PS);
+        }
+        if (m < G && g_act[m]) {
+          double* xr = st.work + (int64_t)(d0 + m) * st.work_stride + 2 * ld;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = p * 32 + 2 * (kq + 4 * r);
+            if (i < n) xr[i] = ce[r];
+            if (i + 1 < n) xr[i + 1] = co[r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- per-date fused updates (admm_grp.hip FUSE form) ------------------------------------
+    if (hmine && g_act[hg]) {
+      GC_HPTRS;
+      const int g = hg;
+      const double su = g_su[g], dinv = g_dinv[g];
+      // Cg x~ = Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / d
+      for (int r = 0; r < mg; ++r) {
+        double a = 0.0;
+        for (int u = hl; u < U; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * CG_MAX + g], a);
+        a = csum32(a);
+        double cw = 0.0;
+        for (int r2 = 0; r2 < mg; ++r2) cw = fma(cc[r * mg + r2], g_cw[g * MGG + r2], cw);
+        if (hl == 0) g_zt[g * MGG + r] = g_cgv[g * MGG + r] - dinv * (a - su * g_cmu[g * MGG + r] + cw);
+      }
+      double mv[7] = {0, 0, 0, 0, 0, 0, 0};   // |Cx-z| |Cx| |z| |dres| |Px| |C'y| |q|
+      if (hl < mg) {
+        const int e = g * MGG + hl;
+        const double rg = g_rg[e], zt = g_zt[e];
+        const double zh = alpha * zt + (1.0 - alpha) * g_zg[e];
+        const double zn = fmin(fmax(zh + g_yg[e] / rg, g_lg[e]), g_ug[e]);
+        const double yn = g_yg[e] + rg * (zh - zn);
+        const double cx = alpha * zt + (1.0 - alpha) * g_cgx[e];
+        mv[0] = fabs(cx - zn);
+        mv[1] = fabs(cx);
+        mv[2] = fabs(zn);
+        g_rgz[e] = rg * zt;
+        g_zg[e] = zn;
+        g_yg[e] = yn;
+        g_cgx[e] = cx;
+        g_wg[e] = rg * zn - yn;
+      }
+      double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 2
+      for (int i = hl; i < n; i += 32) {
+        const double rb = has_box ? crho(lo_h[i], up_h[i], rho, s) : 0.0;
+        const double rr0 = R_h[i];
+        double corr = X_h[i] - su * mu_h[i];
+        double cgi[CMG];
+#pragma unroll
+        for (int r = 0; r < CMG; ++r) {
+          cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
+          if (r < mg) corr = fma(g_cw[g * MGG + r], cgi[r], corr);
+        }
+        const double xt = (rr0 - corr) * dinv;
+        double pxt = rr0 - sigma * xt - rb * xt;
+        double cgy = 0.0, cgw = 0.0;
+#pragma unroll
+        for (int r = 0; r < CMG; ++r) {
+          if (r < mg) {
+            pxt -= cgi[r] * g_rgz[g * MGG + r];
+            cgy = fma(cgi[r], g_yg[g * MGG + r], cgy);
+            cgw = fma(cgi[r], g_wg[g * MGG + r], cgw);
+          }
+        }
+        const double xn = alpha * xt + (1.0 - alpha) * x_h[i];
+        const double pxn = alpha * pxt + (1.0 - alpha) * Px_h[i];
+        const double qi = q_h[i];
+        double rr = sigma * xn - qi + cgw;
+        double cty = 0.0;
+        if (has_box) {
+          const double zh = alpha * xt + (1.0 - alpha) * zb_h[i];
+          const double zn = fmin(fmax(zh + yb_h[i] / rb, lo_h[i]), up_h[i]);
+          const double yn = yb_h[i] + rb * (zh - zn);
+          zb_h[i] = zn;
+          yb_h[i] = yn;
+          cty = yn;
+          rr += rb * zn - yn;
+          mv[0] = fmax(mv[0], fabs(xn - zn));
+          mv[1] = fmax(mv[1], fabs(xn));
+          mv[2] = fmax(mv[2], fabs(zn));
+        }
+        x_h[i] = xn;
+        Px_h[i] = pxn;
+        mv[4] = fmax(mv[4], fabs(pxn));
+        mv[6] = fmax(mv[6], fabs(qi));
+        const double cy = cty + cgy;
+        mv[3] = fmax(mv[3], fabs((pxn + qi + cty) + (cy - cty)));
+        mv[5] = fmax(mv[5], fabs(cy));
+        const double v = rr * dinv;
+        R_h[i] = rr;
+        muv = fma(mu_h[i], v, muv);
+#pragma unroll
+        for (int r = 0; r < CMG; ++r) cvp[r] = fma(cgi[r], v, cvp[r]);
+      }
+#pragma unroll
+      for (int e = 0; e < 7; ++e) mv[e] = cmax32(mv[e]);
+      muv = csum32(muv);
+#pragma unroll
+      for (int r = 0; r < CMG; ++r) cvp[r] = csum32(cvp[r]);
+      const int it = g_it[g] + 1;
+      int stat = PQ_UNSOLVED;
+      const double eps_p = s.eps_abs + s.eps_rel * fmax(mv[1], mv[2]);
+      const double eps_d = s.eps_abs + s.eps_rel * fmax(mv[4], fmax(mv[5], mv[6]));
+      double rn = 0.0;   // this date's rho request (0: none)
+      if (mv[0] <= eps_p && mv[3] <= eps_d) {
+        stat = PQ_SOLVED;
+      } else if (s.adapt_interval > 0 && it % s.adapt_interval == 0) {
+        const double rp = mv[0] / (fmax(mv[1], mv[2]) + 1e-30);
+        const double rd = mv[3] / (fmax(mv[4], fmax(mv[5], mv[6])) + 1e-30);
+        rn = fmin(fmax(rho * sqrt(rp / (rd + 1e-30)), s.rho_min), s.rho_max);
+      }
+      if (stat == PQ_UNSOLVED && it >= s.max_iter) stat = PQ_MAX_ITER;
+      if (hl == 0) {
+        g_it[g] = it;
+        g_stat[g] = stat;
+        g_act[g] = (stat == PQ_UNSOLVED) && it < g_end[g];
+        g_rn[g] = rn;
+        g_muv[g] = muv;
+        for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      // group rho: the geometric mean of the requests of the dates that are still running;
+      // a change beyond adapt_tol stops them all for one refactorisation of M_U
+      double lsum = 0.0;
+      int nreq = 0;
+      for (int g = 0; g < G; ++g)
+        if (g_rn[g] > 0.0 && g_stat[g] == PQ_UNSOLVED) { lsum += log(g_rn[g]); ++nreq; }
+      int adapt = 0;
+      if (nreq) {
+        const double rnew = exp(lsum / nreq);
+        if (rnew > rho * s.adapt_tol || rnew < rho / s.adapt_tol) {
+          adapt = 1;
+          s_rho = rnew;
+        }
+      }
+      int any = 0;
+      for (int g = 0; g < G; ++g) {
+        g_rn[g] = 0.0;
+        if (adapt && g_stat[g] == PQ_UNSOLVED) {
+          g_stat[g] = PQ_NEED_REFACTOR;
+          g_act[g] = 0;
+        }
+        any |= g_act[g];
+      }
+      s_any = any;
+    }
+    __syncthreads();
+  }
+
+  // ---- write back ---------------------------------------------------------------------------
+  if (t < G) {
+    const int b = d0 + t;
+    const int stt0 = st.status[b];
+    if (stt0 == PQ_UNSOLVED || stt0 == PQ_NEED_REFACTOR) {
+      st.iters[b] = g_it[t];
+      st.status[b] = g_stat[t];
+      st.rho[b] = s_rho;
+    }
+  }
+  if (t == 0) gc.grho[grp] = s_rho;
+  for (int e = t; e < CG_MAX * MGG; e += CT) {
+    const int g = e / MGG, r = e % MGG;
+    if (g < G && r < mg) {
+      const int b = d0 + g;
+      st.z[(int64_t)b * st.m_ld + r] = g_zg[e];
+      st.y[(int64_t)b * st.m_ld + r] = g_yg[e];
+    }
+  }
+#undef GC_HPTRS
+}
+
+}  // namespace pq
+
+static int gcap_check(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap* gc, const char* who) {
+  PQ_CHECK_ARG(lr && pb && gc, "%s: null argument", who);
+  PQ_CHECK_ARG(gc->gdates && gc->urows && gc->ucnt && gc->uoff && gc->gidx && gc->grho && gc->ngroups > 0,
+               "%s: group plan missing", who);
+  PQ_CHECK_ARG(gc->umax > 0 && gc->umax <= pq::CU_MAX, "%s: umax must be in (0, %d]", who, pq::CU_MAX);
+  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::CMG && pb->Cg_stride == 0 && pb->g_stride == 0,
+               "%s: needs shared general rows, mg <= %d", who, pq::CMG);
+  // (the caller guarantees ucnt[g] + mg <= k_ld for every group; U <= umax <= 320)
+  PQ_CHECK_ARG(gc->k_ld % 64 == 0 && gc->k_ld >= 64 && gc->k_ld <= 384,
+               "%s: need 64 <= k_ld <= 384, a multiple of 64 (k_ld=%d)", who, gc->k_ld);
+  PQ_CHECK_ARG(lr->mu != nullptr, "%s: the group form needs the window means (centred covariance)", who);
+  return 0;
+}
+
+extern "C" int pq_gcap_assemble(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap* gc,
+                                const pq_settings* s, const double* band, int64_t ldo, int32_t r0,
+                                const double* pc, int64_t ldpc, const double* cc, void* stream) {
+  if (gcap_check(lr, pb, gc, "pq_gcap_assemble")) return -1;
+  PQ_CHECK_ARG(s && band && gc->M, "pq_gcap_assemble: null argument");
+  PQ_CHECK_ARG(pb->mg == 0 || (pc && cc), "pq_gcap_assemble: general rows need pc and cc");
+  hipLaunchKernelGGL(pq::k_gcap_assemble, dim3(gc->ngroups), dim3(256), 0, (hipStream_t)stream, *lr, *pb, *gc, *s,
+                     band, ldo, r0, pc, ldpc, cc);
+  PQ_CHECK_LAUNCH("pq_gcap_assemble");
+  return 0;
+}
+
+extern "C" int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
+                               const pq_settings* s, const int32_t* idx, int32_t nidx, const double* band,
+                               int64_t ldo, int32_t r0, const double* pc, int64_t ldpc, void* stream) {
+  if (gcap_check(lr, pb, gc, "pq_gcap_prepare")) return -1;
+  PQ_CHECK_ARG(st && s && band && gc->Minv && gc->aq && gc->hinv, "pq_gcap_prepare: null argument");
+  PQ_CHECK_ARG(gc->aq_stride >= 2 * (int64_t)gc->k_ld && gc->ldh > 0 && gc->ldh <= pq::CH_MAX,
+               "pq_gcap_prepare: aq needs 2 k_ld per date, ldh <= %d", pq::CH_MAX);
+  PQ_CHECK_ARG(pb->mg == 0 || pc, "pq_gcap_prepare: general rows need pc");
+  const int grid = idx ? nidx : pb->batch;
+  if (grid <= 0) return 0;
+  hipLaunchKernelGGL(pq::k_gcap_prep, dim3(grid), dim3(256), 0, (hipStream_t)stream, *lr, *pb, *st, *gc, *s, idx,
+                     band, ldo, r0, pc, ldpc);
+  PQ_CHECK_LAUNCH("pq_gcap_prepare");
+  return 0;
+}
+
+extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
+                               const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
+                               int32_t r0, const double* cc, void* stream) {
+  if (gcap_check(lr, pb, gc, "pq_admm_lr_gcap")) return -1;
+  PQ_CHECK_ARG(st && s && gc->Minv && gc->aq && gc->hinv, "pq_admm_lr_gcap: null argument");
+  PQ_CHECK_ARG(pb->mg == 0 || (pc && cc), "pq_admm_lr_gcap: general rows need pc and cc");
+  PQ_CHECK_ARG(pb->n % 2 == 0 && lr->ldp % 2 == 0, "pq_admm_lr_gcap: needs even n and panel stride");
+  PQ_CHECK_ARG(st->work && st->work_stride >= 3 * (int64_t)pb->ld, "pq_admm_lr_gcap: work buffer too small");
+  hipLaunchKernelGGL(pq::k_admm_gcap, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st, *gc,
+                     *s, iters_this_call, pc, ldpc, r0, cc);
+  PQ_CHECK_LAUNCH("pq_admm_lr_gcap");
+  return 0;
+}

@@ -485,13 +485,15 @@ def _uniform_box(qb: QPBatch) -> bool:
     return bool((cls == cls[:, :1]).all().item()) and (qb.lb.shape[0] == 1 or bool((cls[:, 0] == cls[0, 0]).all().item()))
 
 
-def _band_setup(qb: QPBatch, lr: LowRank, strm):
+def _band_setup(qb: QPBatch, lr: LowRank, strm, w_min: int = 0):
     """Band Gram of the panel rows + PC / CC tables for pq_lr_capacitance_band, or None when
-    the band form does not apply (per-problem constraints, non-uniform box rho, tmax > 1024)."""
+    the band form does not apply (per-problem constraints, non-uniform box rho, tmax > 1024).
+    ``w_min``: band width at least this (the group capacitance needs the widest union span)."""
     if not qb.shared or lr.tmax > 1024 or not _uniform_box(qb):
         return None
     lib = _lib.load()
     r0, nrows, W = lr.span()
+    W = min(max(W, int(w_min)), nrows)
     dev, n, mg = qb.device, qb.n, qb.mg
     ldo = round_up(W, 2)
     band = torch.empty((nrows, ldo), dtype=F64, device=dev)
@@ -505,10 +507,63 @@ def _band_setup(qb: QPBatch, lr: LowRank, strm):
     return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc}
 
 
+def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan", settings: Settings):
+    """Buffers and C structs of the group capacitance (admm_gcap.hip), or None when the dates
+    of some group do not share c = p_scale w_scale and p_diag.  Also sets one rho per group
+    (the mean of its dates' initial rho) in ws.rho."""
+    B, dev, mg = qb.batch, qb.device, qb.mg
+    ps = qb.p_scale if qb.p_scale is not None else torch.ones(B, dtype=F64, device=dev)
+    wsc = lr.w_scale if lr.w_scale is not None else torch.ones(B, dtype=F64, device=dev)
+    c = ps * wsc
+    pd = qb.p_diag if qb.p_diag is not None else torch.zeros(B, dtype=F64, device=dev)
+    first = groups.gdates[:-1].long()[groups.gidx.long()]
+    if not bool(((c == c[first]) & (pd == pd[first])).all().item()):
+        return None
+    G = groups.ngroups
+    k_ld = round_up(groups.ucnt_max + mg, 64)
+    ldh = min(64, round_up(groups.corr_max, 8))
+    key = (B, G, k_ld, ldh)
+    buf = getattr(ws, "_gcap", None)
+    if buf is None or buf["key"] != key:
+        buf = {"key": key,
+               "M": torch.empty((G, k_ld, k_ld), dtype=F64, device=dev),
+               "Minv": torch.empty((G, k_ld, k_ld), dtype=F64, device=dev),
+               "Dt": torch.empty((G, k_ld // 64, 64, 64), dtype=F64, device=dev),
+               "grho": torch.empty(G, dtype=F64, device=dev),
+               "iters": torch.zeros(G, dtype=torch.int32, device=dev),
+               "status": torch.zeros(G, dtype=torch.int32, device=dev),
+               "info": torch.zeros(G, dtype=torch.int32, device=dev),
+               "aq": torch.empty((B, 2 * k_ld), dtype=F64, device=dev),
+               "hinv": torch.empty((B, ldh, ldh), dtype=F64, device=dev)}
+        ws._gcap = buf
+    # one rho per group: the mean of the dates' initial rho (scale-aware, _rho_floor_q included)
+    gr = torch.zeros(G, dtype=F64, device=dev).index_add_(0, groups.gidx.long(), ws.rho)
+    gr /= torch.from_numpy(groups.sizes.astype(np.float64)).to(dev)
+    buf["grho"].copy_(gr)
+    ws.rho.copy_(gr[groups.gidx.long()])
+    kmax = groups.ucnt_max + mg
+    buf["c"] = _lib.PQGcap(gdates=groups.gdates.data_ptr(), ngroups=G, urows=groups.urows.data_ptr(),
+                           ucnt=groups.ucnt.data_ptr(), uoff=groups.uoff.data_ptr(), umax=groups.umax,
+                           gidx=groups.gidx.data_ptr(), grho=buf["grho"].data_ptr(), M=buf["M"].data_ptr(),
+                           Minv=buf["Minv"].data_ptr(), k_ld=k_ld, M_stride=k_ld * k_ld,
+                           aq=buf["aq"].data_ptr(), aq_stride=2 * k_ld, hinv=buf["hinv"].data_ptr(), ldh=ldh)
+    # the factor sees each M_U as a k x k "problem" (identity padding beyond its U + mg rows)
+    buf["pb"] = _lib.PQProblem(n=kmax, ld=k_ld, batch=G, mg=0, P=buf["M"].data_ptr(), P_stride=k_ld * k_ld,
+                               q=qb.q.data_ptr(), q_stride=qb.q.stride(0), Cg=qb.Cg.data_ptr(),
+                               lg=qb.lg.data_ptr(), ug=qb.ug.data_ptr())
+    buf["st"] = _lib.PQState(K=buf["Minv"].data_ptr(), K_stride=k_ld * k_ld, Dt=buf["Dt"].data_ptr(),
+                             Dt_stride=(k_ld // 64) * 4096, x=ws.x.data_ptr(), Px=ws.Px.data_ptr(),
+                             z=ws.z.data_ptr(), y=ws.y.data_ptr(), m_ld=ws.m_ld, mg_pad=ws.mg_pad,
+                             rho=buf["grho"].data_ptr(), iters=buf["iters"].data_ptr(),
+                             status=buf["status"].data_ptr(), info=buf["info"].data_ptr(), out=ws.out.data_ptr(),
+                             work=ws.work.data_ptr(), work_stride=ws.work_stride)
+    return buf
+
+
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
-                  fuse: bool = True, grouped_polish: bool = True) -> BatchResult:
+                  fuse: bool = True, grouped_polish: bool = True, gcap: bool = True) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -558,12 +613,35 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                                              k_ld * k_ld, strm), "pq_lr_capacitance")
         _lib.check(lib.pq_factor_batched(PM_, SM_, _ptr(idx), nidx, SSM, 1, strm), "pq_factor_batched(M)")
 
-    if band:
-        bd = tl("gram", lambda: _band_setup(qb, lr, strm))
-    tl("factor", lambda: refactor(None, 0))
     grouped = grouped_applicable(qb, lr, groups, ws)
+    gcap_try = (gcap and grouped and fuse and qb.mg <= 4 and lr.mu is not None and qb.shared
+                and groups.ucnt_max + qb.mg <= 384 and groups.corr_max <= 64)
+    if band:
+        bd = tl("gram", lambda: _band_setup(qb, lr, strm, w_min=groups.span_max if gcap_try else 0))
+    gc = _gcap_setup(qb, lr, ws, groups, settings or Settings()) if (gcap_try and bd is not None) else None
+
+    def refactor_groups():
+        """Group capacitance: one M_U per group (current group rho), its inverse, and every
+        date's a_b, q_b, H_b^-1."""
+        g = gc
+        GC_ = ctypes.byref(g["c"])
+        _lib.check(lib.pq_gcap_assemble(L_, P_, GC_, SS, bd["band"].data_ptr(), bd["ldo"], bd["r0"],
+                                        bd["pc"].data_ptr(), bd["pc"].stride(0), bd["cc"].data_ptr(), strm),
+                   "pq_gcap_assemble")
+        _lib.check(lib.pq_factor_batched(ctypes.byref(g["pb"]), ctypes.byref(g["st"]), None, 0, SSM, 2, strm),
+                   "pq_factor_batched(M_U)")
+        _lib.check(lib.pq_gcap_prepare(L_, P_, S_, GC_, SS, None, 0, bd["band"].data_ptr(), bd["ldo"], bd["r0"],
+                                       bd["pc"].data_ptr(), bd["pc"].stride(0), strm), "pq_gcap_prepare")
+
+    if gc is not None:
+        tl("factor", refactor_groups)
+    else:
+        tl("factor", lambda: refactor(None, 0))
 
     def admm(idx, nidx):
+        if gc is not None:   # group capacitance (admm_gcap.hip)
+            return lib.pq_admm_lr_gcap(L_, P_, S_, ctypes.byref(gc["c"]), SS, int(s.max_iter), bd["pc"].data_ptr(),
+                                       bd["pc"].stride(0), bd["r0"], bd["cc"].data_ptr(), strm)
         if grouped:   # every group relaunches; solved dates are skipped inside
             fz = bd is not None and fuse and qb.mg <= 4   # uniform D + shared Cg: the fused form
             return lib.pq_admm_lr_grouped(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
@@ -588,7 +666,10 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             if kk == 0:
                 break
             idx, nidx = need.contiguous(), kk
-            tl("factor", lambda: refactor(idx, nidx))
+            if gc is not None:    # the kernel agreed a new rho per group: rebuild every M_U
+                tl("factor", refactor_groups)
+            else:
+                tl("factor", lambda: refactor(idx, nidx))
             cnt["refactors"] += kk
         SS = SS0
 
@@ -652,7 +733,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
-                       admm_launches=launches, capacitance="band" if bd is not None else "direct")
+                       admm_launches=launches,
+                       capacitance="group" if gc is not None else ("band" if bd is not None else "direct"))
 
 
 def factor_only(qb: QPBatch, invert: bool = False, sigma: float = 0.0):
@@ -797,10 +879,18 @@ class GroupPlan:
             urows[gi, :len(u)] = u
             ucnt[gi] = len(u)
         self.sizes = np.diff(gdates)
+        gidx = np.repeat(np.arange(max(self.ngroups, 0), dtype=np.int32), self.sizes) if B else np.zeros(0, np.int32)
+        # widest union span in panel rows (the band Gram must cover it for the group capacitance)
+        self.span_max = int(max((urows[g, :ucnt[g]].max() - urows[g, :ucnt[g]].min() + 1)
+                                for g in range(self.ngroups) if ucnt[g] > 0)) if self.ngroups else 0
+        self.ucnt_max = int(ucnt.max()) if self.ngroups else 0
+        # rank of the Woodbury correction of a date: union rows outside its window + the mean
+        self.corr_max = int((ucnt[gidx] - tlen).max()) + 1 if B else 1
         self.gdates = torch.from_numpy(gdates).to(device)
         self.urows = torch.from_numpy(urows).to(device)
         self.ucnt = torch.from_numpy(ucnt).to(device)
         self.uoff = torch.from_numpy(uoff).to(device)
+        self.gidx = torch.from_numpy(gidx).to(device)
 
 
 class Panel:
