@@ -32,13 +32,30 @@
 
 namespace pq {
 
-constexpr int CT = 512;        // threads per group workgroup
-constexpr int CNW = CT / 64;
+constexpr int CT = 256;        // threads per group workgroup (two workgroups per CU: the
+constexpr int CNW = CT / 64;   // phases of two groups overlap -- MFMA passes vs memory-bound)
+constexpr int CHW = CT / 32;   // half-waves (each serves dates hg, hg + CHW, ...)
+constexpr int CTP1 = 5;        // pass-1 row tiles per wave (U <= 320: 20 tiles)
+constexpr int CTP2 = 6;        // GEMM row tiles per wave (U + mg <= 324: 21 tiles)
 constexpr int CG_MAX = 16;     // dates per group (MFMA N)
 constexpr int CU_MAX = 320;    // union rows per group
 constexpr int CMG = 4;         // general rows (register-resident, fused form)
 constexpr int CK_MAX = CU_MAX + CMG;   // capacitance rows
 constexpr int CH_MAX = 64;     // m + 1 = U - T + 1 <= 64
+
+#ifdef PQ_PROFILE
+#define CSTAMP(k)                                                 \
+  do {                                                            \
+    __syncthreads();                                              \
+    if (threadIdx.x == 0) {                                       \
+      const long long now_ = wall_clock64();                      \
+      pclk[k] += now_ - tclk;                                     \
+      tclk = now_;                                                \
+    }                                                             \
+  } while (0)
+#else
+#define CSTAMP(k) do { } while (0)
+#endif
 
 __device__ __forceinline__ double crho(double l, double u, double rho, const pq_settings& s) {
   if (l == u) return rho * s.eq_scale;
@@ -223,7 +240,7 @@ __global__ __launch_bounds__(256) void k_gcap_prep(pq_lowrank lr, pq_problem pb,
 }
 
 // ---- the ADMM iterations -------------------------------------------------------------------
-__global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
+__global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
                                                   pq_settings s, int iters_call, const double* pc, int64_t ldpc,
                                                   int r0, const double* cc) {
   constexpr int MGG = 8;
@@ -231,6 +248,9 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
   double* const UT = WU;
   __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX];
   __shared__ double g_y[CG_MAX * CH_MAX];   // y_b = H_b^-1 s_b of every date
+  constexpr int NPART = 8 + CMG;              // per wave and date: 7 maxima, mu.V, Cg.V
+  __shared__ double g_part[CNW * CG_MAX * NPART];
+  __shared__ double g_gm[CG_MAX * 3];
   __shared__ double g_zg[CG_MAX * MGG], g_yg[CG_MAX * MGG], g_rg[CG_MAX * MGG], g_lg[CG_MAX * MGG],
       g_ug[CG_MAX * MGG], g_cgv[CG_MAX * MGG], g_cgx[CG_MAX * MGG], g_wg[CG_MAX * MGG],
       g_cw[CG_MAX * MGG], g_zt[CG_MAX * MGG], g_rgz[CG_MAX * MGG], g_cmu[CG_MAX * MGG];
@@ -250,6 +270,10 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
   const bool has_box = pb.lb != nullptr;
   const double sigma = s.sigma, alpha = s.alpha;
   const double* Mi = gc.Minv + (int64_t)grp * gc.M_stride;
+#ifdef PQ_PROFILE
+  long long pclk[5] = {0, 0, 0, 0, 0};
+  long long tclk = wall_clock64();
+#endif
 
   // ---- setup -------------------------------------------------------------------------------
   for (int u = t; u < CU_MAX; u += CT) s_urow[u] = u < U ? gc.urows[(int64_t)grp * gc.umax + u] : 0;
@@ -295,8 +319,7 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
   __syncthreads();
 
   const int hg = t >> 5, hl = t & 31;
-  const bool hmine = hg < G;
-  const int hb = d0 + (hmine ? hg : 0);
+  const int hbase = (hg & 1) * 32;   // first lane of this half-wave within its wave
 #define GC_HPTRS                                                                              \
   const double* __restrict__ q_h = pb.q + (int64_t)hb * pb.q_stride;                          \
   const double* __restrict__ lo_h = has_box ? pb.lb + (int64_t)hb * pb.box_stride : nullptr;  \
@@ -313,9 +336,10 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
   (void)zb_h; (void)yb_h; (void)R_h; (void)X_h
 
   // ---- prologue: Cg x, the first rhs, mu.V, Cg.V, Cg.mu (admm_grp.hip's next_rhs, fused) --
-  if (hmine && g_act[hg]) {
+  for (int g = hg; g < G; g += CHW) {
+    if (!g_act[g]) continue;
+    const int hb = d0 + g;
     GC_HPTRS;
-    const int g = hg;
     const double dinv = g_dinv[g];
     for (int r = 0; r < mg; ++r) {
       double a = 0.0, am = 0.0;
@@ -369,29 +393,29 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       const int kq = l >> 4, m = l & 15;
       const double* Vp = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride + ld : nullptr;
       const double wsc1 = m < G ? g_dinv[m] : 1.0;
-      f64x4 c[3];
-      const double* arow[3];
-      bool tv[3], aval[3];
+      f64x4 c[CTP1];
+      const double* arow[CTP1];
+      bool tv[CTP1], aval[CTP1];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < CTP1; ++j) {
         c[j] = f64x4{0.0, 0.0, 0.0, 0.0};
         const int u = (w + CNW * j) * 16 + m;
         tv[j] = w + CNW * j < ntile;
         aval[j] = u < U;
         arow[j] = lr.panel + (int64_t)s_urow[u < CU_MAX ? u : 0] * lr.ldp;
       }
-      struct Buf { double2 b; double2 a[3]; };
+      struct Buf { double2 b; double2 a[CTP1]; };
       auto load = [&](Buf& f, int k0) {
         const int kk = k0 + 2 * kq;
         const bool kin = kk + 1 < n;
         f.b = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < CTP1; ++j)
           f.a[j] = (tv[j] && aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
       };
       auto mma = [&](const Buf& f) {
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < CTP1; ++j)
           if (tv[j]) {
             c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].x, f.b.x, c[j], 0, 0, 0);
             c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].y, f.b.y, c[j], 0, 0, 0);
@@ -407,7 +431,7 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       }
       // B operand of the group GEMM in place: rows < U = sqrt(c) W, rows U + r = sqrt(R_r) Cg_r V
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < CTP1; ++j) {
         const int tile = w + CNW * j;
         if (tv[j]) {
 #pragma unroll
@@ -423,14 +447,15 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       }
     }
     __syncthreads();
+    CSTAMP(0);
     // ---- z' = M_U^-1 B (MFMA, A from the full symmetric M_U^-1 rows, B from LDS) -------------
     {
       const int kq = l >> 4, m = l & 15;
-      f64x4 z[3];
-      const double* mrow[3];
-      bool zv[3], rv[3];
+      f64x4 z[CTP2];
+      const double* mrow[CTP2];
+      bool zv[CTP2], rv[CTP2];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < CTP2; ++j) {
         z[j] = f64x4{0.0, 0.0, 0.0, 0.0};
         const int row = (w + CNW * j) * 16 + m;
         zv[j] = w + CNW * j < ktile;
@@ -445,7 +470,7 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
         const double b0 = kin ? WU[kk * CG_MAX + m] : 0.0;
         const double b1 = kin1 ? WU[(kk + 1) * CG_MAX + m] : 0.0;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
+        for (int j = 0; j < CTP2; ++j) {
           if (zv[j]) {
             double2 a = double2{0.0, 0.0};
             if (rv[j] && kin1) a = *reinterpret_cast<const double2*>(mrow[j] + kk);
@@ -457,7 +482,7 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       }
       __syncthreads();   // every wave is done reading B
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < CTP2; ++j) {
         const int tile = w + CNW * j;
         if (zv[j]) {
 #pragma unroll
@@ -469,9 +494,11 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       }
     }
     __syncthreads();
+    CSTAMP(1);
     // ---- per date: s, y = H^-1 s, Ut / cw / su (half-wave per date) ---------------------------
-    if (hmine && g_act[hg]) {
-      const int g = hg, b = hb;
+    for (int g = hg; g < G; g += CHW) {
+      if (!g_act[g]) continue;
+      const int b = d0 + g;
       const int T = g_T[g], off = g_off[g];
       const int m = U - T, mh = m + 1;
       const double d = gk.d, sct = sqrt(gk.c * T);
@@ -498,14 +525,14 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       // y = H^-1 s (H^-1 row i . s): lane i computes y_i for i = hl, hl + 32
       double yi[2] = {0.0, 0.0};
       for (int j = 0; j < mh; ++j) {
-        const double sv = __shfl(j < 32 ? sj[0] : sj[1], (hg & 1) * 32 + (j & 31), 64);
+        const double sv = __shfl(j < 32 ? sj[0] : sj[1], hbase + (j & 31), 64);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int i = hl + 32 * h;
           if (i < mh) yi[h] = fma(Hi[(int64_t)i * gc.ldh + j], sv, yi[h]);
         }
       }
-      const double ymu = __shfl(m < 32 ? yi[0] : yi[1], (hg & 1) * 32 + (m & 31), 64);
+      const double ymu = __shfl(m < 32 ? yi[0] : yi[1], hbase + (m & 31), 64);
       const double coef = sct / d * ymu;
       // y to LDS: the loop below has a lane-dependent trip count, so no shuffles inside it
       // (an inactive source lane would read as garbage)
@@ -522,14 +549,123 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
         if (u < U) UT[u * CG_MAX + g] = gk.sqc * v;
         else g_cw[g * MGG + (u - U)] = s_sr[u - U] * v;
       }
-      if (hl == 0) g_su[g] = sct * ymu;
+      const double su = sct * ymu;
+      if (hl == 0) g_su[g] = su;
+      __builtin_amdgcn_wave_barrier();   // this half-wave's Ut / cw writes precede the reads below
+      // Cg x~ = Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / d, then the general rows' z / y
+      const double dinv = g_dinv[g];
+      for (int r = 0; r < mg; ++r) {
+        double a = 0.0;
+        for (int u = hl; u < U; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * CG_MAX + g], a);
+        a = csum32(a);
+        double cwv = 0.0;
+        for (int r2 = 0; r2 < mg; ++r2) cwv = fma(cc[r * mg + r2], g_cw[g * MGG + r2], cwv);
+        if (hl == 0) g_zt[g * MGG + r] = g_cgv[g * MGG + r] - dinv * (a - su * g_cmu[g * MGG + r] + cwv);
+      }
+      __builtin_amdgcn_wave_barrier();
+      double gm[3] = {0.0, 0.0, 0.0};   // |Cx - z| |Cx| |z| of the general rows
+      if (hl < mg) {
+        const int e = g * MGG + hl;
+        const double rg = g_rg[e], zt = g_zt[e];
+        const double zh = alpha * zt + (1.0 - alpha) * g_zg[e];
+        const double zn = fmin(fmax(zh + g_yg[e] / rg, g_lg[e]), g_ug[e]);
+        const double yn = g_yg[e] + rg * (zh - zn);
+        const double cx = alpha * zt + (1.0 - alpha) * g_cgx[e];
+        gm[0] = fabs(cx - zn);
+        gm[1] = fabs(cx);
+        gm[2] = fabs(zn);
+        g_rgz[e] = rg * zt;
+        g_zg[e] = zn;
+        g_yg[e] = yn;
+        g_cgx[e] = cx;
+        g_wg[e] = rg * zn - yn;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gm[k] = cmax32(gm[k]);
+      if (hl == 0)
+        for (int k = 0; k < 3; ++k) g_gm[g * 3 + k] = gm[k];
     }
     __syncthreads();
-    // ---- pass 2: X~raw (n x G) = X_union' Ut ---------------------------------------------------
+    CSTAMP(2);
+    // ---- pass 2 fused with the per-date updates: the MFMA epilogue of every 32-asset tile
+    //      updates those assets of its date (x~, x, Px, box z / y, residual terms, next rhs);
+    //      per-date maxima / sums go through LDS (NP partial slots per date) --------------------
     {
       const int kq = l >> 4, m = l & 15;
       const int Uk = (U + 3) & ~3;
       constexpr int PS = 4;
+      const bool mact = m < G && g_act[m];
+      const int bm = d0 + (m < G ? m : 0);
+      const double* __restrict__ q_m = pb.q + (int64_t)bm * pb.q_stride;
+      const double* __restrict__ lo_m = has_box ? pb.lb + (int64_t)bm * pb.box_stride : nullptr;
+      const double* __restrict__ up_m = has_box ? pb.ub + (int64_t)bm * pb.box_stride : nullptr;
+      const double* __restrict__ mu_m = lr.mu + (int64_t)bm * lr.mu_stride;
+      double* __restrict__ x_m = st.x + (int64_t)bm * ld;
+      double* __restrict__ Px_m = st.Px + (int64_t)bm * ld;
+      double* __restrict__ zb_m = st.z + (int64_t)bm * st.m_ld + st.mg_pad;
+      double* __restrict__ yb_m = st.y + (int64_t)bm * st.m_ld + st.mg_pad;
+      double* __restrict__ R_m = st.work + (int64_t)bm * st.work_stride + ld;
+      const double su = mact ? g_su[m] : 0.0, dinv = mact ? g_dinv[m] : 0.0;
+      double cwm[CMG], rgzm[CMG], ygm[CMG], wgm[CMG];
+#pragma unroll
+      for (int r = 0; r < CMG; ++r) {
+        const bool ok = mact && r < mg;
+        cwm[r] = ok ? g_cw[m * MGG + r] : 0.0;
+        rgzm[r] = ok ? g_rgz[m * MGG + r] : 0.0;
+        ygm[r] = ok ? g_yg[m * MGG + r] : 0.0;
+        wgm[r] = ok ? g_wg[m * MGG + r] : 0.0;
+      }
+      double mv[7] = {0, 0, 0, 0, 0, 0, 0};   // |Cx-z| |Cx| |z| |dres| |Px| |C'y| |q|
+      double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
+      auto update = [&](int i, double xr) {   // asset i of date m, X~raw = xr
+        const double rb = has_box ? crho(lo_m[i], up_m[i], rho, s) : 0.0;
+        const double rr0 = R_m[i];
+        double corr = xr - su * mu_m[i];
+        double cgi[CMG];
+#pragma unroll
+        for (int r = 0; r < CMG; ++r) {
+          cgi[r] = r < mg ? pb.Cg[(int64_t)r * ld + i] : 0.0;
+          corr = fma(cwm[r], cgi[r], corr);
+        }
+        const double xt = (rr0 - corr) * dinv;
+        double pxt = rr0 - sigma * xt - rb * xt;
+        double cgy = 0.0, cgw = 0.0;
+#pragma unroll
+        for (int r = 0; r < CMG; ++r) {
+          pxt -= cgi[r] * rgzm[r];
+          cgy = fma(cgi[r], ygm[r], cgy);
+          cgw = fma(cgi[r], wgm[r], cgw);
+        }
+        const double xn = alpha * xt + (1.0 - alpha) * x_m[i];
+        const double pxn = alpha * pxt + (1.0 - alpha) * Px_m[i];
+        const double qi = q_m[i];
+        double rr = sigma * xn - qi + cgw;
+        double cty = 0.0;
+        if (has_box) {
+          const double zh = alpha * xt + (1.0 - alpha) * zb_m[i];
+          const double zn = fmin(fmax(zh + yb_m[i] / rb, lo_m[i]), up_m[i]);
+          const double yn = yb_m[i] + rb * (zh - zn);
+          zb_m[i] = zn;
+          yb_m[i] = yn;
+          cty = yn;
+          rr += rb * zn - yn;
+          mv[0] = fmax(mv[0], fabs(xn - zn));
+          mv[1] = fmax(mv[1], fabs(xn));
+          mv[2] = fmax(mv[2], fabs(zn));
+        }
+        x_m[i] = xn;
+        Px_m[i] = pxn;
+        mv[4] = fmax(mv[4], fabs(pxn));
+        mv[6] = fmax(mv[6], fabs(qi));
+        const double cy = cty + cgy;
+        mv[3] = fmax(mv[3], fabs((pxn + qi + cty) + (cy - cty)));
+        mv[5] = fmax(mv[5], fabs(cy));
+        const double v = rr * dinv;
+        R_m[i] = rr;
+        muv = fma(mu_m[i], v, muv);
+#pragma unroll
+        for (int r = 0; r < CMG; ++r) cvp[r] = fma(cgi[r], v, cvp[r]);
+      };
       for (int p = w; p * 32 < n; p += CNW) {
         const int col = p * 32 + 2 * m;
         const bool cin = col < n;
@@ -560,107 +696,52 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
           load(f0, u0 + 8 * PS);
           mma(f1, u0 + 4 * PS);
         }
-        if (m < G && g_act[m]) {
-          double* xr = st.work + (int64_t)(d0 + m) * st.work_stride + 2 * ld;
+        if (mact) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int i = p * 32 + 2 * (kq + 4 * r);
-            if (i < n) xr[i] = ce[r];
-            if (i + 1 < n) xr[i + 1] = co[r];
+            if (i < n) {   // n even: i + 1 < n too
+              update(i, ce[r]);
+              update(i + 1, co[r]);
+            }
           }
         }
+      }
+      // the four lanes of a wave that share date m (m, m + 16, m + 32, m + 48)
+#pragma unroll
+      for (int e = 0; e < 7; ++e) {
+        mv[e] = fmax(mv[e], __shfl_xor(mv[e], 16, 64));
+        mv[e] = fmax(mv[e], __shfl_xor(mv[e], 32, 64));
+      }
+      muv += __shfl_xor(muv, 16, 64);
+      muv += __shfl_xor(muv, 32, 64);
+#pragma unroll
+      for (int r = 0; r < CMG; ++r) {
+        cvp[r] += __shfl_xor(cvp[r], 16, 64);
+        cvp[r] += __shfl_xor(cvp[r], 32, 64);
+      }
+      if (kq == 0) {
+        double* pp = g_part + (w * CG_MAX + m) * NPART;
+#pragma unroll
+        for (int e = 0; e < 7; ++e) pp[e] = mv[e];
+        pp[7] = muv;
+#pragma unroll
+        for (int r = 0; r < CMG; ++r) pp[8 + r] = cvp[r];
       }
     }
     __syncthreads();
-    // ---- per-date fused updates (admm_grp.hip FUSE form) ------------------------------------
-    if (hmine && g_act[hg]) {
-      GC_HPTRS;
-      const int g = hg;
-      const double su = g_su[g], dinv = g_dinv[g];
-      // Cg x~ = Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / d
-      for (int r = 0; r < mg; ++r) {
-        double a = 0.0;
-        for (int u = hl; u < U; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * CG_MAX + g], a);
-        a = csum32(a);
-        double cw = 0.0;
-        for (int r2 = 0; r2 < mg; ++r2) cw = fma(cc[r * mg + r2], g_cw[g * MGG + r2], cw);
-        if (hl == 0) g_zt[g * MGG + r] = g_cgv[g * MGG + r] - dinv * (a - su * g_cmu[g * MGG + r] + cw);
+    CSTAMP(3);
+    // ---- per date: residuals, convergence, rho request (one thread per date) ------------------
+    if (t < G && g_act[t]) {
+      const int g = t;
+      double mv[7], muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
+      for (int e = 0; e < 7; ++e) mv[e] = e < 3 ? g_gm[g * 3 + e] : 0.0;
+      for (int ww = 0; ww < CNW; ++ww) {
+        const double* pp = g_part + (ww * CG_MAX + g) * NPART;
+        for (int e = 0; e < 7; ++e) mv[e] = fmax(mv[e], pp[e]);
+        muv += pp[7];
+        for (int r = 0; r < CMG; ++r) cvp[r] += pp[8 + r];
       }
-      double mv[7] = {0, 0, 0, 0, 0, 0, 0};   // |Cx-z| |Cx| |z| |dres| |Px| |C'y| |q|
-      if (hl < mg) {
-        const int e = g * MGG + hl;
-        const double rg = g_rg[e], zt = g_zt[e];
-        const double zh = alpha * zt + (1.0 - alpha) * g_zg[e];
-        const double zn = fmin(fmax(zh + g_yg[e] / rg, g_lg[e]), g_ug[e]);
-        const double yn = g_yg[e] + rg * (zh - zn);
-        const double cx = alpha * zt + (1.0 - alpha) * g_cgx[e];
-        mv[0] = fabs(cx - zn);
-        mv[1] = fabs(cx);
-        mv[2] = fabs(zn);
-        g_rgz[e] = rg * zt;
-        g_zg[e] = zn;
-        g_yg[e] = yn;
-        g_cgx[e] = cx;
-        g_wg[e] = rg * zn - yn;
-      }
-      double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 2
-      for (int i = hl; i < n; i += 32) {
-        const double rb = has_box ? crho(lo_h[i], up_h[i], rho, s) : 0.0;
-        const double rr0 = R_h[i];
-        double corr = X_h[i] - su * mu_h[i];
-        double cgi[CMG];
-#pragma unroll
-        for (int r = 0; r < CMG; ++r) {
-          cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
-          if (r < mg) corr = fma(g_cw[g * MGG + r], cgi[r], corr);
-        }
-        const double xt = (rr0 - corr) * dinv;
-        double pxt = rr0 - sigma * xt - rb * xt;
-        double cgy = 0.0, cgw = 0.0;
-#pragma unroll
-        for (int r = 0; r < CMG; ++r) {
-          if (r < mg) {
-            pxt -= cgi[r] * g_rgz[g * MGG + r];
-            cgy = fma(cgi[r], g_yg[g * MGG + r], cgy);
-            cgw = fma(cgi[r], g_wg[g * MGG + r], cgw);
-          }
-        }
-        const double xn = alpha * xt + (1.0 - alpha) * x_h[i];
-        const double pxn = alpha * pxt + (1.0 - alpha) * Px_h[i];
-        const double qi = q_h[i];
-        double rr = sigma * xn - qi + cgw;
-        double cty = 0.0;
-        if (has_box) {
-          const double zh = alpha * xt + (1.0 - alpha) * zb_h[i];
-          const double zn = fmin(fmax(zh + yb_h[i] / rb, lo_h[i]), up_h[i]);
-          const double yn = yb_h[i] + rb * (zh - zn);
-          zb_h[i] = zn;
-          yb_h[i] = yn;
-          cty = yn;
-          rr += rb * zn - yn;
-          mv[0] = fmax(mv[0], fabs(xn - zn));
-          mv[1] = fmax(mv[1], fabs(xn));
-          mv[2] = fmax(mv[2], fabs(zn));
-        }
-        x_h[i] = xn;
-        Px_h[i] = pxn;
-        mv[4] = fmax(mv[4], fabs(pxn));
-        mv[6] = fmax(mv[6], fabs(qi));
-        const double cy = cty + cgy;
-        mv[3] = fmax(mv[3], fabs((pxn + qi + cty) + (cy - cty)));
-        mv[5] = fmax(mv[5], fabs(cy));
-        const double v = rr * dinv;
-        R_h[i] = rr;
-        muv = fma(mu_h[i], v, muv);
-#pragma unroll
-        for (int r = 0; r < CMG; ++r) cvp[r] = fma(cgi[r], v, cvp[r]);
-      }
-#pragma unroll
-      for (int e = 0; e < 7; ++e) mv[e] = cmax32(mv[e]);
-      muv = csum32(muv);
-#pragma unroll
-      for (int r = 0; r < CMG; ++r) cvp[r] = csum32(cvp[r]);
       const int it = g_it[g] + 1;
       int stat = PQ_UNSOLVED;
       const double eps_p = s.eps_abs + s.eps_rel * fmax(mv[1], mv[2]);
@@ -674,14 +755,12 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
         rn = fmin(fmax(rho * sqrt(rp / (rd + 1e-30)), s.rho_min), s.rho_max);
       }
       if (stat == PQ_UNSOLVED && it >= s.max_iter) stat = PQ_MAX_ITER;
-      if (hl == 0) {
-        g_it[g] = it;
-        g_stat[g] = stat;
-        g_act[g] = (stat == PQ_UNSOLVED) && it < g_end[g];
-        g_rn[g] = rn;
-        g_muv[g] = muv;
-        for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
-      }
+      g_it[g] = it;
+      g_stat[g] = stat;
+      g_act[g] = (stat == PQ_UNSOLVED) && it < g_end[g];
+      g_rn[g] = rn;
+      g_muv[g] = muv;
+      for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
     }
     __syncthreads();
     if (t == 0) {
@@ -711,6 +790,7 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       s_any = any;
     }
     __syncthreads();
+    CSTAMP(4);
   }
 
   // ---- write back ---------------------------------------------------------------------------
@@ -732,6 +812,14 @@ __global__ __launch_bounds__(CT) void k_admm_gcap(pq_lowrank lr, pq_problem pb, 
       st.y[(int64_t)b * st.m_ld + r] = g_yg[e];
     }
   }
+#ifdef PQ_PROFILE
+  if (t == 0) {   // phase times shared over the group's dates (tools/prof_polish.py --gcap)
+    for (int g = 0; g < G; ++g) {
+      double* dstp = st.work + (int64_t)(d0 + g) * st.work_stride + PQ_WORK_PROF(ld, st.mg_pad) + 16;
+      for (int k2 = 0; k2 < 5; ++k2) dstp[k2] += (double)pclk[k2] / G;
+    }
+  }
+#endif
 #undef GC_HPTRS
 }
 

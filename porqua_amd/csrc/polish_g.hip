@@ -218,114 +218,109 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
 }
 
 // ---------------------------------------------------------------------------------------
-// form: P_FF (lower tiles, diagonal tiles in full) into the date's K scratch (pitch ldk)
+// form: P_FF (lower 16x16 tiles, diagonal tiles in full) into the date's K scratch (pitch
+// ldk).  16-granular tiles: a free set of k needs only round16(k)^2 / 2 of MFMA work (a
+// 64-granular tiling computes up to 3x more for the typical k = 65..96), and the small
+// register footprint keeps several workgroups per CU to hide the gather latency.
 // ---------------------------------------------------------------------------------------
-template <int NB>
-__global__ __launch_bounds__(PT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, const double* rec,
+constexpr int FKCH = 16;            // window rows per staged chunk
+constexpr int FPIT = PG_KMAX + 4;   // LDS pitch (doubles)
+constexpr int FT = 512;             // threads (8 waves)
+constexpr int FNW = FT / 64;
+constexpr int FTW = 5;              // 16x16 tiles per wave (36 lower tiles for k <= 128)
+
+__global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, const double* rec,
                                                 int ldk) {
-  constexpr int PIT = NB * TB + 16;
-  constexpr int KCH = 16;   // window rows per staged chunk (one per 16-thread row group)
-  __shared__ __attribute__((aligned(16))) double S[2 * KCH * PIT];
+  __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPIT];
   const int b = blockIdx.x;
   const double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING) return;
   const int k = (int)R[R_K];
-  if (k <= (NB - 1) * TB || k > NB * TB) return;   // another instantiation's range
+  if (k > PG_KMAX) return;
   const int ld = pb.ld;
-  const int t = threadIdx.x, kr = t >> 4, c4 = (t & 15) * 4;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
   PGWork wk(st, b, ld);
   const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
   const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
   const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
   if (R[R_NZB] != 0.0)   // rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F  (pass 0 left it in pxb)
-    for (int p = t; p < k; p += PT) wk.rF[p] -= ps * wk.pxb[wk.Fl[p]];
+    for (int p = t; p < k; p += FT) wk.rF[p] -= ps * wk.pxb[wk.Fl[p]];
   const int T = lr.tlen[b];
   const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
-  int col[NB][4];
-  double mc[NB][4];
+  const int nt = (k + 15) >> 4, ntile = nt * (nt + 1) / 2;
+  const int kp = nt * 16;
+  // gather map: thread t -> window row t / 32 of a chunk, free columns (t % 32) + 32 c
+  const int gr = t >> 5, gc = t & 31;
+  int col[4];
+  double mc[4];
 #pragma unroll
-  for (int h = 0; h < NB; ++h)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int p = h * TB + c4 + e;
-      col[h][e] = p < k ? wk.Fl[p] : -1;
-      mc[h][e] = (col[h][e] >= 0 && mu) ? mu[col[h][e]] : 0.0;
-    }
-  double v[NB][4];
+  for (int c = 0; c < 4; ++c) {
+    const int p = gc + 32 * c;
+    col[c] = p < k ? wk.Fl[p] : -1;
+    mc[c] = (col[c] >= 0 && mu) ? mu[col[c]] : 0.0;
+  }
+  double v[4];
   auto gather = [&](int t0) {
-    const int tt = t0 + kr;
+    const int tt = t0 + gr;
     const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
 #pragma unroll
-    for (int h = 0; h < NB; ++h)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[h][e] = (row && col[h][e] >= 0) ? row[col[h][e]] - mc[h][e] : 0.0;
+    for (int c = 0; c < 4; ++c) v[c] = (row && col[c] >= 0) ? row[col[c]] - mc[c] : 0.0;
   };
   auto put = [&](double* Sb) {
 #pragma unroll
-    for (int h = 0; h < NB; ++h)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) Sb[kr * PIT + h * TB + c4 + e] = v[h][e];
+    for (int c = 0; c < 4; ++c)
+      if (gc + 32 * c < kp) Sb[gr * FPIT + gc + 32 * c] = v[c];
   };
-  constexpr int NT = NB * (NB + 1) / 2;
-  Acc acc[NT];
+  // this wave's tiles (I, J), I >= J, in column-major order of the lower triangle
+  int tI[FTW], tJ[FTW];
 #pragma unroll
-  for (int qq = 0; qq < NT; ++qq) acc[qq].zero();
-  const int l = lane_id(), w = wave_id();
-  const int i0 = (w >> 1) * 32 + (l & 15), j0 = (w & 1) * 32 + (l & 15), krd = l >> 4;
+  for (int j = 0; j < FTW; ++j) {
+    const int q = w + FNW * j;
+    int I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= q) ++I;
+    while (I * (I + 1) / 2 > q) --I;
+    tI[j] = I;
+    tJ[j] = q - I * (I + 1) / 2;
+  }
+  f64x4 acc[FTW];
+#pragma unroll
+  for (int j = 0; j < FTW; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
   auto mma = [&](const double* Sb) {
 #pragma unroll
-    for (int kk = 0; kk < KCH; kk += 4) {
-      const double* r = Sb + (kk + krd) * PIT;
-      double a[NB][2], bj[NB][2];
+    for (int kk = 0; kk < FKCH; kk += 4) {
+      const double* r = Sb + (kk + (l >> 4)) * FPIT + (l & 15);
 #pragma unroll
-      for (int h = 0; h < NB; ++h) {
-        a[h][0] = r[h * TB + i0];
-        a[h][1] = r[h * TB + i0 + 16];
-        bj[h][0] = r[h * TB + j0];
-        bj[h][1] = r[h * TB + j0 + 16];
-      }
-      int qq = 0;
-#pragma unroll
-      for (int I = 0; I < NB; ++I)
-#pragma unroll
-        for (int J = 0; J <= I; ++J, ++qq)
-#pragma unroll
-          for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int nn = 0; nn < 2; ++nn)
-              acc[qq].c[m][nn] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[I][m], bj[J][nn], acc[qq].c[m][nn], 0, 0, 0);
+      for (int j = 0; j < FTW; ++j)
+        if (w + FNW * j < ntile)
+          acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 * tI[j]], r[16 * tJ[j]], acc[j], 0, 0, 0);
     }
   };
   double* S0 = S;
-  double* S1 = S + KCH * PIT;
+  double* S1 = S + FKCH * FPIT;
   gather(0);
   put(S0);
   __syncthreads();
   int buf = 0;
-  for (int t0 = 0; t0 < T; t0 += KCH) {
-    const bool more = t0 + KCH < T;
-    if (more) gather(t0 + KCH);
+  for (int t0 = 0; t0 < T; t0 += FKCH) {
+    const bool more = t0 + FKCH < T;
+    if (more) gather(t0 + FKCH);
     mma(buf ? S1 : S0);
     if (more) put(buf ? S0 : S1);
     __syncthreads();
     buf ^= 1;
   }
   double* K = st.K + (int64_t)b * st.K_stride;
-  int qq = 0;
 #pragma unroll
-  for (int I = 0; I < NB; ++I)
+  for (int j = 0; j < FTW; ++j) {
+    if (w + FNW * j < ntile) {
 #pragma unroll
-    for (int J = 0; J <= I; ++J, ++qq)
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int nn = 0; nn < 2; ++nn)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int gi = I * TB + acc_row(m, r), gj = J * TB + acc_col(nn);
-            K[(int64_t)gi * ldk + gj] = psw * acc[qq].c[m][nn][r] + (gi == gj ? pd : 0.0);
-          }
+      for (int r = 0; r < 4; ++r) {
+        const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
+        K[(int64_t)gi * ldk + gj] = psw * acc[j][r] + (gi == gj ? pd : 0.0);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -941,8 +936,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax);
   hipLaunchKernelGGL(pq::k_pg_pass<0>, dim3(ngroups), dim3(pq::QT), 0, str, *lr, *pb, *st, rec, *s, gdates, urows,
                      ucnt, uoff, umax);
-  hipLaunchKernelGGL(pq::k_pg_form<1>, dim3(B), dim3(pq::PT), 0, str, *lr, *pb, *st, rec, ldk);
-  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_form<2>, dim3(B), dim3(pq::PT), 0, str, *lr, *pb, *st, rec, ldk);
+  hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
   hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 0);
   if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 64);
   if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 96);

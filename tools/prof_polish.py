@@ -35,18 +35,19 @@ def main():
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)
     lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
     ws = engine.Workspace(qb, dense=False)
-    gp = engine.GroupPlan(rows, tlen, dev) if "--group" in sys.argv else None
+    gp = engine.GroupPlan(rows, tlen, dev) if ("--group" in sys.argv or "--gcap" in sys.argv) else None
     off = (9 + ws.mg_pad) * qb.ld   # PQ_WORK_PROF
     for _ in range(2):
         ev = []
         ws.work[:, off + 16:off + 24].zero_()
-        res = engine.solve_lowrank(qb, lr, engine.Settings(), ws, events=ev, groups=gp)
+        res = engine.solve_lowrank(qb, lr, engine.Settings(), ws, events=ev, groups=gp, gcap="--gcap" in sys.argv)
         torch.cuda.synchronize()
-    ad = ws.work[:, off + 16:off + 24].cpu().numpy() * 10e-3
+    ad = ws.work[:, off + 16:off + 24].cpu().numpy() * 10e-3   # wall_clock64 ticks (100 MHz) -> us
     its = res.iters.cpu().numpy().astype(float)
     atot = ad.sum(1)
     if gp is not None:
-        names = ["pass 1 (MFMA)", "M^-1 symv", "pass 2 (MFMA)", "updates/resid/rhs"]
+        names = (["pass 1 (MFMA)", "M_U^-1 GEMM", "per-date Woodbury", "pass 2 (MFMA)", "updates/resid/rhs"]
+                 if "--gcap" in sys.argv else ["pass 1 (MFMA)", "M^-1 symv", "pass 2 (MFMA)", "updates/resid/rhs"])
         print("grouped admm, chip-wide ms per phase (sum over groups / 256 CUs):")
         for i, p in enumerate(names):
             print("  %-18s %8.2f ms" % (p, ad[:, i].sum() / 256 / 1e3))
