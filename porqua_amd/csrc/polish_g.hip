@@ -126,6 +126,9 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
     R[R_K] = 0;
     R[R_NZB] = 0;
   }
+#ifdef PQ_PROFILE
+  if (t >= 8 && t < 20) R[t] = 0.0;
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -324,249 +327,283 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
 }
 
 // ---------------------------------------------------------------------------------------
-// LDS-resident packed Cholesky and triangular solves (k <= KS, 256 threads)
+// solve, one WAVE per date: factor P_FF + delta I in LDS, Schur complement of the active
+// rows, proximal iterative refinement -- wave-synchronous (no block barriers, no idle waves
+// waiting on the serial pivot chain); the concurrency comes from several dates per CU
+// (LDS: one packed triangle per date).  Same arithmetic as polish_w.hip's compact mode.
 // ---------------------------------------------------------------------------------------
-// Lp holds the lower triangle row by row (element (r, c) at r (r + 1) / 2 + c).  16-column
-// panels: wave 0 factors the 16 x 16 diagonal block in registers (lane i = row i, pivot
-// values exchanged by shuffles), every thread solves one row of the panel below it, and
-// the trailing lower triangle is updated with 16x16x4 FP64 MFMA tiles spread over the
-// waves.  Returns 0 or the failing column + 1 (uniform).
-__device__ int lds_potrf(double* Lp, int k, int* flag) {
-  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+#define WSYNC()                                                   \
+  do {                                                            \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");        \
+    __builtin_amdgcn_wave_barrier();                              \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");        \
+  } while (0)
+
+constexpr int WMA = 8;   // active general rows handled by the wave solve (more: fallback)
+
+// Packed lower Cholesky by one wave.  16-column panels: the 16x16 diagonal block lives in
+// registers in the MFMA C layout (lane l: rows l>>4 + 4q of column l&15, both triangles);
+// each pivot step reads the pivot, row kk and column kk by cross-lane shuffles (uniform, no
+// LDS round trip) and updates the trailing block in registers; the block's inverse follows
+// by forward substitution on the identity in the same layout and REPLACES L11 in Lp (the
+// solves and the panel below use only the inverse).  The panel below is L21 = A21 L11^-T
+// and the trailing update A22 -= L21 L21', both 16x16x4 MFMA tiles by the same wave.
+__device__ __forceinline__ double sel4(const double (&v)[4], int i) {
+  return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
+}
+
+__device__ int w_potrf(double* Lp, int k) {
+  const int l = lane_id();
+  const int cc = l & 15, gg = l >> 4;
   for (int p0 = 0; p0 < k; p0 += 16) {
     const int nb = min(16, k - p0);
-    __syncthreads();
-    if (w == 0) {
-      const int i = l;
-      double r[16];
+    // the 16x16 diagonal block in the MFMA C layout: lane l holds A[gg + 4q][cc], q = 0..3,
+    // both triangles (padding rows/cols beyond nb are the identity)
+    double A[4], Bv[4];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) r[j] = (i < nb && j <= i) ? Lp[pk(p0 + i, p0 + j)] : 0.0;
-      int bad = 0;
+    for (int q = 0; q < 4; ++q) {
+      const int r = gg + 4 * q;
+      A[q] = (r < nb && cc < nb) ? (cc <= r ? Lp[pk(p0 + r, p0 + cc)] : Lp[pk(p0 + cc, p0 + r)])
+                                 : (r == cc ? 1.0 : 0.0);
+      Bv[q] = (r == cc) ? 1.0 : 0.0;
+    }
+    int bad = 0;
+    // right-looking Cholesky: pivot, column and row kk by cross-lane shuffles (uniform: no
+    // divergence), the symmetric trailing update in registers
+#pragma unroll 1
+    for (int kk = 0; kk < 16; ++kk) {
+      const double akk = sel4(A, kk >> 2);
+      const double piv = __shfl(akk, ((kk & 3) << 4) | kk, 64);
+      const double rowk = __shfl(akk, ((kk & 3) << 4) | cc, 64);   // A[kk][cc] = A[cc][kk]
+      if (!(piv > 0.0) || !isfinite(piv)) bad = 1;
+      const double rs = 1.0 / sqrt(piv);
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        if (kk < nb && !bad) {
-          const double d = __shfl(r[kk], kk, 64);
-          if (!(d > 0.0) || !isfinite(d)) {
-            bad = p0 + kk + 1;
-          } else {
-            const double sd = sqrt(d);
-            const double lik = (i > kk) ? r[kk] / sd : (i == kk ? sd : 0.0);
-            r[kk] = lik;
+      for (int q = 0; q < 4; ++q) {
+        const int r = gg + 4 * q;
+        const double colr = __shfl(A[q], (gg << 4) | kk, 64);            // A[r][kk]
+        if (cc == kk && r >= kk) A[q] = colr * rs;
+        else if (cc > kk && r > kk) A[q] = fma(-colr * rs, rowk * rs, A[q]);
+      }
+    }
+    if (bad) return p0 + 1;
+    // L11^-1 by forward substitution on the identity, same layout
+#pragma unroll 1
+    for (int kk = 0; kk < 16; ++kk) {
+      const double lkk = __shfl(sel4(A, kk >> 2), ((kk & 3) << 4) | kk, 64);
+      const double rl = 1.0 / lkk;
+      const double bk = __shfl(sel4(Bv, kk >> 2), ((kk & 3) << 4) | cc, 64) * rl;   // final row kk
 #pragma unroll
-            for (int j = kk + 1; j < 16; ++j) {
-              const double ljk = __shfl(lik, j, 64);
-              if (j <= i) r[j] = fma(-lik, ljk, r[j]);
-            }
+      for (int q = 0; q < 4; ++q) {
+        const int r = gg + 4 * q;
+        const double lr_ = __shfl(A[q], (gg << 4) | kk, 64);             // L[r][kk]
+        if (r == kk) Bv[q] = bk;
+        else if (r > kk) Bv[q] = fma(-lr_, bk, Bv[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // the diagonal block now holds L11^-1
+      const int r = gg + 4 * q;
+      if (r < nb && cc <= r) Lp[pk(p0 + r, p0 + cc)] = Bv[q];
+    }
+    WSYNC();
+    const int j16 = l & 15, kq = l >> 4;
+    for (int r1 = p0 + 16; r1 < k; r1 += 16) {   // L21 = A21 L11^-T
+      const int ri = r1 + j16;
+      f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int kc = 4 * s4 + kq;
+        const double av = (ri < k && kc < nb) ? Lp[pk(ri, p0 + kc)] : 0.0;
+        const double bv = (kc <= j16 && j16 < nb) ? Lp[pk(p0 + j16, p0 + kc)] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int gr = r1 + kq + 4 * rr;
+        if (gr < k && j16 < nb) Lp[pk(gr, p0 + j16)] = acc[rr];
+      }
+      WSYNC();
+    }
+    const int q0 = p0 + 16;
+    if (q0 < k) {   // A22 -= L21 L21' (lower 16x16 tiles)
+      const int nt = (k - q0 + 15) >> 4;
+      for (int I = 0; I < nt; ++I)
+        for (int J = 0; J <= I; ++J) {
+          const int ri = q0 + 16 * I + j16, cj = q0 + 16 * J + j16;
+          f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int kc = p0 + 4 * s4 + kq;
+            const double av = ri < k ? Lp[pk(ri, kc)] : 0.0;
+            const double bv = cj < k ? Lp[pk(cj, kc)] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int gr = q0 + 16 * I + kq + 4 * rr, gc = q0 + 16 * J + j16;
+            if (gr < k && gc <= gr) Lp[pk(gr, gc)] -= acc[rr];
           }
         }
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (i < nb && j <= i) Lp[pk(p0 + i, p0 + j)] = r[j];
-      if (l == 0) *flag = bad;
-    }
-    __syncthreads();
-    const int bad = *flag;
-    if (bad) return bad;
-    for (int r = p0 + nb + t; r < k; r += PT) {   // panel rows below the diagonal block
-      double* lr_ = Lp + pk(r, p0);                   // row r, panel columns (no register arrays)
-#pragma unroll 1
-      for (int j = 0; j < nb; ++j) {
-        const double* lj = Lp + pk(p0 + j, p0);
-        double v = lr_[j];
-#pragma unroll 4
-        for (int m = 0; m < j; ++m) v = fma(-lr_[m], lj[m], v);
-        lr_[j] = v / lj[j];
-      }
-    }
-    __syncthreads();
-    const int q0 = p0 + 16;
-    if (q0 < k) {   // trailing update A22 -= L21 L21' (lower 16x16 tiles)
-      const int nt = (k - q0 + 15) >> 4;
-      const int ntile = nt * (nt + 1) / 2;
-      for (int tile = w; tile < ntile; tile += PW) {
-        int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-        while ((I + 1) * (I + 2) / 2 <= tile) ++I;
-        while (I * (I + 1) / 2 > tile) --I;
-        const int J = tile - I * (I + 1) / 2;
-        const int ri = q0 + 16 * I + (l & 15), cj = q0 + 16 * J + (l & 15);
-        f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int kc = p0 + 4 * s4 + (l >> 4);
-          const double av = ri < k ? Lp[pk(ri, kc)] : 0.0;
-          const double bv = cj < k ? Lp[pk(cj, kc)] : 0.0;
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int gr = q0 + 16 * I + (l >> 4) + 4 * rr, gc = q0 + 16 * J + (l & 15);
-          if (gr < k && gc <= gr) Lp[pk(gr, gc)] -= acc[rr];
-        }
-      }
+      WSYNC();
     }
   }
-  __syncthreads();
   return 0;
 }
 
-// y <- L^-1 y (in place, k entries in LDS)
-__device__ void lds_fwd(const double* Lp, int k, double* y) {
-  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+// yo <- L^-1 y (y consumed), one wave; diagonal blocks of Lp hold their inverses
+__device__ void w_fwd(const double* Lp, int k, double* y, double* yo) {
+  const int l = lane_id();
   for (int p0 = 0; p0 < k; p0 += 16) {
     const int nb = min(16, k - p0);
-    __syncthreads();
-    if (w == 0) {
-      const int i = l;
-      double v = i < nb ? y[p0 + i] : 0.0;
-      const double dii = i < nb ? Lp[pk(p0 + i, p0 + i)] : 1.0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (j < nb) {
-          const double yj = __shfl(v / dii, j, 64);
-          if (i > j && i < nb) v = fma(-Lp[pk(p0 + i, p0 + j)], yj, v);
-        }
-      }
-      if (i < nb) y[p0 + i] = v / dii;
+    if (l < nb) {
+      double v = 0.0;
+      for (int m = 0; m <= l; ++m) v = fma(Lp[pk(p0 + l, p0 + m)], y[p0 + m], v);
+      yo[p0 + l] = v;
     }
-    __syncthreads();
-    for (int r = p0 + nb + t; r < k; r += PT) {
+    WSYNC();
+    for (int r = p0 + nb + l; r < k; r += 64) {
       double v = y[r];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j < nb) v = fma(-Lp[pk(r, p0 + j)], y[p0 + j], v);
+      const double* lr_ = Lp + pk(r, p0);
+#pragma unroll 4
+      for (int j = 0; j < nb; ++j) v = fma(-lr_[j], yo[p0 + j], v);
       y[r] = v;
     }
+    WSYNC();
   }
-  __syncthreads();
 }
 
-// y <- L^-T y (in place)
-__device__ void lds_bwd(const double* Lp, int k, double* y) {
-  const int t = threadIdx.x, w = wave_id(), l = lane_id();
-  const int nblk = (k + 15) >> 4;
-  for (int B = nblk - 1; B >= 0; --B) {
+// xo <- L^-T y (y consumed)
+__device__ void w_bwd(const double* Lp, int k, double* y, double* xo) {
+  const int l = lane_id();
+  for (int B = ((k + 15) >> 4) - 1; B >= 0; --B) {
     const int p0 = 16 * B, nb = min(16, k - p0);
-    __syncthreads();
-    if (w == 0) {
-      const int i = l;
-      double v = i < nb ? y[p0 + i] : 0.0;
-      const double dii = i < nb ? Lp[pk(p0 + i, p0 + i)] : 1.0;
-#pragma unroll
-      for (int j = 15; j >= 0; --j) {
-        if (j < nb) {
-          const double xj = __shfl(v / dii, j, 64);
-          if (i < j) v = fma(-Lp[pk(p0 + j, p0 + i)], xj, v);
-        }
-      }
-      if (i < nb) y[p0 + i] = v / dii;
+    if (l < nb) {
+      double v = 0.0;
+      for (int m = l; m < nb; ++m) v = fma(Lp[pk(p0 + m, p0 + l)], y[p0 + m], v);
+      xo[p0 + l] = v;
     }
-    __syncthreads();
-    for (int c = t; c < p0; c += PT) {
+    WSYNC();
+    for (int c = l; c < p0; c += 64) {
       double v = y[c];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j < nb) v = fma(-Lp[pk(p0 + j, c)], y[p0 + j], v);
+#pragma unroll 4
+      for (int j = 0; j < nb; ++j) v = fma(-Lp[pk(p0 + j, c)], xo[p0 + j], v);
       y[c] = v;
     }
+    WSYNC();
   }
-  __syncthreads();
 }
 
-// ---------------------------------------------------------------------------------------
-// solve: factor P_FF + delta I in LDS, Schur complement of the active rows, refinement
-// ---------------------------------------------------------------------------------------
 template <int KS>
-__global__ __launch_bounds__(PT) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(128))) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
                                                  int klo) {
   constexpr int NP = KS * (KS + 1) / 2;
   __shared__ double Lp[NP];
-  __shared__ double xF[KS], t1[KS], rx[KS];
-  __shared__ double Sm[PG_MGMAX * PG_MGMAX];
-  __shared__ double lamv[PG_MGMAX], wl[PG_MGMAX], rl[PG_MGMAX], dAv[PG_MGMAX];
-  __shared__ int s_al[PG_MGMAX];
-  __shared__ int flag;
-  __shared__ double red[16];
+  __shared__ double xF[KS], t1[KS], t2[KS], rx[KS];
+  __shared__ double Sm[WMA * WMA], lamv[WMA], wl[WMA], rl[WMA], dAv[WMA];
+  __shared__ int s_al[WMA];
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING) return;
   const int k = (int)R[R_K];
   if (k <= klo || k > KS) return;
   const int ma = (int)R[R_MA];
-  const int n = pb.n, ld = pb.ld, mg = pb.mg;
-  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  if (ma > WMA) {
+    if (threadIdx.x == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  const int n = pb.n, ld = pb.ld;
+  const int l = lane_id();
   const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
   PGWork wk(st, b, ld);
   const double sc = R[R_SC];
   const double delta = s.delta * sc;
   const double* K = st.K + (int64_t)b * st.K_stride;   // P_FF (lower), kept for the residuals
-  for (int r = w; r < k; r += PW)
-    for (int c = l; c <= r; c += 64) Lp[pk(r, c)] = K[(int64_t)r * ldk + c] + (r == c ? delta : 0.0);
-  for (int p = t; p < k; p += PT) xF[p] = wk.solx[p];
-  if (t < ma) {
-    s_al[t] = (int)R[R_AL + t];
-    lamv[t] = R[R_SOL + t];
-    dAv[t] = R[R_DA + t];
+#ifdef PQ_PROFILE
+  long long t_last_ = wall_clock64();
+#define WSTAMP(k_)                                                         \
+  do {                                                                     \
+    WSYNC();                                                               \
+    if (l == 0) { const long long n_ = wall_clock64(); R[8 + (k_)] += (double)(n_ - t_last_); t_last_ = n_; } \
+  } while (0)
+#else
+#define WSTAMP(k_) do { } while (0)
+#endif
+  {   // packed triangle, flat index (independent loads, 64 per trip)
+    const int np_ = k * (k + 1) / 2;
+    int r = 0, e0 = 0;   // row of element l: advance incrementally
+    for (int e = l; e < np_; e += 64) {
+      while (e >= e0 + r + 1) { e0 += r + 1; ++r; }
+      const int c = e - e0;
+      Lp[e] = K[(int64_t)r * ldk + c] + (r == c ? delta : 0.0);
+    }
   }
-  if (lds_potrf(Lp, k, &flag)) {
-    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+  for (int p = l; p < k; p += 64) xF[p] = wk.solx[p];
+  if (l < ma) {
+    s_al[l] = (int)R[R_AL + l];
+    lamv[l] = R[R_SOL + l];
+    dAv[l] = R[R_DA + l];
+  }
+  WSTAMP(0);
+  if (w_potrf(Lp, k)) {
+    if (l == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
-  // U = L^-1 C_aF' (column a -> row a of the global U scratch), S = U'U + delta I
+  WSTAMP(1);
+  // U = L^-1 C_aF' (row a of the global U scratch), S = U'U + delta I
   for (int a = 0; a < ma; ++a) {
     const double* cr = Cg + (int64_t)s_al[a] * ld;
-    for (int p = t; p < k; p += PT) t1[p] = cr[wk.Fl[p]];
-    lds_fwd(Lp, k, t1);
-    for (int p = t; p < k; p += PT) wk.U[(int64_t)a * ld + p] = t1[p];
+    for (int p = l; p < k; p += 64) t1[p] = cr[wk.Fl[p]];
+    WSYNC();
+    w_fwd(Lp, k, t1, t2);
+    for (int p = l; p < k; p += 64) wk.U[(int64_t)a * ld + p] = t2[p];
   }
-  __syncthreads();
-  for (int e = w; e < ma * ma; e += PW) {
-    const int i = e / ma, j = e % ma;
-    if (j > i) continue;
-    const double* ui = wk.U + (int64_t)i * ld;
-    const double* uj = wk.U + (int64_t)j * ld;
+  WSYNC();
+  for (int e = 0; e < ma * ma; ++e) {
+    const int ii = e / ma, jj = e % ma;
+    if (jj > ii) continue;
+    const double* ui = wk.U + (int64_t)ii * ld;
+    const double* uj = wk.U + (int64_t)jj * ld;
     double sum = 0.0;
     for (int p = l; p < k; p += 64) sum += ui[p] * uj[p];
     sum = wave_sum(sum);
-    if (l == 0) Sm[i * PG_MGMAX + j] = sum + (i == j ? delta : 0.0);
+    if (l == 0) Sm[ii * WMA + jj] = sum + (ii == jj ? delta : 0.0);
   }
-  __syncthreads();
-  if (t == 0) {   // tiny Cholesky of S (ma <= 32), one thread
-    int bad = 0;
-    for (int c = 0; c < ma && !bad; ++c) {
-      double d = Sm[c * PG_MGMAX + c];
-      for (int m = 0; m < c; ++m) d -= Sm[c * PG_MGMAX + m] * Sm[c * PG_MGMAX + m];
-      if (!(d > 0.0) || !isfinite(d)) { bad = 1; break; }
+  WSYNC();
+  int sbad = 0;
+  if (l == 0) {   // tiny Cholesky of S (ma <= 8), one lane
+    for (int c = 0; c < ma && !sbad; ++c) {
+      double d = Sm[c * WMA + c];
+      for (int m = 0; m < c; ++m) d -= Sm[c * WMA + m] * Sm[c * WMA + m];
+      if (!(d > 0.0) || !isfinite(d)) { sbad = 1; break; }
       d = sqrt(d);
-      Sm[c * PG_MGMAX + c] = d;
+      Sm[c * WMA + c] = d;
       for (int r = c + 1; r < ma; ++r) {
-        double v = Sm[r * PG_MGMAX + c];
-        for (int m = 0; m < c; ++m) v -= Sm[r * PG_MGMAX + m] * Sm[c * PG_MGMAX + m];
-        Sm[r * PG_MGMAX + c] = v / d;
+        double v = Sm[r * WMA + c];
+        for (int m = 0; m < c; ++m) v -= Sm[r * WMA + m] * Sm[c * WMA + m];
+        Sm[r * WMA + c] = v / d;
       }
     }
-    flag = bad;
   }
-  __syncthreads();
-  if (flag) {
-    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+  sbad = __shfl(sbad, 0, 64);
+  if (sbad) {
+    if (l == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
+  WSTAMP(2);
   // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------
   for (int itr = 0; itr < s.refine_iters; ++itr) {
-    // rx = rF - P_FF x - C_aF' lam ;  rl = dA - C_aF x
-    for (int p = w; p < k; p += PW) {
+    // rx = rF - P_FF x - C_aF' lam  (lane per row, P_FF from the K scratch)
+    for (int p = l; p < k; p += 64) {
       double sum = 0.0;
-      for (int qq = l; qq < k; qq += 64)
-        sum += (qq <= p ? K[(int64_t)p * ldk + qq] : K[(int64_t)qq * ldk + p]) * xF[qq];
-      sum = wave_sum(sum);
-      if (l == 0) {
-        double v = wk.rF[p] - sum;
-        for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + wk.Fl[p]] * lamv[a];
-        rx[p] = v;
-      }
+      const double* kp_ = K + (int64_t)p * ldk;
+      for (int qq = 0; qq <= p; ++qq) sum = fma(kp_[qq], xF[qq], sum);
+      for (int qq = p + 1; qq < k; ++qq) sum = fma(K[(int64_t)qq * ldk + p], xF[qq], sum);
+      double v = wk.rF[p] - sum;
+      const int fp = wk.Fl[p];
+      for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + fp] * lamv[a];
+      rx[p] = v;
     }
-    for (int a = w; a < ma; a += PW) {
+    for (int a = 0; a < ma; ++a) {
       const double* cr = Cg + (int64_t)s_al[a] * ld;
       double sum = 0.0;
       for (int p = l; p < k; p += 64) sum += cr[wk.Fl[p]] * xF[p];
@@ -576,60 +613,63 @@ __global__ __launch_bounds__(PT) void k_pg_solve(pq_problem pb, pq_state st, dou
         rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dAv[a]) + fabs(sum)) ? 0.0 : v;
       }
     }
-    __syncthreads();
-    {
-      double rm = 0.0;
-      for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
-      if (t < ma) rm = fmax(rm, fabs(rl[t]));
-      if (block_max(rm, red) <= 1e-13 * sc) break;
-    }
-    for (int p = t; p < k; p += PT) t1[p] = rx[p];
-    lds_fwd(Lp, k, t1);
-    for (int a = w; a < ma; a += PW) {   // wl = U' t1 - rl
+    WSYNC();
+    WSTAMP(3);
+    double rm = 0.0;
+    for (int p = l; p < k; p += 64) rm = fmax(rm, fabs(rx[p]));
+    if (l < ma) rm = fmax(rm, fabs(rl[l]));
+    if (wave_max(rm) <= 1e-13 * sc) break;
+    for (int p = l; p < k; p += 64) t1[p] = rx[p];
+    WSYNC();
+    w_fwd(Lp, k, t1, t2);   // t2 = L^-1 rx
+    for (int a = 0; a < ma; ++a) {   // wl = U' t2 - rl
       const double* ua = wk.U + (int64_t)a * ld;
       double sum = 0.0;
-      for (int p = l; p < k; p += 64) sum += ua[p] * t1[p];
+      for (int p = l; p < k; p += 64) sum += ua[p] * t2[p];
       sum = wave_sum(sum);
       if (l == 0) wl[a] = sum - rl[a];
     }
-    __syncthreads();
-    if (t == 0) {   // dlam = S^-1 wl
-      for (int i = 0; i < ma; ++i) {
-        double v = wl[i];
-        for (int j = 0; j < i; ++j) v -= Sm[i * PG_MGMAX + j] * wl[j];
-        wl[i] = v / Sm[i * PG_MGMAX + i];
+    WSYNC();
+    if (l == 0) {   // dlam = S^-1 wl
+      for (int ii = 0; ii < ma; ++ii) {
+        double v = wl[ii];
+        for (int jj = 0; jj < ii; ++jj) v -= Sm[ii * WMA + jj] * wl[jj];
+        wl[ii] = v / Sm[ii * WMA + ii];
       }
-      for (int i = ma - 1; i >= 0; --i) {
-        double v = wl[i];
-        for (int j = i + 1; j < ma; ++j) v -= Sm[j * PG_MGMAX + i] * wl[j];
-        wl[i] = v / Sm[i * PG_MGMAX + i];
+      for (int ii = ma - 1; ii >= 0; --ii) {
+        double v = wl[ii];
+        for (int jj = ii + 1; jj < ma; ++jj) v -= Sm[jj * WMA + ii] * wl[jj];
+        wl[ii] = v / Sm[ii * WMA + ii];
       }
     }
-    __syncthreads();
-    for (int p = t; p < k; p += PT) {
-      double v = t1[p];
+    WSYNC();
+    for (int p = l; p < k; p += 64) {
+      double v = t2[p];
       for (int a = 0; a < ma; ++a) v -= wk.U[(int64_t)a * ld + p] * wl[a];
       t1[p] = v;
     }
-    lds_bwd(Lp, k, t1);
-    for (int p = t; p < k; p += PT) xF[p] += t1[p];
-    if (t < ma) lamv[t] += wl[t];
-    __syncthreads();
+    WSYNC();
+    w_bwd(Lp, k, t1, t2);   // t2 = L^-T (t2 - U dlam)
+    for (int p = l; p < k; p += 64) xF[p] += t2[p];
+    if (l < ma) lamv[l] += wl[l];
+    WSYNC();
+    WSTAMP(4);
   }
   // ---- expand: xs = x_B off F, x_F on F; general multipliers by row ------------------------
-  for (int i = t; i < n; i += PT) wk.xs[i] = wk.xb[i];
-  __syncthreads();
-  for (int p = t; p < k; p += PT) {
+  for (int ii = l; ii < n; ii += 64) wk.xs[ii] = wk.xb[ii];
+  WSYNC();
+  for (int p = l; p < k; p += 64) {
     wk.xs[wk.Fl[p]] = xF[p];
     wk.solx[p] = xF[p];
   }
-  if (t < 64) R[R_LAM + t] = 0.0;
-  __syncthreads();
-  if (t < ma) {
-    R[R_LAM + s_al[t]] = lamv[t];
-    R[R_SOL + t] = lamv[t];
+  R[R_LAM + l] = 0.0;   // 64 lanes clear the 64 row slots
+  WSYNC();
+  if (l < ma) {
+    R[R_LAM + s_al[l]] = lamv[l];
+    R[R_SOL + l] = lamv[l];
   }
-  (void)mg;
+  WSTAMP(5);
+#undef WSTAMP
 }
 
 // ---------------------------------------------------------------------------------------
@@ -937,9 +977,12 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   hipLaunchKernelGGL(pq::k_pg_pass<0>, dim3(ngroups), dim3(pq::QT), 0, str, *lr, *pb, *st, rec, *s, gdates, urows,
                      ucnt, uoff, umax);
   hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
-  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 0);
-  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 64);
-  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, *s, ldk, 96);
+  // one wave per date, the LDS triangle sized to the free set (more dates per CU when small)
+  hipLaunchKernelGGL(pq::k_pg_solve<48>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 0);
+  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 48);
+  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 64);
+  if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 80);
+  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 96);
   hipLaunchKernelGGL(pq::k_pg_pass<1>, dim3(ngroups), dim3(pq::QT), 0, str, *lr, *pb, *st, rec, *s, gdates, urows,
                      ucnt, uoff, umax);
   PQ_CHECK_LAUNCH("pq_polish_grouped_round");

@@ -60,6 +60,16 @@ def main():
     print("polish us per problem: mean %.1f  p50 %.1f  p90 %.1f" % (tot.mean(), np.median(tot), np.percentile(tot, 90)))
     for i, p in enumerate(PHASES):
         print("  %-16s %8.1f us  (%4.1f %%)" % (p, prof[:, i].mean(), 100 * prof[:, i].mean() / tot.mean()))
+    if "--gcap" in sys.argv or "--group" in sys.argv:
+        rec = ws.pg_record()[:, 8:14].cpu().numpy() * 10e-3
+        done = ws.pg_record()[:, 4].cpu().numpy()
+        print("grouped polish solve kernel, us per date (sum over rounds), mean over dates:")
+        for i, nm in enumerate(["load P_FF", "potrf", "U + S", "residual", "solves", "write back"]):
+            print("  %-12s %8.1f us" % (nm, rec[:, i].mean()))
+        print("  rounds mean %.2f" % done.mean())
+        pp = ws.pg_record()[:, 16:19].cpu().numpy() * 10e-3
+        for i, nm in enumerate(["potrf: diag 16x16", "potrf: panel trsm", "potrf: MFMA update"]):
+            print("  %-20s %8.1f us" % (nm, pp[:, i].mean()))
     for name, a, b in ev:
         print("stage", name, "%.1f ms" % a.elapsed_time(b))
     out = res.out.cpu().numpy()
