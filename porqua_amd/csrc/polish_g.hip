@@ -221,7 +221,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
 }
 
 // ---------------------------------------------------------------------------------------
-// form: P_FF (lower 16x16 tiles, diagonal tiles in full) into the date's K scratch (pitch
+// form: P_FF (both triangles, from the lower 16x16 tiles) into the date's K scratch (pitch
 // ldk).  16-granular tiles: a free set of k needs only round16(k)^2 / 2 of MFMA work (a
 // 64-granular tiling computes up to 3x more for the typical k = 65..96), and the small
 // register footprint keeps several workgroups per CU to hide the gather latency.
@@ -320,7 +320,9 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
-        K[(int64_t)gi * ldk + gj] = psw * acc[j][r] + (gi == gj ? pd : 0.0);
+        const double v = psw * acc[j][r] + (gi == gj ? pd : 0.0);
+        K[(int64_t)gi * ldk + gj] = v;
+        if (tI[j] != tJ[j]) K[(int64_t)gj * ldk + gi] = v;   // both triangles: column reads in the solve
       }
     }
   }
@@ -348,12 +350,53 @@ constexpr int WMA = 8;   // active general rows handled by the wave solve (more:
 // by forward substitution on the identity in the same layout and REPLACES L11 in Lp (the
 // solves and the panel below use only the inverse).  The panel below is L21 = A21 L11^-T
 // and the trailing update A22 -= L21 L21', both 16x16x4 MFMA tiles by the same wave.
-__device__ __forceinline__ double sel4(const double (&v)[4], int i) {
-  return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
 }
 
-__device__ int w_potrf(double* Lp, int k) {
+// lane (l & ~15) | k of every 16-lane row (DPP row_newbcast; k folds to an immediate in
+// unrolled loops)
+template <int K>
+__device__ __forceinline__ double row_bcast16_k(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + K, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + K, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double row_bcast16(double v, int k) {
+  switch (k) {
+    case 0: return row_bcast16_k<0>(v);
+    case 1: return row_bcast16_k<1>(v);
+    case 2: return row_bcast16_k<2>(v);
+    case 3: return row_bcast16_k<3>(v);
+    case 4: return row_bcast16_k<4>(v);
+    case 5: return row_bcast16_k<5>(v);
+    case 6: return row_bcast16_k<6>(v);
+    case 7: return row_bcast16_k<7>(v);
+    case 8: return row_bcast16_k<8>(v);
+    case 9: return row_bcast16_k<9>(v);
+    case 10: return row_bcast16_k<10>(v);
+    case 11: return row_bcast16_k<11>(v);
+    case 12: return row_bcast16_k<12>(v);
+    case 13: return row_bcast16_k<13>(v);
+    case 14: return row_bcast16_k<14>(v);
+    default: return row_bcast16_k<15>(v);
+  }
+}
+
+__device__ int w_potrf(double* Lp, int k, double* prof = nullptr) {
   const int l = lane_id();
+#ifdef PQ_PROFILE
+  long long tp_ = wall_clock64();
+#define WP_STAMP(k_)                                                                  \
+  do {                                                                                \
+    WSYNC();                                                                          \
+    if (l == 0 && prof) { const long long n_ = wall_clock64(); prof[k_] += (double)(n_ - tp_); tp_ = n_; } \
+  } while (0)
+#else
+#define WP_STAMP(k_) do { } while (0)
+#endif
   const int cc = l & 15, gg = l >> 4;
   for (int p0 = 0; p0 < k; p0 += 16) {
     const int nb = min(16, k - p0);
@@ -368,44 +411,44 @@ __device__ int w_potrf(double* Lp, int k) {
       Bv[q] = (r == cc) ? 1.0 : 0.0;
     }
     int bad = 0;
-    // right-looking Cholesky: pivot, column and row kk by cross-lane shuffles (uniform: no
-    // divergence), the symmetric trailing update in registers
-#pragma unroll 1
+    // right-looking Cholesky with the inverse built in the same pass (one serial chain of 16
+    // steps): the pivot by readlane, row kk by one cross-lane permute, column kk by a DPP row
+    // broadcast (lane kk of every 16-lane row); the symmetric trailing update and the
+    // inverse's row operations stay in registers
+#pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
-      const double akk = sel4(A, kk >> 2);
-      const double piv = __shfl(akk, ((kk & 3) << 4) | kk, 64);
-      const double rowk = __shfl(akk, ((kk & 3) << 4) | cc, 64);   // A[kk][cc] = A[cc][kk]
+      const int src = ((kk & 3) << 4);
+      const double akk = A[kk >> 2];
+      const double piv = readlane_f64(akk, src | kk);
+      const double rowk = __shfl(akk, src | cc, 64);                   // A[kk][cc] = A[cc][kk]
+      const double bkr = __shfl(Bv[kk >> 2], src | cc, 64);            // row kk of the inverse, unscaled
+      double colv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) colv[q] = row_bcast16(A[q], kk);     // A[gg + 4q][kk]
       if (!(piv > 0.0) || !isfinite(piv)) bad = 1;
-      const double rs = 1.0 / sqrt(piv);
+      double rs = __builtin_amdgcn_rsq(piv);                           // 1/sqrt, two Newton steps
+      rs = rs * fma(-0.5 * piv * rs, rs, 1.5);
+      rs = rs * fma(-0.5 * piv * rs, rs, 1.5);
+      const double bk = bkr * rs;                                      // final row kk of L11^-1
+      const double lck = rowk * rs;                                    // L[cc][kk]
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = gg + 4 * q;
-        const double colr = __shfl(A[q], (gg << 4) | kk, 64);            // A[r][kk]
-        if (cc == kk && r >= kk) A[q] = colr * rs;
-        else if (cc > kk && r > kk) A[q] = fma(-colr * rs, rowk * rs, A[q]);
+        const double lrk = colv[q] * rs;                               // L[r][kk]
+        if (cc == kk && r >= kk) A[q] = lrk;
+        else if (cc > kk && r > kk) A[q] = fma(-lrk, lck, A[q]);
+        if (r == kk) Bv[q] = bk;
+        else if (r > kk) Bv[q] = fma(-lrk, bk, Bv[q]);
       }
     }
     if (bad) return p0 + 1;
-    // L11^-1 by forward substitution on the identity, same layout
-#pragma unroll 1
-    for (int kk = 0; kk < 16; ++kk) {
-      const double lkk = __shfl(sel4(A, kk >> 2), ((kk & 3) << 4) | kk, 64);
-      const double rl = 1.0 / lkk;
-      const double bk = __shfl(sel4(Bv, kk >> 2), ((kk & 3) << 4) | cc, 64) * rl;   // final row kk
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = gg + 4 * q;
-        const double lr_ = __shfl(A[q], (gg << 4) | kk, 64);             // L[r][kk]
-        if (r == kk) Bv[q] = bk;
-        else if (r > kk) Bv[q] = fma(-lr_, bk, Bv[q]);
-      }
-    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {   // the diagonal block now holds L11^-1
       const int r = gg + 4 * q;
       if (r < nb && cc <= r) Lp[pk(p0 + r, p0 + cc)] = Bv[q];
     }
     WSYNC();
+    WP_STAMP(0);
     const int j16 = l & 15, kq = l >> 4;
     for (int r1 = p0 + 16; r1 < k; r1 += 16) {   // L21 = A21 L11^-T
       const int ri = r1 + j16;
@@ -424,6 +467,7 @@ __device__ int w_potrf(double* Lp, int k) {
       }
       WSYNC();
     }
+    WP_STAMP(1);
     const int q0 = p0 + 16;
     if (q0 < k) {   // A22 -= L21 L21' (lower 16x16 tiles)
       const int nt = (k - q0 + 15) >> 4;
@@ -446,7 +490,9 @@ __device__ int w_potrf(double* Lp, int k) {
         }
       WSYNC();
     }
+    WP_STAMP(2);
   }
+#undef WP_STAMP
   return 0;
 }
 
@@ -494,7 +540,7 @@ __device__ void w_bwd(const double* Lp, int k, double* y, double* xo) {
 }
 
 template <int KS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(128))) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
+__global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
                                                  int klo) {
   constexpr int NP = KS * (KS + 1) / 2;
   __shared__ double Lp[NP];
@@ -517,7 +563,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(128))) void k_pg
   PGWork wk(st, b, ld);
   const double sc = R[R_SC];
   const double delta = s.delta * sc;
-  const double* K = st.K + (int64_t)b * st.K_stride;   // P_FF (lower), kept for the residuals
+  const double* K = st.K + (int64_t)b * st.K_stride;   // P_FF (both triangles), kept for the residuals
 #ifdef PQ_PROFILE
   long long t_last_ = wall_clock64();
 #define WSTAMP(k_)                                                         \
@@ -530,11 +576,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(128))) void k_pg
 #endif
   {   // packed triangle, flat index (independent loads, 64 per trip)
     const int np_ = k * (k + 1) / 2;
-    int r = 0, e0 = 0;   // row of element l: advance incrementally
-    for (int e = l; e < np_; e += 64) {
-      while (e >= e0 + r + 1) { e0 += r + 1; ++r; }
-      const int c = e - e0;
-      Lp[e] = K[(int64_t)r * ldk + c] + (r == c ? delta : 0.0);
+    int r = 0, e0 = 0;   // row of the lane's element: advance incrementally
+    for (int eb = 0; eb < np_; eb += 64 * 8) {   // 8 loads in flight per lane
+      double v[8];
+      int dg = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = eb + 64 * j + l;
+        v[j] = 0.0;
+        if (e < np_) {
+          while (e >= e0 + r + 1) { e0 += r + 1; ++r; }
+          const int c = e - e0;
+          v[j] = K[(int64_t)r * ldk + c];
+          dg |= (r == c) << j;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = eb + 64 * j + l;
+        if (e < np_) Lp[e] = v[j] + ((dg >> j) & 1 ? delta : 0.0);
+      }
     }
   }
   for (int p = l; p < k; p += 64) xF[p] = wk.solx[p];
@@ -544,7 +605,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(128))) void k_pg
     dAv[l] = R[R_DA + l];
   }
   WSTAMP(0);
-  if (w_potrf(Lp, k)) {
+  if (w_potrf(Lp, k, R + 16)) {
     if (l == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
@@ -593,11 +654,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(128))) void k_pg
   // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------
   for (int itr = 0; itr < s.refine_iters; ++itr) {
     // rx = rF - P_FF x - C_aF' lam  (lane per row, P_FF from the K scratch)
-    for (int p = l; p < k; p += 64) {
+    for (int p = l; p < k; p += 64) {   // P_FF is symmetric in K: column p, coalesced over lanes
       double sum = 0.0;
-      const double* kp_ = K + (int64_t)p * ldk;
-      for (int qq = 0; qq <= p; ++qq) sum = fma(kp_[qq], xF[qq], sum);
-      for (int qq = p + 1; qq < k; ++qq) sum = fma(K[(int64_t)qq * ldk + p], xF[qq], sum);
+#pragma unroll 8
+      for (int qq = 0; qq < k; ++qq) sum = fma(K[(int64_t)qq * ldk + p], xF[qq], sum);
       double v = wk.rF[p] - sum;
       const int fp = wk.Fl[p];
       for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + fp] * lamv[a];
