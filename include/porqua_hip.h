@@ -120,6 +120,17 @@ int pq_window_sumsq(const double* panel, int64_t ldp, int32_t n, const int32_t* 
                     const int32_t* tlen, int32_t tmax, int32_t batch, const double* mu,
                     int64_t mu_stride, double* out, int64_t out_stride, void* stream);
 
+/* Both moments above for the dates of slide groups (engine.GroupPlan: date b's window is
+ * union[uoff[b], uoff[b] + tlen[b]) of its group's union rows urows[g][0..umax), offsets
+ * nondecreasing, one window length per group), in one pass: the first window summed, the
+ * later ones by the rows that enter / leave (shifted sums; matches the two calls to a few
+ * ulps).  Replaces pq_window_mean + pq_window_sumsq for the daily backtest
+ * (src/covariance.py:65-66 per rebalance date of src/backtest.py:209-230).             */
+int pq_window_moments_grouped(const double* panel, int64_t ldp, int32_t n, const int32_t* gdates,
+                              int32_t ngroups, const int32_t* urows, int32_t umax,
+                              const int32_t* uoff, const int32_t* tlen, double* mu,
+                              int64_t mu_stride, double* dg, int64_t dg_stride, void* stream);
+
 /* K1: batched windowed SYRK on FP64 MFMA.  mode 0: centred covariance with ddof=1
  * (Covariance.estimate 'pearson', src/covariance.py:40-56,65-66); mode 1: uncentred Gram
  * X'X (LeastSquares.set_objective, src/optimization.py:215).  out: batch x ld x ld.     */

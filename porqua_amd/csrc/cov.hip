@@ -52,6 +52,56 @@ __global__ __launch_bounds__(256) void k_window_sumsq(const double* panel, int64
   out[(int64_t)b * out_stride + j] = s;
 }
 
+// Window means and diag(Xc'Xc) of a slide group's dates in one pass over its union rows
+// (engine.GroupPlan: date b's window is union[uoff_b, uoff_b + T), offsets nondecreasing,
+// one T per group).  One thread per column: the first window is summed directly, each later
+// window by adding the rows that enter and subtracting the rows that leave -- T + 2 (G - 1)
+// row reads per group instead of G T.  Sums are shifted by the column's first value c
+// (sa = sum (x - c), sb = sum (x - c)^2; mu = c + sa / T, dg = sb - sa^2 / T), so neither
+// the sliding updates nor the centring cancel: the results match pq_window_mean /
+// pq_window_sumsq to a few ulps.
+__global__ __launch_bounds__(256) void k_window_moments_grp(const double* panel, int64_t ldp, int n,
+                                                            const int32_t* gdates, const int32_t* urows,
+                                                            int umax, const int32_t* uoff,
+                                                            const int32_t* tlen, double* mu,
+                                                            int64_t mu_stride, double* dg,
+                                                            int64_t dg_stride) {
+  const int g = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int d0 = gdates[g], d1 = gdates[g + 1];
+  const int32_t* ur = urows + (int64_t)g * umax;
+  const int T = tlen[d0];
+  auto x = [&](int u) { return panel[(int64_t)ur[u] * ldp + j]; };
+  int lo = uoff[d0], hi = lo + T;
+  const double c = x(lo);
+  double sa = 0.0, sb = 0.0;
+#pragma unroll 8
+  for (int u = lo; u < hi; ++u) {
+    const double v = x(u) - c;
+    sa += v;
+    sb = fma(v, v, sb);
+  }
+  for (int b = d0;; ) {
+    mu[(int64_t)b * mu_stride + j] = c + sa / T;
+    dg[(int64_t)b * dg_stride + j] = sb - sa * sa / T;
+    if (++b >= d1) break;
+    const int nlo = uoff[b], nhi = nlo + T;
+    for (int u = hi; u < nhi; ++u) {   // entering
+      const double v = x(u) - c;
+      sa += v;
+      sb = fma(v, v, sb);
+    }
+    for (int u = lo; u < nlo; ++u) {   // leaving
+      const double v = x(u) - c;
+      sa -= v;
+      sb = fma(-v, v, sb);
+    }
+    lo = nlo;
+    hi = nhi;
+  }
+}
+
 __device__ __forceinline__ void tri_index(int t, int& I, int& J) {
   // t enumerates lower tiles row by row: (0,0),(1,0),(1,1),(2,0),...
   I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
@@ -322,6 +372,21 @@ extern "C" int pq_window_sumsq(const double* panel, int64_t ldp, int32_t n, cons
   hipLaunchKernelGGL(pq::k_window_sumsq, dim3((n + 255) / 256, batch), dim3(256), 0,
                      (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mu, mu_stride, out, out_stride);
   PQ_CHECK_LAUNCH("pq_window_sumsq");
+  return 0;
+}
+
+extern "C" int pq_window_moments_grouped(const double* panel, int64_t ldp, int32_t n, const int32_t* gdates,
+                                         int32_t ngroups, const int32_t* urows, int32_t umax,
+                                         const int32_t* uoff, const int32_t* tlen, double* mu,
+                                         int64_t mu_stride, double* dg, int64_t dg_stride, void* stream) {
+  PQ_CHECK_ARG(panel && gdates && urows && uoff && tlen && mu && dg, "pq_window_moments_grouped: null pointer");
+  PQ_CHECK_ARG(n > 0 && umax > 0 && ngroups >= 0, "pq_window_moments_grouped: bad sizes n=%d umax=%d ngroups=%d",
+               n, umax, ngroups);
+  if (ngroups == 0) return 0;
+  hipLaunchKernelGGL(pq::k_window_moments_grp, dim3((n + 255) / 256, ngroups), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, gdates, urows, umax, uoff, tlen, mu, mu_stride, dg,
+                     dg_stride);
+  PQ_CHECK_LAUNCH("pq_window_moments_grouped");
   return 0;
 }
 

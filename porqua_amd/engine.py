@@ -917,6 +917,16 @@ class Panel:
                                        _stream()), "pq_window_sumsq")
         return out
 
+    def window_moments_grouped(self, groups: "GroupPlan", tlen, mu, dg):
+        """Window means and diag(Xc'Xc) of every date of a GroupPlan in one sliding pass over
+        each group's union rows (pq_window_moments_grouped), into ``mu`` and ``dg``."""
+        lib = _lib.load()
+        _lib.check(lib.pq_window_moments_grouped(_ptr(self.R), self.R.stride(0), self.n, _ptr(groups.gdates),
+                                                 groups.ngroups, _ptr(groups.urows), groups.umax,
+                                                 _ptr(groups.uoff), _ptr(tlen), _ptr(mu), mu.stride(0), _ptr(dg),
+                                                 dg.stride(0), _stream()), "pq_window_moments_grouped")
+        return mu, dg
+
     def rows_to_device(self, rows, tlen):
         r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int32)).to(self.device)
         t = torch.from_numpy(np.ascontiguousarray(tlen, dtype=np.int32)).to(self.device)

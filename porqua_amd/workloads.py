@@ -85,9 +85,13 @@ class MinVarianceBacktest:
         if events is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        mu = self.pan.window_means(self.rows_d, self.tlen_d, out=self.mu)
-        if self.use_lr:
-            self.lr.refresh()   # diag(Xc'Xc): the only O(n) per-date moment besides mu
+        if self.use_lr and self.gplan is not None and self.gplan.ok:
+            # mu and diag(Xc'Xc) (the only O(n) per-date moments) in one sliding pass per group
+            mu, _ = self.pan.window_moments_grouped(self.gplan, self.tlen_d, self.mu, self.lr.dg)
+        else:
+            mu = self.pan.window_means(self.rows_d, self.tlen_d, out=self.mu)
+            if self.use_lr:
+                self.lr.refresh()
         if self.with_cov:
             self.pan.cov(self.rows_d, self.tlen_d, mode=0, out=self.qb.P, mu=mu, plan=self.plan,
                          lower_only=self.use_lr)

@@ -140,3 +140,32 @@ def test_qp_synthetic_n1000_min_variance(device, shrink):
         assert abs(o - s.obj) <= 1e-6 * abs(s.obj)
         assert np.abs(x[i] - s.x).max() < 1e-5
         assert max(abs(x[i].sum() - 1), -x[i].min(), x[i].max() - 1) <= 1e-7
+
+
+@pytest.mark.parametrize("n,T,stride,offset", [(1000, 252, 1, 0.0), (130, 60, 3, 0.0), (70, 40, 1, 50.0)])
+def test_grouped_window_moments_match_per_date_kernels(device, n, T, stride, offset):
+    """pq_window_moments_grouped (one sliding pass per slide group, shifted sums) against
+    pq_window_mean + pq_window_sumsq (and numpy); offset: price-like data with a large common
+    mean, where unshifted sliding sums would cancel."""
+    D = T + 60 * stride
+    dates, R, y, _ = factor_panel(D, n, seed=n + stride)
+    R = R + offset
+    reb = dates[T - 1::stride][:60]
+    rows, tlen = engine.window_rows(dates, reb, T)
+    gp = engine.GroupPlan(rows, tlen, device)
+    assert gp.ok and gp.ngroups < len(reb)
+    pan = engine.Panel(R, device=device)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    mu_a = pan.window_means(r_d, t_d)
+    dg_a = pan.window_sumsq(r_d, t_d, mu_a)
+    mu_b = torch.full_like(mu_a, float("nan"))
+    dg_b = torch.full_like(dg_a, float("nan"))
+    pan.window_moments_grouped(gp, t_d, mu_b, dg_b)
+    mu_a, dg_a, mu_b, dg_b = (v.cpu().numpy()[:, :n] for v in (mu_a, dg_a, mu_b, dg_b))
+    scale = np.abs(R).max()
+    assert np.abs(mu_a - mu_b).max() <= 1e-14 * scale
+    assert np.all(np.abs(dg_a - dg_b) <= 1e-12 * dg_a)
+    for b in (0, len(reb) // 2, len(reb) - 1):
+        X = R[rows[b, :tlen[b]]]
+        assert np.abs(mu_b[b] - X.mean(0)).max() <= 1e-14 * scale
+        assert np.all(np.abs(dg_b[b] - ((X - X.mean(0)) ** 2).sum(0)) <= 1e-12 * dg_a[b])
