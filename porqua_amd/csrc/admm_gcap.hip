@@ -240,15 +240,17 @@ __global__ __launch_bounds__(256) void k_gcap_prep(pq_lowrank lr, pq_problem pb,
 }
 
 // ---- the ADMM iterations -------------------------------------------------------------------
+// MGC: general rows compiled in (0 for box-only problems: no Cg registers in the epilogue)
+template <int MGC>
 __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
                                                   pq_settings s, int iters_call, const double* pc, int64_t ldpc,
                                                   int r0, const double* cc) {
   constexpr int MGG = 8;
   __shared__ __attribute__((aligned(16))) double WU[(CU_MAX + 4) * CG_MAX];
   double* const UT = WU;
-  __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX];
+  __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX], g_qmax[CG_MAX];
   __shared__ double g_y[CG_MAX * CH_MAX];   // y_b = H_b^-1 s_b of every date
-  constexpr int NPART = 8 + CMG;              // per wave and date: 7 maxima, mu.V, Cg.V
+  constexpr int NPART = 5;                    // per wave and date: 4 maxima, mu.V
   __shared__ double g_part[CNW * CG_MAX * NPART];
   __shared__ double g_gm[CG_MAX * 3];
   __shared__ double g_zg[CG_MAX * MGG], g_yg[CG_MAX * MGG], g_rg[CG_MAX * MGG], g_lg[CG_MAX * MGG],
@@ -355,8 +357,9 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
     }
     if (hl < mg) g_wg[g * MGG + hl] = g_rg[g * MGG + hl] * g_zg[g * MGG + hl] - g_yg[g * MGG + hl];
-    double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
+    double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0}, qmax = 0.0;
     for (int i = hl; i < n; i += 32) {
+      qmax = fmax(qmax, fabs(q_h[i]));
       const double rb = has_box ? crho(lo_h[i], up_h[i], rho, s) : 0.0;
       double rr = sigma * x_h[i] - q_h[i];
       if (has_box) rr += rb * zb_h[i] - yb_h[i];
@@ -371,10 +374,12 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         if (r < mg) cvp[r] = fma(Cg_h[(int64_t)r * ld + i], v, cvp[r]);
     }
     muv = csum32(muv);
+    qmax = cmax32(qmax);
 #pragma unroll
     for (int r = 0; r < CMG; ++r) cvp[r] = csum32(cvp[r]);
     if (hl == 0) {
       g_muv[g] = muv;
+      g_qmax[g] = qmax;   // |q| (dual scale) is fixed over the iterations
       for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
     }
   }
@@ -385,7 +390,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
   __syncthreads();
 
-  const int ntile = (U + 15) >> 4;
+  const int ntile = (U + mg + 15) >> 4;   // pass 1: union rows, then the general rows (Cg V)
   const int ktile = (kU + 15) >> 4;
   while (s_any) {
     // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs) ----------------------
@@ -401,8 +406,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         c[j] = f64x4{0.0, 0.0, 0.0, 0.0};
         const int u = (w + CNW * j) * 16 + m;
         tv[j] = w + CNW * j < ntile;
-        aval[j] = u < U;
-        arow[j] = lr.panel + (int64_t)s_urow[u < CU_MAX ? u : 0] * lr.ldp;
+        aval[j] = u < U + mg;
+        arow[j] = u < U ? lr.panel + (int64_t)s_urow[u] * lr.ldp : pb.Cg + (int64_t)(u < U + mg ? u - U : 0) * ld;
       }
       struct Buf { double2 b; double2 a[CTP1]; };
       auto load = [&](Buf& f, int k0) {
@@ -437,13 +442,15 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int u = tile * 16 + kq + 4 * r;
-            if (u < U) WU[u * CG_MAX + m] = gk.sqc * wsc1 * c[j][r];
+            if (u < U) {
+              WU[u * CG_MAX + m] = gk.sqc * wsc1 * c[j][r];
+            } else if (u < U + mg) {   // Cg V of date m
+              const double cgv = wsc1 * c[j][r];
+              if (m < G) g_cgv[m * MGG + (u - U)] = cgv;
+              WU[u * CG_MAX + m] = s_sr[u - U] * cgv;
+            }
           }
         }
-      }
-      if (t < CG_MAX * CMG) {
-        const int g = t / CMG, r = t % CMG;
-        if (r < mg) WU[(U + r) * CG_MAX + g] = (g < G) ? s_sr[r] * g_cgv[g * MGG + r] : 0.0;
       }
     }
     __syncthreads();
@@ -587,95 +594,44 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     __syncthreads();
     CSTAMP(2);
-    // ---- pass 2 fused with the per-date updates: the MFMA epilogue of every 32-asset tile
-    //      updates those assets of its date (x~, x, Px, box z / y, residual terms, next rhs);
-    //      per-date maxima / sums go through LDS (NP partial slots per date) --------------------
+    // ---- pass 2 fused with the per-date updates.  The MFMA computes X~raw as (date x asset)
+    //      tiles: lane l ends with dates (l>>4) + 4r, r = 0..3, of the asset pair
+    //      p * 32 + 2 (l & 15) + {0, 1}, so the epilogue's per-date vectors (x, Px, z, y,
+    //      rhs, q, mu) are read and written as 16-byte pairs by 16 consecutive lanes (256
+    //      contiguous bytes per date), and the per-asset data (box, Cg columns) once per
+    //      lane for all its dates.  Per-date maxima / sums: lane partials, reduced over the
+    //      16 lanes of a date, then NP slots per wave in LDS ---------------------------------
     {
-      const int kq = l >> 4, m = l & 15;
+      const int kq = l >> 4, ia = l & 15;
       const int Uk = (U + 3) & ~3;
       constexpr int PS = 4;
-      const bool mact = m < G && g_act[m];
-      const int bm = d0 + (m < G ? m : 0);
-      const double* __restrict__ q_m = pb.q + (int64_t)bm * pb.q_stride;
-      const double* __restrict__ lo_m = has_box ? pb.lb + (int64_t)bm * pb.box_stride : nullptr;
-      const double* __restrict__ up_m = has_box ? pb.ub + (int64_t)bm * pb.box_stride : nullptr;
-      const double* __restrict__ mu_m = lr.mu + (int64_t)bm * lr.mu_stride;
-      double* __restrict__ x_m = st.x + (int64_t)bm * ld;
-      double* __restrict__ Px_m = st.Px + (int64_t)bm * ld;
-      double* __restrict__ zb_m = st.z + (int64_t)bm * st.m_ld + st.mg_pad;
-      double* __restrict__ yb_m = st.y + (int64_t)bm * st.m_ld + st.mg_pad;
-      double* __restrict__ R_m = st.work + (int64_t)bm * st.work_stride + ld;
-      const double su = mact ? g_su[m] : 0.0, dinv = mact ? g_dinv[m] : 0.0;
-      double cwm[CMG], rgzm[CMG], ygm[CMG], wgm[CMG];
+      bool mact[4];
 #pragma unroll
-      for (int r = 0; r < CMG; ++r) {
-        const bool ok = mact && r < mg;
-        cwm[r] = ok ? g_cw[m * MGG + r] : 0.0;
-        rgzm[r] = ok ? g_rgz[m * MGG + r] : 0.0;
-        ygm[r] = ok ? g_yg[m * MGG + r] : 0.0;
-        wgm[r] = ok ? g_wg[m * MGG + r] : 0.0;
+      for (int r = 0; r < 4; ++r) {
+        const int m = kq + 4 * r;
+        mact[r] = m < G && g_act[m];
       }
-      double mv[7] = {0, 0, 0, 0, 0, 0, 0};   // |Cx-z| |Cx| |z| |dres| |Px| |C'y| |q|
-      double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
-      auto update = [&](int i, double xr) {   // asset i of date m, X~raw = xr
-        const double rb = has_box ? crho(lo_m[i], up_m[i], rho, s) : 0.0;
-        const double rr0 = R_m[i];
-        double corr = xr - su * mu_m[i];
-        double cgi[CMG];
+      const bool box_shared = pb.box_stride == 0;
+      // per date of the lane: |x-z|, max(|x|, |z|), |dual res|, max(|Px|, |C'y|) (|q|: prologue;
+      // Cg V: next pass 1, as extra MFMA rows)
+      double mv[4][4];
+      double muv[4];
 #pragma unroll
-        for (int r = 0; r < CMG; ++r) {
-          cgi[r] = r < mg ? pb.Cg[(int64_t)r * ld + i] : 0.0;
-          corr = fma(cwm[r], cgi[r], corr);
-        }
-        const double xt = (rr0 - corr) * dinv;
-        double pxt = rr0 - sigma * xt - rb * xt;
-        double cgy = 0.0, cgw = 0.0;
+      for (int r = 0; r < 4; ++r) {
+        muv[r] = 0.0;
 #pragma unroll
-        for (int r = 0; r < CMG; ++r) {
-          pxt -= cgi[r] * rgzm[r];
-          cgy = fma(cgi[r], ygm[r], cgy);
-          cgw = fma(cgi[r], wgm[r], cgw);
-        }
-        const double xn = alpha * xt + (1.0 - alpha) * x_m[i];
-        const double pxn = alpha * pxt + (1.0 - alpha) * Px_m[i];
-        const double qi = q_m[i];
-        double rr = sigma * xn - qi + cgw;
-        double cty = 0.0;
-        if (has_box) {
-          const double zh = alpha * xt + (1.0 - alpha) * zb_m[i];
-          const double zn = fmin(fmax(zh + yb_m[i] / rb, lo_m[i]), up_m[i]);
-          const double yn = yb_m[i] + rb * (zh - zn);
-          zb_m[i] = zn;
-          yb_m[i] = yn;
-          cty = yn;
-          rr += rb * zn - yn;
-          mv[0] = fmax(mv[0], fabs(xn - zn));
-          mv[1] = fmax(mv[1], fabs(xn));
-          mv[2] = fmax(mv[2], fabs(zn));
-        }
-        x_m[i] = xn;
-        Px_m[i] = pxn;
-        mv[4] = fmax(mv[4], fabs(pxn));
-        mv[6] = fmax(mv[6], fabs(qi));
-        const double cy = cty + cgy;
-        mv[3] = fmax(mv[3], fabs((pxn + qi + cty) + (cy - cty)));
-        mv[5] = fmax(mv[5], fabs(cy));
-        const double v = rr * dinv;
-        R_m[i] = rr;
-        muv = fma(mu_m[i], v, muv);
-#pragma unroll
-        for (int r = 0; r < CMG; ++r) cvp[r] = fma(cgi[r], v, cvp[r]);
-      };
+        for (int e = 0; e < 4; ++e) mv[r][e] = 0.0;
+      }
       for (int p = w; p * 32 < n; p += CNW) {
-        const int col = p * 32 + 2 * m;
-        const bool cin = col < n;
+        const int i = p * 32 + 2 * ia;   // this lane's asset pair (n even: i < n => i + 1 < n)
+        const bool cin = i < n;
         f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
         struct ABuf { double2 a[PS]; };
         auto load = [&](ABuf& f, int u0) {
 #pragma unroll
           for (int h = 0; h < PS; ++h) {
             const int u = u0 + 4 * h + kq;
-            f.a[h] = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + col)
+            f.a[h] = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + i)
                                     : double2{0.0, 0.0};
           }
         };
@@ -683,9 +639,9 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
           for (int h = 0; h < PS; ++h) {
             const int u = u0 + 4 * h + kq;
-            const double bv = u < Uk ? UT[u * CG_MAX + m] : 0.0;
-            ce = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[h].x, bv, ce, 0, 0, 0);
-            co = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[h].y, bv, co, 0, 0, 0);
+            const double av = u < Uk ? UT[u * CG_MAX + ia] : 0.0;   // Ut'[date ia][u]
+            ce = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].x, ce, 0, 0, 0);
+            co = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].y, co, 0, 0, 0);
           }
         };
         ABuf f0, f1;
@@ -696,37 +652,127 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           load(f0, u0 + 8 * PS);
           mma(f1, u0 + 4 * PS);
         }
-        if (mact) {
+        if (!cin) continue;
+        // per-asset data, shared by the lane's dates
+        double2 cg2[MGC > 0 ? MGC : 1];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = p * 32 + 2 * (kq + 4 * r);
-            if (i < n) {   // n even: i + 1 < n too
-              update(i, ce[r]);
-              update(i + 1, co[r]);
+        for (int c = 0; c < MGC; ++c)
+          cg2[c] = c < mg ? *reinterpret_cast<const double2*>(pb.Cg + (int64_t)c * ld + i) : double2{0.0, 0.0};
+        double2 lo2 = double2{0.0, 0.0}, up2 = double2{0.0, 0.0}, rb2 = double2{0.0, 0.0};
+        if (has_box && box_shared) {
+          lo2 = *reinterpret_cast<const double2*>(pb.lb + i);
+          up2 = *reinterpret_cast<const double2*>(pb.ub + i);
+          rb2 = double2{crho(lo2.x, up2.x, rho, s), crho(lo2.y, up2.y, rho, s)};
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          __builtin_amdgcn_sched_barrier(0);   // one date's loads live at a time (VGPR budget)
+          if (!mact[r]) continue;
+          const int m = kq + 4 * r;
+          const int bm = d0 + m;
+          const double su = g_su[m], dinv = g_dinv[m];
+          double2 lo = lo2, up = up2, rb = rb2;
+          if (has_box && !box_shared) {
+            lo = *reinterpret_cast<const double2*>(pb.lb + (int64_t)bm * pb.box_stride + i);
+            up = *reinterpret_cast<const double2*>(pb.ub + (int64_t)bm * pb.box_stride + i);
+            rb = double2{crho(lo.x, up.x, rho, s), crho(lo.y, up.y, rho, s)};
+          }
+          double* R_m = st.work + (int64_t)bm * st.work_stride + ld + i;
+          double* x_m = st.x + (int64_t)bm * ld + i;
+          double* Px_m = st.Px + (int64_t)bm * ld + i;
+          double* zb_m = st.z + (int64_t)bm * st.m_ld + st.mg_pad + i;
+          double* yb_m = st.y + (int64_t)bm * st.m_ld + st.mg_pad + i;
+          const double2 rr2 = *reinterpret_cast<const double2*>(R_m);
+          const double2 mu2 = *reinterpret_cast<const double2*>(lr.mu + (int64_t)bm * lr.mu_stride + i);
+          const double2 x2 = *reinterpret_cast<const double2*>(x_m);
+          const double2 px2 = *reinterpret_cast<const double2*>(Px_m);
+          const double2 q2 = *reinterpret_cast<const double2*>(pb.q + (int64_t)bm * pb.q_stride + i);
+          double2 z2 = double2{0.0, 0.0}, y2 = double2{0.0, 0.0};
+          if (has_box) {
+            z2 = *reinterpret_cast<const double2*>(zb_m);
+            y2 = *reinterpret_cast<const double2*>(yb_m);
+          }
+          double cwm[MGC > 0 ? MGC : 1], rgzm[MGC > 0 ? MGC : 1], ygm[MGC > 0 ? MGC : 1], wgm[MGC > 0 ? MGC : 1];
+#pragma unroll
+          for (int c = 0; c < MGC; ++c) {
+            const bool ok = c < mg;
+            cwm[c] = ok ? g_cw[m * MGG + c] : 0.0;
+            rgzm[c] = ok ? g_rgz[m * MGG + c] : 0.0;
+            ygm[c] = ok ? g_yg[m * MGG + c] : 0.0;
+            wgm[c] = ok ? g_wg[m * MGG + c] : 0.0;
+          }
+          double2 xo, pxo, zo, yo, ro;
+          auto one = [&](double xr, double rr0, double mui, double xi, double pxi, double qi, double zi, double yi,
+                         double loi, double upi, double rbi, int sel, double& xn_o, double& pxn_o, double& zn_o,
+                         double& yn_o, double& rr_o) {
+            double corr = xr - su * mui;
+            double cgi[MGC > 0 ? MGC : 1];
+#pragma unroll
+            for (int c = 0; c < MGC; ++c) {
+              cgi[c] = sel ? cg2[c].y : cg2[c].x;
+              corr = fma(cwm[c], cgi[c], corr);
             }
+            const double xt = (rr0 - corr) * dinv;
+            double pxt = rr0 - sigma * xt - rbi * xt;
+            double cgy = 0.0, cgw = 0.0;
+#pragma unroll
+            for (int c = 0; c < MGC; ++c) {
+              pxt -= cgi[c] * rgzm[c];
+              cgy = fma(cgi[c], ygm[c], cgy);
+              cgw = fma(cgi[c], wgm[c], cgw);
+            }
+            const double xn = alpha * xt + (1.0 - alpha) * xi;
+            const double pxn = alpha * pxt + (1.0 - alpha) * pxi;
+            double rr = sigma * xn - qi + cgw;
+            double cty = 0.0;
+            zn_o = zi;
+            yn_o = yi;
+            if (has_box) {
+              const double zh = alpha * xt + (1.0 - alpha) * zi;
+              const double zn = fmin(fmax(zh + yi / rbi, loi), upi);
+              const double yn = yi + rbi * (zh - zn);
+              zn_o = zn;
+              yn_o = yn;
+              cty = yn;
+              rr += rbi * zn - yn;
+              mv[r][0] = fmax(mv[r][0], fabs(xn - zn));
+              mv[r][1] = fmax(mv[r][1], fmax(fabs(xn), fabs(zn)));
+            }
+            xn_o = xn;
+            pxn_o = pxn;
+            rr_o = rr;
+            const double cy = cty + cgy;
+            mv[r][2] = fmax(mv[r][2], fabs((pxn + qi + cty) + (cy - cty)));
+            mv[r][3] = fmax(mv[r][3], fmax(fabs(pxn), fabs(cy)));
+            muv[r] = fma(mui, rr * dinv, muv[r]);
+          };
+          one(ce[r], rr2.x, mu2.x, x2.x, px2.x, q2.x, z2.x, y2.x, lo.x, up.x, rb.x, 0, xo.x, pxo.x, zo.x, yo.x, ro.x);
+          one(co[r], rr2.y, mu2.y, x2.y, px2.y, q2.y, z2.y, y2.y, lo.y, up.y, rb.y, 1, xo.y, pxo.y, zo.y, yo.y, ro.y);
+          *reinterpret_cast<double2*>(x_m) = xo;
+          *reinterpret_cast<double2*>(Px_m) = pxo;
+          *reinterpret_cast<double2*>(R_m) = ro;
+          if (has_box) {
+            *reinterpret_cast<double2*>(zb_m) = zo;
+            *reinterpret_cast<double2*>(yb_m) = yo;
           }
         }
       }
-      // the four lanes of a wave that share date m (m, m + 16, m + 32, m + 48)
+      // reduce over the 16 lanes of each date (lanes kq * 16 + 0..15), then one slot per wave
 #pragma unroll
-      for (int e = 0; e < 7; ++e) {
-        mv[e] = fmax(mv[e], __shfl_xor(mv[e], 16, 64));
-        mv[e] = fmax(mv[e], __shfl_xor(mv[e], 32, 64));
-      }
-      muv += __shfl_xor(muv, 16, 64);
-      muv += __shfl_xor(muv, 32, 64);
+      for (int r = 0; r < 4; ++r) {
 #pragma unroll
-      for (int r = 0; r < CMG; ++r) {
-        cvp[r] += __shfl_xor(cvp[r], 16, 64);
-        cvp[r] += __shfl_xor(cvp[r], 32, 64);
-      }
-      if (kq == 0) {
-        double* pp = g_part + (w * CG_MAX + m) * NPART;
+        for (int sh = 1; sh < 16; sh <<= 1) {
 #pragma unroll
-        for (int e = 0; e < 7; ++e) pp[e] = mv[e];
-        pp[7] = muv;
+          for (int e = 0; e < 4; ++e) mv[r][e] = fmax(mv[r][e], __shfl_xor(mv[r][e], sh, 64));
+          muv[r] += __shfl_xor(muv[r], sh, 64);
+        }
+        const int m = kq + 4 * r;
+        if (ia == 0) {
+          double* pp = g_part + (w * CG_MAX + m) * NPART;
 #pragma unroll
-        for (int r = 0; r < CMG; ++r) pp[8 + r] = cvp[r];
+          for (int e = 0; e < 4; ++e) pp[e] = mv[r][e];
+          pp[4] = muv[r];
+        }
       }
     }
     __syncthreads();
@@ -734,13 +780,16 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     // ---- per date: residuals, convergence, rho request (one thread per date) ------------------
     if (t < G && g_act[t]) {
       const int g = t;
-      double mv[7], muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0};
-      for (int e = 0; e < 7; ++e) mv[e] = e < 3 ? g_gm[g * 3 + e] : 0.0;
+      // mv: |Cx-z| max(|Cx|,|z|) - |dres| max(|Px|,|C'y|) - |q| (the 7-slot form of admm_grp)
+      double mv[7] = {g_gm[g * 3], fmax(g_gm[g * 3 + 1], g_gm[g * 3 + 2]), 0.0, 0.0, 0.0, 0.0, g_qmax[g]};
+      double muv = 0.0;
       for (int ww = 0; ww < CNW; ++ww) {
         const double* pp = g_part + (ww * CG_MAX + g) * NPART;
-        for (int e = 0; e < 7; ++e) mv[e] = fmax(mv[e], pp[e]);
-        muv += pp[7];
-        for (int r = 0; r < CMG; ++r) cvp[r] += pp[8 + r];
+        mv[0] = fmax(mv[0], pp[0]);
+        mv[1] = fmax(mv[1], pp[1]);
+        mv[3] = fmax(mv[3], pp[2]);
+        mv[4] = fmax(mv[4], pp[3]);
+        muv += pp[4];
       }
       const int it = g_it[g] + 1;
       int stat = PQ_UNSOLVED;
@@ -760,7 +809,6 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       g_act[g] = (stat == PQ_UNSOLVED) && it < g_end[g];
       g_rn[g] = rn;
       g_muv[g] = muv;
-      for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
     }
     __syncthreads();
     if (t == 0) {
@@ -875,8 +923,16 @@ extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(pb->mg == 0 || (pc && cc), "pq_admm_lr_gcap: general rows need pc and cc");
   PQ_CHECK_ARG(pb->n % 2 == 0 && lr->ldp % 2 == 0, "pq_admm_lr_gcap: needs even n and panel stride");
   PQ_CHECK_ARG(st->work && st->work_stride >= 3 * (int64_t)pb->ld, "pq_admm_lr_gcap: work buffer too small");
-  hipLaunchKernelGGL(pq::k_admm_gcap, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st, *gc,
-                     *s, iters_this_call, pc, ldpc, r0, cc);
+  // 16-byte pair access of the per-date vectors
+  PQ_CHECK_ARG(pb->ld % 2 == 0 && st->work_stride % 2 == 0 && st->m_ld % 2 == 0 && st->mg_pad % 2 == 0 &&
+                   pb->q_stride % 2 == 0 && pb->box_stride % 2 == 0 && lr->mu_stride % 2 == 0,
+               "pq_admm_lr_gcap: strides must be even");
+  if (pb->mg == 0)
+    hipLaunchKernelGGL(pq::k_admm_gcap<0>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
+                       *gc, *s, iters_this_call, pc, ldpc, r0, cc);
+  else
+    hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMG>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
+                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc);
   PQ_CHECK_LAUNCH("pq_admm_lr_gcap");
   return 0;
 }
