@@ -248,7 +248,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   constexpr int MGG = 8;
   __shared__ __attribute__((aligned(16))) double WU[(CU_MAX + 4) * CG_MAX];
   double* const UT = WU;
-  __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX], g_qmax[CG_MAX];
+  __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX], g_qmax[CG_MAX], g_coef[CG_MAX];
   __shared__ double g_y[CG_MAX * CH_MAX];   // y_b = H_b^-1 s_b of every date
   constexpr int NPART = 5;                    // per wave and date: 4 maxima, mu.V
   __shared__ double g_part[CNW * CG_MAX * NPART];
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     __syncthreads();
     CSTAMP(1);
-    // ---- per date: s, y = H^-1 s, Ut / cw / su (half-wave per date) ---------------------------
+    // ---- per date: s, y = H^-1 s (half-wave per date) -------------------------------------------
     for (int g = hg; g < G; g += CHW) {
       if (!g_act[g]) continue;
       const int b = d0 + g;
@@ -510,7 +510,6 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const int m = U - T, mh = m + 1;
       const double d = gk.d, sct = sqrt(gk.c * T);
       const double* A = gc.aq + (int64_t)b * gc.aq_stride;
-      const double* Q = A + k_ld;
       const double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
       double az = 0.0;
       for (int u = hl; u < kU; u += 32) az = fma(A[u], WU[u * CG_MAX + g], az);
@@ -540,57 +539,96 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
       }
       const double ymu = __shfl(m < 32 ? yi[0] : yi[1], hbase + (m & 31), 64);
-      const double coef = sct / d * ymu;
-      // y to LDS: the loop below has a lane-dependent trip count, so no shuffles inside it
-      // (an inactive source lane would read as garbage)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        if (hl + 32 * h < mh) g_y[g * CH_MAX + hl + 32 * h] = yi[h];
-      // base = z' - M^-1[:, C] y_C + coef q ; Ut = sqrt(c) base on X rows, cw = sqrt(R) base on G rows
-      for (int u = hl; u < kU; u += 32) {
-        double v = WU[u * CG_MAX + g] + coef * Q[u];
-        for (int j = 0; j < m; ++j) {
-          const int cj = j < off ? j : j + T;
-          v = fma(-Mi[(int64_t)cj * k_ld + u], g_y[g * CH_MAX + j], v);
+        if (hl + 32 * h < m) g_y[g * CH_MAX + hl + 32 * h] = yi[h];
+      if (hl == 0) {
+        g_coef[g] = sct / d * ymu;
+        g_su[g] = sct * ymu;
+        g_gm[g * 3] = g_gm[g * 3 + 1] = g_gm[g * 3 + 2] = 0.0;
+      }
+    }
+    __syncthreads();
+    // ---- base = z' - M^-1[:, C_g] y_g + coef_g q_g for every date at once (MFMA): C_g are the
+    //      union rows outside date g's window, all among the NH head rows [0, NH) and the tail
+    //      rows [T, U) (offsets nondecreasing, off_0 = 0), so it is one (kU x NE) x (NE x 16)
+    //      product with NE = NH + U - T edge rows; Ut = sqrt(c) base on union rows, cw =
+    //      sqrt(R) base on general rows (in place of z' in WU) -------------------------------------
+    {
+      const int kq = l >> 4, gl = l & 15;
+      const int T0 = g_T[0];
+      const int NH = g_off[G - 1], NE = NH + (U - T0);
+      const bool gact = gl < G && g_act[gl];
+      const int offg = gl < G ? g_off[gl] : 0;
+      for (int tile = w; tile < ktile; tile += CNW) {
+        const int ua = tile * 16 + gl;   // A row of this lane
+        f64x4 z = f64x4{0.0, 0.0, 0.0, 0.0};
+        for (int e0 = 0; e0 < NE; e0 += 4) {
+          const int e = e0 + kq;
+          const int cu = e < NH ? e : T0 + (e - NH);   // union row of edge e
+          double av = 0.0, bv = 0.0;
+          if (e < NE) {
+            if (ua < kU) av = Mi[(int64_t)cu * k_ld + ua];
+            if (gact) {
+              if (e < NH) bv = e < offg ? g_y[gl * CH_MAX + e] : 0.0;
+              else bv = cu >= offg + T0 ? g_y[gl * CH_MAX + (cu - T0)] : 0.0;
+            }
+          }
+          z = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, z, 0, 0, 0);
         }
-        if (u < U) UT[u * CG_MAX + g] = gk.sqc * v;
-        else g_cw[g * MGG + (u - U)] = s_sr[u - U] * v;
-      }
-      const double su = sct * ymu;
-      if (hl == 0) g_su[g] = su;
-      __builtin_amdgcn_wave_barrier();   // this half-wave's Ut / cw writes precede the reads below
-      // Cg x~ = Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / d, then the general rows' z / y
-      const double dinv = g_dinv[g];
-      for (int r = 0; r < mg; ++r) {
-        double a = 0.0;
-        for (int u = hl; u < U; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * CG_MAX + g], a);
-        a = csum32(a);
-        double cwv = 0.0;
-        for (int r2 = 0; r2 < mg; ++r2) cwv = fma(cc[r * mg + r2], g_cw[g * MGG + r2], cwv);
-        if (hl == 0) g_zt[g * MGG + r] = g_cgv[g * MGG + r] - dinv * (a - su * g_cmu[g * MGG + r] + cwv);
-      }
-      __builtin_amdgcn_wave_barrier();
-      double gm[3] = {0.0, 0.0, 0.0};   // |Cx - z| |Cx| |z| of the general rows
-      if (hl < mg) {
-        const int e = g * MGG + hl;
-        const double rg = g_rg[e], zt = g_zt[e];
-        const double zh = alpha * zt + (1.0 - alpha) * g_zg[e];
-        const double zn = fmin(fmax(zh + g_yg[e] / rg, g_lg[e]), g_ug[e]);
-        const double yn = g_yg[e] + rg * (zh - zn);
-        const double cx = alpha * zt + (1.0 - alpha) * g_cgx[e];
-        gm[0] = fabs(cx - zn);
-        gm[1] = fabs(cx);
-        gm[2] = fabs(zn);
-        g_rgz[e] = rg * zt;
-        g_zg[e] = zn;
-        g_yg[e] = yn;
-        g_cgx[e] = cx;
-        g_wg[e] = rg * zn - yn;
-      }
+        // lane holds rows tile * 16 + kq + 4 r of date gl
+        if (gact) {
+          const double coef = g_coef[gl];
+          const double* Q = gc.aq + (int64_t)(d0 + gl) * gc.aq_stride + k_ld;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) gm[k] = cmax32(gm[k]);
-      if (hl == 0)
-        for (int k = 0; k < 3; ++k) g_gm[g * 3 + k] = gm[k];
+          for (int r = 0; r < 4; ++r) {
+            const int u = tile * 16 + kq + 4 * r;
+            if (u < kU) {
+              const double v = WU[u * CG_MAX + gl] - z[r] + coef * Q[u];
+              if (u < U) UT[u * CG_MAX + gl] = gk.sqc * v;
+              else g_cw[gl * MGG + (u - U)] = s_sr[u - U] * v;
+            }
+          }
+        }
+      }
+    }
+    if (MGC > 0) {
+      __syncthreads();
+      // Cg x~ = Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / d, then the general rows' z / y
+      for (int g = hg; g < G; g += CHW) {
+        if (!g_act[g]) continue;
+        const double dinv = g_dinv[g], su = g_su[g];
+        for (int r = 0; r < mg; ++r) {
+          double a = 0.0;
+          for (int u = hl; u < U; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * CG_MAX + g], a);
+          a = csum32(a);
+          double cwv = 0.0;
+          for (int r2 = 0; r2 < mg; ++r2) cwv = fma(cc[r * mg + r2], g_cw[g * MGG + r2], cwv);
+          if (hl == 0) g_zt[g * MGG + r] = g_cgv[g * MGG + r] - dinv * (a - su * g_cmu[g * MGG + r] + cwv);
+        }
+        __builtin_amdgcn_wave_barrier();
+        double gm[3] = {0.0, 0.0, 0.0};   // |Cx - z| |Cx| |z| of the general rows
+        if (hl < mg) {
+          const int e = g * MGG + hl;
+          const double rg = g_rg[e], zt = g_zt[e];
+          const double zh = alpha * zt + (1.0 - alpha) * g_zg[e];
+          const double zn = fmin(fmax(zh + g_yg[e] / rg, g_lg[e]), g_ug[e]);
+          const double yn = g_yg[e] + rg * (zh - zn);
+          const double cx = alpha * zt + (1.0 - alpha) * g_cgx[e];
+          gm[0] = fabs(cx - zn);
+          gm[1] = fabs(cx);
+          gm[2] = fabs(zn);
+          g_rgz[e] = rg * zt;
+          g_zg[e] = zn;
+          g_yg[e] = yn;
+          g_cgx[e] = cx;
+          g_wg[e] = rg * zn - yn;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) gm[k] = cmax32(gm[k]);
+        if (hl == 0)
+          for (int k = 0; k < 3; ++k) g_gm[g * 3 + k] = gm[k];
+      }
     }
     __syncthreads();
     CSTAMP(2);
