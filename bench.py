@@ -188,7 +188,18 @@ def main():
     k_lr = T + qb.mg
     grouped = use_lr and engine.grouped_applicable(qb, lr, gplan, ws)
     l2_bytes = None
-    if grouped:
+    if grouped and res.capacitance == "group":
+        # k_admm_gcap, per group-iteration: the union rows twice (pass 1 X_U V, pass 2 X_U' Ut;
+        # 2.1 MB per group, too big to stay on-chip between the passes), the lower triangle of
+        # the group's M_U^-1, and per date the ADMM state read + written (x, Px, z, y, rhs: 10
+        # n-vectors) plus q and mu read -- amortised per date-iteration over the mean group
+        kern = "k_admm_gcap"
+        u_mean = float(gplan.ucnt.double().mean().item())
+        g_mean = float(gplan.sizes.mean())
+        k_u = u_mean + qb.mg
+        it_bytes = (2 * 8.0 * u_mean * n + 8.0 * k_u * (k_u + 1) / 2) / g_mean + 12 * 8.0 * n
+        admm_bytes = it_bytes * total_iters
+    elif grouped:
         # HBM level: the date's lower-triangle M^-1 (the only per-date O(k^2) stream; 4749 x
         # 512 KB is far beyond the caches) + the ADMM state read and written (x, z, y, Px);
         # the window passes read the group's union rows, which sit in the XCD's L2
@@ -223,6 +234,9 @@ def main():
     gram_flops = 2.0 * (T - 1 + D) * T * n * args.steps if band else None
     n_factor = D * args.steps + res.refactors * args.steps
     factor_flops = factor_flops_per * n_factor
+    if use_lr and res.capacitance == "group":   # one M_U (k = U + mg) per slide group
+        k_u = float(gplan.ucnt.double().mean().item()) + qb.mg
+        factor_flops = k_u ** 3 * gplan.ngroups * args.steps
 
     traffic, traffic_src = None, None
     mfma_busy, mfma_src = None, None
@@ -235,7 +249,8 @@ def main():
                 traffic, traffic_src = k["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
                 if "mfma_busy_fraction" in pm:
                     mfma_busy = {kk: pm["mfma_busy_fraction"][kk] for kk in
-                                 ("k_band_gram", "k_factor", "k_admm_grp", "k_polish_w") if kk in pm["mfma_busy_fraction"]}
+                                 ("k_band_gram", "k_factor", "k_admm_grp", "k_admm_gcap", "k_polish_w", "k_pg_form",
+                                  "k_pg_solve", "k_pg_pass") if kk in pm["mfma_busy_fraction"]}
                     mfma_src = os.path.relpath(f, ROOT)
         except Exception:
             pass
@@ -265,13 +280,18 @@ def main():
                                      "gfx950 correction; committed rocprofv3 pass)",
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_iteration": int(it_bytes),
-                     "algorithmic_bytes_note": ("per date-iteration: lower-triangle M^-1 8k(k+1)/2 (k = T + mg) "
+                     "algorithmic_bytes_note": ("per date-iteration: (union rows 2 x 8Un + lower-triangle M_U^-1 "
+                                                "8k(k+1)/2, k = U + mg) / dates per group + ADMM state 12 x 8n"
+                                                if kern == "k_admm_gcap" else
+                                                "per date-iteration: lower-triangle M^-1 8k(k+1)/2 (k = T + mg) "
                                                 "+ ADMM state 8 x 8n" if grouped else
                                                 "per date-iteration: window rows 2 x 8Tn + M^-1 8k(k+1)/2"
                                                 if use_lr else "per date-iteration: lower-triangle K^-1 8n(n+1)/2"),
                      "l2_window_bytes_per_iteration": None if l2_bytes is None else int(l2_bytes),
                      "l2_window_gbs": None if l2_bytes is None else l2_bytes * total_iters / tk["admm"] / 1e9,
-                     "path": ("lowrank grouped (Woodbury; MFMA passes over the union of sliding windows)"
+                     "path": ("lowrank grouped, group capacitance (one M_U^-1 per slide group + per-date "
+                              "Woodbury correction; MFMA passes over the union rows)" if kern == "k_admm_gcap" else
+                              "lowrank grouped (Woodbury; MFMA passes over the union of sliding windows)"
                               if grouped else "lowrank (Woodbury: window rows + M^-1)" if use_lr
                               else "dense K^-1 (lower)"),
                      "admm_iterations_per_step": total_iters // args.steps},

@@ -16,8 +16,9 @@ Two ways of running it, as BASELINE.md §3 plans, and the better one is the deno
   (b) pool: one single-threaded worker process per host core, dates spread over them.
 A solver-only variant (no nearestPD: the IPM takes the PSD P as it is) is timed beside it.
 
-Run as a CHILD process (``python -m oracle.cpu_baseline ...``) so that the pool's forks
-never copy a GPU-initialised parent; prints one JSON object.
+Run as a CHILD process (``python -m oracle.cpu_baseline ...``), before the bench touches the
+GPU; the pool's workers are spawned (fresh interpreters, single-threaded BLAS); prints one
+JSON object.
 """
 from __future__ import annotations
 
@@ -46,14 +47,33 @@ def reference_date(X: np.ndarray, ub: float = 1.0, shrink: float = 0.0, repair: 
     if shrink > 0:
         S = S + shrink * np.mean(np.diag(S)) * np.eye(n)
     if repair and not is_pd(S):
-        S = nearest_pd(S)
+        S = _nearest_pd(S)
     P = 2.0 * S
     q = np.zeros(n)
     if repair and not is_pd(P):
-        P = nearest_pd(P)
+        P = _nearest_pd(P)
     sol = solve_qp(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.full(n, ub),
                    tol=1e-7, refine=False)
     return sol
+
+
+def _nearest_pd(A: np.ndarray) -> np.ndarray:
+    """nearest_pd, retrying once with LAPACK gesvd when gesdd (numpy's SVD) does not converge
+    -- the same repair, so the timed work is unchanged."""
+    try:
+        return nearest_pd(A)
+    except np.linalg.LinAlgError:
+        import scipy.linalg
+        B = (A + A.T) / 2
+        _, s, V = scipy.linalg.svd(B, lapack_driver="gesvd")
+        A2 = (B + V.T @ (np.diag(s) @ V)) / 2
+        A3 = (A2 + A2.T) / 2
+        k = 1
+        while not is_pd(A3):
+            mineig = np.min(np.real(np.linalg.eigvals(A3)))
+            A3 += np.eye(A.shape[0]) * (-mineig * k**2 + np.spacing(np.linalg.norm(A)))
+            k += 1
+        return A3
 
 
 def time_reference(R: np.ndarray, ends, T: int, budget_s: float = 20.0, max_dates: int = 8, repair=True):
@@ -90,7 +110,7 @@ def time_pool(n_dates, n, T, ends, workers, seed, repair=True):
     """(b): ``workers`` single-threaded processes over ``ends``; returns (qps, done, seconds)
     timed from the first submitted date to the last result (pool start-up excluded)."""
     import multiprocessing as mp
-    ctx = mp.get_context("fork")
+    ctx = mp.get_context("spawn")   # fresh interpreters: no BLAS thread state copied by fork
     with ctx.Pool(workers, initializer=_pool_init, initargs=(n_dates, n, T, seed)) as pool:
         pool.map(_pool_date, [(ends[0], False)] * workers)     # warm: panel built, BLAS loaded
         t0 = time.perf_counter()

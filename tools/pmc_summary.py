@@ -18,13 +18,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def kname(s):
+    """Kernel name without template arguments (k_pg_solve<80> -> k_pg_solve)."""
+    return s.split("<")[0].strip()
+
+
 def per_kernel(path, counter):
     agg = collections.defaultdict(float)
     calls = collections.Counter()
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            agg[r["Kernel_Name"]] += float(r["Counter_Value"])
-            calls[r["Kernel_Name"]] += 1
+            agg[kname(r["Kernel_Name"])] += float(r["Counter_Value"])
+            calls[kname(r["Kernel_Name"])] += 1
     return agg, calls
 
 
@@ -40,7 +45,15 @@ def main():
     line = [l for l in open(os.path.join(src, "pmc_fetch.log")) if l.startswith('{"metric"')][-1]
     bench_pmc = json.loads(line)
     iters = bench_pmc["roofline"]["admm_iterations_per_step"]
-    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
+    stats = {}
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
+        k = kname(r["Name"])   # template instances merged (calls summed, time-weighted mean)
+        if k in stats:
+            c0, c1 = int(stats[k]["Calls"]), int(r["Calls"])
+            stats[k] = {"Calls": c0 + c1, "AverageNs": (float(stats[k]["AverageNs"]) * c0 +
+                                                         float(r["AverageNs"]) * c1) / (c0 + c1)}
+        else:
+            stats[k] = r
     out = {"round": rnd, "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of "
                                    "`bench.py --steps 1 --warmup 0` (one step = the whole backtest)",
            "admm_iterations_per_step": iters, "kernels": {}}
