@@ -5,6 +5,10 @@ f ~ N(3e-4, 0.01^2), 10 sector factors g ~ N(0, 0.005^2), eps ~ N(0, 0.02^2), a 
 sector id per asset; benchmark y_t = R_t w_cap + N(0, 1e-4^2) with w_cap ~ Dirichlet(1);
 business-day calendar starting 2005-01-03.  Seeds are fixed per configuration
 (20240314 for configs 3-5).
+
+Configs 1/2 (SPTR index replication on ``usa_returns``, absent from the reference tree) use
+``usa_panel``: 494 synthetic assets on the last 4795 dates of the real SPTR calendar, each
+loading on the real SPTR return, so least-squares tracking of SPTR is meaningful.
 """
 from __future__ import annotations
 
@@ -37,3 +41,23 @@ def factor_panel(n_dates: int, n_assets: int, seed: int = SEED, n_sectors: int =
     w_cap = rng.dirichlet(np.ones(n_assets))
     y = R @ w_cap + rng.normal(0.0, 1e-4, size=n_dates)
     return business_days("2005-01-03", n_dates), R, y, sector
+
+
+USA_SEED = 20240101
+
+
+def usa_panel(sptr_days: np.ndarray, sptr: np.ndarray, n_assets: int = 494, n_rows: int = 4795,
+              seed: int = USA_SEED, n_sectors: int = 11):
+    """usa-shaped panel for configs 1/2 on the SPTR calendar: the last ``n_rows`` SPTR dates,
+    r_t = beta * sptr_t + B_s g_t + eps_t with beta ~ N(1, 0.25^2), 11 sector factors
+    g ~ N(0, 0.004^2), eps ~ N(0, 0.015^2).  Returns (dates datetime64[D], R [n_rows x
+    n_assets], y = the real SPTR returns on those dates)."""
+    days = np.asarray(sptr_days)[-n_rows:]
+    y = np.asarray(sptr, dtype=np.float64)[-n_rows:]
+    rng = np.random.default_rng(seed)
+    beta = rng.normal(1.0, 0.25, size=n_assets)
+    sector = rng.integers(0, n_sectors, size=n_assets)
+    g = rng.normal(0.0, 0.004, size=(n_rows, n_sectors))
+    eps = rng.normal(0.0, 0.015, size=(n_rows, n_assets))
+    R = np.ascontiguousarray(y[:, None] * beta[None, :] + g[:, sector] + eps)
+    return days.astype("datetime64[D]"), R, y

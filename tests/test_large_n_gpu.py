@@ -7,9 +7,11 @@ kernels, on the window path (grouped low-rank ADMM + window polish):
     long-only box -- 21 general rows;
   * config 5 shape: n = 5000 mean-variance risk-aversion x date sweep (porqua_amd.sweep).
 
-Rank(P) <= T = 252 < n, so the optimum is a face: the checks are the objective against
-the oracle IPM (n = 3000), feasibility, and the KKT certificate (tests/kkt.py), which is
-size-independent."""
+Both compare every solved problem against oracle optima committed as fixtures
+(tools/capture_large.py -> tests/golden/config4_oracle.npz, config5_oracle.npz; oracle.qp_ipm,
+KKT-certified): the objective to 1e-6 relative everywhere, the weights to 1e-5 where the
+optimum is unique (support well below rank(P) <= T = 252), plus feasibility and the
+relative KKT certificate (tests/kkt.py)."""
 import numpy as np
 import pytest
 import torch
@@ -19,6 +21,7 @@ from oracle.ref_pipeline import cov_pearson
 from porqua_amd import _lib, engine
 from porqua_amd.sweep import mean_variance_sweep
 from porqua_amd.synthetic import factor_panel
+from tests.conftest import load_golden
 from tests.kkt import kkt_residuals
 
 pytestmark = pytest.mark.gpu
@@ -51,6 +54,8 @@ def test_config4_tracking_n3000_sector_caps(device):
     yv = res.y.cpu().numpy()
     zb = res.z_box.cpu().numpy()
     assert np.all(st == _lib.PQ_SOLVED), st
+    gold = load_golden("config4_oracle")
+    assert list(gold["ends"]) == ends
     for i, e in enumerate(ends):
         X = R[e - T + 1:e + 1]
         P, q = 2 * X.T @ X, -2 * X.T @ y[e - T + 1:e + 1]
@@ -58,10 +63,15 @@ def test_config4_tracking_n3000_sector_caps(device):
         k = kkt_residuals(P, q, x[i], A=np.ones((1, n)), b=np.ones(1), G=G, h=h, lb=np.zeros(n),
                           ub=np.ones(n), y=yv[i], z_box=zb[i])
         assert max(k.values()) <= 1e-7, k
-        if i == 0:
-            o = solve_qp(P, q, G=G, h=h, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n))
-            obj = 0.5 * x[i] @ P @ x[i] + q @ x[i]
-            assert abs(obj - o.obj) <= 1e-6 * abs(o.obj)
+        obj = 0.5 * x[i] @ P @ x[i] + q @ x[i]
+        assert abs(obj - gold["obj"][i]) <= 1e-6 * abs(gold["obj"][i]), (e, obj, gold["obj"][i])
+        if (gold["x"][i] > 1e-9).sum() < T // 2:   # unique optimum: the weights too
+            assert np.abs(x[i] - gold["x"][i]).max() <= 1e-5
+    # the first date once more against a fresh oracle solve (the fixture's own pin)
+    X = R[ends[0] - T + 1:ends[0] + 1]
+    o = solve_qp(2 * X.T @ X, -2 * X.T @ y[ends[0] - T + 1:ends[0] + 1], G=G, h=h, A=np.ones((1, n)), b=np.ones(1),
+                 lb=np.zeros(n), ub=np.ones(n))
+    assert abs(o.obj - gold["obj"][0]) <= 1e-8 * abs(o.obj)
 
 
 def test_config5_risk_aversion_sweep_n5000(device):
@@ -78,18 +88,24 @@ def test_config5_risk_aversion_sweep_n5000(device):
     yv = res.y.cpu().numpy()
     zb = res.z_box.cpu().numpy()
     assert np.all(st == _lib.PQ_SOLVED), st
+    gold = load_golden("config5_oracle")
+    assert np.allclose(gold["lambdas"], lambdas)
     for d, e in enumerate(ends):
         W = R[e - T + 1:e + 1]
         S = cov_pearson(W)
         mu = np.exp(np.mean(np.log1p(W), axis=0)) - 1.0
         for j, lam in enumerate(lambdas):
             p = d * len(lambdas) + j
+            assert tuple(gold["pairs"][p]) == (e, j)
             P = 2 * lam * S
             k = kkt_residuals(P, -mu, x[p], A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n),
                               y=yv[p], z_box=zb[p])
             assert max(k.values()) <= 1e-7, (lam, k)
             obj = 0.5 * x[p] @ P @ x[p] - mu @ x[p]
             assert abs(res.obj[p].item() - obj) <= 1e-9 * max(1.0, abs(obj))
+            assert abs(obj - gold["obj"][p]) <= 1e-6 * abs(gold["obj"][p]), (e, lam, obj, gold["obj"][p])
+            if (gold["x"][p] > 1e-9).sum() < T // 2:
+                assert np.abs(x[p] - gold["x"][p]).max() <= 1e-5, (e, lam)
 
 
 def test_sweep_small_risk_aversion_needs_no_admm_retry(device):

@@ -1,5 +1,12 @@
 #!/usr/bin/env python3
-"""Throughput of BASELINE.json configs 4 and 5 on one MI355X (the bench line is config 3).
+"""Throughput of BASELINE.json configs 1/2, 4 and 5 on one MI355X (the bench line is config 3).
+
+* configs 1/2: SPTR index replication on the usa-shaped panel (494 assets on the last 4795
+  real SPTR dates, porqua_amd.synthetic.usa_panel), least-squares tracking, budget + LongOnly
+  box, width 252 (example/backtest.ipynb): config 2 = Backtest.run with solver_name='mi355x'
+  (drop-in, host staging included) on the 13 monthly dates and on every date of the panel
+  (4543 daily QPs); config 1 = the CPU reference path restated by the oracle (window, P = 2X'X,
+  q = -2X'y, oracle.qp_ipm) on the monthly dates, serial, timed on this host.
 
 * config 4: synthetic 3000 assets x 10000 dates, 252-day windows, daily rebalance
   (9749 QPs), tracking-error least squares (P = 2 X'X uncentred, q = -2 X'y) with budget,
@@ -83,16 +90,53 @@ def config5(steps, dev, settings=None):
                  "qps": nd * L / dt, "ms_per_step": dt * 1e3, "qps_per_step": nd * L}, **summary(res))
 
 
+def config12(steps, dev):
+    import pandas as pd
+    from oracle.qp_ipm import solve_qp
+    from oracle.ref_pipeline import objective_least_squares, window_rows
+    from porqua_amd.backtest import Backtest
+    from tests.test_configs12_gpu import service, usa_data
+    X, y = usa_data()
+    d = X.index.values.astype("datetime64[D]")
+    monthly = [str(r) for r in d[d > np.datetime64("2022-06-01")][::21]]
+    daily = [str(r) for r in d[251:]]
+    out = []
+    for tag, reb in (("monthly", monthly), ("daily", daily)):
+        def run():
+            bt = Backtest()
+            bt.run(service(X, y, reb))
+            return bt
+        bt, dt = timed(run, steps)
+        out.append({"config": f"config2: SPTR replication, n=494 LS tracking, {tag} ({len(reb)} dates), "
+                              "Backtest.run(solver_name='mi355x')", "qps": len(reb) / dt, "ms_per_run": dt * 1e3,
+                    "dates": len(reb), "solved": bt.stats["solved"], "path": bt.stats["path"]})
+    Xv, yv = X.to_numpy(), y.to_numpy()[:, 0]
+    n = Xv.shape[1]
+    t0 = time.perf_counter()
+    for rd in monthly:
+        rows = window_rows(d, rd, 252)
+        P, q, _ = objective_least_squares(Xv[rows], yv[rows])
+        solve_qp(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n))
+    dt = time.perf_counter() - t0
+    out.append({"config": "config1: same monthly backtest, CPU reference path (oracle restatement, serial, "
+                          "multithreaded BLAS; qpsolvers/cvxopt unavailable)", "qps": len(monthly) / dt,
+                "seconds": dt, "dates": len(monthly)})
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--dates", type=int, default=9749, help="config 4 rebalance dates")
-    ap.add_argument("--only", choices=["4", "5"], default=None)
+    ap.add_argument("--only", choices=["12", "4", "5"], default=None)
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="engine.Settings override for config 5 (experiments)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if args.only in (None, "12"):
+        for line in config12(args.steps, dev):
+            print(json.dumps(line), flush=True)
     if args.only in (None, "4"):
         print(json.dumps(config4(args.dates, args.steps, dev)), flush=True)
     if args.only in (None, "5"):
