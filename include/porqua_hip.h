@@ -131,6 +131,24 @@ int pq_window_moments_grouped(const double* panel, int64_t ldp, int32_t n, const
                               const int32_t* uoff, const int32_t* tlen, double* mu,
                               int64_t mu_stride, double* dg, int64_t dg_stride, void* stream);
 
+/* Windows with missing values (NaN): column means over the present rows (NaN when none)
+ * -- the shift passed to pq_cov_pairwise_batched; geometric != 0: exp(mean log(1 + x)) - 1
+ * over the present rows (MeanEstimator.estimate_geometric, src/mean_estimation.py:39-48,
+ * pandas skipna).                                                                          */
+int pq_window_nanmean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                      const int32_t* tlen, int32_t tmax, int32_t batch, double* mu, int64_t mu_stride,
+                      int32_t geometric, void* stream);
+
+/* pandas' pairwise-complete covariance, the result of DataFrame.cov() on a window with NaN
+ * (src/covariance.py:65-66): entry (i, j) from the rows where both are present, with their
+ * pairwise means and N_ij - 1 degrees of freedom; NaN when N_ij < 2.  Four masked FP64-MFMA
+ * Grams per 64x64 tile (N = M'M, X~'M, M'X~, X~'X~; X~ shifted by `shift`, may be NULL).
+ * out: batch x ld x ld, full symmetric, padding zero.                                    */
+int pq_cov_pairwise_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                            const int32_t* tlen, int32_t tmax, int32_t batch, const double* shift,
+                            int64_t shift_stride, double* out, int32_t ld, int64_t out_stride,
+                            void* stream);
+
 /* K1: batched windowed SYRK on FP64 MFMA.  mode 0: centred covariance with ddof=1
  * (Covariance.estimate 'pearson', src/covariance.py:40-56,65-66); mode 1: uncentred Gram
  * X'X (LeastSquares.set_objective, src/optimization.py:215).  out: batch x ld x ld.     */

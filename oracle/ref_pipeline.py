@@ -47,6 +47,25 @@ def cov_pearson(X: np.ndarray) -> np.ndarray:
     return c
 
 
+def cov_pairwise(X: np.ndarray) -> np.ndarray:
+    """DataFrame.cov() of a window with missing values (src/covariance.py:65-66 on NaN data):
+    pandas' pairwise-complete covariance -- entry (i, j) from the rows where both columns are
+    present, centred by those rows' own means, ddof 1; NaN when fewer than 2 common rows."""
+    X = np.asarray(X, dtype=np.float64)
+    n = X.shape[1]
+    ok = ~np.isnan(X)
+    S = np.full((n, n), np.nan)
+    for i in range(n):
+        for j in range(i + 1):
+            m = ok[:, i] & ok[:, j]
+            N = int(m.sum())
+            if N < 2:
+                continue
+            xi, xj = X[m, i], X[m, j]
+            S[i, j] = S[j, i] = ((xi - xi.mean()) * (xj - xj.mean())).sum() / (N - 1)
+    return S
+
+
 def cov_linear_shrinkage(X: np.ndarray, lam) -> np.ndarray:
     """src/covariance.py:71-84: Sigma + lam * mean(diag Sigma) * I (lam<0/None/NaN -> 0)."""
     if lam is None or np.isnan(lam) or lam < 0:

@@ -113,6 +113,10 @@ _EXPORTS = {
                               c_dp, c_int32, c_int64, c_dp, c_int32, c_dp, c_int32, c_dp], c_int32),
     "pq_window_sumsq": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_dp, c_int64,
                          c_dp], c_int32),
+    "pq_window_nanmean": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_int32, c_dp],
+                          c_int32),
+    "pq_cov_pairwise_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_dp,
+                                 c_int32, c_int64, c_dp], c_int32),
     "pq_window_moments_grouped": ([c_dp, c_int64, c_int32, c_dp, c_int32, c_dp, c_int32, c_dp, c_dp, c_dp,
                                    c_int64, c_dp, c_int64, c_dp], c_int32),
     "pq_init_state_lr": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp,

@@ -294,8 +294,10 @@ class Backtest:
         if width is None:
             return False
         Xs = X[universe]
-        if Xs.isna().to_numpy().any():
-            return False                      # NaN windows: pairwise covariance, serial path
+        # windows with missing values: the objectives that support them batch with the
+        # pairwise-complete covariance (MeanVariance); the others keep the serial path
+        if Xs.isna().to_numpy().any() and not getattr(opt, "batch_handles_nan", False):
+            return False
         idx = pd.DatetimeIndex(Xs.index)
         dates = idx.values.astype("datetime64[D]")
         rows, tlen = engine.window_rows(dates, np.array(rebdates, dtype="datetime64[D]"), width)

@@ -7,7 +7,8 @@
 
 ``Covariance.estimate(X)`` keeps the reference signature (T x n DataFrame in, n x n
 DataFrame out) and computes the two-pass np.cov / DataFrame.cov() result with K1
-(window mean + FP64-MFMA SYRK), the PD check with K2's Cholesky info and the repair with
+(window mean + FP64-MFMA SYRK; windows with NaN: pandas' pairwise-complete covariance from
+four masked MFMA Grams), the PD check with K2's Cholesky info and the repair with
 ``helper_functions.nearestPD``.  ``estimate_batch`` is the batched backtest entry: all
 rebalance dates of a device-resident panel at once, results left on the device.
 """
@@ -62,6 +63,11 @@ class Covariance:
                 if isinstance(covmat, pd.DataFrame) else fixed
         return covmat
 
+    def _estimate_batch_pairwise(self, panel, rows, tlen, out, method):
+        r = _pairwise_batch(panel, rows, tlen, out, method, self.spec.get("lambda_covmat_regularization"),
+                            bool(self.spec.get("check_positive_definite")))
+        return (None, None, None, None) if r is None else r
+
     # -- batched (backtest) entry --------------------------------------------------------
     def estimate_batch(self, panel, rows, tlen, out=None, plan=None, lower_only=False):
         """All dates at once on the device.  Returns (S, p_diag): S is the (B, ld, ld)
@@ -83,8 +89,10 @@ class Covariance:
             return None, None, None, None
         if method not in ("pearson", "linear_shrinkage"):
             raise NotImplementedError("This method is not implemented yet")
-        mu = panel.window_means(rows, tlen)
         B, n = int(rows.shape[0]), panel.n
+        if panel.has_nan:
+            return self._estimate_batch_pairwise(panel, rows, tlen, out, method)
+        mu = panel.window_means(rows, tlen)
         S = dg = None
         if materialise:
             S = panel.cov(rows, tlen, mode=0, out=out, mu=mu, plan=plan,
@@ -102,16 +110,44 @@ class Covariance:
         return S, pdiag, mu, dg
 
 
+def _pairwise_batch(panel, rows, tlen, out, method, lam_raw, check_pd):
+    """Windows with missing values, all dates at once: pairwise-complete covariance
+    (pq_cov_pairwise_batched), the linear-shrinkage term, then Covariance.estimate's PD check
+    and nearestPD repair for the dates that need it (src/covariance.py:50-54) -> (S, 0, None,
+    None); None when some pair has fewer than 2 common rows (the reference fails there too)."""
+    import torch
+    from .helper_functions import nearestPD, pd_info
+    S = panel.cov_pairwise(rows, tlen, out=out)
+    n = panel.n
+    if bool(torch.isnan(S[:, :n, :n]).any().item()):
+        return None
+    B = S.shape[0]
+    idx = torch.arange(n, device=S.device)
+    if method == "linear_shrinkage":
+        lam = _shrink_lambda(lam_raw)
+        if lam > 0:
+            md = torch.diagonal(S, dim1=1, dim2=2)[:, :n].mean(dim=1)
+            S[:, idx, idx] += (lam * md)[:, None]
+    if check_pd:
+        Sn = S[:, :n, :n].cpu().numpy()
+        bad = np.flatnonzero(pd_info(Sn, S.device) != 0)
+        if bad.size:
+            fixed = nearestPD(Sn[bad], S.device)
+            S[torch.from_numpy(bad).to(S.device), :n, :n] = torch.from_numpy(np.ascontiguousarray(fixed)).to(S.device)
+    return S, torch.zeros(B, dtype=torch.float64, device=S.device), None, None
+
+
 def _device_cov(X, mode=0):
     from . import engine
     Xv = np.ascontiguousarray(X.to_numpy() if hasattr(X, "to_numpy") else X, dtype=np.float64)
-    if np.isnan(Xv).any():
-        raise NotImplementedError(
-            "windows with NaN (pandas' pairwise-complete covariance) are not supported by the device path")
     T, n = Xv.shape
     pan = engine.Panel(Xv)
     rows, tlen = pan.rows_to_device(np.arange(T, dtype=np.int32)[None], np.array([T], dtype=np.int32))
-    S = pan.cov(rows, tlen, mode=mode)
+    if mode == 0 and np.isnan(Xv).any():
+        # missing values: pandas' pairwise-complete DataFrame.cov() (pq_cov_pairwise_batched)
+        S = pan.cov_pairwise(rows, tlen)
+    else:
+        S = pan.cov(rows, tlen, mode=mode)
     return S[0, :n, :n].cpu().numpy()
 
 

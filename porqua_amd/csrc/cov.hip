@@ -183,6 +183,128 @@ __global__ __launch_bounds__(256) void k_syrk(const double* panel, int64_t ldp, 
   if (I != J) acc_store_T(acc, o, ld, J * TB, I * TB);
 }
 
+// ---- windows with missing values: pandas' pairwise-complete covariance -------------------
+//
+// DataFrame.cov() on a window with NaN (src/covariance.py:65-66, pandas nancorr with cov=True)
+// uses, for each pair (i, j), only the rows where both are present: their own pairwise means
+// and N_ij - 1 degrees of freedom.  With X~ = (X - c) on present entries and 0 elsewhere
+// (c: the column's mean over its present rows, a shift that keeps the correction term small)
+// and M the presence mask, every entry follows from four masked Grams:
+//     N = M'M,  S_A = X~'M,  S_B = M'X~,  S_2 = X~'X~,
+//     Sigma_ij = (S_2 - S_A S_B / N)_ij / (N_ij - 1)      (NaN when N_ij < 2, as pandas)
+// -- four 64x64 MFMA tile products per workgroup over the same staged rows.
+__device__ __forceinline__ void load_win_masked(double (&v)[4], double (&m)[4], const double* panel, int64_t ldp,
+                                                int n, const int32_t* rw, int T, int k0, int c0,
+                                                const double* c) {
+  const int t = threadIdx.x;
+  const int k = t >> 4, i = (t & 15) * 4;
+  const int kk = k0 + k;
+  const int64_t row = kk < T ? (int64_t)rw[kk] : -1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int col = c0 + i + e;
+    double x = 0.0, p = 0.0;
+    if (row >= 0 && col < n) {
+      const double v0 = panel[row * ldp + col];
+      if (!isnan(v0)) {
+        x = v0 - (c ? c[col] : 0.0);
+        p = 1.0;
+      }
+    }
+    v[e] = x;
+    m[e] = p;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_syrk_pairwise(const double* panel, int64_t ldp, int n,
+                                                       const int32_t* rows, const int32_t* tlen, int tmax,
+                                                       const double* shift, int64_t shift_stride, double* out,
+                                                       int ld, int64_t out_stride) {
+  __shared__ __attribute__((aligned(16))) double smem[8 * STAGE];   // 2 buffers x (xa, ma, xb, mb)
+  const int b = blockIdx.y;
+  int I, J;
+  tri_index(blockIdx.x, I, J);
+  const int T = tlen[b];
+  const int32_t* rw = rows + (int64_t)b * tmax;
+  const double* c = shift ? shift + (int64_t)b * shift_stride : nullptr;
+  Acc s2, sa, sb, cn;
+  s2.zero();
+  sa.zero();
+  sb.zero();
+  cn.zero();
+  double xa[4], ma[4], xb[4], mb[4];
+  auto stage = [&](double* S) {
+    store_win(xa, S);
+    store_win(ma, S + STAGE);
+    store_win(xb, S + 2 * STAGE);
+    store_win(mb, S + 3 * STAGE);
+  };
+  load_win_masked(xa, ma, panel, ldp, n, rw, T, 0, I * TB, c);
+  load_win_masked(xb, mb, panel, ldp, n, rw, T, 0, J * TB, c);
+  stage(smem);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < T; k0 += KC) {
+    const bool more = (k0 + KC) < T;
+    if (more) {
+      load_win_masked(xa, ma, panel, ldp, n, rw, T, k0 + KC, I * TB, c);
+      load_win_masked(xb, mb, panel, ldp, n, rw, T, k0 + KC, J * TB, c);
+    }
+    const double* S = smem + buf * 4 * STAGE;
+    mma_lds(s2, S, S + 2 * STAGE, KC);
+    mma_lds(sa, S, S + 3 * STAGE, KC);
+    mma_lds(sb, S + STAGE, S + 2 * STAGE, KC);
+    mma_lds(cn, S + STAGE, S + 3 * STAGE, KC);
+    if (more) stage(smem + (buf ^ 1) * 4 * STAGE);
+    __syncthreads();
+    buf ^= 1;
+  }
+  const double qnan = __builtin_nan("");
+#pragma unroll
+  for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double N = cn.c[mm][nn][r];
+        s2.c[mm][nn][r] = N >= 2.0 ? (s2.c[mm][nn][r] - sa.c[mm][nn][r] * sb.c[mm][nn][r] / N) / (N - 1.0) : qnan;
+      }
+  double* o = out + (int64_t)b * out_stride;
+  // padding rows / columns >= n stay 0 like the dense kernel's
+#pragma unroll
+  for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (I * TB + acc_row(mm, r) >= n || J * TB + acc_col(nn) >= n) s2.c[mm][nn][r] = 0.0;
+  acc_store(s2, o, ld, I * TB, J * TB);
+  if (I != J) acc_store_T(s2, o, ld, J * TB, I * TB);
+}
+
+// column means over the present (non-NaN) rows of each window (NaN when none): the shift
+// of k_syrk_pairwise and pandas' skipna DataFrame.mean(); geo: exp(mean log(1 + x)) - 1,
+// MeanEstimator.estimate_geometric on a window with gaps (src/mean_estimation.py:39-48)
+__global__ __launch_bounds__(256) void k_window_nanmean(const double* panel, int64_t ldp, int n,
+                                                        const int32_t* rows, const int32_t* tlen, int tmax,
+                                                        double* mu, int64_t mu_stride, int geo) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int T = tlen[b];
+  const int32_t* rw = rows + (int64_t)b * tmax;
+  double s = 0.0;
+  int cnt = 0;
+  for (int k = 0; k < T; ++k) {
+    const double v = panel[(int64_t)rw[k] * ldp + j];
+    if (!isnan(v)) {
+      s += geo ? log1p(v) : v;
+      ++cnt;
+    }
+  }
+  mu[(int64_t)b * mu_stride + j] = cnt ? (geo ? expm1(s / cnt) : s / cnt) : __builtin_nan("");
+}
+
 // ---- sliding windows: anchor SYRK + rank-2s updates -----------------------------------
 //
 // A daily backtest's consecutive windows share T - s of their T rows (s = 1 for daily,
@@ -387,6 +509,32 @@ extern "C" int pq_window_moments_grouped(const double* panel, int64_t ldp, int32
                      (hipStream_t)stream, panel, ldp, n, gdates, urows, umax, uoff, tlen, mu, mu_stride, dg,
                      dg_stride);
   PQ_CHECK_LAUNCH("pq_window_moments_grouped");
+  return 0;
+}
+
+extern "C" int pq_window_nanmean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                                 const int32_t* tlen, int32_t tmax, int32_t batch, double* mu, int64_t mu_stride,
+                                 int32_t geometric, void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(mu != nullptr, "pq_window_nanmean: mu is null");
+  if (batch == 0) return 0;
+  hipLaunchKernelGGL(pq::k_window_nanmean, dim3((n + 255) / 256, batch), dim3(256), 0, (hipStream_t)stream, panel,
+                     ldp, n, rows, tlen, tmax, mu, mu_stride, geometric);
+  PQ_CHECK_LAUNCH("pq_window_nanmean");
+  return 0;
+}
+
+extern "C" int pq_cov_pairwise_batched(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
+                                       const int32_t* tlen, int32_t tmax, int32_t batch, const double* shift,
+                                       int64_t shift_stride, double* out, int32_t ld, int64_t out_stride,
+                                       void* stream) {
+  if (int e = check_win(panel, n, rows, tlen, tmax, batch)) return e;
+  PQ_CHECK_ARG(out && ld >= n && ld % 64 == 0, "pq_cov_pairwise_batched: ld must be a multiple of 64 >= n");
+  if (batch == 0) return 0;
+  const int nb = ld / 64;
+  hipLaunchKernelGGL(pq::k_syrk_pairwise, dim3(nb * (nb + 1) / 2, batch), dim3(256), 0, (hipStream_t)stream, panel,
+                     ldp, n, rows, tlen, tmax, shift, shift_stride, out, ld, out_stride);
+  PQ_CHECK_LAUNCH("pq_cov_pairwise_batched");
   return 0;
 }
 

@@ -941,6 +941,37 @@ class Panel:
                       mu.stride(0), _stream()), "window means")
         return mu
 
+    def window_nanmeans(self, rows, tlen, geometric=False, out=None):
+        """Column means over the present rows of every window (NaN-aware; pandas skipna),
+        arithmetic or geometric -> (B, round_up(n, 64))."""
+        lib = _lib.load()
+        B, tmax = rows.shape
+        mu = out if out is not None else torch.zeros((B, round_up(self.n, 64)), dtype=F64, device=self.device)
+        _lib.check(lib.pq_window_nanmean(_ptr(self.R), self.R.stride(0), self.n, _ptr(rows), _ptr(tlen), tmax, B,
+                                         _ptr(mu), mu.stride(0), int(geometric), _stream()), "pq_window_nanmean")
+        return mu
+
+    @property
+    def has_nan(self) -> bool:
+        if getattr(self, "_has_nan", None) is None:
+            self._has_nan = bool(torch.isnan(self.R).any().item())
+        return self._has_nan
+
+    def cov_pairwise(self, rows, tlen, out=None):
+        """Pairwise-complete covariance of windows with missing values (pandas
+        DataFrame.cov() with NaN, src/covariance.py:65-66) -> (B, ld, ld); NaN where a pair
+        has fewer than 2 common rows."""
+        lib = _lib.load()
+        B, tmax = rows.shape
+        ld = round_up(self.n, 64)
+        c = torch.nan_to_num(self.window_nanmeans(rows, tlen), nan=0.0)   # all-missing column: no shift
+        if out is None:
+            out = torch.empty((B, ld, ld), dtype=F64, device=self.device)
+        _lib.check(lib.pq_cov_pairwise_batched(_ptr(self.R), self.R.stride(0), self.n, _ptr(rows), _ptr(tlen), tmax,
+                                               B, _ptr(c), c.stride(0), _ptr(out), ld, out.stride(0), _stream()),
+                   "pq_cov_pairwise_batched")
+        return out
+
     def cov(self, rows, tlen, mode=0, out=None, mu=None, plan: SlidePlan | None = None,
             lower_only: bool = False):
         """K1: per-date centred covariance (mode 0, ddof=1) or Gram X'X (mode 1) -> (B, ld, ld).

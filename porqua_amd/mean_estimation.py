@@ -44,7 +44,10 @@ class MeanEstimator:
         if L == 0:
             mu = np.full(n, np.nan)
         else:
-            g = pan.window_means(rows, tlen, geometric=True)[0, :n].cpu().numpy()
+            if isinstance(X, pd.DataFrame) and np.isnan(Xv[a:b]).any():   # pandas mean: skipna
+                g = pan.window_nanmeans(rows, tlen, geometric=True)[0, :n].cpu().numpy()
+            else:
+                g = pan.window_means(rows, tlen, geometric=True)[0, :n].cpu().numpy()
             mu = g if sf == 1 else np.exp(np.log1p(g) * sf) - 1
         if isinstance(X, pd.DataFrame):
             return pd.Series(mu, index=X.columns)

@@ -134,6 +134,8 @@ class EmptyOptimization(Optimization):
 class MeanVariance(Optimization):
     """P = 2 * risk_aversion * Sigma, q = -mu_geometric (src/optimization.py:157-177)."""
 
+    batch_handles_nan = True   # windows with gaps: pairwise covariance + skipna means, batched
+
     def __init__(self, covariance: Optional[Covariance] = None,
                  mean_estimator: Optional[MeanEstimator] = None, **kwargs):
         super().__init__(**kwargs)
@@ -150,14 +152,17 @@ class MeanVariance(Optimization):
     def objective_batch(self, stage):
         import torch
         from . import engine
-        lowrank = stage.prefer_lowrank and self.covariance.spec["method"] != "duv"
+        nan = stage.panel.has_nan   # missing values: pairwise covariance, dense P (no window form)
+        lowrank = stage.prefer_lowrank and self.covariance.spec["method"] != "duv" and not nan
         S, pdiag, mu_c, dg = self.covariance.estimate_batch_lr(
             stage.panel, stage.rows, stage.tlen, out=None if lowrank else stage.P_buffer(),
-            plan=stage.slide_plan(), materialise=not lowrank)
+            plan=None if nan else stage.slide_plan(), materialise=not lowrank)
         ra = float(self.params["risk_aversion"])
         B = stage.batch
         dev = stage.device
-        if mu_c is None:  # duv: identity covariance
+        if nan and S is None:
+            return None
+        if mu_c is None and not nan:  # duv: identity covariance
             S = stage.identity_P()
             pdiag = torch.zeros(B, dtype=torch.float64, device=dev)
         elif lowrank:   # factored form S = Xc'Xc / (T - 1) for the Woodbury solver (no n x n S)
@@ -170,7 +175,12 @@ class MeanVariance(Optimization):
         if not np.all(stage.tlen_host == stage.tlen_host[0]) and (a, b) != (0, int(stage.tlen_host[0])):
             return None
         mrows, mtlen = stage.sub_windows(a, b)
-        mu = stage.panel.window_means(mrows, mtlen, geometric=True)
+        if nan:
+            mu = stage.panel.window_nanmeans(mrows, mtlen, geometric=True)
+            if bool(torch.isnan(mu[:, :stage.n]).any().item()):
+                return None
+        else:
+            mu = stage.panel.window_means(mrows, mtlen, geometric=True)
         sf = me.spec.get("scalefactor")
         if sf not in (None, 1):
             mu = torch.expm1(torch.log1p(mu) * sf)
@@ -196,14 +206,24 @@ class QEQW(Optimization):
                 None, torch.zeros((B, stage.ld), dtype=torch.float64, device=dev), None)
 
 
+def _tracking_rho_defaults(params) -> None:
+    """ADMM start for tracking objectives (uncentred Gram P = 2 X'X, q = -2 X'y): rho =
+    0.2 mean(diag P) and no |q| floor.  The floor (Settings.rho0_qrel) is for nearly linear
+    mean-variance objectives; here |q| ~ diag P and it would start rho ~10x too high.
+    Measured on the usa-shaped SPTR replication (494 assets, 4544 daily dates): 22 ADMM
+    iterations and no refactorisation, against 168 iterations and 3744 refactorisations with
+    the mean-variance defaults (7.6k -> 67.6k QPs/s, tools/diag_ls.py)."""
+    params.setdefault("rho0_rel", 0.2)
+    params.setdefault("rho0_qrel", 0.0)
+
+
 class LeastSquares(Optimization):
     """P = 2 X'X (+ 2 l2 I), q = -2 X'y, constant y'y (src/optimization.py:198-229)."""
 
     def __init__(self, covariance: Optional[Covariance] = None, **kwargs):
         super().__init__(**kwargs)
         self.covariance = covariance
-        # tracking problems: P = 2 X'X is well scaled, a smaller initial rho converges faster
-        self.params.setdefault("rho0_rel", 0.5)
+        _tracking_rho_defaults(self.params)
 
     def set_objective(self, optimization_data: OptimizationData) -> None:
         X = optimization_data["return_series"]
@@ -248,6 +268,10 @@ class LeastSquares(Optimization):
 
 class WeightedLeastSquares(Optimization):
     """P = 2 X'WX, q = -2 X'Wy with half-life tau weights (src/optimization.py:232-259)."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        _tracking_rho_defaults(self.params)
 
     def _weights(self, T):
         lam = np.exp(-np.log(2) / self.params["tau"])

@@ -137,3 +137,15 @@ def test_lad_lp_matches_reference(tag):
         assert np.array_equal(lb, g["lb"][i]) and np.array_equal(ub, g["ub"][i])
         s = olad.solve_lp(q, A, b, lb, ub)
         assert abs(s.fun - g["obj"][i]) <= 1e-9 * g["obj"][i]
+
+
+def test_pairwise_cov_oracle_matches_reference_nan_windows():
+    """oracle cov_pairwise == the reference's DataFrame.cov() on NaN-bearing windows
+    (tools/capture_nan_cov.py), NaN pattern included."""
+    g = load_golden("nan_cov")
+    for case in ("msci_holes", "wide", "sparse"):
+        S = rp.cov_pairwise(g[f"{case}__X"])
+        ref = g[f"{case}__raw"]
+        assert np.array_equal(np.isnan(S), np.isnan(ref)), case
+        ok = ~np.isnan(ref)
+        assert np.abs(S[ok] - ref[ok]).max() <= 1e-14 * np.abs(ref[ok]).max(), case

@@ -49,7 +49,7 @@ def summary(res):
             "mean_iters": float(res.iters.float().mean().item()), "max_iters": int(res.iters.max().item())}
 
 
-def config4(dates_limit, steps, dev):
+def config4(dates_limit, steps, dev, overrides=None):
     n, T, ns, cap = 3000, 252, 20, 0.15
     dates, R, y, sec = factor_panel(10000, n, n_sectors=ns)
     ends = np.arange(T - 1, 10000)[:dates_limit]
@@ -65,7 +65,7 @@ def config4(dates_limit, steps, dev):
     lr = engine.LowRank(pan, r_d, t_d, mu=None)
     gp = engine.GroupPlan(rows, tlen, dev)
     ws = engine.Workspace(qb, dense=False)
-    settings = engine.Settings(rho0_rel=0.5)
+    settings = engine.Settings.from_params(dict({"rho0_rel": 0.1, "rho0_qrel": 0.0}, **(overrides or {})))
 
     def run():
         xty, _ = pan.gram_xy(r_d, t_d)                 # q = -2 X'y per date, inside the step
@@ -138,7 +138,8 @@ def main():
         for line in config12(args.steps, dev):
             print(json.dumps(line), flush=True)
     if args.only in (None, "4"):
-        print(json.dumps(config4(args.dates, args.steps, dev)), flush=True)
+        ov = dict(kv.split("=", 1) for kv in args.set)
+        print(json.dumps(dict(config4(args.dates, args.steps, dev, ov), settings_overrides=args.set)), flush=True)
     if args.only in (None, "5"):
         st = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set)) if args.set else None
         print(json.dumps(dict(config5(args.steps, dev, st), settings_overrides=args.set)), flush=True)
