@@ -59,4 +59,5 @@ def test_pairwise_cov_large_window_matches_oracle(device):
     S = cov_pearson(pd.DataFrame(R)).to_numpy()
     ref = rp.cov_pairwise(R)
     assert np.array_equal(np.isnan(S), np.isnan(ref))
-    assert _rel(S, ref) <= 1e-12
+    ok = ~np.isnan(ref)
+    assert np.abs(S[ok] - ref[ok]).max() <= 1e-12 * np.abs(ref[ok]).max()

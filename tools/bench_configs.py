@@ -85,9 +85,17 @@ def config5(steps, dev, settings=None):
     rows, tlen = engine.window_rows(dates, dates[ends], T)
     pan = engine.Panel(R, device=dev)
     lambdas = np.logspace(-1, 2, L)
-    res, dt = timed(lambda: mean_variance_sweep(pan, rows, tlen, lambdas, settings=settings)[0], steps)
+    meta = {}
+
+    def run():
+        r, m = mean_variance_sweep(pan, rows, tlen, lambdas, settings=settings)
+        meta.update(m)
+        return r
+    res, dt = timed(run, steps)
     return dict({"config": "config5: n=5000 mean-variance, 64 monthly dates x 64 risk aversions",
-                 "qps": nd * L / dt, "ms_per_step": dt * 1e3, "qps_per_step": nd * L}, **summary(res))
+                 "qps": nd * L / dt, "ms_per_step": dt * 1e3, "qps_per_step": nd * L,
+                 "capacitance": meta.get("capacitance"), "factorizations_per_step": meta.get("factorizations"),
+                 "shared_factor": meta.get("shared_factor")}, **summary(res))
 
 
 def config12(steps, dev):
