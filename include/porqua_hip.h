@@ -264,7 +264,8 @@ int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
  *   pq_gcap_assemble   M_U per group from the band Gram (W >= the widest union span), pc, cc;
  *   (pq_factor_batched on {n = k, ld = k_ld, P = M, batch = ngroups}, invert = 2 -> Minv)
  *   pq_gcap_prepare    per date a_b = W_U mu_b, q_b = M_U^-1 a_b (aq: a | q, 2 k_ld each)
- *                      and H_b^-1 (ldh x ldh, ldh >= U - T + 1 <= 64);
+ *                      and H_b^-1 (ldh x ldh, ldh >= U - T + 1 <= 64); one workgroup per
+ *                      group (idx, nidx: a subset of GROUPS, or NULL for all);
  *   pq_admm_lr_gcap    the fused grouped ADMM (pq_admm_lr_grouped with pc / cc) with the
  *                      per-date M_b^-1 symv replaced by one MFMA GEMM with M_U^-1 per
  *                      group plus the small per-date correction.  Adaptive rho is decided

@@ -126,116 +126,212 @@ __global__ __launch_bounds__(256) void k_gcap_assemble(pq_lowrank lr, pq_problem
   }
 }
 
-// ---- per-date preparation: a_b, q_b = M_U^-1 a_b, H_b^-1 ---------------------------------
-__global__ __launch_bounds__(256) void k_gcap_prep(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
+// ---- preparation, one workgroup per GROUP: a_b, q_b = M_U^-1 a_b, H_b^-1 for its dates ------
+// The dates of a group share the union rows, so
+//   a_b[u] = sqrt(c) (1/T) sum_{t in window b} G_U[u][t]     (G_U: band Gram of the union)
+// is one pass over G_U's rows for all of them (masked sums per date), and Q = M_U^-1 A is one
+// MFMA GEMM over the group's dates (the ADMM's z' = M_U^-1 B loop) instead of a symv per date.
+// Then per date: mu'mu, a'q, H_b (m + 1 x m + 1) assembled in LDS, its Cholesky, and H_b^-1
+// column by column (lane t solves for column t, x in LDS).
+constexpr int PT_PREP = 1024;   // 16 waves: a row of G_U / a GEMM tile / a date per wave
+constexpr int PW_PREP = PT_PREP / 64;
+
+__global__ __launch_bounds__(PT_PREP) void k_gcap_prep(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
                                                    pq_settings s, const int32_t* idx, const double* band,
                                                    int64_t ldo, int r0, const double* pc, int64_t ldpc) {
   __shared__ int s_w[CU_MAX];
-  __shared__ double s_a[CK_MAX], s_q[CK_MAX];
-  __shared__ double H[CH_MAX * (CH_MAX + 1)];
-  __shared__ double red[16];
-  __shared__ int s_bad;
-  const int slot = xcd_slot(blockIdx.x, gridDim.x);
-  const int b = idx ? idx[slot] : slot;
-  const int grp = gc.gidx[b];
-  const int U = gc.ucnt[grp], mg = pb.mg, n = pb.n;
-  const int T = lr.tlen[b], off = gc.uoff[b];
-  const int m = U - T, kU = U + mg, k_ld = gc.k_ld;
-  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  __shared__ __attribute__((aligned(16))) double s_a[(CK_MAX + 16) * CG_MAX];   // a_b: row u, column (date) g
+  __shared__ double s_q[CK_MAX * CG_MAX];
   constexpr int HP = CH_MAX + 1;
-  for (int u = t; u < U; u += 256) s_w[u] = gc.urows[(int64_t)grp * gc.umax + u] - r0;
+  __shared__ double H[CH_MAX * HP];
+  __shared__ double X[CH_MAX * CH_MAX];
+  __shared__ double s_mm[CG_MAX], s_aq[CG_MAX], s_sr[CMG];
+  __shared__ int s_off[CG_MAX], s_T[CG_MAX];
+  const int slot = xcd_slot(blockIdx.x, gridDim.x);
+  const int grp = idx ? idx[slot] : slot;
+  const int d0 = gc.gdates[grp];
+  const int G = gc.gdates[grp + 1] - d0;
+  const int U = gc.ucnt[grp], mg = pb.mg, n = pb.n;
+  const int kU = U + mg, k_ld = gc.k_ld;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  for (int u = t; u < U; u += PT_PREP) s_w[u] = gc.urows[(int64_t)grp * gc.umax + u] - r0;
+  if (t < CG_MAX) {
+    s_off[t] = t < G ? gc.uoff[d0 + t] : 0;
+    s_T[t] = t < G ? lr.tlen[d0 + t] : 1;
+  }
+  const GConst g = gconst(lr, pb, s, d0, gc.grho[grp]);   // c, d, rho uniform in the group
+  if (t < mg) s_sr[t] = sqrt(crho(pb.lg[t], pb.ug[t], g.rho, s));
+  const int ktile = (kU + 15) >> 4;
+  for (int e = t; e < (CK_MAX + 16) * CG_MAX; e += PT_PREP) s_a[e] = 0.0;
   __syncthreads();
-  const GConst g = gconst(lr, pb, s, b, gc.grho[grp]);
-  // a = [sqrt(c) X_U mu ; sqrt(R) Cg mu],  X_U mu = (1/T) G_U[:, window] 1
-  for (int u = w; u < U; u += 4) {
-    double sum = 0.0;
-    for (int tt = l; tt < T; tt += 64) sum += band_at(band, ldo, s_w[u], s_w[off + tt]);
-    sum = wave_sum(sum);
-    if (l == 0) s_a[u] = g.sqc * sum / T;
+  // ---- A: a_b for every date (wave per union row; the row of G_U in registers) ------------
+  for (int u = w; u < U; u += PW_PREP) {
+    double gv[CU_MAX / 64];
+#pragma unroll
+    for (int j = 0; j < CU_MAX / 64; ++j) {
+      const int v = l + 64 * j;
+      gv[j] = v < U ? band_at(band, ldo, s_w[u], s_w[v]) : 0.0;
+    }
+    for (int gg = 0; gg < G; ++gg) {
+      const int lo = s_off[gg], hi = lo + s_T[gg];
+      double sum = 0.0;
+#pragma unroll
+      for (int j = 0; j < CU_MAX / 64; ++j) {
+        const int v = l + 64 * j;
+        if (v >= lo && v < hi) sum += gv[j];
+      }
+      sum = wave_sum(sum);
+      if (l == 0) s_a[u * CG_MAX + gg] = g.sqc * sum / s_T[gg];
+    }
   }
-  for (int r = w; r < mg; r += 4) {
+  for (int e = w; e < mg * G; e += PW_PREP) {   // general rows: sqrt(R_r) Cg_r mu_b = sqrt(R_r) (1/T) sum PC
+    const int r = e / G, gg = e % G;
     double sum = 0.0;
-    for (int tt = l; tt < T; tt += 64) sum += pc[(int64_t)s_w[off + tt] * ldpc + r];
+    for (int tt = l; tt < s_T[gg]; tt += 64) sum += pc[(int64_t)s_w[s_off[gg] + tt] * ldpc + r];
     sum = wave_sum(sum);
-    if (l == 0) s_a[U + r] = sqrt(crho(pb.lg[r], pb.ug[r], g.rho, s)) * sum / T;
-  }
-  double mm = 0.0;
-  const double* mu = lr.mu + (int64_t)b * lr.mu_stride;
-  for (int i = t; i < n; i += 256) mm = fma(mu[i], mu[i], mm);
-  mm = block_sum(mm, red);   // (barrier: s_a complete)
-  const double* Mi = gc.Minv + (int64_t)grp * gc.M_stride;   // full symmetric M_U^-1
-  for (int u = w; u < kU; u += 4) {
-    double sum = 0.0;
-    for (int v = l; v < kU; v += 64) sum += Mi[(int64_t)u * k_ld + v] * s_a[v];
-    sum = wave_sum(sum);
-    if (l == 0) s_q[u] = sum;
+    if (l == 0) s_a[(U + r) * CG_MAX + gg] = s_sr[r] * sum / s_T[gg];
   }
   __syncthreads();
-  double aq = 0.0;
-  for (int u = t; u < kU; u += 256) aq += s_a[u] * s_q[u];
-  aq = block_sum(aq, red);
-  double* A = gc.aq + (int64_t)b * gc.aq_stride;
-  for (int u = t; u < k_ld; u += 256) {
-    A[u] = u < kU ? s_a[u] : 0.0;
-    A[k_ld + u] = u < kU ? s_q[u] : 0.0;
+  // ---- B: Q = M_U^-1 A (MFMA; A rows from the full symmetric M_U^-1, B from LDS) -----------
+  const double* Mi = gc.Minv + (int64_t)grp * gc.M_stride;
+  {
+    const int kq = l >> 4, m = l & 15;
+    const int kU4 = (kU + 7) & ~7;
+    for (int tile = w; tile < ktile; tile += PW_PREP) {
+      const int row = tile * 16 + m;
+      const bool rv = row < kU;
+      const double* mrow = Mi + (int64_t)(rv ? row : 0) * k_ld;
+      f64x4 z = f64x4{0.0, 0.0, 0.0, 0.0};
+      for (int k0 = 0; k0 < kU4; k0 += 8) {
+        const int kk = k0 + 2 * kq;
+        const bool kin = kk < kU, kin1 = kk + 1 < kU;
+        const double b0 = s_a[kk * CG_MAX + m];   // rows >= kU of s_a are zero
+        const double b1 = s_a[(kk + 1) * CG_MAX + m];
+        double2 av = double2{0.0, 0.0};
+        if (rv && kin1) av = *reinterpret_cast<const double2*>(mrow + kk);
+        else if (rv && kin) av.x = mrow[kk];
+        z = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, b0, z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, b1, z, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = tile * 16 + kq + 4 * r;
+        if (u < kU) s_q[u * CG_MAX + m] = z[r];
+      }
+    }
   }
-  // H (m + 1) x (m + 1): C = union rows outside [off, off + T)
-  const int mh = m + 1;
-  const double sct = sqrt(g.c * T);
-  for (int e = t; e < mh * mh; e += 256) {
-    const int i = e / mh, j = e % mh;
-    double v;
+  __syncthreads();
+  // ---- a, q out; mu'mu and a'q per date (wave per date) --------------------------------------
+  for (int e = t; e < G * k_ld; e += PT_PREP) {
+    const int gg = e / k_ld, u = e % k_ld;
+    double* A = gc.aq + (int64_t)(d0 + gg) * gc.aq_stride;
+    A[u] = u < kU ? s_a[u * CG_MAX + gg] : 0.0;
+    A[k_ld + u] = u < kU ? s_q[u * CG_MAX + gg] : 0.0;
+  }
+  for (int gg = w; gg < G; gg += PW_PREP) {
+    const double* mu = lr.mu + (int64_t)(d0 + gg) * lr.mu_stride;
+    double mm = 0.0, aq = 0.0;
+    for (int i = l; i < n; i += 64) mm = fma(mu[i], mu[i], mm);
+    for (int u = l; u < kU; u += 64) aq = fma(s_a[u * CG_MAX + gg], s_q[u * CG_MAX + gg], aq);
+    mm = wave_sum(mm);
+    aq = wave_sum(aq);
+    if (l == 0) {
+      s_mm[gg] = mm;
+      s_aq[gg] = aq;
+    }
+  }
+  __syncthreads();
+  // ---- C: per date H_b (C = union rows outside [off, off + T)), its Cholesky and H_b^-1 ---------
+  const double sct_c = g.c / g.d;
+  auto h_entry = [&](int gg, int i, int j) -> double {   // H_b[i][j], i, j < m + 1
+    const int T = s_T[gg], off = s_off[gg], m = U - T;
+    const double sct = sqrt(g.c * T);
     if (i < m && j < m) {
       const int ci = i < off ? i : i + T, cj = j < off ? j : j + T;
-      v = Mi[(int64_t)ci * k_ld + cj];
-    } else if (i < m) {
-      const int ci = i < off ? i : i + T;
-      v = -(sct / g.d) * s_q[ci];
-    } else if (j < m) {
-      const int cj = j < off ? j : j + T;
-      v = -(sct / g.d) * s_q[cj];
-    } else {
-      v = 1.0 - (g.c * T / g.d) * (mm - aq / g.d);
+      return Mi[(int64_t)ci * k_ld + cj];
     }
-    H[i * HP + j] = v;
+    if (i < m) return -(sct / g.d) * s_q[(i < off ? i : i + T) * CG_MAX + gg];
+    if (j < m) return -(sct / g.d) * s_q[(j < off ? j : j + T) * CG_MAX + gg];
+    return 1.0 - sct_c * T * (s_mm[gg] - s_aq[gg] / g.d);
+  };
+  // m + 1 <= 16 (the slide groups' usual case): one wave per date, H in registers (MFMA C
+  // layout), Cholesky + L^-1 in one shuffle chain (wave_chol_inv16), H^-1 = L^-T L^-1 by four
+  // 16x16x4 MFMAs -- no LDS, no barriers
+  for (int gg = w; gg < G; gg += PW_PREP) {
+    const int mh = U - s_T[gg] + 1;
+    if (mh > 16) continue;
+    const int cc = l & 15, g4 = l >> 4;
+    double A[4], Bv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = g4 + 4 * q;
+      A[q] = (r < mh && cc < mh) ? h_entry(gg, r, cc) : (r == cc ? 1.0 : 0.0);
+      Bv[q] = (r == cc) ? 1.0 : 0.0;
+    }
+    const int b = d0 + gg;
+    if (wave_chol_inv16(A, Bv)) {
+      if (l == 0) st.status[b] = PQ_NON_CONVEX;   // not SPD to rounding: no group form for it
+      continue;
+    }
+    f64x4 hi = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hi = __builtin_amdgcn_mfma_f64_16x16x4f64(Bv[q], Bv[q], hi, 0, 0, 0);
+    double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
+    for (int e = l; e < gc.ldh * gc.ldh; e += 64)   // entries outside the mh x mh block
+      if (e / gc.ldh >= mh || e % gc.ldh >= mh) Hi[e] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = g4 + 4 * q;
+      if (r < mh && cc < mh) Hi[(int64_t)r * gc.ldh + cc] = hi[q];
+    }
   }
-  __syncthreads();
-  // Cholesky of H (LDS, one column per step), then H^-1 = L^-T L^-1 column by column
-  for (int k = 0; k < mh; ++k) {
-    const double dk = H[k * HP + k];
+  // m + 1 > 16: the whole workgroup per date, H in LDS
+  for (int gg = 0; gg < G; ++gg) {
+    const int b = d0 + gg;
+    const int mh = U - s_T[gg] + 1;
+    if (mh <= 16) continue;   // uniform
     __syncthreads();
-    if (t == 0) s_bad = !(dk > 0.0) || !isfinite(dk);
+    for (int e = t; e < mh * mh; e += PT_PREP) H[(e / mh) * HP + e % mh] = h_entry(gg, e / mh, e % mh);
     __syncthreads();
-    if (s_bad) break;
-    const double sd = sqrt(dk);
-    if (t > k && t < mh) H[t * HP + k] /= sd;
-    __syncthreads();
-    if (t == 0) H[k * HP + k] = sd;
-    const int rem = mh - 1 - k;
-    for (int e = t; e < rem * rem; e += 256) {
-      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
-      if (j <= i) H[i * HP + j] -= H[i * HP + k] * H[j * HP + k];
+    for (int k = 0; k < mh; ++k) {   // right-looking Cholesky in LDS (lower)
+      const double dk = H[k * HP + k];
+      if (!(dk > 0.0) || !isfinite(dk)) break;   // uniform: every thread reads the same dk
+      const double sd = sqrt(dk);
+      __syncthreads();
+      if (t > k && t < mh) H[t * HP + k] /= sd;
+      if (t == 0) H[k * HP + k] = sd;
+      __syncthreads();
+      const int rem = mh - 1 - k;
+      for (int e = t; e < rem * rem; e += PT_PREP) {
+        const int i = k + 1 + e / rem, j = k + 1 + e % rem;
+        if (j <= i) H[i * HP + j] -= H[i * HP + k] * H[j * HP + k];
+      }
+      __syncthreads();
+    }
+    int bad = 0;   // a failed pivot leaves H[k][k] unscaled and non-positive
+    for (int k = 0; k < mh; ++k) bad |= !(H[k * HP + k] > 0.0) || !isfinite(H[k * HP + k]);
+    if (bad) {
+      if (t == 0) st.status[b] = PQ_NON_CONVEX;
+      continue;
+    }
+    double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
+    if (t < mh) {   // column t of H^-1: L L' x = e_t, x in LDS column t
+      for (int i = 0; i < mh; ++i) {
+        double v = (i == t) ? 1.0 : 0.0;
+        for (int j = 0; j < i; ++j) v -= H[i * HP + j] * X[j * CH_MAX + t];
+        X[i * CH_MAX + t] = v / H[i * HP + i];
+      }
+      for (int i = mh - 1; i >= 0; --i) {
+        double v = X[i * CH_MAX + t];
+        for (int j = i + 1; j < mh; ++j) v -= H[j * HP + i] * X[j * CH_MAX + t];
+        X[i * CH_MAX + t] = v / H[i * HP + i];
+      }
     }
     __syncthreads();
-  }
-  double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
-  if (s_bad) {   // not SPD to rounding: the date cannot use the group form
-    if (t == 0) st.status[b] = PQ_NON_CONVEX;
-    return;
-  }
-  if (t < mh) {   // column t of H^-1: solve L L' x = e_t (forward then backward, one thread)
-    double x[CH_MAX];
-    for (int i = 0; i < mh; ++i) {
-      double v = (i == t) ? 1.0 : 0.0;
-      for (int j = 0; j < i; ++j) v -= H[i * HP + j] * x[j];
-      x[i] = v / H[i * HP + i];
+    for (int e = t; e < gc.ldh * gc.ldh; e += PT_PREP) {
+      const int i = e / gc.ldh, j = e % gc.ldh;
+      Hi[e] = (i < mh && j < mh) ? X[i * CH_MAX + j] : 0.0;
     }
-    for (int i = mh - 1; i >= 0; --i) {
-      double v = x[i];
-      for (int j = i + 1; j < mh; ++j) v -= H[j * HP + i] * x[j];
-      x[i] = v / H[i * HP + i];
-    }
-    for (int i = 0; i < gc.ldh; ++i) Hi[(int64_t)i * gc.ldh + t] = i < mh ? x[i] : 0.0;
   }
 }
 
@@ -945,9 +1041,10 @@ extern "C" int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(gc->aq_stride >= 2 * (int64_t)gc->k_ld && gc->ldh > 0 && gc->ldh <= pq::CH_MAX,
                "pq_gcap_prepare: aq needs 2 k_ld per date, ldh <= %d", pq::CH_MAX);
   PQ_CHECK_ARG(pb->mg == 0 || pc, "pq_gcap_prepare: general rows need pc");
-  const int grid = idx ? nidx : pb->batch;
+  PQ_CHECK_ARG(gc->umax <= pq::CU_MAX && pb->mg <= pq::CMG, "pq_gcap_prepare: union or general rows too many");
+  const int grid = idx ? nidx : gc->ngroups;   // one workgroup per group (idx: group subset)
   if (grid <= 0) return 0;
-  hipLaunchKernelGGL(pq::k_gcap_prep, dim3(grid), dim3(256), 0, (hipStream_t)stream, *lr, *pb, *st, *gc, *s, idx,
+  hipLaunchKernelGGL(pq::k_gcap_prep, dim3(grid), dim3(pq::PT_PREP), 0, (hipStream_t)stream, *lr, *pb, *st, *gc, *s, idx,
                      band, ldo, r0, pc, ldpc);
   PQ_CHECK_LAUNCH("pq_gcap_prepare");
   return 0;

@@ -185,6 +185,83 @@ __device__ __forceinline__ void acc_store_T(const Acc& acc, double* G, int64_t l
         G[(int64_t)(row0 + acc_col(n)) * ld + col0 + acc_row(m, r)] = acc.c[m][n][r];
 }
 
+// ---- wave-level helpers ---------------------------------------------------------------
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// lane (l & ~15) | k of every 16-lane row (DPP row_newbcast; k folds to an immediate in
+// unrolled loops)
+template <int K>
+__device__ __forceinline__ double row_bcast16_k(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + K, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + K, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double row_bcast16(double v, int k) {
+  switch (k) {
+    case 0: return row_bcast16_k<0>(v);
+    case 1: return row_bcast16_k<1>(v);
+    case 2: return row_bcast16_k<2>(v);
+    case 3: return row_bcast16_k<3>(v);
+    case 4: return row_bcast16_k<4>(v);
+    case 5: return row_bcast16_k<5>(v);
+    case 6: return row_bcast16_k<6>(v);
+    case 7: return row_bcast16_k<7>(v);
+    case 8: return row_bcast16_k<8>(v);
+    case 9: return row_bcast16_k<9>(v);
+    case 10: return row_bcast16_k<10>(v);
+    case 11: return row_bcast16_k<11>(v);
+    case 12: return row_bcast16_k<12>(v);
+    case 13: return row_bcast16_k<13>(v);
+    case 14: return row_bcast16_k<14>(v);
+    default: return row_bcast16_k<15>(v);
+  }
+}
+
+
+// One wave, a 16x16 SPD block in the MFMA C layout (lane l holds A[(l>>4) + 4q][l&15], both
+// triangles; identity padding): right-looking Cholesky with the inverse of the factor built
+// in the same serial chain of 16 steps -- the pivot by readlane, row kk by one cross-lane
+// permute, column kk by a DPP row broadcast (lane kk of every 16-lane row), the trailing
+// update and the inverse's row operations in registers.  On return A holds L (lower, column
+// layout as above; the strictly upper part is stale) and Bv = L^-1; returns 1 when a pivot is
+// not positive (uniform), 0 otherwise.
+__device__ __forceinline__ int wave_chol_inv16(double (&A)[4], double (&Bv)[4]) {
+  const int l = lane_id();
+  const int cc = l & 15, gg = l >> 4;
+  int bad = 0;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const int src = ((kk & 3) << 4);
+    const double akk = A[kk >> 2];
+    const double piv = readlane_f64(akk, src | kk);
+    const double rowk = __shfl(akk, src | cc, 64);                   // A[kk][cc] = A[cc][kk]
+    const double bkr = __shfl(Bv[kk >> 2], src | cc, 64);            // row kk of the inverse, unscaled
+    double colv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) colv[q] = row_bcast16(A[q], kk);     // A[gg + 4q][kk]
+    if (!(piv > 0.0) || !isfinite(piv)) bad = 1;
+    double rs = __builtin_amdgcn_rsq(piv);                           // 1/sqrt, two Newton steps
+    rs = rs * fma(-0.5 * piv * rs, rs, 1.5);
+    rs = rs * fma(-0.5 * piv * rs, rs, 1.5);
+    const double bk = bkr * rs;                                      // final row kk of L^-1
+    const double lck = rowk * rs;                                    // L[cc][kk]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = gg + 4 * q;
+      const double lrk = colv[q] * rs;                               // L[r][kk]
+      if (cc == kk && r >= kk) A[q] = lrk;
+      else if (cc > kk && r > kk) A[q] = fma(-lrk, lck, A[q]);
+      if (r == kk) Bv[q] = bk;
+      else if (r > kk) Bv[q] = fma(-lrk, bk, Bv[q]);
+    }
+  }
+  return bad;
+}
+
 // XCD-contiguous block order: the hardware deals workgroups round-robin over the 8 XCDs
 // (each with its own L2); slot g' = xcd_slot(blockIdx.x) gives XCD x a contiguous range of
 // slots, so neighbouring problems (overlapping windows) share one L2.
