@@ -551,7 +551,10 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     __syncthreads();
     CSTAMP(0);
-    // ---- z' = M_U^-1 B (MFMA, A from the full symmetric M_U^-1 rows, B from LDS) -------------
+    // ---- z' = M_U^-1 B (MFMA, B from LDS).  A = M_U^-1 is symmetric: entries left of the row
+    //      tile's diagonal block come from its rows (16-byte pairs), the rest from the
+    //      transposed position (rows below, 16 consecutive lanes per row), so only the lower
+    //      triangle plus the diagonal blocks is streamed -- about half of the matrix ----------
     {
       const int kq = l >> 4, m = l & 15;
       f64x4 z[CTP2];
@@ -566,22 +569,43 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         mrow[j] = Mi + (int64_t)(rv[j] ? row : 0) * k_ld;
       }
       const int kU4 = (kU + 7) & ~7;
-      for (int k0 = 0; k0 < kU4; k0 += 8) {
+      // double-buffered: the A loads of step k0 + 8 are in flight during step k0's MFMAs
+      auto loadA = [&](double2 (&a)[CTP2], int k0) {
         const int kk = k0 + 2 * kq;   // k_ld padding: rows / columns >= kU of M^-1 are never read
-        const bool kin = kk < kU;
-        const bool kin1 = kk + 1 < kU;
-        const double b0 = kin ? WU[kk * CG_MAX + m] : 0.0;
-        const double b1 = kin1 ? WU[(kk + 1) * CG_MAX + m] : 0.0;
+        const bool kin = kk < kU, kin1 = kk + 1 < kU;
+#pragma unroll
+        for (int j = 0; j < CTP2; ++j) {
+          a[j] = double2{0.0, 0.0};
+          if (!zv[j] || !rv[j]) continue;
+          const int ts = (w + CNW * j) * 16;
+          if (kk < ts) {   // strictly left of the diagonal block: kk + 1 < ts <= row, both in range
+            a[j] = *reinterpret_cast<const double2*>(mrow[j] + kk);
+          } else {
+            const double* mc = Mi + (ts + m);
+            if (kin) a[j].x = mc[(int64_t)kk * k_ld];
+            if (kin1) a[j].y = mc[(int64_t)(kk + 1) * k_ld];
+          }
+        }
+      };
+      auto mmaA = [&](const double2 (&a)[CTP2], int k0) {
+        const int kk = k0 + 2 * kq;
+        const double b0 = kk < kU ? WU[kk * CG_MAX + m] : 0.0;
+        const double b1 = kk + 1 < kU ? WU[(kk + 1) * CG_MAX + m] : 0.0;
 #pragma unroll
         for (int j = 0; j < CTP2; ++j) {
           if (zv[j]) {
-            double2 a = double2{0.0, 0.0};
-            if (rv[j] && kin1) a = *reinterpret_cast<const double2*>(mrow[j] + kk);
-            else if (rv[j] && kin) a.x = mrow[j][kk];
-            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b0, z[j], 0, 0, 0);
-            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b1, z[j], 0, 0, 0);
+            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].x, b0, z[j], 0, 0, 0);
+            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].y, b1, z[j], 0, 0, 0);
           }
         }
+      };
+      double2 a0[CTP2], a1[CTP2];
+      loadA(a0, 0);
+      for (int k0 = 0; k0 < kU4; k0 += 16) {
+        loadA(a1, k0 + 8);
+        mmaA(a0, k0);
+        loadA(a0, k0 + 16);
+        if (k0 + 8 < kU4) mmaA(a1, k0 + 8);
       }
       __syncthreads();   // every wave is done reading B
 #pragma unroll
