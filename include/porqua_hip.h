@@ -365,6 +365,18 @@ int pq_lad_mv_batched(const double* M, int64_t ldm, int64_t sm, int32_t n, int32
                       const double* V, int64_t sv, int32_t k, const double* S, int64_t ss,
                       double* out, int64_t so, void* stream);
 
+/* Window-form interior-point methods (porqua_amd/ipm_lr.py; the LAD LP behind
+ * LAD.model_qpsolvers, src/optimization.py:296-345, and QPs with both l1 linearisations,
+ * src/qp_problems.py:40-118): the Woodbury capacitance of H = Lam + U' diag(e) U,
+ *   M[b] = diag(d[b]) + diag(r[b]) U[b] diag(w[b]) U[b]' diag(r[b])   (k x k, lower tiles)
+ * for U[b] k x n (row stride ldu, batch stride su), column weights w (b, n; w = 1/Lam), row
+ * scales r (b, k; r = sqrt(e); NULL = 1) and diagonal d (b, k; NULL = 1).  Rows k..k_ld-1 of
+ * M are identity padding (k_ld a multiple of 64), so K2 (pq_factor_batched on {n = k_ld,
+ * P = M}) factors it as is.  batch <= 65535 per launch.                                   */
+int pq_wgram_batched(const double* U, int64_t ldu, int64_t su, int32_t k, int32_t n, int32_t batch,
+                     const double* w, int64_t sw, const double* r, int64_t sr, const double* d, int64_t sd,
+                     double* M, int32_t k_ld, int64_t sm, void* stream);
+
 /* Device bytes of the per-batch buffers a caller allocates before the solve entry points
  * (the pq_state arrays, the polish scratch and, for the window path, the capacitance
  * matrices M, M^-1 and their factor scratch), so a non-Python host can size one arena.

@@ -166,6 +166,8 @@ _EXPORTS = {
                              ctypes.c_double, ctypes.c_double, c_dp, c_dp, c_int64, c_dp, c_int32, c_dp], c_int32),
     "pq_lad_mv_batched": ([c_dp, c_int64, c_int64, c_int32, c_int32, c_dp, c_int64, c_int32, c_dp, c_int64,
                            c_dp, c_int64, c_dp], c_int32),
+    "pq_wgram_batched": ([c_dp, c_int64, c_int64, c_int32, c_int32, c_int32, c_dp, c_int64, c_dp, c_int64,
+                          c_dp, c_int64, c_dp, c_int32, c_int64, c_dp], c_int32),
 }
 
 _lib = None

@@ -341,7 +341,13 @@ class Backtest:
         if lad:
             if l1term is not None:
                 return False
-            chunk = min(chunk, max(1, (1 << 34) // (8 * (n + 64) ** 2 + 64 * n * int(tlen.max()))))
+            tm = int(tlen.max())
+            if tm < n:    # m-space normal equations: (mc + T) x n rows + k_ld^2 factor buffers
+                k_ld = (tm + mg + 63) // 64 * 64
+                per = 8 * (4 * (tm + mg) * n + 3 * k_ld * k_ld) + 64 * n * 8
+            else:         # w-space n x n normal matrix
+                per = 8 * (n + 64) ** 2 + 64 * n * tm
+            chunk = min(chunk, max(1, (1 << 35) // per))
         path = "lp-ipm" if lad else "dense"
         # batchability of a chunk depends on its own windows (window lengths, WLS runs): a
         # rank that cannot batch must not return while the others block in the all-gather,

@@ -29,6 +29,14 @@ _REFINE = 2
 _INACCURATE = 1e-6
 
 
+# window-form (Woodbury) normal equations when T < n; False forces the dense n x n H
+WOODBURY = True
+
+
+def round_up64(v: int) -> int:
+    return (int(v) + 63) // 64 * 64
+
+
 class LPResult:
     """x: the best iterate by the merit max(rel. primal residual, rel. dual residual, rel.
     gap); status PQ_SOLVED (merit < tol), PQ_SOLVED_INACCURATE (< 1e-6) or PQ_MAX_ITER."""
@@ -156,9 +164,12 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
     """Mehrotra predictor-corrector IPM for min c'x, A x = b, lo <= x <= hi on the LAD
     structure, batched over windows; converged problems are frozen.
 
-    Newton directions come from the w-space normal equations (the Koenker / Portnoy form of
-    LAD interior-point methods): u, v, s and the T window rows are eliminated exactly, which
-    leaves H dw - C' dlam_C = f (n x n, K2 Cholesky) bordered by the few rows of C."""
+    Newton directions: with T < n (every backtest window here) from the LP's m-space normal
+    equations (A Theta A') dlam = r, (mc + T) x (mc + T), formed by the weighted-SYRK kernel
+    pq_wgram_batched and factored on K2 (porqua_amd/woodbury.py); otherwise from the w-space
+    normal equations (the Koenker / Portnoy form of LAD interior-point methods): u, v, s and
+    the T window rows are eliminated exactly, which leaves H dw - C' dlam_C = f (n x n, K2
+    Cholesky) bordered by the few rows of C."""
     B, m, N, n, T = pr.B, pr.m, pr.N, pr.n, pr.T
     dev = pr.dev
     c, lo, hi, b = pr.c, pr.lo, pr.hi, pr.b
@@ -176,7 +187,17 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
     lam = torch.zeros((B, m), dtype=F64, device=dev)
     zl = FL.clone()
     zh = FH.clone()
-    nfac = _NormalFactor(B, n, dev)
+    mc, me, X, C = pr.mc, pr.me, pr.X, pr.C
+    # window shorter than the universe (the backtest configurations, T = 252 < n): the LP's
+    # m-space normal equations M = [C; X] diag(theta_w) [C; X]' + diag(0, theta_s, theta_u +
+    # theta_v), (mc + T) x (mc + T), on the weighted-SYRK kernel; the w-space n x n H otherwise
+    nm = None
+    nfac = None
+    if WOODBURY and T < n and round_up64(mc + T) <= 1024:
+        from .woodbury import NormalM
+        nm = NormalM(torch.cat([C.expand(B, mc, n), X], 1).contiguous() if mc else X.contiguous())
+    else:
+        nfac = _NormalFactor(B, n, dev)
     ncomp = (FL + FH).sum(1).clamp(min=1)
     bn = 1.0 + b.abs().amax(1)
     cn = 1.0 + c.abs().amax()
@@ -185,7 +206,6 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
     best_x = x.clone()
     best_merit = torch.full((B,), np.inf, dtype=F64, device=dev)
     best_it = torch.zeros(B, dtype=torch.int64, device=dev)
-    mc, me, X, C = pr.mc, pr.me, pr.X, pr.C
 
     for it in range(max_iter):
         sl = torch.where(FL > 0, (x - lo_).clamp(min=1e-200), torch.ones_like(x))
@@ -216,11 +236,15 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
         th = 1.0 / Dg
         th_w, th_u, th_v, th_s = pr.split(th)
         e_inv = torch.where(done[:, None], torch.ones_like(th_u), 1.0 / (th_u + th_v))
-        H = torch.bmm(X.transpose(1, 2), X * e_inv.unsqueeze(2))
-        H.diagonal(dim1=1, dim2=2).add_(Dg[:, :n])
-        # factor a slightly shifted H (rank-deficient X'E^-1 X at degenerate vertices); the
-        # refinement step in hsolve is taken against the unshifted H
-        failed = nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2))
+        if nm is not None:
+            dM = torch.cat([torch.zeros((B, me), dtype=F64, device=dev), th_s, th_u + th_v], 1)
+            failed = nm.factor(th_w, dM)
+        else:
+            H = torch.bmm(X.transpose(1, 2), X * e_inv.unsqueeze(2))
+            H.diagonal(dim1=1, dim2=2).add_(Dg[:, :n])
+            # factor a slightly shifted H (rank-deficient X'E^-1 X at degenerate vertices); the
+            # refinement step in hsolve is taken against the unshifted H
+            failed = nfac.factor(H, 1e-12 * H.diagonal(dim1=1, dim2=2))
         if bool(failed.any()):               # K2 broke down even shifted: freeze at the best iterate
             done = done | failed
             if bool(done.all()):
@@ -232,7 +256,7 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
                 Y = Y + nfac.solve_mat(_mv(H, Y, R))
             return Y
 
-        if mc:
+        if mc and nm is None:
             HiC = hsolve(C.T.expand(B, n, mc).contiguous())          # H^-1 C'
             S = C @ HiC                                              # C H^-1 C' (B, mc, mc)
             theta_S = torch.cat([torch.zeros((B, me), dtype=F64, device=dev), th_s], 1)
@@ -245,6 +269,8 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
             return Hf + torch.bmm(HiC, dlc.unsqueeze(2)).squeeze(2), dlc
 
         def direction(rl, rh):
+            if nm is not None:
+                return direction_m(rl, rh)
             rx = rd - rl / sl + rh / sh              # D dx - A' dlam = -rx,  A dx = rp
             rx_w, rx_u, rx_v, rx_s = pr.split(rx)
             r_c, r_t = rp[:, :mc], rp[:, mc:]
@@ -269,6 +295,16 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
             ds = th_s * (dlc[:, me:] - rx_s)
             dx = torch.cat([dw, du, dv, ds], 1)
             dl = torch.cat([dlc, dlt], 1)
+            dzl = FL * (rl - zl * dx) / sl
+            dzh = FH * (rh + zh * dx) / sh
+            return dx, dl, dzl, dzh
+
+        def direction_m(rl, rh):
+            # D dx - A' dlam = -rx, A dx = rp  =>  (A Theta A') dlam = rp + A Theta rx,
+            # dx = Theta (A' dlam - rx)
+            rx = rd - rl / sl + rh / sh
+            dl = nm.solve(rp + pr.A(th * rx), refine=_REFINE)
+            dx = th * (pr.At(dl) - rx)
             dzl = FL * (rl - zl * dx) / sl
             dzh = FH * (rh + zh * dx) / sh
             return dx, dl, dzl, dzh

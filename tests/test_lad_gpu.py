@@ -130,3 +130,57 @@ def test_lad_mv_kernel_matches_torch(device, n, k, strided):
     assert torch.allclose(out, ref, rtol=1e-12, atol=1e-12)
     out2 = _mv(M, V, S)
     assert torch.allclose(out2, S - ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("B,k,n,diag", [(3, 252, 1000, False), (2, 70, 131, True), (4, 64, 64, False)])
+def test_wgram_kernel_matches_torch(device, B, k, n, diag):
+    """pq_wgram_batched: M = diag(d) + diag(r) U diag(w) U' diag(r) (lower tiles, identity
+    padding to k_ld) against a torch FP64 product."""
+    import torch
+    from porqua_amd import _lib, engine
+    g = torch.Generator(device="cpu").manual_seed(k + n)
+    U = torch.randn(B, k, n + 3, generator=g, dtype=torch.float64)[:, :, :n].to("cuda")   # row stride > n
+    w = torch.rand(B, n, generator=g, dtype=torch.float64).to("cuda") + 0.1
+    r = torch.rand(B, k, generator=g, dtype=torch.float64).to("cuda") + 0.5
+    d = (torch.rand(B, k, generator=g, dtype=torch.float64).to("cuda") + 1.0) if diag else None
+    k_ld = (k + 63) // 64 * 64
+    M = torch.full((B, k_ld, k_ld), np.nan, dtype=torch.float64, device="cuda")
+    lib = _lib.load()
+    _lib.check(lib.pq_wgram_batched(U.data_ptr(), U.stride(1), U.stride(0), k, n, B, w.data_ptr(), w.stride(0),
+                                    r.data_ptr(), r.stride(0), None if d is None else d.data_ptr(),
+                                    0 if d is None else d.stride(0), M.data_ptr(), k_ld, M.stride(0),
+                                    engine._stream()), "pq_wgram_batched")
+    S = r.unsqueeze(2) * U
+    ref = torch.bmm(S * w.unsqueeze(1), S.transpose(1, 2))
+    ref.diagonal(dim1=1, dim2=2).add_(1.0 if d is None else d)
+    low = torch.tril(torch.ones(k, k, dtype=torch.bool, device="cuda"))
+    got = M[:, :k, :k]
+    assert torch.allclose(got[:, low], ref[:, low], rtol=1e-12, atol=1e-12 * float(ref.abs().max()))
+    pad = M[:, k:, k:]
+    if k < k_ld:
+        eye = torch.eye(k_ld - k, dtype=torch.float64, device="cuda")
+        assert torch.equal(torch.tril(pad), eye.expand_as(pad))
+
+
+def test_normal_m_solve_matches_dense(device):
+    """woodbury.NormalM: M^-1 g and M y against the dense M = U diag(w) U' + diag(d), with
+    IPM-like scaling spreads (w over 1e-6 .. 1e6, d over 1e-4 .. 1e4, one row d = 0): the
+    refined solve's backward error is at the rounding level."""
+    import torch
+    from porqua_amd.woodbury import NormalM
+    g = torch.Generator(device="cpu").manual_seed(7)
+    B, k, n = 3, 121, 400
+    U = (0.01 * torch.randn(B, k, n, generator=g, dtype=torch.float64)).to("cuda")
+    w = torch.exp(torch.empty(B, n, dtype=torch.float64).uniform_(-14, 14, generator=g)).to("cuda")
+    d = torch.exp(torch.empty(B, k, dtype=torch.float64).uniform_(-9, 9, generator=g)).to("cuda")
+    d[:, 0] = 0.0                                         # an equality row
+    R = torch.randn(B, k, 2, generator=g, dtype=torch.float64).to("cuda")
+    nm = NormalM(U.contiguous())
+    assert not bool(nm.factor(w, d).any())
+    M = torch.bmm(U * w.unsqueeze(1), U.transpose(1, 2))
+    M.diagonal(dim1=1, dim2=2).add_(d)
+    Y = nm.solve(R)
+    res = (R - torch.bmm(M, Y)).abs().amax() / (torch.bmm(M.abs(), Y.abs()).amax() + R.abs().amax())
+    assert float(res) < 1e-12
+    MY = torch.bmm(M, Y)
+    assert float((nm.apply(Y) - MY).abs().amax() / torch.bmm(M.abs(), Y.abs()).amax()) < 1e-13
