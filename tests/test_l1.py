@@ -255,8 +255,10 @@ def test_device_backtest_window_path_transaction_cost(shrink):
 @pytest.mark.gpu
 def test_device_backtest_turnover_and_leverage_together():
     """A turnover budget and a leverage constraint together (two l1 terms: the reference's
-    linearised rows, 2n + 2 inequality and n + 1 equality rows) run through the device IPM
-    (porqua_amd/ipm.py) date by date; each date's QP is checked against the oracle IPM."""
+    linearised rows, 2n + 2 inequality and n + 1 equality rows).  The serial loop solves each
+    date's linearised QP on the device IPM (porqua_amd/ipm.py); with static_builders the
+    batched backtest solves all dates at once on the per-asset-block IPM
+    (porqua_amd/ipm_l1.py).  Both are checked against the oracle IPM on the captured QPs."""
     from oracle.qp_ipm import solve_qp
     from porqua_amd.backtest import Backtest
     from porqua_amd.builders import OptimizationItemBuilder
@@ -277,20 +279,84 @@ def test_device_backtest_turnover_and_leverage_together():
         m = bs.optimization.model
         seen.append(({k: m.get(k) for k in ("P", "q", "G", "h", "A", "b", "lb", "ub")}, m["solution"]))
 
-    opt = MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1),
-                       solver_name="mi355x", risk_aversion=3.0)
-    rebdates = [str(d.date()) for d in X.index[1000:2600:200]]
-    bs = _service(opt, X, y, rebdates, extra=OptimizationItemBuilder(bibfn=add_l1),
-                  box_kw={"box_type": "LongShort", "lower": -0.1, "upper": 0.3})
+    def opt():
+        return MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1),
+                            solver_name="mi355x", risk_aversion=3.0)
+    rebdates = [str(d.date()) for d in X.index[1000:2600:100]]
+    box = {"box_type": "LongShort", "lower": -0.1, "upper": 0.3}
+    bs = _service(opt(), X, y, rebdates, extra=OptimizationItemBuilder(bibfn=add_l1), box_kw=box)
     bs.settings["append_fun"] = keep
     bt = Backtest()
-    bt.run(bs)
+    bt.run(bs)                                          # custom builder: serial loop
     assert len(seen) == len(rebdates)
-    for prob, sol in seen:
+    bs2 = _service(opt(), X, y, rebdates, extra=OptimizationItemBuilder(bibfn=add_l1), box_kw=box)
+    bs2.settings["static_builders"] = True
+    bt2 = Backtest()
+    bt2.run(bs2)
+    assert bt2.stats["path"] == "l1-ipm" and bt2.stats["solved"] == len(rebdates)
+    W = bt2.strategy.get_weights_df().to_numpy(dtype=float)
+    xv = np.array(list(x0.values()))
+    for i, (prob, sol) in enumerate(seen):
         assert sol.found and sol.extras.get("solver", "").startswith("device IPM")
         o = solve_qp(prob["P"], prob["q"], G=prob["G"], h=prob["h"], A=prob["A"], b=prob["b"],
                      lb=prob["lb"], ub=prob["ub"])
         assert abs(sol.obj - o.obj) <= 1e-6 * max(abs(o.obj), 1e-3), (sol.obj, o.obj)
-        w = sol.x[:n]
-        assert np.abs(w).sum() <= 1.3 + 1e-7 and abs(w.sum() - 1) < 1e-8
-        assert np.abs(w - np.array(list(x0.values()))).sum() <= 0.4 + 1e-7
+        for w in (sol.x[:n], W[i]):
+            assert np.abs(w).sum() <= 1.3 + 1e-7 and abs(w.sum() - 1) < 1e-8
+            assert np.abs(w - xv).sum() <= 0.4 + 1e-7
+        assert np.abs(W[i] - o.x[:n]).max() < 1e-6, (i, np.abs(W[i] - o.x[:n]).max())
+
+
+@pytest.mark.gpu
+def test_device_backtest_turnover_and_leverage_window_path():
+    """n = 300 > window = 252: the per-asset-block IPM on the window form (coupling matrix
+    from the weighted-SYRK kernel), mean-variance with shrinkage, long-short box, turnover
+    budget + leverage, 12 daily dates in one batch; three dates against the oracle IPM on the
+    reference's linearised problem built from the oracle's own covariance and mean."""
+    import pandas as pd
+    from oracle import ref_pipeline as rp
+    from oracle.qp_ipm import solve_qp
+    from porqua_amd.backtest import Backtest
+    from porqua_amd.builders import OptimizationItemBuilder
+    from porqua_amd.covariance import Covariance
+    from porqua_amd.optimization import MeanVariance
+    from porqua_amd.qp_problems import QuadraticProgram
+    from porqua_amd.synthetic import factor_panel
+    n, D, width = 300, 300, 252
+    dates, R, yv, _ = factor_panel(D, n, seed=11)
+    idx = pd.DatetimeIndex(dates)
+    X = pd.DataFrame(R, index=idx, columns=[f"a{i}" for i in range(n)])
+    y = pd.DataFrame({"bm": yv}, index=idx)
+    rebdates = [str(d.date()) for d in idx[width + 5:width + 17]]
+    w0 = np.random.default_rng(2).dirichlet(np.ones(n))
+    x0 = dict(zip(X.columns, w0))
+
+    def add_l1(bs, rebdate, **kw):
+        bs.optimization.constraints.add_l1("turnover", rhs=0.5, x0=x0)
+        bs.optimization.constraints.add_l1("leverage", rhs=1.2)
+
+    opt = MeanVariance(covariance=Covariance(method="linear_shrinkage", lambda_covmat_regularization=0.1),
+                       solver_name="mi355x", risk_aversion=1.0)
+    bs = _service(opt, X, y, rebdates, extra=OptimizationItemBuilder(bibfn=add_l1), width=width,
+                  box_kw={"box_type": "LongShort", "lower": -0.02, "upper": 0.05})
+    bs.settings["static_builders"] = True
+    bt = Backtest()
+    bt.run(bs)
+    assert bt.stats["path"] == "l1-ipm" and bt.stats["solved"] == len(rebdates)
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    for i in (0, 5, len(rebdates) - 1):
+        e = X.index.get_loc(pd.Timestamp(rebdates[i]))
+        Xw = R[e - width + 1:e + 1]
+        S = rp.cov_pearson(Xw)
+        S = S + 0.1 * np.mean(np.diag(S)) * np.eye(n)
+        P, q = 2 * S, -rp.mean_geometric(Xw, None, None, None)
+        qp = QuadraticProgram(P=P, q=q, A=np.ones((1, n)), b=np.ones(1), G=None, h=None,
+                              lb=np.full(n, -0.02), ub=np.full(n, 0.05), params={"solver_name": "cvxopt"})
+        qp.linearize_turnover_constraint(w0, 0.5)
+        qp.linearize_leverage_constraint(N=n, leverage_budget=1.2)
+        o = solve_qp(qp["P"], qp["q"], G=qp["G"], h=qp["h"], A=qp["A"], b=qp["b"], lb=qp["lb"], ub=qp["ub"])
+        f = lambda x: 0.5 * x @ P @ x + q @ x                # noqa: E731
+        assert abs(f(W[i]) - f(o.x[:n])) <= 1e-7 * max(abs(f(o.x[:n])), 1e-6), (i, f(W[i]), f(o.x[:n]))
+        assert np.abs(W[i] - o.x[:n]).max() < 1e-6, (i, np.abs(W[i] - o.x[:n]).max())
+        assert np.abs(W[i]).sum() <= 1.2 + 1e-7 and np.abs(W[i] - w0).sum() <= 0.5 + 1e-7
+        assert abs(W[i].sum() - 1) < 1e-8 and W[i].min() > -0.02 - 1e-8 and W[i].max() < 0.05 + 1e-8
