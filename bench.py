@@ -238,6 +238,11 @@ def main():
         k_u = float(gplan.ucnt.double().mean().item()) + qb.mg
         factor_flops = k_u ** 3 * gplan.ngroups * args.steps
 
+    # polish (K4) algorithmic flops per step: per problem and active-set round the P_FF Gram
+    # of the free columns over the window (|F|^2 T) and its Cholesky (|F|^3 / 3), plus the
+    # two exact P x window passes (2 x 2 T n)
+    polish_flops = float(((prounds * (nfree ** 2 * T + nfree ** 3 / 3.0)).sum() + 4.0 * T * n * D) * args.steps)
+
     traffic, traffic_src = None, None
     mfma_busy, mfma_src = None, None
     import glob
@@ -304,6 +309,8 @@ def main():
                         "full SYRK per date" if plan is None else
                         f"sliding: {plan.ngroups} anchor SYRKs + rank-2 updates",
             "factor_tflops": factor_flops / tk.get("factor", float("nan")) / 1e12,
+            "polish_tflops": polish_flops / tk["polish"] / 1e12 if tk.get("polish") else None,
+            "polish_flops_note": "sum over problems of rounds x (|F|^2 T + |F|^3/3) + 4 T n (two P x window passes)",
             "gram_tflops": gram_flops / tk["gram"] / 1e12 if band and tk.get("gram") else None,
             "capacitance": res.capacitance or None,
             "fp64_peak_tflops": FP64_PEAK_TFLOPS,

@@ -438,11 +438,21 @@ class Backtest:
             print(f"Rebalanced {len(rebdates)} dates on the device ({int(solved.sum())} solved)")
         keys = list(universe)
         none = [None] * n
+        append_fun = bs.settings.get("append_fun")
+        portfolios = self.strategy.portfolios
         for i, d in enumerate(rebdates):
-            # == pd.Series(w, index=universe).to_dict() (Python floats), without 4749 Series
+            if append_fun is None and solved[i]:
+                # the weights stay a row of W until read (Portfolio._from_row); the dict is
+                # == pd.Series(w, index=universe).to_dict() (Python floats)
+                portfolios.append(Portfolio._from_row(d, keys, W[i]))
+                continue
             w = W[i].tolist() if solved[i] else none
             opt.results = {"weights": dict(zip(keys, w)), "status": bool(solved[i])}
             self._after_solve(bs, d)
+        if rebdates:   # the optimisation's results hold the last date's, as after the serial loop
+            last = len(rebdates) - 1
+            w = W[last].tolist() if solved[last] else none
+            opt.results = {"weights": dict(zip(keys, w)), "status": bool(solved[last])}
         return True
 
     def save(self, filename: str, path: Optional[str] = None) -> None:

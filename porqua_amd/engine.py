@@ -838,7 +838,10 @@ class GroupPlan:
     when some window cannot be grouped (the per-date kernel is used then)."""
 
     def __init__(self, rows, tlen, device, gmax: int = GROUP_MAX_DATES, umax: int = GROUP_MAX_UNION,
-                 smax: int = 64, cus: int = 256, gmin: int = 4):
+                 smax: int = 64, cus: int = 256, gmin: int = 4, breaks=None):
+        """``breaks`` (bool per problem, optional): True starts a new group at that problem
+        (e.g. the risk-aversion buckets of porqua_amd.sweep, whose problems may share a
+        capacitance only within a rho bucket)."""
         rows = np.asarray(rows)
         tlen = np.asarray(tlen)
         B = len(tlen)
@@ -858,6 +861,13 @@ class GroupPlan:
                 else:
                     U += int(sh[d])
             groups.append((start, b))
+        if breaks is not None:
+            brk = np.flatnonzero(np.asarray(breaks, dtype=bool))
+            split = []
+            for a, b in groups:
+                cut = [a] + [int(c) for c in brk if a < c < b] + [b]
+                split += list(zip(cut[:-1], cut[1:]))
+            groups = split
         self.ngroups = len(groups)
         self.umax = umax
         gdates = np.array([a for a, _ in groups] + [B], dtype=np.int32)

@@ -30,8 +30,24 @@ class Portfolio:
     def empty() -> "Portfolio":
         return Portfolio()
 
+    @classmethod
+    def _from_row(cls, rebalancing_date: str, keys: list, row: np.ndarray) -> "Portfolio":
+        """A portfolio of the batched backtest: the weights stay a row of the solved weight
+        panel until first read, then become the reference's {asset: float} dict (cached)."""
+        p = cls.__new__(cls)
+        p.rebalancing_date = rebalancing_date
+        p._name = None
+        p.init_weights = {}
+        p._weights = None
+        p._row = (keys, row)
+        return p
+
     @property
     def weights(self):
+        if self._weights is None and getattr(self, "_row", None) is not None:
+            keys, row = self._row
+            self._weights = dict(zip(keys, row.tolist()))
+            self._row = None
         return self._weights
 
     @weights.setter
@@ -42,6 +58,7 @@ class Portfolio:
             else:
                 raise TypeError("weights must be a dictionary")
         self._weights = new_weights
+        self._row = None
 
     @property
     def rebalancing_date(self):
@@ -64,7 +81,7 @@ class Portfolio:
         self._name = new_name
 
     def get_weights_series(self) -> pd.Series:
-        return pd.Series(self._weights)
+        return pd.Series(self.weights)
 
     def __repr__(self):
         return f"Portfolio(rebalancing_date={self.rebalancing_date}, weights={self.weights})"
@@ -129,7 +146,15 @@ class Strategy:
         return None
 
     def get_weights_df(self) -> pd.DataFrame:
-        return pd.DataFrame({p.rebalancing_date: p.weights for p in self.portfolios}).T
+        ps = self.portfolios
+        rows = [getattr(p, "_row", None) for p in ps]
+        if ps and all(r is not None for r in rows) and all(r[0] is rows[0][0] for r in rows) \
+                and len({p.rebalancing_date for p in ps}) == len(ps):
+            # batched backtest, weights not yet materialised: the same frame straight from the
+            # weight panel (dates x assets, float64)
+            return pd.DataFrame(np.stack([r[1] for r in rows]), index=[p.rebalancing_date for p in ps],
+                                columns=list(rows[0][0]))
+        return pd.DataFrame({p.rebalancing_date: p.weights for p in ps}).T
 
     def clear(self) -> None:
         self.portfolios.clear()

@@ -28,6 +28,9 @@ import torch
 from . import engine
 
 
+RHO_BUCKET = 2.0       # shared factorisation: largest rho0 ratio inside one group
+
+
 def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0, budget=1.0,
                         geometric=True, settings: engine.Settings | None = None, group=True,
                         shared_factor=False, gmax: int = engine.GROUP_MAX_DATES):
@@ -63,7 +66,22 @@ def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0
         qb.p_scale = 2.0 * lam_p
     mu_p = mu_c.repeat_interleave(L, dim=0).contiguous()
     lr = engine.LowRank(panel, rp_d, tp_d, mu=mu_p, w_scale=1.0 / (tp_d.to(torch.float64) - 1.0))
-    gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax) if group else None
+    breaks = None
+    if shared_factor and group:
+        # one capacitance per group needs one rho per group: the problems of a date share
+        # P = 2 Sigma_d, and rho0 = max(4 mean diag P, 10 |q|_max) (engine.Settings) varies
+        # with lam only through q = -mu_d / lam -- so a group holds the risk aversions of one
+        # date whose rho0 lie within a factor RHO_BUCKET of each other (bucket breaks here)
+        Tw = torch.as_tensor(tlen, dtype=torch.float64, device=dev)
+        dg = panel.window_sumsq(r_d, t_d, mu_c)[:, :n]
+        pdiag = (2.0 * dg.mean(1) / (Tw - 1.0)).cpu().numpy()
+        qmax = mu_q[:, :n].abs().amax(1).cpu().numpy()
+        r0 = np.maximum(4.0 * pdiag[:, None], 10.0 * qmax[:, None] / lam[None, :])     # (nd, L)
+        bucket = np.floor(np.log(r0 / r0.min(1, keepdims=True)) / np.log(RHO_BUCKET)).astype(np.int64)
+        brk = np.ones((nd, L), dtype=bool)
+        brk[:, 1:] = bucket[:, 1:] != bucket[:, :-1]
+        breaks = brk.reshape(-1)
+    gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax, breaks=breaks) if group else None
     res = engine.solve_lowrank(qb, lr, settings, groups=gp)
     if shared_factor:   # back to lam x'Sigma x - mu'x: objective and multipliers times lam
         res.obj.mul_(lam_p)

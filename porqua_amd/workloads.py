@@ -15,6 +15,8 @@ kernel cannot certify itself.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -57,7 +59,8 @@ class MinVarianceBacktest:
         self.pan = engine.Panel(self.R_rank, device=dev)
         self.rows_d, self.tlen_d = self.pan.rows_to_device(self.rows, self.tlen)
         self.plan = engine.SlidePlan(self.rows, self.tlen, dev) if slide else None
-        self.gplan = engine.GroupPlan(self.rows, self.tlen, dev) if group else None
+        gmin = int(os.environ.get("PQ_GROUP_MIN", "4"))     # experiments: smallest slide group size
+        self.gplan = engine.GroupPlan(self.rows, self.tlen, dev, gmin=gmin) if group else None
         qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)),
                                        b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), device=dev)
         qb.batch = D                                             # D problems sharing constraints

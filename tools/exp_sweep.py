@@ -23,9 +23,10 @@ def main():
     rows, tlen = engine.window_rows(dates, dates[ends], T)
     pan = engine.Panel(R, device=torch.device("cuda", 0))
     lambdas = np.logspace(-1, 2, L)
-    variants = [(False, {}), (True, {}), (True, {"eps_abs": 1e-6}), (True, {"eps_abs": 1e-6, "rho0_qrel": 0.0}),
-                (True, {"refine_retry": 1}), (True, {"adapt_interval": 0})]
-    for shared, kw in variants:
+    from porqua_amd import sweep
+    variants = [(False, {}, 2.0), (True, {}, 2.0), (True, {}, 1.5), (True, {}, 4.0), (True, {}, 1e9)]
+    for shared, kw, bucket in variants:
+        sweep.RHO_BUCKET = bucket
         gmax = 16
         st = engine.Settings.from_params(kw)
         mean_variance_sweep(pan, rows, tlen, lambdas, shared_factor=shared, gmax=gmax, settings=st)
@@ -36,7 +37,7 @@ def main():
         dt = time.perf_counter() - t0
         it = res.iters.cpu().numpy()
         slow = np.flatnonzero(res.iters.cpu().numpy() > 200)
-        print(json.dumps({"shared": shared, "kw": kw, "slow_lambda_idx": sorted(set((slow % L).tolist()))[:20], "qps": nd * L / dt, "s": dt, "iters_mean": float(it.mean()),
+        print(json.dumps({"shared": shared, "kw": kw, "rho_bucket": bucket, "slow_lambda_idx": sorted(set((slow % L).tolist()))[:20], "qps": nd * L / dt, "s": dt, "iters_mean": float(it.mean()),
                           "iters_max": int(it.max()), "factorizations": meta["factorizations"],
                           "capacitance": meta["capacitance"],
                           "status": {str(k): int(v) for k, v in zip(*np.unique(res.status.cpu().numpy(), return_counts=True))}}),
