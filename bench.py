@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--path", choices=["auto", "dense", "lowrank"], default="auto",
                     help="dense K^-1 (K2 n^3 + K3 n^2 stream) or Woodbury low-rank (T + mg < n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the end-to-end Backtest.run line")
     ap.add_argument("--no-group", action="store_true",
                     help="low-rank ADMM one workgroup per date instead of per group of sliding windows")
     ap.add_argument("--no-slide", action="store_true",
@@ -372,6 +373,43 @@ def main():
         "lps": nl, "lps_per_s": nl / lad_s, "ipm_iterations_max": int(lad_res.iters.max().item()),
         "status_counts": {str(k): int(v) for k, v in
                           zip(*np.unique(lad_res.status.cpu().numpy(), return_counts=True))}}
+    # ---- drop-in line, outside the timed region (rank 0, N = 1): the same panel and dates
+    # through the reference API -- Backtest.run(bs) with MeanVariance (Pearson covariance,
+    # geometric mean: q = -mu, the closest API objective to the step's q = 0), from the host
+    # DataFrame to the Portfolio objects (panel upload, staging and result download included) --
+    if world == 1 and not args.no_dropin:
+        import pandas as pd
+        from porqua_amd.backtest import Backtest, BacktestService
+        from porqua_amd.builders import (OptimizationItemBuilder, SelectionItemBuilder, bibfn_box_constraints,
+                                         bibfn_budget_constraint, bibfn_return_series, bibfn_selection_data)
+        from porqua_amd.optimization import MeanVariance
+        idx = pd.DatetimeIndex(wl.dates_rank)
+        Xdf = pd.DataFrame(R_rank, index=idx, columns=[f"a{i}" for i in range(n)])
+        reb = [str(d.date()) for d in idx[wl.ends_local]]
+
+        def dropin():
+            svc = BacktestService(
+                data={"return_series": Xdf},
+                selection_item_builders={"data": SelectionItemBuilder(bibfn=bibfn_selection_data)},
+                optimization_item_builders={
+                    "return_series": OptimizationItemBuilder(bibfn=bibfn_return_series, width=T),
+                    "budget_constraint": OptimizationItemBuilder(bibfn=bibfn_budget_constraint, budget=1),
+                    "box_constraints": OptimizationItemBuilder(bibfn=bibfn_box_constraints)},
+                optimization=MeanVariance(solver_name="mi355x"), rebdates=reb, quiet=True)
+            bt = Backtest()
+            bt.run(svc)
+            torch.cuda.synchronize()
+            return bt
+        dropin()
+        t_d = time.perf_counter()
+        bt = dropin()
+        t_d = time.perf_counter() - t_d
+        out["end_to_end"] = {
+            "api": "porqua_amd.backtest.Backtest.run(bs), MeanVariance(solver_name='mi355x')",
+            "qps": len(reb) / t_d, "s": t_d, "dates": len(reb), "solved": bt.stats["solved"],
+            "path": bt.stats["path"],
+            "note": "host DataFrame in, Portfolio objects out: panel upload, window staging, device solve "
+                    "and weight download included; q = -mu (geometric) instead of the step's q = 0"}
     if cpu is not None:
         legs = {"serial": cpu["serial"], "pool": cpu["pool"]}
         best = max(legs, key=lambda k: legs[k]["qps"])

@@ -57,6 +57,15 @@ constexpr int CH_MAX = 64;     // m + 1 = U - T + 1 <= 64
 #define CSTAMP(k) do { } while (0)
 #endif
 
+// An opaque zero, re-materialised every time it is evaluated: indices built from it inside the
+// ADMM loop are not hoisted out of the loop by LICM (hoisted row pointers stay live across all
+// phases and were spilled to scratch)
+__device__ __forceinline__ int loop_zero() {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+
 __device__ __forceinline__ double crho(double l, double u, double rho, const pq_settings& s) {
   if (l == u) return rho * s.eq_scale;
   if (isinf(l) && isinf(u)) return s.rho_min;
@@ -491,7 +500,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   while (s_any) {
     // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs) ----------------------
     {
-      const int kq = l >> 4, m = l & 15;
+      const int z0 = loop_zero();
+      const int kq = l >> 4, m = (l & 15) + z0;
       const double* Vp = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride + ld : nullptr;
       const double wsc1 = m < G ? g_dinv[m] : 1.0;
       f64x4 c[CTP1];
@@ -556,7 +566,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     //      transposed position (rows below, 16 consecutive lanes per row), so only the lower
     //      triangle plus the diagonal blocks is streamed -- about half of the matrix ----------
     {
-      const int kq = l >> 4, m = l & 15;
+      const int z0 = loop_zero();
+      const int kq = l >> 4, m = (l & 15) + z0;
       f64x4 z[CTP2];
       const double* mrow[CTP2];
       bool zv[CTP2], rv[CTP2];
@@ -675,7 +686,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     //      product with NE = NH + U - T edge rows; Ut = sqrt(c) base on union rows, cw =
     //      sqrt(R) base on general rows (in place of z' in WU) -------------------------------------
     {
-      const int kq = l >> 4, gl = l & 15;
+      const int z0 = loop_zero();
+      const int kq = l >> 4, gl = (l & 15) + z0;
       const int T0 = g_T[0];
       const int NH = g_off[G - 1], NE = NH + (U - T0);
       const bool gact = gl < G && g_act[gl];
@@ -760,7 +772,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     //      lane for all its dates.  Per-date maxima / sums: lane partials, reduced over the
     //      16 lanes of a date, then NP slots per wave in LDS ---------------------------------
     {
-      const int kq = l >> 4, ia = l & 15;
+      const int z0 = loop_zero();
+      const int kq = l >> 4, ia = (l & 15) + z0;
       const int Uk = (U + 3) & ~3;
       constexpr int PS = 4;
       bool mact[4];
@@ -1088,6 +1101,9 @@ extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_st
                "pq_admm_lr_gcap: strides must be even");
   if (pb->mg == 0)
     hipLaunchKernelGGL(pq::k_admm_gcap<0>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
+                       *gc, *s, iters_this_call, pc, ldpc, r0, cc);
+  else if (pb->mg == 1)   // the budget row alone (the usual case): one general row in registers
+    hipLaunchKernelGGL(pq::k_admm_gcap<1>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
                        *gc, *s, iters_this_call, pc, ldpc, r0, cc);
   else
     hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMG>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,

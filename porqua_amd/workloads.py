@@ -54,6 +54,7 @@ class MinVarianceBacktest:
         self.ends_local = np.arange(T - 1, T - 1 + D)            # rebalance row within the slice
         self.row_offset = lo
         sl_dates = dates[lo:lo + T - 1 + D]
+        self.dates_rank = sl_dates
         self.rebdates = sl_dates[self.ends_local]
         self.rows, self.tlen = engine.window_rows(sl_dates, self.rebdates, T)
         self.pan = engine.Panel(self.R_rank, device=dev)
