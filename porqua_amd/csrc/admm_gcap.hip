@@ -498,6 +498,16 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int ntile = (U + mg + 15) >> 4;   // pass 1: union rows, then the general rows (Cg V)
   const int ktile = (kU + 15) >> 4;
   while (s_any) {
+    // lane ids re-materialised every iteration (loop_zero): the per-lane LDS / global
+    // addresses derived from them are then computed where they are used instead of being
+    // hoisted above the loop and spilled to scratch for its whole duration
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wshadow"
+    const int t = threadIdx.x + loop_zero();
+    const int w = t >> 6, l = t & 63, hg = t >> 5, hl = t & 31;
+    const int hbase = (hg & 1) * 32;
+#pragma clang diagnostic pop
+    (void)hbase;
     // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs) ----------------------
     {
       const int z0 = loop_zero();
