@@ -57,15 +57,6 @@ constexpr int CH_MAX = 64;     // m + 1 = U - T + 1 <= 64
 #define CSTAMP(k) do { } while (0)
 #endif
 
-// An opaque zero, re-materialised every time it is evaluated: indices built from it inside the
-// ADMM loop are not hoisted out of the loop by LICM (hoisted row pointers stay live across all
-// phases and were spilled to scratch)
-__device__ __forceinline__ int loop_zero() {
-  int z;
-  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-  return z;
-}
-
 __device__ __forceinline__ double crho(double l, double u, double rho, const pq_settings& s) {
   if (l == u) return rho * s.eq_scale;
   if (isinf(l) && isinf(u)) return s.rho_min;

@@ -234,6 +234,12 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
 
   const int ntile = (U + 15) >> 4;
   while (s_any) {
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wshadow"
+    const int t = threadIdx.x + loop_zero();   // re-materialised lane ids (common.h: loop_zero)
+    const int w = t >> 6, l = t & 63, hg = t >> 5, hl = t & 31;
+#pragma clang diagnostic pop
+    (void)hl;
     // ---- pass 1: W = X_union V (MFMA f64 16x16x4; a 16-B load feeds two k-slices) -------
     {
       const int kq = l >> 4, m = l & 15;

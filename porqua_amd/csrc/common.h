@@ -185,6 +185,17 @@ __device__ __forceinline__ void acc_store_T(const Acc& acc, double* G, int64_t l
         G[(int64_t)(row0 + acc_col(n)) * ld + col0 + acc_row(m, r)] = acc.c[m][n][r];
 }
 
+// An opaque zero, re-materialised every time it is evaluated.  Lane ids rebuilt from it at
+// the top of an iteration loop (threadIdx.x + loop_zero()) keep LICM from hoisting every
+// per-lane address derived from them above the loop, where they stay live across all
+// phases and were spilled to scratch (k_admm_gcap: 207 spilled VGPRs -> 41, ADMM 10.8 ->
+// 8.6 ms on config 3)
+__device__ __forceinline__ int loop_zero() {
+  int z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+
 // ---- wave-level helpers ---------------------------------------------------------------
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
