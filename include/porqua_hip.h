@@ -291,6 +291,22 @@ int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, co
                     const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc, int32_t r0,
                     const double* cc, void* stream);
 
+/* K2, eigen form (the risk-aversion x date sweep, BASELINE configs[4]): M_b^-1 of every
+ * problem b (or idx[0..nidx)) of the window path from ONE symmetric eigendecomposition per
+ * date d = pdate[b] of the centred window Gram Xc_d Xc_d' = V diag(evals) V' instead of a
+ * Cholesky factorisation per problem: V (k_ld x k_ld per date, row-major, V[i][k] = entry i
+ * of eigenvector k, zero beyond tmax), evals (k_ld per date), What = V' Xc_d Cg' (k_ld x 4
+ * per date), cc = Cg Cg' (mg x mg).  Every window has tlen == tmax, mg <= 4, uniform box rho.
+ * The result (full symmetric, identity padding) is what pq_factor_batched's inverse mode
+ * leaves for pq_admm_lr_batched / pq_admm_lr_grouped; a new rho is a re-form, not a
+ * refactorisation.  scratch: 8 k_ld doubles per problem.  Replaces the per-(date, lambda)
+ * KKT factorisation inside qpsolvers.solve_problem (src/qp_problems.py:211-214) for
+ * P = 2 lambda Sigma_d (src/optimization.py:168-174).                                   */
+int pq_eigcap_form(const pq_lowrank* lr, const pq_problem* pb, const pq_state* st, const pq_settings* s,
+                   const int32_t* pdate, const double* V, const double* evals, const double* What,
+                   const double* cc, int32_t k_ld, const int32_t* idx, int32_t nidx, double* Minv,
+                   int64_t M_stride, double* scratch, void* stream);
+
 /* K4: active-set polish of the ADMM point (reduced KKT by masked Cholesky + Schur +
  * proximal iterative refinement), then exact residuals / objective of the final point
  * into out[] (Solution.obj / primal_residual / dual_residual / duality_gap).            */

@@ -297,7 +297,7 @@ class BatchResult:
     out: torch.Tensor        # (B, PQ_OUT_FIELDS)
     refactors: int = 0
     admm_launches: int = 0
-    capacitance: str = ""    # window path: "band" (pq_lr_capacitance_band) or "direct"
+    capacitance: str = ""    # window path: "band" (pq_lr_capacitance_band), "group", "eig" or "direct"
 
     @property
     def obj(self):
@@ -457,6 +457,74 @@ class LowRank:
                               dg=self.dg.data_ptr(), dg_stride=self.dg.stride(0))
 
 
+class EigCap:
+    """One symmetric eigendecomposition per DATE of the centred window Gram Xc Xc' (T x T),
+    shared by every problem of that date (pq_eigcap_form): the risk aversions of the sweep
+    (P = 2 lam Sigma_d, src/optimization.py:168-174) differ only in the scale of P and in
+    rho, and each capacitance inverse M_b^-1 is formed from the date's eigenvectors for the
+    problem's own scale and rho -- no per-problem factorisation, and an adaptive-rho change
+    is a re-form.  The Gram and the border W = Xc Cg' come from the hand-written window Gram
+    kernel (pq_lr_capacitance with D = I, unit row weights); the eigendecomposition itself
+    is rocSOLVER's (torch.linalg.eigh), once per date.
+
+    rows / tlen / mu: per-date device tensors (every tlen == tmax); pdate: date of each
+    problem (int32, device); Cg: the shared general rows (qb.Cg, mg <= 4)."""
+
+    MG = 4
+
+    def __init__(self, panel, rows, tlen, mu, qb: "QPBatch", pdate, k_ld: int):
+        lib = _lib.load()
+        nd, tmax = int(rows.shape[0]), int(rows.shape[1])
+        mg, n, dev = qb.mg, qb.n, qb.device
+        if mg > self.MG or not qb.shared:
+            raise _lib.PorquaHipError("EigCap: shared general rows, at most 4")
+        if not bool((tlen == tmax).all().item()):
+            raise _lib.PorquaHipError("EigCap: every window must have tmax rows")
+        self.k_ld, self.nd, self.tmax = int(k_ld), nd, tmax
+        self.pdate = pdate.to(torch.int32).contiguous()
+        lgf = torch.full((max(mg, 1),), -np.inf, dtype=F64, device=dev)
+        ugf = torch.full((max(mg, 1),), np.inf, dtype=F64, device=dev)
+        one = torch.ones(nd, dtype=F64, device=dev)
+        pb = _lib.PQProblem(n=n, ld=qb.ld, batch=nd, mg=mg, P=None, P_stride=0, p_scale=None, p_diag=None,
+                            q=qb.q.data_ptr(), q_stride=0, Cg=qb.Cg.data_ptr(), Cg_stride=0,
+                            lg=lgf.data_ptr(), ug=ugf.data_ptr(), g_stride=0, lb=None, ub=None, box_stride=0)
+        lr = _lib.PQLowRank(panel=panel.R.data_ptr(), ldp=panel.R.stride(0), rows=rows.data_ptr(),
+                            tlen=tlen.data_ptr(), tmax=tmax, mu=mu.data_ptr(), mu_stride=mu.stride(0),
+                            w_scale=None, dg=None, dg_stride=0)
+        st = _lib.PQState(rho=one.data_ptr())
+        s = Settings(sigma=1.0, rho_min=1.0).to_c()   # D = I, unit weight on the Cg rows: M = I + U U'
+        M = torch.zeros((nd, k_ld, k_ld), dtype=F64, device=dev)
+        _lib.check(lib.pq_lr_capacitance(ctypes.byref(lr), ctypes.byref(pb), ctypes.byref(st), None, 0,
+                                         ctypes.byref(s), M.data_ptr(), k_ld, k_ld * k_ld, _stream()),
+                   "pq_lr_capacitance (window Gram)")
+        T = tmax
+        Mt = M[:, :T, :T]
+        G = torch.tril(Mt) + torch.tril(Mt, -1).mT - torch.eye(T, dtype=F64, device=dev)
+        ev, V = torch.linalg.eigh(G)
+        self.V = torch.zeros((nd, k_ld, k_ld), dtype=F64, device=dev)
+        self.V[:, :T, :T] = V
+        self.evals = torch.zeros((nd, k_ld), dtype=F64, device=dev)
+        self.evals[:, :T] = ev
+        self.What = torch.zeros((nd, k_ld, self.MG), dtype=F64, device=dev)
+        if mg:
+            W = M[:, T:T + mg, :T].mT                      # Xc Cg' (rows T.. of the lower triangle)
+            self.What[:, :T, :mg] = V.mT @ W
+            C = qb.Cg[0, :mg, :n]
+            self.cc = (C @ C.T).contiguous()
+        else:
+            self.cc = torch.zeros((1, 1), dtype=F64, device=dev)
+        self.scratch = torch.empty((qb.batch, 2 * self.MG * k_ld), dtype=F64, device=dev)
+
+    def form(self, lrs, pbs, sts, ss, Minv, idx, nidx, strm):
+        """M_b^-1 of problems idx[0..nidx) (None: all) into Minv (B, k_ld, k_ld)."""
+        lib = _lib.load()
+        k = self.k_ld
+        _lib.check(lib.pq_eigcap_form(lrs, pbs, sts, ss, self.pdate.data_ptr(), self.V.data_ptr(),
+                                      self.evals.data_ptr(), self.What.data_ptr(), self.cc.data_ptr(), k,
+                                      _ptr(idx), nidx, Minv.data_ptr(), k * k, self.scratch.data_ptr(), strm),
+                   "pq_eigcap_form")
+
+
 def lowrank_shape_ok(n: int, tmax: int, mg: int) -> bool:
     """The Woodbury path applies (and pays): T + mg < n, k <= 512, and the window-form polish
     can run (even panel stride n, tmax <= 1024) so nothing needs the dense upper triangle."""
@@ -563,7 +631,8 @@ def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan"
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
-                  fuse: bool = True, grouped_polish: bool = True, gcap: bool = True) -> BatchResult:
+                  fuse: bool = True, grouped_polish: bool = True, gcap: bool = True,
+                  eig: "EigCap | None" = None) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -603,6 +672,9 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     bd = None
 
     def refactor(idx, nidx):
+        if eig is not None:   # from the per-date eigendecompositions: no factorisation
+            eig.form(L_, P_, S_, SS, M["Minv"], idx, nidx, strm)
+            return
         if bd is not None:
             _lib.check(lib.pq_lr_capacitance_band(L_, P_, S_, _ptr(idx), nidx, SS, bd["band"].data_ptr(), bd["ldo"],
                                                   bd["r0"], bd["pc"].data_ptr(), bd["pc"].stride(0),
@@ -614,7 +686,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         _lib.check(lib.pq_factor_batched(PM_, SM_, _ptr(idx), nidx, SSM, 1, strm), "pq_factor_batched(M)")
 
     grouped = grouped_applicable(qb, lr, groups, ws)
-    gcap_try = (gcap and grouped and fuse and qb.mg <= 4 and lr.mu is not None and qb.shared
+    gcap_try = (gcap and eig is None and grouped and fuse and qb.mg <= 4 and lr.mu is not None and qb.shared
                 and groups.ucnt_max + qb.mg <= 384 and groups.corr_max <= 64)
     if band:
         bd = tl("gram", lambda: _band_setup(qb, lr, strm, w_min=groups.span_max if gcap_try else 0))
@@ -734,7 +806,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
                        admm_launches=launches,
-                       capacitance="group" if gc is not None else ("band" if bd is not None else "direct"))
+                       capacitance="group" if gc is not None else ("eig" if eig is not None else
+                                                                    ("band" if bd is not None else "direct")))
 
 
 def factor_only(qb: QPBatch, invert: bool = False, sigma: float = 0.0):

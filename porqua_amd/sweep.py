@@ -8,17 +8,17 @@ problem of a single batch, date-major: all problems of a date share its window r
 the grouped low-rank ADMM (engine.GroupPlan with identical windows) streams those rows
 once per iteration for up to 16 risk aversions.  Nothing n x n is formed.
 
-Factor once per date (``shared_factor=True``, off by default): lam x'Sigma x - mu'x and x'Sigma x -
-(mu / lam)'x have the same minimiser, so every problem of a date is given P = 2 Sigma_d and
-q = -mu_d / lam: the KKT operator no longer depends on lam, a slide group of one date's risk
-aversions shares one capacitance matrix (engine group capacitance: one factorisation per 16
-problems instead of one per problem), and the ADMM runs them as a multi-right-hand-side
-block.  Objectives and multipliers are scaled back by lam afterwards, so the results are
-those of the reference's objective.  Measured (tools/exp_sweep.py, n = 5000, 16 dates x 64
-lam): 256 factorisations instead of 1024, but the nearly linear problems (lam <= 0.13, q
-dominating) then share one rho with their group and fall through to the eps_retry ADMM
-(up to 4000 iterations): 102 QPs/s against 12.7k QPs/s with one capacitance per problem and
-a per-problem, |q|-aware rho -- so the per-problem form stays the default.
+Factor once per date (``factor='eig'``, the default; SURVEY.md §8(e) "keep all lambda of a
+date on one rank so the factorisation is shared"): the capacitance of problem (d, lam) is
+M = I + (2 lam w / c) Xc_d Xc_d' + border rows, so one symmetric eigendecomposition of the
+date's T x T window Gram diagonalises M for EVERY lam and every rho
+(engine.EigCap / pq_eigcap_form): each problem keeps its own |q|-aware rho and its adaptive
+rho updates, and its M^-1 is formed from the shared eigenvectors by one MFMA tile product
+instead of a Cholesky factorisation per problem.  ``factor='chol'`` keeps the per-problem
+factorisation (rounds 1-2).  A round-2 attempt that instead rescaled every problem of a date
+to P = 2 Sigma_d, q = -mu_d / lam (one capacitance per slide group) had to share one rho
+per group and left the nearly linear problems (lam <= 0.13) on 4000-iteration ADMM tails:
+102 QPs/s against 12.7k -- the eigen form needs no shared rho.
 """
 from __future__ import annotations
 
@@ -28,21 +28,22 @@ import torch
 from . import engine
 
 
-RHO_BUCKET = 2.0       # shared factorisation: largest rho0 ratio inside one group
-
-
 def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0, budget=1.0,
                         geometric=True, settings: engine.Settings | None = None, group=True,
-                        shared_factor=False, gmax: int = engine.GROUP_MAX_DATES):
+                        factor: str = "eig", gmax: int = engine.GROUP_MAX_DATES,
+                        events: list | None = None):
     """Solve min lam x'Sigma_d x - mu_d'x  s.t. 1'x = budget, lb <= x <= ub for every
     rebalance window (rows, tlen: host arrays of engine.window_rows) and every lam.
 
     Returns (BatchResult, meta): problem p = d * len(lambdas) + j is (date d, lambdas[j])."""
+    if factor not in ("eig", "chol"):
+        raise ValueError("mean_variance_sweep: factor must be 'eig' or 'chol'")
     rows = np.asarray(rows, dtype=np.int32)
     tlen = np.asarray(tlen, dtype=np.int32)
     lam = np.asarray(lambdas, dtype=np.float64).reshape(-1)
     nd, L, n = len(tlen), len(lam), panel.n
     dev = panel.device
+    tl = engine._Timeline(events)
     r_d, t_d = panel.rows_to_device(rows, tlen)
     mu_c = panel.window_means(r_d, t_d)                               # centring of Sigma
     mu_q = panel.window_means(r_d, t_d, geometric=geometric) if geometric else mu_c
@@ -58,38 +59,23 @@ def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0
     qb.ub[0, :n] = ub
     qb.lb[0, n:] = qb.ub[0, n:] = 0.0
     lam_p = torch.from_numpy(np.tile(lam, nd)).to(dev)
-    if shared_factor:   # P = 2 Sigma_d for every lam, q = -mu_d / lam
-        qb.q = (-mu_q.repeat_interleave(L, dim=0) / lam_p[:, None]).contiguous()
-        qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=dev)
-    else:
-        qb.q = -mu_q.repeat_interleave(L, dim=0).contiguous()
-        qb.p_scale = 2.0 * lam_p
+    qb.q = -mu_q.repeat_interleave(L, dim=0).contiguous()
+    qb.p_scale = 2.0 * lam_p
     mu_p = mu_c.repeat_interleave(L, dim=0).contiguous()
     lr = engine.LowRank(panel, rp_d, tp_d, mu=mu_p, w_scale=1.0 / (tp_d.to(torch.float64) - 1.0))
-    breaks = None
-    if shared_factor and group:
-        # one capacitance per group needs one rho per group: the problems of a date share
-        # P = 2 Sigma_d, and rho0 = max(4 mean diag P, 10 |q|_max) (engine.Settings) varies
-        # with lam only through q = -mu_d / lam -- so a group holds the risk aversions of one
-        # date whose rho0 lie within a factor RHO_BUCKET of each other (bucket breaks here)
-        Tw = torch.as_tensor(tlen, dtype=torch.float64, device=dev)
-        dg = panel.window_sumsq(r_d, t_d, mu_c)[:, :n]
-        pdiag = (2.0 * dg.mean(1) / (Tw - 1.0)).cpu().numpy()
-        qmax = mu_q[:, :n].abs().amax(1).cpu().numpy()
-        r0 = np.maximum(4.0 * pdiag[:, None], 10.0 * qmax[:, None] / lam[None, :])     # (nd, L)
-        bucket = np.floor(np.log(r0 / r0.min(1, keepdims=True)) / np.log(RHO_BUCKET)).astype(np.int64)
-        brk = np.ones((nd, L), dtype=bool)
-        brk[:, 1:] = bucket[:, 1:] != bucket[:, :-1]
-        breaks = brk.reshape(-1)
-    gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax, breaks=breaks) if group else None
-    res = engine.solve_lowrank(qb, lr, settings, groups=gp)
-    if shared_factor:   # back to lam x'Sigma x - mu'x: objective and multipliers times lam
-        res.obj.mul_(lam_p)
-        res.y.mul_(lam_p[:, None])
-        res.z_box.mul_(lam_p[:, None])
+    eig = None
+    full = bool((tlen == rows.shape[1]).all())
+    if factor == "eig" and full and engine.lowrank_shape_ok(n, rows.shape[1], qb.mg):
+        k_ld = engine.round_up(rows.shape[1] + qb.mg, 64)
+        pdate = torch.arange(nd, dtype=torch.int32, device=dev).repeat_interleave(L)
+        eig = tl("eig", lambda: engine.EigCap(panel, r_d, t_d, mu_c, qb, pdate, k_ld))
+    gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax) if group else None
+    res = engine.solve_lowrank(qb, lr, settings, groups=gp, events=events, eig=eig)
     meta = {"dates": nd, "lambdas": lam, "grouped": gp is not None and gp.ok,
             "ngroups": None if gp is None else gp.ngroups, "capacitance": res.capacitance,
-            "shared_factor": shared_factor,
-            # capacitance factorisations: one per slide group (group form) or per problem
-            "factorizations": (gp.ngroups if res.capacitance == "group" else B) + res.refactors}
+            "factor": "eig" if eig is not None else "chol",
+            # factorisations: one eigendecomposition per date (eig) or one Cholesky per
+            # problem and per adaptive-rho change (chol; the eig form re-forms instead)
+            "factorizations": nd if eig is not None else
+            ((gp.ngroups if res.capacitance == "group" else B) + res.refactors)}
     return res, meta

@@ -67,18 +67,31 @@ def config4(dates_limit, steps, dev, overrides=None):
     ws = engine.Workspace(qb, dense=False)
     settings = engine.Settings.from_params(dict({"rho0_rel": 0.1, "rho0_qrel": 0.0}, **(overrides or {})))
 
+    ev = []
+
     def run():
+        ev.clear()
         xty, _ = pan.gram_xy(r_d, t_d)                 # q = -2 X'y per date, inside the step
         qb.q = (-2.0 * xty).contiguous()
         lr.refresh()
-        return engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp)
+        return engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, events=ev)
 
     res, dt = timed(run, steps)
+    torch.cuda.synchronize()
     return dict({"config": "config4: n=3000 tracking LS, budget + box + 20 sector caps, daily",
-                 "qps": B / dt, "ms_per_step": dt * 1e3, "dates": B}, **summary(res))
+                 "qps": B / dt, "ms_per_step": dt * 1e3, "dates": B, "stage_ms": stage_ms(ev)},
+                **summary(res))
 
 
-def config5(steps, dev, settings=None):
+def stage_ms(events):
+    """Per-stage milliseconds of the last timed step (engine._Timeline HIP event pairs)."""
+    out = {}
+    for name, e0, e1 in events:
+        out[name] = out.get(name, 0.0) + e0.elapsed_time(e1)
+    return {k: round(v, 3) for k, v in out.items()}
+
+
+def config5(steps, dev, settings=None, factor="eig"):
     n, T, nd, L = 5000, 252, 64, 64
     dates, R, _, _ = factor_panel(T - 1 + 21 * nd, n)
     ends = np.arange(T - 1, T - 1 + 21 * nd, 21)
@@ -86,16 +99,19 @@ def config5(steps, dev, settings=None):
     pan = engine.Panel(R, device=dev)
     lambdas = np.logspace(-1, 2, L)
     meta = {}
+    ev = []
 
     def run():
-        r, m = mean_variance_sweep(pan, rows, tlen, lambdas, settings=settings)
+        ev.clear()
+        r, m = mean_variance_sweep(pan, rows, tlen, lambdas, settings=settings, events=ev, factor=factor)
         meta.update(m)
         return r
     res, dt = timed(run, steps)
+    torch.cuda.synchronize()
     return dict({"config": "config5: n=5000 mean-variance, 64 monthly dates x 64 risk aversions",
                  "qps": nd * L / dt, "ms_per_step": dt * 1e3, "qps_per_step": nd * L,
                  "capacitance": meta.get("capacitance"), "factorizations_per_step": meta.get("factorizations"),
-                 "shared_factor": meta.get("shared_factor")}, **summary(res))
+                 "factor": meta.get("factor"), "stage_ms": stage_ms(ev)}, **summary(res))
 
 
 def config12(steps, dev):
@@ -137,6 +153,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--dates", type=int, default=9749, help="config 4 rebalance dates")
     ap.add_argument("--only", choices=["12", "4", "5"], default=None)
+    ap.add_argument("--factor", default="eig", help="config 5 capacitance factor(s): eig, chol or eig,chol")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="engine.Settings override for config 5 (experiments)")
     args = ap.parse_args()
@@ -150,7 +167,8 @@ def main():
         print(json.dumps(dict(config4(args.dates, args.steps, dev, ov), settings_overrides=args.set)), flush=True)
     if args.only in (None, "5"):
         st = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set)) if args.set else None
-        print(json.dumps(dict(config5(args.steps, dev, st), settings_overrides=args.set)), flush=True)
+        for fac in args.factor.split(","):
+            print(json.dumps(dict(config5(args.steps, dev, st, factor=fac), settings_overrides=args.set)), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Config-5 sweep variants (shared factor / group size): QPs/s, iterations, factorisations.
-Experiment tool:  python tools/exp_sweep.py"""
+"""Config-5 sweep variants (capacitance factor form x group size): QPs/s, iterations,
+factorisations.  Experiment tool:  python tools/exp_sweep.py  (ND dates, default 16)"""
 import json
 import os
 import sys
@@ -23,24 +23,24 @@ def main():
     rows, tlen = engine.window_rows(dates, dates[ends], T)
     pan = engine.Panel(R, device=torch.device("cuda", 0))
     lambdas = np.logspace(-1, 2, L)
-    from porqua_amd import sweep
-    variants = [(False, {}, 2.0), (True, {}, 2.0), (True, {}, 1.5), (True, {}, 4.0), (True, {}, 1e9)]
-    for shared, kw, bucket in variants:
-        sweep.RHO_BUCKET = bucket
-        gmax = 16
-        st = engine.Settings.from_params(kw)
-        mean_variance_sweep(pan, rows, tlen, lambdas, shared_factor=shared, gmax=gmax, settings=st)
+    for factor, gmax in (("chol", 16), ("eig", 16)):
+        st = engine.Settings()
+        mean_variance_sweep(pan, rows, tlen, lambdas, factor=factor, gmax=gmax, settings=st)
         torch.cuda.synchronize()
+        ev = []
         t0 = time.perf_counter()
-        res, meta = mean_variance_sweep(pan, rows, tlen, lambdas, shared_factor=shared, gmax=gmax, settings=st)
+        res, meta = mean_variance_sweep(pan, rows, tlen, lambdas, factor=factor, gmax=gmax, settings=st, events=ev)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        stages = {}
+        for name, e0, e1 in ev:
+            stages[name] = round(stages.get(name, 0.0) + e0.elapsed_time(e1), 3)
         it = res.iters.cpu().numpy()
-        slow = np.flatnonzero(res.iters.cpu().numpy() > 200)
-        print(json.dumps({"shared": shared, "kw": kw, "rho_bucket": bucket, "slow_lambda_idx": sorted(set((slow % L).tolist()))[:20], "qps": nd * L / dt, "s": dt, "iters_mean": float(it.mean()),
-                          "iters_max": int(it.max()), "factorizations": meta["factorizations"],
-                          "capacitance": meta["capacitance"],
-                          "status": {str(k): int(v) for k, v in zip(*np.unique(res.status.cpu().numpy(), return_counts=True))}}),
+        print(json.dumps({"factor": factor, "gmax": gmax, "qps": nd * L / dt, "s": dt, "stage_ms": stages,
+                          "iters_mean": float(it.mean()), "iters_max": int(it.max()),
+                          "factorizations": meta["factorizations"], "capacitance": meta["capacitance"],
+                          "status": {str(k): int(v) for k, v in zip(*np.unique(res.status.cpu().numpy(),
+                                                                                return_counts=True))}}),
               flush=True)
 
 
