@@ -342,9 +342,12 @@ int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st
  * (status PQ_SOLVED, out[]); FALLBACK problems (free set outside 1..min(128, ldk), more
  * than 32 active rows, a failed factorisation, or not accepted within polish_rounds) are
  * left at their ADMM point for pq_polish_w_batched.  K scratch: ldk x ldk per problem
- * (indexed by problem id).  Needs even n and ldp, mg <= 32, umax <= 320, lr->dg.
+ * (indexed by problem id).  Needs even n and ldp, mg <= 32, umax <= 320, lr->dg.  The
+ * window passes of a group run split over 4 workgroups (column slices), with
+ * pass_scratch = ngroups * PQ_PG_PASS_SCRATCH doubles for their partial products.
  * Replaces, with pq_polish_w_batched, the accuracy of qpsolvers (src/qp_problems.py:211-214). */
 #define PQ_PG_RECORD 320
+#define PQ_PG_PASS_SCRATCH 20816   /* doubles per group: 4 x 324 x 16 + 4 x 16 + 16 */
 #define PQ_PG_PENDING 0
 #define PQ_PG_DONE 1
 #define PQ_PG_FALLBACK 2
@@ -353,7 +356,8 @@ int pq_polish_grouped_init(const pq_lowrank* lr, const pq_problem* pb, pq_state*
                            const pq_settings* s, void* stream);
 int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec, int32_t ldk,
                             const int32_t* gdates, int32_t ngroups, const int32_t* urows, const int32_t* ucnt,
-                            const int32_t* uoff, int32_t umax, const pq_settings* s, void* stream);
+                            const int32_t* uoff, int32_t umax, const pq_settings* s, double* pass_scratch,
+                            void* stream);
 
 /* Strategy simulation: one holding period per rebalance date.
  * Replaces Strategy.simulate (src/portfolio.py:209-248) with floating_weights

@@ -26,6 +26,7 @@ PQ_DUAL_INFEASIBLE = -4
 PQ_NON_CONVEX = -5
 
 PQ_PG_RECORD = 320                   # doubles per problem of the grouped polish record
+PQ_PG_PASS_SCRATCH = 20816           # doubles per slide group of the split polish window passes
 PQ_PG_PENDING, PQ_PG_DONE, PQ_PG_FALLBACK, PQ_PG_SKIP = range(4)
 PQ_PG_STATE = 3                      # record field holding the state
 
@@ -152,7 +153,7 @@ _EXPORTS = {
                                 c_dp, ctypes.POINTER(PQSettings), c_dp], c_int32),
     "pq_polish_grouped_round": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                                  c_dp, c_int32, c_dp, c_int32, c_dp, c_dp, c_dp, c_int32,
-                                 ctypes.POINTER(PQSettings), c_dp], c_int32),
+                                 ctypes.POINTER(PQSettings), c_dp, c_dp], c_int32),
     "pq_gcap_assemble": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQGcap),
                           ctypes.POINTER(PQSettings), c_dp, c_int64, c_int32, c_dp, c_int64, c_dp, c_dp], c_int32),
     "pq_gcap_prepare": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),

@@ -306,11 +306,8 @@ class Backtest:
                 width = bld.arguments.get("width")
         if width is None:
             return False
-        Xs = X[universe]
-        # windows with missing values: the objectives that support them batch with the
-        # pairwise-complete covariance (MeanVariance); the others keep the serial path
-        if Xs.isna().to_numpy().any() and not getattr(opt, "batch_handles_nan", False):
-            return False
+        # the whole frame when the selection is every column in order (no 8 T n-byte copy)
+        Xs = X if list(X.columns) == list(universe) else X[universe]
         idx = pd.DatetimeIndex(Xs.index)
         dates = idx.values.astype("datetime64[D]")
         rows, tlen = engine.window_rows(dates, np.array(rebdates, dtype="datetime64[D]"), width)
@@ -339,6 +336,11 @@ class Backtest:
         settings = engine.Settings.from_params(opt.params)
         panel = engine.Panel(Xs.to_numpy(dtype=np.float64), bm, device=dev)
         n = panel.n
+        # windows with missing values (checked on the device copy): the objectives that
+        # support them batch with the pairwise-complete covariance (MeanVariance); the others
+        # keep the serial path
+        if panel.has_nan and not getattr(opt, "batch_handles_nan", False):
+            return False
         chunk = int(bs.settings.get("batch_chunk", 0) or _auto_chunk(n))
         W = np.zeros((hi - lo, n))
         ST = np.zeros(hi - lo, dtype=np.int32)
@@ -387,8 +389,8 @@ class Backtest:
             Pm, scale, pdiag, q, _const = obj
             if stage.lowrank is not None:
                 path = "lowrank"
-            qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=GhAb["A"], b=GhAb["b"],
-                                           G=GhAb["G"], h=GhAb["h"], lb=lb, ub=ub, device=dev)
+            qb = engine.QPBatch.from_dense(None, None, n=n, A=GhAb["A"], b=GhAb["b"], G=GhAb["G"], h=GhAb["h"],
+                                           lb=lb, ub=ub, device=dev)
             qb.batch = e - s
             qb.P = Pm
             qb.p_scale = scale

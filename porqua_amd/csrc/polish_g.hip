@@ -687,148 +687,234 @@ __device__ __forceinline__ double hmax32(double v) {
   return v;
 }
 
+// The two window passes of a group run split over PQ_PG_SPLIT workgroups each (the union
+// rows' columns divided between them), so a late round with few pending groups is not one
+// latency-bound workgroup per group:
+//   k_pg_passA  (group, column slice)  partial W = X_union[:, slice] V[slice] and mu.V partials
+//   k_pg_passB  (group, column slice)  W = sum of the partials (fixed order: deterministic),
+//                                      Ut = window-masked W - mu.V, X~[slice] = X_union[:, slice]' Ut
+//   k_pg_post   (group)                the per-date post-processing on the complete X~
+constexpr int QS = 4;      // workgroups per group and pass
+
+struct PassGroup {
+  int grp, part, d0, G, U;
+};
+
 template <int MODE>
-__global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
-                                                pq_settings s, const int32_t* gdates, const int32_t* urows_all,
-                                                const int32_t* ucnt_all, const int32_t* uoff, int umax) {
+__device__ __forceinline__ bool pass_setup(const PassGroup& pg, const pq_lowrank& lr, const double* rec,
+                                           const int32_t* uoff, int* g_on, int* g_T, int* g_off, int* s_any) {
+  const int t = threadIdx.x;
+  if (t < QG) {
+    int on = 0;
+    if (t < pg.G) {
+      const double* R = rec + (int64_t)(pg.d0 + t) * PGR;
+      on = R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || R[R_NZB] != 0.0);
+      g_T[t] = lr.tlen[pg.d0 + t];
+      g_off[t] = uoff[pg.d0 + t];
+    }
+    g_on[t] = on;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int any = 0;
+    for (int g = 0; g < pg.G; ++g) any |= g_on[g];
+    *s_any = any;
+  }
+  __syncthreads();
+  return *s_any != 0;
+}
+
+__device__ __forceinline__ PassGroup pass_group(const int32_t* gdates, const int32_t* ucnt_all) {
+  const int id = xcd_slot(blockIdx.x, gridDim.x);   // the slices of a group on one XCD
+  PassGroup pg;
+  pg.grp = id / QS;
+  pg.part = id % QS;
+  pg.d0 = gdates[pg.grp];
+  pg.G = gdates[pg.grp + 1] - pg.d0;
+  pg.U = ucnt_all[pg.grp];
+  return pg;
+}
+
+// scratch per group: QS partial W images ((QU + 4) x QG) + QS x QG mu.V partials + QG sums
+constexpr int64_t QSCR = (int64_t)QS * (QU + 4) * QG + QS * QG + QG;
+
+template <int MODE>
+__global__ __launch_bounds__(QT) void k_pg_passA(pq_lowrank lr, pq_problem pb, pq_state st, const double* rec,
+                                                 const int32_t* gdates, const int32_t* urows_all,
+                                                 const int32_t* ucnt_all, const int32_t* uoff, int umax,
+                                                 double* scr) {
+  __shared__ int s_urow[QU];
+  __shared__ int g_on[QG], g_T[QG], g_off[QG];
+  __shared__ int s_any;
+  const PassGroup pg = pass_group(gdates, ucnt_all);
+  const int U = pg.U, G = pg.G, d0 = pg.d0;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int n = pb.n, ld = pb.ld;
+  for (int u = t; u < QU; u += QT) s_urow[u] = u < U ? urows_all[(int64_t)pg.grp * umax + u] : 0;
+  if (!pass_setup<MODE>(pg, lr, rec, uoff, g_on, g_T, g_off, &s_any)) return;
+  const int per = ((n + QS - 1) / QS + 7) & ~7;
+  const int k_lo = pg.part * per, k_hi = min(n, k_lo + per);
+  double* Wp = scr + pg.grp * QSCR + (int64_t)pg.part * (QU + 4) * QG;
+  double* Mp = scr + pg.grp * QSCR + (int64_t)QS * (QU + 4) * QG + pg.part * QG;
+  // mu . v partial of every participating date (half-wave per date)
+  const int hg = t >> 5, hl = t & 31;
+  if (hg < G && g_on[hg]) {
+    PGWork wk(st, d0 + hg, ld);
+    const double* v = MODE == 0 ? wk.xb : wk.xs;
+    const double* mu = lr.mu ? lr.mu + (int64_t)(d0 + hg) * lr.mu_stride : nullptr;
+    double a = 0.0;
+    if (mu)
+      for (int i = k_lo + hl; i < k_hi; i += 32) a = fma(mu[i], v[i], a);
+    a = hsum32(a);
+    if (hl == 0) Mp[hg] = a;
+  } else if (hg < QG && hl == 0) {
+    Mp[hg] = 0.0;
+  }
+  // partial W (U x 16) = X_union[:, k_lo:k_hi] V[k_lo:k_hi]
+  const int ntile = (U + 15) >> 4;
+  const int kq = l >> 4, m = l & 15;
+  const double* Vp = nullptr;
+  if (m < G && g_on[m]) {
+    PGWork wk(st, d0 + m, ld);
+    Vp = MODE == 0 ? wk.xb : wk.xs;
+  }
+  f64x4 c[3];
+  const double* arow[3];
+  bool tv[3], aval[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    c[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int u = (w + QNW * j) * 16 + m;
+    tv[j] = w + QNW * j < ntile;
+    aval[j] = u < U;
+    arow[j] = lr.panel + (int64_t)s_urow[u < QU ? u : 0] * lr.ldp;
+  }
+  for (int k0 = k_lo; k0 < k_hi; k0 += 8) {
+    const int kk = k0 + 2 * kq;
+    const bool kin = kk + 1 < k_hi;   // slice ends and n are even
+    const double2 bv = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (tv[j]) {
+        const double2 av = (aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
+        c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c[j], 0, 0, 0);
+        c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c[j], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int tile = w + QNW * j;
+    if (tv[j]) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = tile * 16 + kq + 4 * r;
+        if (u < QU) Wp[u * QG + m] = c[j][r];
+      }
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(QT) void k_pg_passB(pq_lowrank lr, pq_problem pb, pq_state st, const double* rec,
+                                                 const int32_t* gdates, const int32_t* urows_all,
+                                                 const int32_t* ucnt_all, const int32_t* uoff, int umax,
+                                                 double* scr) {
   __shared__ __attribute__((aligned(16))) double WU[(QU + 4) * QG];
   __shared__ int s_urow[QU];
   __shared__ int g_on[QG], g_T[QG], g_off[QG];
   __shared__ double g_mux[QG];
   __shared__ int s_any;
-  const int grp = xcd_slot(blockIdx.x, gridDim.x);
-  const int d0 = gdates[grp];
-  const int G = gdates[grp + 1] - d0;
-  const int U = ucnt_all[grp];
+  const PassGroup pg = pass_group(gdates, ucnt_all);
+  const int U = pg.U, G = pg.G, d0 = pg.d0;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
-  const int n = pb.n, ld = pb.ld, mg = pb.mg;
+  const int n = pb.n, ld = pb.ld;
+  for (int u = t; u < QU; u += QT) s_urow[u] = u < U ? urows_all[(int64_t)pg.grp * umax + u] : 0;
+  if (!pass_setup<MODE>(pg, lr, rec, uoff, g_on, g_T, g_off, &s_any)) return;
+  const double* S = scr + pg.grp * QSCR;
+  const double* Mp = S + (int64_t)QS * (QU + 4) * QG;
   if (t < QG) {
-    int on = 0;
-    if (t < G) {
-      const double* R = rec + (int64_t)(d0 + t) * PGR;
-      on = R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || R[R_NZB] != 0.0);
-      g_T[t] = lr.tlen[d0 + t];
-      g_off[t] = uoff[d0 + t];
-    }
-    g_on[t] = on;
-  }
-  for (int u = t; u < QU; u += QT) s_urow[u] = u < U ? urows_all[(int64_t)grp * umax + u] : 0;
-  for (int e = t; e < (QU + 4) * QG; e += QT) WU[e] = 0.0;
-  __syncthreads();
-  if (t == 0) {
-    int any = 0;
-    for (int g = 0; g < G; ++g) any |= g_on[g];
-    s_any = any;
-  }
-  __syncthreads();
-  if (!s_any) return;
-  const int hg = t >> 5, hl = t & 31;
-  const bool hmine = hg < G && g_on[hg];
-  const int hb = d0 + (hg < G ? hg : 0);
-  // mu . v of every participating date (half-wave per date)
-  if (hmine) {
-    PGWork wk(st, hb, ld);
-    const double* v = MODE == 0 ? wk.xb : wk.xs;
-    const double* mu = lr.mu ? lr.mu + (int64_t)hb * lr.mu_stride : nullptr;
     double a = 0.0;
-    if (mu)
-      for (int i = hl; i < n; i += 32) a = fma(mu[i], v[i], a);
-    a = hsum32(a);
-    if (hl == 0) g_mux[hg] = a;
+    for (int q = 0; q < QS; ++q) a += Mp[q * QG + t];
+    g_mux[t] = a;
   }
-  // ---- pass 1: W (U x 16) = X_union V ---------------------------------------------------
+  __syncthreads();
+  // Ut = sum of the partial W images (fixed order), masked to each date's own window rows
   const int ntile = (U + 15) >> 4;
-  {
-    const int kq = l >> 4, m = l & 15;
-    const double* Vp = nullptr;
-    if (m < G && g_on[m]) {
-      PGWork wk(st, d0 + m, ld);
-      Vp = MODE == 0 ? wk.xb : wk.xs;
+  for (int e = t; e < (QU + 4) * QG; e += QT) {
+    const int u = e / QG, m = e % QG;
+    double v = 0.0;
+    if (u < ntile * 16) {
+      double a = 0.0;
+      for (int q = 0; q < QS; ++q) a += S[(int64_t)q * (QU + 4) * QG + e];
+      const bool inw = m < G && g_on[m] && u >= g_off[m] && u < g_off[m] + g_T[m];
+      v = inw ? a - g_mux[m] : 0.0;
     }
-    f64x4 c[3];
-    const double* arow[3];
-    bool tv[3], aval[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      c[j] = f64x4{0.0, 0.0, 0.0, 0.0};
-      const int u = (w + QNW * j) * 16 + m;
-      tv[j] = w + QNW * j < ntile;
-      aval[j] = u < U;
-      arow[j] = lr.panel + (int64_t)s_urow[u < QU ? u : 0] * lr.ldp;
+    WU[e] = v;
+  }
+  __syncthreads();
+  if (pg.part == 0 && t < QG) {   // sum of Ut per date (the centring term of the post)
+    double a = 0.0;
+    for (int u = 0; u < U; ++u) a += WU[u * QG + t];
+    scr[pg.grp * QSCR + (int64_t)QS * (QU + 4) * QG + QS * QG + t] = a;
+  }
+  // X~ (slice x 16) = X_union[:, slice]' Ut -> raw into the date's target vector
+  const int kq = l >> 4, m = l & 15;
+  const int Uk = (U + 3) & ~3;
+  double* dst = nullptr;
+  if (m < G && g_on[m]) {
+    PGWork wk(st, d0 + m, ld);
+    dst = MODE == 0 ? wk.pxb : wk.g;
+  }
+  const int nch = (n + 31) / 32;
+  const int cper = (nch + QS - 1) / QS;
+  const int p_lo = pg.part * cper, p_hi = min(nch, p_lo + cper);
+  for (int p = p_lo + w; p < p_hi; p += QNW) {
+    const int col = p * 32 + 2 * m;
+    const bool cin = col < n;
+    f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int u0 = 0; u0 < Uk; u0 += 4) {
+      const int u = u0 + kq;
+      const double2 a = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + col)
+                                       : double2{0.0, 0.0};
+      const double bv = WU[u * QG + m];
+      ce = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, bv, ce, 0, 0, 0);
+      co = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, bv, co, 0, 0, 0);
     }
-    for (int k0 = 0; k0 < n; k0 += 8) {
-      const int kk = k0 + 2 * kq;
-      const bool kin = kk + 1 < n;   // n even (host check)
-      const double2 bv = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+    if (dst) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (tv[j]) {
-          const double2 av = (aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
-          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c[j], 0, 0, 0);
-          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c[j], 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();   // g_mux visible
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int tile = w + QNW * j;
-      if (tv[j]) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int u = tile * 16 + kq + 4 * r;
-          // u_t = X_t . v - mu . v on the date's own window rows, 0 elsewhere
-          const bool inw = m < G && g_on[m] && u >= g_off[m] && u < g_off[m] + g_T[m];
-          if (u < QU) WU[u * QG + m] = inw ? c[j][r] - g_mux[m] : 0.0;
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int i = p * 32 + 2 * (kq + 4 * r);
+        if (i < n) dst[i] = ce[r];
+        if (i + 1 < n) dst[i + 1] = co[r];
       }
     }
   }
-  __syncthreads();
-  // ---- pass 2: X~ (n x 16) = X_union' Ut -> raw into the date's target vector ----------
-  {
-    const int kq = l >> 4, m = l & 15;
-    const int Uk = (U + 3) & ~3;
-    double* dst = nullptr;
-    if (m < G && g_on[m]) {
-      PGWork wk(st, d0 + m, ld);
-      dst = MODE == 0 ? wk.pxb : wk.g;
-    }
-    for (int p = w; p * 32 < n; p += QNW) {
-      const int col = p * 32 + 2 * m;
-      const bool cin = col < n;
-      f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
-      for (int u0 = 0; u0 < Uk; u0 += 4) {
-        const int u = u0 + kq;
-        const double2 a = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + col)
-                                         : double2{0.0, 0.0};
-        const double bv = WU[u * QG + m];
-        ce = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, bv, ce, 0, 0, 0);
-        co = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, bv, co, 0, 0, 0);
-      }
-      if (dst) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = p * 32 + 2 * (kq + 4 * r);
-          if (i < n) dst[i] = ce[r];
-          if (i + 1 < n) dst[i + 1] = co[r];
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (!hmine) return;
-  // ---- per-date post (half-wave) ---------------------------------------------------------
-  const int b = hb;
+}
+
+// one wave per pending date (the rows of a date's vectors spread over 64 lanes; thousands of
+// waves in flight instead of one 512-thread workgroup per group)
+template <int MODE>
+__global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                pq_settings s, const int32_t* gdates, int ngroups,
+                                                const double* scr) {
+  const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
+  if (!(R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || R[R_NZB] != 0.0))) return;
+  int lo = 0, hi = ngroups;   // group of date b: gdates[grp] <= b < gdates[grp + 1]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (gdates[mid] <= b) lo = mid; else hi = mid;
+  }
+  const int grp = lo, hg = b - gdates[grp];
+  const int hl = lane_id();
+  const int n = pb.n, ld = pb.ld, mg = pb.mg;
   PGWork wk(st, b, ld);
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
-  double su = 0.0;
-  for (int u = hl; u < U; u += 32) su += WU[u * QG + hg];
-  su = hsum32(su);
+  const double su = scr[(int64_t)grp * QSCR + (int64_t)QS * (QU + 4) * QG + QS * QG + hg];
   const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
   if (MODE == 0) {
-    for (int i = hl; i < n; i += 32) wk.pxb[i] = wsc * (wk.pxb[i] - (mu ? mu[i] * su : 0.0));
+    for (int i = hl; i < n; i += 64) wk.pxb[i] = wsc * (wk.pxb[i] - (mu ? mu[i] * su : 0.0));
     return;
   }
   const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
@@ -845,7 +931,7 @@ __global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq
   const double ptol = 1e-12;
   // exact P x and gradient g = P x + q + Cg' lam; box checks
   int bad = 0;
-  for (int i = hl; i < n; i += 32) {
+  for (int i = hl; i < n; i += 64) {
     const double xi = wk.xs[i];
     const double pxi = ps * (wsc * (wk.g[i] - (mu ? mu[i] * su : 0.0))) + pd * xi;
     double gi = pxi + q[i];
@@ -863,8 +949,8 @@ __global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq
   for (int r = 0; r < mg; ++r) {
     const double* cr = Cg + (int64_t)r * ld;
     double sum = 0.0;
-    for (int j = hl; j < n; j += 32) sum += cr[j] * wk.xs[j];
-    sum = hsum32(sum);
+    for (int j = hl; j < n; j += 64) sum += cr[j] * wk.xs[j];
+    sum = wave_sum(sum);
     if (hl == 0) {
       if (lg[r] != ug[r]) {
         const int a = (int)R[R_ACT + r];
@@ -878,7 +964,7 @@ __global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq
       }
     }
   }
-  bad = hmax32((double)bad) > 0.5;
+  bad = wave_max((double)bad) > 0.5;
   if (bad) {
     if (hl == 0 && R[R_ROUNDS] >= s.polish_rounds) R[R_STATE] = PQ_PG_FALLBACK;
     return;
@@ -888,7 +974,7 @@ __global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq
   double* sz = st.z + (int64_t)b * st.m_ld;
   double* sy = st.y + (int64_t)b * st.m_ld;
   double xpx = 0.0, qx = 0.0, pres = 0.0, dres = 0.0, gapb = 0.0;
-  for (int i = hl; i < n; i += 32) {
+  for (int i = hl; i < n; i += 64) {
     const double xi = wk.xs[i];
     double zb = 0.0;
     if (has_box) zb = wk.fl[i] ? -wk.g[i] : 0.0;
@@ -905,8 +991,8 @@ __global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq
   for (int r = 0; r < mg; ++r) {
     const double* cr = Cg + (int64_t)r * ld;
     double sum = 0.0;
-    for (int j = hl; j < n; j += 32) sum += cr[j] * wk.xs[j];
-    sum = hsum32(sum);
+    for (int j = hl; j < n; j += 64) sum += cr[j] * wk.xs[j];
+    sum = wave_sum(sum);
     const double lam = R[R_LAM + r];
     double v;
     if (lg[r] == ug[r]) v = fabs(sum - ug[r]);
@@ -918,11 +1004,11 @@ __global__ __launch_bounds__(QT) void k_pg_pass(pq_lowrank lr, pq_problem pb, pq
       sz[r] = sum;
     }
   }
-  xpx = hsum32(xpx);
-  qx = hsum32(qx);
-  gapb = hsum32(gapb);
-  pres = hmax32(pres);
-  dres = hmax32(dres);
+  xpx = wave_sum(xpx);
+  qx = wave_sum(qx);
+  gapb = wave_sum(gapb);
+  pres = wave_max(pres);
+  dres = wave_max(dres);
   if (hl == 0) {
     double* o = st.out + (int64_t)b * PQ_OUT_FIELDS;
     o[PQ_OUT_OBJ] = 0.5 * xpx + qx;
@@ -956,8 +1042,9 @@ extern "C" int pq_polish_grouped_init(const pq_lowrank* lr, const pq_problem* pb
 extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
                                        int32_t ldk, const int32_t* gdates, int32_t ngroups, const int32_t* urows,
                                        const int32_t* ucnt, const int32_t* uoff, int32_t umax, const pq_settings* s,
-                                       void* stream) {
-  PQ_CHECK_ARG(lr && pb && st && s && rec, "pq_polish_grouped_round: null argument");
+                                       double* pass_scratch, void* stream) {
+  PQ_CHECK_ARG(lr && pb && st && s && rec && pass_scratch, "pq_polish_grouped_round: null argument");
+  static_assert(pq::QSCR == PQ_PG_PASS_SCRATCH, "PQ_PG_PASS_SCRATCH out of date");
   PQ_CHECK_ARG(gdates && urows && ucnt && uoff && umax > 0 && umax <= pq::QU,
                "pq_polish_grouped_round: group plan missing (umax <= %d)", pq::QU);
   PQ_CHECK_ARG(pb->n % 2 == 0 && lr->ldp % 2 == 0, "pq_polish_grouped_round: needs even n and panel stride");
@@ -969,8 +1056,13 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   const int B = pb->batch;
   const int kmax = ldk < pq::PG_KMAX ? ldk : pq::PG_KMAX;
   hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax);
-  hipLaunchKernelGGL(pq::k_pg_pass<0>, dim3(ngroups), dim3(pq::QT), 0, str, *lr, *pb, *st, rec, *s, gdates, urows,
-                     ucnt, uoff, umax);
+  const dim3 gsplit(ngroups * pq::QS);
+  hipLaunchKernelGGL(pq::k_pg_passA<0>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
+                     umax, pass_scratch);
+  hipLaunchKernelGGL(pq::k_pg_passB<0>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
+                     umax, pass_scratch);
+  hipLaunchKernelGGL(pq::k_pg_post<0>, dim3(B), dim3(64), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
+                     pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
   // one wave per date, the LDS triangle sized to the free set (more dates per CU when small)
   hipLaunchKernelGGL(pq::k_pg_solve<48>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 0);
@@ -978,8 +1070,12 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 64);
   if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 80);
   if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 96);
-  hipLaunchKernelGGL(pq::k_pg_pass<1>, dim3(ngroups), dim3(pq::QT), 0, str, *lr, *pb, *st, rec, *s, gdates, urows,
-                     ucnt, uoff, umax);
+  hipLaunchKernelGGL(pq::k_pg_passA<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
+                     umax, pass_scratch);
+  hipLaunchKernelGGL(pq::k_pg_passB<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
+                     umax, pass_scratch);
+  hipLaunchKernelGGL(pq::k_pg_post<1>, dim3(B), dim3(64), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
+                     pass_scratch);
   PQ_CHECK_LAUNCH("pq_polish_grouped_round");
   return 0;
 }

@@ -144,14 +144,19 @@ class QPBatch:
             ub=None if self.ub is None else self.ub.data_ptr(), box_stride=bs)
 
     @classmethod
-    def from_dense(cls, P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, device=None):
+    def from_dense(cls, P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, device=None, n=None):
         """Build from host arrays: P (B,n,n), q (B,n); A (me,n)|(B,me,n), b; G, h; lb, ub
-        ((n,) shared or (B,n)).  Equality rows are stored first (lg == ug)."""
-        P = np.asarray(P, dtype=np.float64)
-        if P.ndim == 2:
-            P = P[None]
-        B, n, _ = P.shape
-        q = np.asarray(q, dtype=np.float64).reshape(B, n)
+        ((n,) shared or (B,n)).  Equality rows are stored first (lg == ug).  P = None (with
+        ``n``): constraints only -- one problem, P left None and q zero, for callers that set
+        the objective on the device afterwards (no n x n host array or upload)."""
+        if P is None:
+            B, n = 1, int(n)
+        else:
+            P = np.asarray(P, dtype=np.float64)
+            if P.ndim == 2:
+                P = P[None]
+            B, n, _ = P.shape
+            q = np.asarray(q, dtype=np.float64).reshape(B, n)
 
         def per(M, rows):
             if M is None:
@@ -181,7 +186,8 @@ class QPBatch:
         if shared and ((lb_ is not None and lb_.ndim == 2) or (ub_ is not None and ub_.ndim == 2)):
             shared = False
         has_box = lb_ is not None or ub_ is not None
-        self = cls(n, B, me + mi, device=device, shared_constraints=shared, has_box=has_box)
+        self = cls(n, B, me + mi, device=device, shared_constraints=shared, has_box=has_box,
+                   P=None if P is not None else torch.empty(0, dtype=F64))
         nc = 1 if shared else B
         ld = self.ld
         Cg = np.zeros((nc, max(me + mi, 1), ld))
@@ -199,12 +205,15 @@ class QPBatch:
             Cg[:, me:me + mi, :n] = Gb
             ug[:, me:me + mi] = hb
         dev = self.device
-        Pp = np.zeros((B, ld, ld))
-        Pp[:, :n, :n] = P
-        self.P = torch.from_numpy(Pp).to(dev)
-        qp = np.zeros((B, ld))
-        qp[:, :n] = q
-        self.q = torch.from_numpy(qp).to(dev)
+        if P is None:
+            self.P = None
+        else:
+            Pp = np.zeros((B, ld, ld))
+            Pp[:, :n, :n] = P
+            self.P = torch.from_numpy(Pp).to(dev)
+            qp = np.zeros((B, ld))
+            qp[:, :n] = q
+            self.q = torch.from_numpy(qp).to(dev)
         self.Cg = torch.from_numpy(Cg).to(dev)
         self.lg = torch.from_numpy(lg).to(dev)
         self.ug = torch.from_numpy(ug).to(dev)
@@ -772,9 +781,13 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         rp = rec.data_ptr()
         g = groups
         _lib.check(lib.pq_polish_grouped_init(L_, P_, S_, rp, SS_main, strm), "pq_polish_grouped_init")
+        scr = getattr(ws, "_pg_pass", None)
+        if scr is None or scr.numel() < g.ngroups * _lib.PQ_PG_PASS_SCRATCH:
+            scr = torch.empty(g.ngroups * _lib.PQ_PG_PASS_SCRATCH, dtype=F64, device=dev)
+            ws._pg_pass = scr
         for r in range(int(s.polish_rounds)):
             _lib.check(lib.pq_polish_grouped_round(L_, P_, S_, rp, ldk, _ptr(g.gdates), g.ngroups, _ptr(g.urows),
-                                                   _ptr(g.ucnt), _ptr(g.uoff), g.umax, SS_main, strm),
+                                                   _ptr(g.ucnt), _ptr(g.uoff), g.umax, SS_main, scr.data_ptr(), strm),
                        "pq_polish_grouped_round")
             if r >= 1 and not bool((rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_PENDING).any()):   # host sync
                 break
@@ -839,20 +852,19 @@ def window_rows(dates: np.ndarray, rebdates, width: int):
     reb = np.asarray(rebdates, dtype="datetime64[D]")
     ends = np.searchsorted(dates, reb, side="right")
     starts = np.maximum(0, ends - int(width))
-    wd = (dates.astype("int64") + 3) % 7
-    weekday = wd < 5
-    lists = []
-    for s, e in zip(starts, ends):
-        r = np.arange(s, e, dtype=np.int32)
-        if not weekday[s:e].all():
-            r = r[weekday[s:e]]
-        lists.append(r)
-    tmax = max(1, max(len(r) for r in lists)) if lists else 1
-    rows = np.zeros((len(lists), tmax), dtype=np.int32)
-    tlen = np.zeros(len(lists), dtype=np.int32)
-    for i, r in enumerate(lists):
-        rows[i, :len(r)] = r
-        tlen[i] = len(r)
+    B = len(ends)
+    weekday = (dates.astype("int64") + 3) % 7 < 5
+    # the weekdays of [s, e) are the positions wpos[cw[s] .. cw[e]) (prefix counts)
+    wpos = np.flatnonzero(weekday).astype(np.int32)
+    cw = np.concatenate([[0], np.cumsum(weekday)]).astype(np.int64)
+    first = cw[starts]
+    tlen = (cw[ends] - first).astype(np.int32)
+    tmax = max(1, int(tlen.max())) if B else 1
+    if not len(wpos):
+        return np.zeros((B, tmax), dtype=np.int32), tlen
+    j = np.arange(tmax, dtype=np.int64)[None, :]
+    rows = np.take(wpos, first[:, None] + j, mode="clip")
+    rows[j >= tlen[:, None]] = 0
     return rows, tlen
 
 
@@ -869,26 +881,29 @@ def slide_plan(rows, tlen, group: int = 32, smax: int = 64, smin: int = 1):
     B, tmax = rows.shape
     shift = np.zeros(B, dtype=np.int32)
     if B > 1:
-        col = np.arange(tmax)[None, :]
+        col = np.arange(tmax)
         prev, cur = rows[:-1], rows[1:]
         tp, tc = tlen[:-1], tlen[1:]
-        s = ((prev < cur[:, :1]) & (col < tp[:, None])).sum(1)
-        gathered = np.take_along_axis(prev, np.minimum(col + s[:, None], tmax - 1), axis=1)
-        match = np.where(col < (tc - s)[:, None], gathered == cur, True).all(1)
-        good = (tp == tc) & (tc > 1) & match & (s >= smin) & (s <= smax)
+        # s = #rows of the previous window before the current window's first row; only
+        # s <= smax can join, so the first smax + 1 columns decide it
+        h = min(tmax, int(smax) + 1)
+        s = ((prev[:, :h] < cur[:, :1]) & (col[None, :h] < tp[:, None])).sum(1)
+        cand = (tp == tc) & (tc > 1) & (s >= smin) & (s <= smax)
+        match = np.zeros(B - 1, dtype=bool)
+        for sv in np.unique(s[cand]).tolist():   # rows[d][:T-s] == rows[d-1][s:T], per shift value
+            w = tmax - sv
+            ok = ((prev[:, sv:] == cur[:, :w]) | (col[None, :w] >= (tc - sv)[:, None])).all(1)
+            match |= cand & (s == sv) & ok
+        good = cand & match
         shift[1:] = np.where(good, s, 0)
     else:
         good = np.zeros(0, dtype=bool)
     joins = np.concatenate([[False], good])
-    gstart = []
-    cnt = 0
-    for d in range(B):
-        if not joins[d] or cnt == group:
-            gstart.append(d)
-            cnt = 0
-        cnt += 1
-    gstart.append(B)
-    return np.asarray(gstart, dtype=np.int32), shift
+    # runs of joined dates, cut every ``group`` dates: d starts a group when it does not
+    # join its predecessor or sits at a multiple of ``group`` inside its run
+    run_start = np.maximum.accumulate(np.where(~joins, np.arange(B), 0)) if B else np.zeros(0, np.int64)
+    starts = np.flatnonzero((np.arange(B) - run_start) % max(int(group), 1) == 0)
+    return np.concatenate([starts, [B]]).astype(np.int32), shift
 
 
 class SlidePlan:
@@ -925,14 +940,15 @@ class GroupPlan:
         self.ok = B > 0 and int(tlen.min()) >= 2 and int(tlen.max()) <= umax
         gs, sh = slide_plan(rows, tlen, group=gmax, smax=smax, smin=0)
         groups = []
-        for a, b in zip(gs[:-1], gs[1:]):
-            start, U = a, int(tlen[a])
+        tl_l, sh_l = tlen.tolist(), sh.tolist()
+        for a, b in zip(gs[:-1].tolist(), gs[1:].tolist()):
+            start, U = a, tl_l[a]
             for d in range(a + 1, b):
-                if U + int(sh[d]) > umax:
+                if U + sh_l[d] > umax:
                     groups.append((start, d))
-                    start, U = d, int(tlen[d])
+                    start, U = d, tl_l[d]
                 else:
-                    U += int(sh[d])
+                    U += sh_l[d]
             groups.append((start, b))
         if breaks is not None:
             brk = np.flatnonzero(np.asarray(breaks, dtype=bool))
@@ -947,25 +963,42 @@ class GroupPlan:
         urows = np.zeros((max(1, self.ngroups), umax), dtype=np.int32)
         ucnt = np.zeros(max(1, self.ngroups), dtype=np.int32)
         uoff = np.zeros(B, dtype=np.int32)
-        for gi, (a, b) in enumerate(groups):
-            u = [rows[a, :tlen[a]]]
-            off = 0
-            for d in range(a + 1, b):
-                s = int(sh[d])
-                off += s
-                uoff[d] = off
-                u.append(rows[d, tlen[d] - s:tlen[d]])
-            u = np.concatenate(u)
-            if len(u) > umax:
+        if B and self.ngroups:
+            # a group's union = its first window, then the rows each later date adds (its last
+            # sh[d] window rows); every (date, column) entry gathered at once
+            sizes = np.diff(gdates)
+            gof = np.repeat(np.arange(self.ngroups), sizes)                 # group of each date
+            isfirst = np.zeros(B, dtype=bool)
+            isfirst[gdates[:-1]] = True
+            shd = np.where(isfirst, 0, sh).astype(np.int64)
+            cnt = np.where(isfirst, tlen, shd).astype(np.int64)             # entries per date
+            col0 = np.where(isfirst, 0, tlen - shd)
+            cum = np.cumsum(shd)
+            uoff[:] = cum - cum[gdates[:-1]][gof]                           # sum of shifts since the group start
+            estart = np.concatenate([[0], np.cumsum(cnt)])
+            tot = int(estart[-1])
+            dte = np.repeat(np.arange(B), cnt)
+            k = np.arange(tot) - estart[dte]
+            vals = rows[dte, col0[dte] + k]
+            gstart_e = estart[gdates[:-1]]                                  # first entry of each group
+            pos = np.arange(tot) - gstart_e[gof[dte]]
+            cnts = np.add.reduceat(cnt, gdates[:-1]) if self.ngroups else np.zeros(0, np.int64)
+            over = cnts > umax
+            if over.any():
                 self.ok = False
-                continue
-            urows[gi, :len(u)] = u
-            ucnt[gi] = len(u)
+            keep = ~over[gof[dte]]
+            urows[gof[dte][keep], pos[keep]] = vals[keep]
+            ucnt[:] = np.where(over, 0, cnts)
         self.sizes = np.diff(gdates)
         gidx = np.repeat(np.arange(max(self.ngroups, 0), dtype=np.int32), self.sizes) if B else np.zeros(0, np.int32)
         # widest union span in panel rows (the band Gram must cover it for the group capacitance)
-        self.span_max = int(max((urows[g, :ucnt[g]].max() - urows[g, :ucnt[g]].min() + 1)
-                                for g in range(self.ngroups) if ucnt[g] > 0)) if self.ngroups else 0
+        if self.ngroups and ucnt.max() > 0:
+            valid = np.arange(umax)[None, :] < ucnt[:, None]
+            hi = np.where(valid, urows, np.iinfo(np.int32).min).max(1)
+            lo = np.where(valid, urows, np.iinfo(np.int32).max).min(1)
+            self.span_max = int((hi - lo + 1)[ucnt > 0].max())
+        else:
+            self.span_max = 0
         self.ucnt_max = int(ucnt.max()) if self.ngroups else 0
         # rank of the Woodbury correction of a date: union rows outside its window + the mean
         self.corr_max = int((ucnt[gidx] - tlen).max()) + 1 if B else 1

@@ -8,14 +8,19 @@ problem of a single batch, date-major: all problems of a date share its window r
 the grouped low-rank ADMM (engine.GroupPlan with identical windows) streams those rows
 once per iteration for up to 16 risk aversions.  Nothing n x n is formed.
 
-Factor once per date (``factor='eig'``, the default; SURVEY.md §8(e) "keep all lambda of a
-date on one rank so the factorisation is shared"): the capacitance of problem (d, lam) is
+Factor once per date (``factor='eig'``; SURVEY.md §8(e) "keep all lambda of a date on one
+rank so the factorisation is shared"): the capacitance of problem (d, lam) is
 M = I + (2 lam w / c) Xc_d Xc_d' + border rows, so one symmetric eigendecomposition of the
 date's T x T window Gram diagonalises M for EVERY lam and every rho
 (engine.EigCap / pq_eigcap_form): each problem keeps its own |q|-aware rho and its adaptive
 rho updates, and its M^-1 is formed from the shared eigenvectors by one MFMA tile product
 instead of a Cholesky factorisation per problem.  ``factor='chol'`` keeps the per-problem
-factorisation (rounds 1-2).  A round-2 attempt that instead rescaled every problem of a date
+factorisation (rounds 1-2).  Measured at the config-5 shape (profiles/r02g_*, tools/exp_eigh.py):
+the 64 eigendecompositions cost 10.4 ms (rocSOLVER syevd, strided-batched; its Jacobi variant
+71 ms) + 3.7 ms of forming, the 4096 batched Choleskys 8.2 ms -- 2.0 us per problem against
+190 us per date + 0.9 us per problem, so ``factor='auto'`` (the default) takes the eigen form
+from EIG_MIN_PER_DATE risk aversions per date (and whenever the windows are not all full, the
+Cholesky form).  A round-2 attempt that instead rescaled every problem of a date
 to P = 2 Sigma_d, q = -mu_d / lam (one capacitance per slide group) had to share one rho
 per group and left the nearly linear problems (lam <= 0.13) on 4000-iteration ADMM tails:
 102 QPs/s against 12.7k -- the eigen form needs no shared rho.
@@ -27,17 +32,19 @@ import torch
 
 from . import engine
 
+EIG_MIN_PER_DATE = 192   # factor='auto': eigen form from this many problems per date
+
 
 def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0, budget=1.0,
                         geometric=True, settings: engine.Settings | None = None, group=True,
-                        factor: str = "eig", gmax: int = engine.GROUP_MAX_DATES,
+                        factor: str = "auto", gmax: int = engine.GROUP_MAX_DATES,
                         events: list | None = None):
     """Solve min lam x'Sigma_d x - mu_d'x  s.t. 1'x = budget, lb <= x <= ub for every
     rebalance window (rows, tlen: host arrays of engine.window_rows) and every lam.
 
     Returns (BatchResult, meta): problem p = d * len(lambdas) + j is (date d, lambdas[j])."""
-    if factor not in ("eig", "chol"):
-        raise ValueError("mean_variance_sweep: factor must be 'eig' or 'chol'")
+    if factor not in ("auto", "eig", "chol"):
+        raise ValueError("mean_variance_sweep: factor must be 'auto', 'eig' or 'chol'")
     rows = np.asarray(rows, dtype=np.int32)
     tlen = np.asarray(tlen, dtype=np.int32)
     lam = np.asarray(lambdas, dtype=np.float64).reshape(-1)
@@ -65,6 +72,8 @@ def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0
     lr = engine.LowRank(panel, rp_d, tp_d, mu=mu_p, w_scale=1.0 / (tp_d.to(torch.float64) - 1.0))
     eig = None
     full = bool((tlen == rows.shape[1]).all())
+    if factor == "auto":
+        factor = "eig" if L >= EIG_MIN_PER_DATE else "chol"
     if factor == "eig" and full and engine.lowrank_shape_ok(n, rows.shape[1], qb.mg):
         k_ld = engine.round_up(rows.shape[1] + qb.mg, 64)
         pdate = torch.arange(nd, dtype=torch.int32, device=dev).repeat_interleave(L)

@@ -91,7 +91,7 @@ def stage_ms(events):
     return {k: round(v, 3) for k, v in out.items()}
 
 
-def config5(steps, dev, settings=None, factor="eig"):
+def config5(steps, dev, settings=None, factor="auto"):
     n, T, nd, L = 5000, 252, 64, 64
     dates, R, _, _ = factor_panel(T - 1 + 21 * nd, n)
     ends = np.arange(T - 1, T - 1 + 21 * nd, 21)
@@ -153,7 +153,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--dates", type=int, default=9749, help="config 4 rebalance dates")
     ap.add_argument("--only", choices=["12", "4", "5"], default=None)
-    ap.add_argument("--factor", default="eig", help="config 5 capacitance factor(s): eig, chol or eig,chol")
+    ap.add_argument("--factor", default="auto", help="config 5 capacitance factor(s): auto, eig, chol or eig,chol")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="engine.Settings override for config 5 (experiments)")
     args = ap.parse_args()

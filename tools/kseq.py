@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Per-dispatch kernel timeline of one bench step from a rocprofv3 kernel trace:
+python tools/kseq.py <run_kernel_trace.csv> [step index, default 1] [name prefix filter]"""
+import collections
+import csv
+import sys
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    step = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    pref = sys.argv[3] if len(sys.argv) > 3 else "k_"
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    seq = []
+    for r in rows:
+        k = r["Kernel_Name"]
+        for pre in ("void pq::", "pq::(anonymous namespace)::", "pq::"):
+            if k.startswith(pre):
+                k = k[len(pre):].split("(")[0]
+                seq.append((k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+                break
+    starts = [i for i, (k, _) in enumerate(seq) if k.startswith("k_window_moments_grp")]
+    i0 = starts[step]
+    i1 = starts[step + 1] if len(starts) > step + 1 else len(seq)
+    tot = collections.defaultdict(float)
+    for k, d in seq[i0:i1]:
+        if k.startswith(pref):
+            print(f"{k:40s} {d:9.1f} us")
+        tot[k.split("<")[0]] += d
+    print("--- totals per kernel (us)")
+    for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
+        print(f"{k:40s} {v:9.1f}")
+
+
+if __name__ == "__main__":
+    main()
