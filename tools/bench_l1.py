@@ -15,9 +15,16 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from porqua_amd import engine  # noqa: E402
+from porqua_amd import _lib, engine  # noqa: E402
 from porqua_amd.l1split import L1Split, merge_batch, split_batch  # noqa: E402
 from porqua_amd.synthetic import factor_panel  # noqa: E402
+
+
+def stage_ms(events):
+    out = {}
+    for name, e0, e1 in events:
+        out[name] = round(out.get(name, 0.0) + e0.elapsed_time(e1), 3)
+    return out
 
 
 def main():
@@ -52,12 +59,15 @@ def main():
     split_panel = engine.Panel(torch.cat([pan.R, -pan.R], 1).contiguous(), None, device=dev)
     from porqua_amd.l1split import split_settings
     ov = dict(kv.split("=", 1) for kv in args.set)
-    settings = split_settings(engine.Settings.from_params(ov), ov)
+    settings = split_settings(engine.Settings.from_params(ov), ov, term.kind)
+
+    ev = []
 
     def step():
+        ev.clear()
         qb2, lr2, const = split_batch(qb, lr, term, split_panel, np.ones((1, n)), np.ones(1), None, None,
                                       np.zeros(n), np.ones(n))
-        res = engine.solve_lowrank(qb2, lr2, settings, groups=gplan)
+        res = engine.solve_lowrank(qb2, lr2, settings, groups=gplan, events=ev)
         return res, merge_batch(res.x, term)
 
     step()
@@ -76,7 +86,10 @@ def main():
                       "mean_iters": float(res.iters.float().mean().item()),
                       "max_budget_violation": float(np.abs(xh.sum(1) - 1).max()),
                       "mean_turnover": float(np.abs(xh - x0[None, :]).sum(1).mean()),
-                      "settings_overrides": args.set}))
+                      "max_iters": int(res.iters.max().item()), "refactors": res.refactors,
+                      "admm_launches": res.admm_launches, "capacitance": res.capacitance,
+                      "polish_rounds_mean": float(res.out[:, _lib.PQ_OUT_ROUNDS].mean().item()),
+                      "stage_ms": stage_ms(ev), "settings_overrides": args.set}))
 
 
 def both(args):
