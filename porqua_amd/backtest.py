@@ -410,7 +410,7 @@ class Backtest:
             elif l1term is not None:   # one turnover term: the signed split (porqua_amd/l1split.py)
                 qb2, lr2, const = split_batch(qb, stage.lowrank, l1term, split_panel, GhAb["A"], GhAb["b"],
                                               GhAb["G"], GhAb["h"], lb, ub)
-                s_split = split_settings(settings, opt.params)
+                s_split = split_settings(settings, opt.params, l1term.kind)
                 if lr2 is not None:
                     res = engine.solve_lowrank(qb2, lr2, s_split, groups=stage.group_plan())
                 else:

@@ -105,15 +105,24 @@ def merge_solution(w: np.ndarray, term: L1Split) -> tuple[np.ndarray, np.ndarray
 # 177 vs 190), while the plain problems are fastest at 1.6 -- so only split solves use it,
 # and only when the caller did not set alpha
 SPLIT_ALPHA = 1.8
+# initial rho of the budget (turnover / leverage constraint) splits, relative to mean diag P:
+# measured on config 3 + turnover budget 0.5 (tools/bench_l1.py, profiles/r02h_bench_l1.log)
+# 4 -> 168 mean / 1093 max ADMM iterations, 5.6k QPs/s; 16 -> 35 / 397, 12.9k; 32 -> 25 / 537,
+# 9.6k (the grouped kernel runs each slide group to its slowest date, so the tail decides)
+SPLIT_BUDGET_RHO0_REL = 16.0
 
 
-def split_settings(settings, params):
-    """Settings for a split solve: ``settings`` with alpha = SPLIT_ALPHA unless ``params``
-    sets it."""
+def split_settings(settings, params, kind: str = "cost"):
+    """Settings for a split solve: ``settings`` with alpha = SPLIT_ALPHA (and, for a budget
+    term, rho0_rel = SPLIT_BUDGET_RHO0_REL) unless ``params`` sets them."""
     import dataclasses
-    if params is not None and any(k in params for k in ("alpha", "admm_alpha")):
-        return settings
-    return dataclasses.replace(settings, alpha=SPLIT_ALPHA)
+    params = params or {}
+    upd = {}
+    if not any(k in params for k in ("alpha", "admm_alpha")):
+        upd["alpha"] = SPLIT_ALPHA
+    if kind == "budget" and not any(k in params for k in ("rho0_rel", "admm_rho0_rel")):
+        upd["rho0_rel"] = SPLIT_BUDGET_RHO0_REL
+    return dataclasses.replace(settings, **upd) if upd else settings
 
 
 def term_from_model(constraints, params, universe):
@@ -190,8 +199,8 @@ def split_batch(qb, lowrank, term: L1Split, split_panel, A, b, G, h, lb, ub):
     const = 0.5 * xpx + q @ x0
     base = dict(P=np.zeros((n, n)), q=np.zeros(n), A=A, b=b, G=G, h=h, lb=lb, ub=ub)
     sp = split_problem(base, term)
-    qb2 = engine.QPBatch.from_dense(np.zeros((1, 2 * n, 2 * n)), np.zeros((1, 2 * n)), A=sp["A"], b=sp["b"],
-                                    G=sp["G"], h=sp["h"], lb=sp["lb"], ub=sp["ub"], device=dev)
+    qb2 = engine.QPBatch.from_dense(None, None, n=2 * n, A=sp["A"], b=sp["b"], G=sp["G"], h=sp["h"], lb=sp["lb"],
+                                    ub=sp["ub"], device=dev)
     qb2.batch = B
     c = term.value if term.kind == "cost" else 0.0
     q2 = torch.zeros((B, qb2.ld), dtype=F64, device=dev)

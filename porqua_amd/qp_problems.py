@@ -161,7 +161,7 @@ class QuadraticProgram(dict):
         from . import engine
         from .l1split import split_settings
         sol = solve_batch([sub], settings=split_settings(engine.Settings.from_params(self["params"]),
-                                                         self["params"]))[0]
+                                                         self["params"], term.kind))[0]
         if sol.x is not None:
             x, aux = merge_solution(sol.x, term)
             sol.x = np.concatenate([x, aux])
