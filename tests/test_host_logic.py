@@ -297,3 +297,63 @@ def test_kkt_certificate_accepts_oracle_and_rejects_perturbed():
     k2 = kkt_residuals(P, q, xp, A=np.ones((1, n)), b=np.ones(1), G=G, h=h, lb=np.zeros(n),
                        ub=np.full(n, 0.2), y=y, z_box=o.z_box)
     assert max(k2.values()) > 1e-7
+
+
+def _loop_slide_plan(rows, tlen, group, smax, smin):
+    """Direct restatement of engine.slide_plan's contract: d joins d-1 when its window is
+    that window shifted by smin <= s <= smax rows (same length), groups of <= ``group``."""
+    B = len(tlen)
+    shift = np.zeros(B, dtype=np.int32)
+    gs = [0] if B else []
+    cnt = 1
+    for d in range(1, B):
+        tp, tc = int(tlen[d - 1]), int(tlen[d])
+        prev, cur = rows[d - 1, :tp], rows[d, :tc]
+        s = int((prev < cur[0]).sum()) if tc else 0
+        ok = tp == tc and tc > 1 and smin <= s <= smax and np.array_equal(prev[s:], cur[:tc - s])
+        if ok:
+            shift[d] = s
+        if not ok or cnt == group:
+            gs.append(d)
+            cnt = 0
+        cnt += 1
+    gs.append(B)
+    return np.asarray(gs, dtype=np.int32), shift
+
+
+def test_planners_match_their_contracts_on_random_calendars():
+    """window_rows (vs the oracle's per-date restatement of src/builders.py:208-211),
+    slide_plan (vs a per-date loop) and GroupPlan (every date's window is its union slice
+    [uoff, uoff + T), unions within umax) on calendars with weekends, gaps, repeated
+    rebalance dates and short histories."""
+    import torch
+    rng = np.random.default_rng(11)
+    for trial in range(30):
+        n = int(rng.integers(30, 1500))
+        cal = np.arange(np.datetime64("2003-01-01"), np.datetime64("2003-01-01") + n)
+        if trial % 3:
+            cal = cal[((cal.astype("int64") + 3) % 7) < 5]
+        if trial % 2:
+            cal = cal[rng.random(len(cal)) < 0.93]
+        if len(cal) < 3:
+            continue
+        T = int(rng.integers(2, 120))
+        reb = cal[int(rng.integers(0, min(len(cal) - 1, T + 3))):][::int(rng.choice([1, 1, 3, 21]))]
+        if trial % 4 == 0:
+            reb = np.repeat(reb, int(rng.integers(1, 4)))
+        rows, tlen = engine.window_rows(cal, reb, T)
+        for b in range(0, len(reb), max(1, len(reb) // 17)):
+            assert np.array_equal(rows[b, :tlen[b]], rp.window_rows(cal, reb[b], T))
+        for group, smax, smin in ((32, 64, 1), (16, 64, 0), (3, 5, 0)):
+            gs, sh = engine.slide_plan(rows, tlen, group, smax, smin)
+            gs2, sh2 = _loop_slide_plan(rows, tlen, group, smax, smin)
+            assert np.array_equal(gs, gs2) and np.array_equal(sh, sh2)
+        gp = engine.GroupPlan(rows, tlen, torch.device("cpu"), gmax=16, gmin=16)
+        if not gp.ok:
+            continue
+        gd, ur, uc, uo = (gp.gdates.numpy(), gp.urows.numpy(), gp.ucnt.numpy(), gp.uoff.numpy())
+        assert gd[0] == 0 and gd[-1] == len(tlen) and (np.diff(gd) >= 1).all() and (uc <= gp.umax).all()
+        for g in range(gp.ngroups):
+            for d in range(gd[g], gd[g + 1]):
+                t = int(tlen[d])
+                assert np.array_equal(ur[g, uo[d]:uo[d] + t], rows[d, :t])
