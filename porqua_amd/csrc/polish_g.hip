@@ -173,7 +173,11 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     k += wcnt[ww];
   }
   const int ma = s_al[PG_MGMAX];
-  if (k == 0 || k > kmax || ma > PG_MGMAX) {   // uniform: the per-date kernel takes it
+  // every variable at a bound (a vertex, e.g. nearly linear objectives): x = x_B, and the
+  // multiplier of at most one active equality row is chosen in the post from the dual
+  // feasibility interval of the bound variables (k_pg_post); otherwise the per-date kernel
+  const bool vertex_ok = ma == 0 || (ma == 1 && lg[s_al[0]] == ug[s_al[0]]);
+  if ((k == 0 && !vertex_ok) || k > kmax || ma > PG_MGMAX) {   // uniform
     if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
@@ -190,6 +194,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     const int f = wk.fl[i];
     const double v = i < n ? (f == 1 ? lb[i] : (f == 2 ? ub[i] : 0.0)) : 0.0;
     wk.xb[i] = v;
+    if (k == 0) wk.xs[i] = v;
     nzb |= (v != 0.0);
   }
   nzb = block_or(nzb, red);   // barrier: Fl complete below
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   const double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING) return;
   const int k = (int)R[R_K];
-  if (k > PG_KMAX) return;
+  if (k > PG_KMAX || k == 0) return;
   const int ld = pb.ld;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   PGWork wk(st, b, ld);
@@ -929,13 +934,37 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
   const double sc = R[R_SC];
   const double dtol = s.dual_tol * sc;
   const double ptol = 1e-12;
+  // vertex (k == 0, set up with at most one active equality row r0): its multiplier is the
+  // middle of the interval in which every bound variable's multiplier has the right sign,
+  //   at lb: g0_i + lam c_i >= 0,  at ub: g0_i + lam c_i <= 0   (g0 = P x + q)
+  // (an empty interval leaves violations for the checks below, as any wrong active set)
+  const bool vtx = R[R_K] == 0.0 && R[R_MA] == 1.0;
+  const int r0 = vtx ? (int)R[R_AL] : -1;
+  double lam0 = 0.0;
+  if (vtx) {
+    const double* c0 = Cg + (int64_t)r0 * ld;
+    double lo = -INFINITY, hi = INFINITY;
+    for (int i = hl; i < n; i += 64) {
+      const int f = wk.fl[i];
+      const double c = c0[i];
+      if (f == 0 || c == 0.0 || (has_box && lb[i] == ub[i])) continue;
+      const double pxi = ps * (wsc * (wk.g[i] - (mu ? mu[i] * su : 0.0))) + pd * wk.xs[i];
+      const double bnd = -(pxi + q[i]) / c;
+      if ((f == 1) == (c > 0.0)) lo = fmax(lo, bnd);
+      else hi = fmin(hi, bnd);
+    }
+    lo = wave_max(lo);
+    hi = -wave_max(-hi);
+    lam0 = (isfinite(lo) && isfinite(hi)) ? 0.5 * (lo + hi) : (isfinite(lo) ? lo : (isfinite(hi) ? hi : 0.0));
+  }
+  auto lamof = [&](int r) -> double { return r == r0 ? lam0 : R[R_LAM + r]; };
   // exact P x and gradient g = P x + q + Cg' lam; box checks
   int bad = 0;
   for (int i = hl; i < n; i += 64) {
     const double xi = wk.xs[i];
     const double pxi = ps * (wsc * (wk.g[i] - (mu ? mu[i] * su : 0.0))) + pd * xi;
     double gi = pxi + q[i];
-    for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * R[R_LAM + r];
+    for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * lamof(r);
     wk.Px[i] = pxi;
     wk.g[i] = gi;
     const int f = wk.fl[i];
@@ -954,7 +983,7 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
     if (hl == 0) {
       if (lg[r] != ug[r]) {
         const int a = (int)R[R_ACT + r];
-        const double lam = R[R_LAM + r];
+        const double lam = lamof(r);
         if (a == 0 && sum > ug[r] + ptol * (1.0 + fabs(ug[r]))) { R[R_ACT + r] = 2; bad = 1; }
         else if (a == 0 && sum < lg[r] - ptol * (1.0 + fabs(lg[r]))) { R[R_ACT + r] = 1; bad = 1; }
         else if (a == 2 && lam < -dtol) { R[R_ACT + r] = 0; bad = 1; }
@@ -965,6 +994,10 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
     }
   }
   bad = wave_max((double)bad) > 0.5;
+  if (vtx && hl == 0) {   // the next round starts from it (setup's R_SOL), or the scoring uses it
+    R[R_LAM + r0] = lam0;
+    R[R_SOL] = lam0;
+  }
   if (bad) {
     if (hl == 0 && R[R_ROUNDS] >= s.polish_rounds) R[R_STATE] = PQ_PG_FALLBACK;
     return;
@@ -993,7 +1026,7 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
     double sum = 0.0;
     for (int j = hl; j < n; j += 64) sum += cr[j] * wk.xs[j];
     sum = wave_sum(sum);
-    const double lam = R[R_LAM + r];
+    const double lam = lamof(r);
     double v;
     if (lg[r] == ug[r]) v = fabs(sum - ug[r]);
     else v = fmax(isinf(ug[r]) ? 0.0 : sum - ug[r], isinf(lg[r]) ? 0.0 : lg[r] - sum);

@@ -306,6 +306,7 @@ class BatchResult:
     out: torch.Tensor        # (B, PQ_OUT_FIELDS)
     refactors: int = 0
     admm_launches: int = 0
+    polish_fallbacks: int = 0   # dates the grouped polish handed to the per-date kernel
     capacitance: str = ""    # window path: "band" (pq_lr_capacitance_band), "group", "eig" or "direct"
 
     @property
@@ -353,7 +354,7 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
     _rho_floor_q(qb, ws, settings or Settings())
     _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, None, 0, SS, 1, strm)),
                "pq_factor_batched")
-    cnt = {"refactors": 0, "launches": 0}
+    cnt = {"refactors": 0, "launches": 0, "pg_fallback": 0}
 
     def admm_rounds(idx, nidx, SSx):
         for _ in range(max_rounds):
@@ -793,7 +794,9 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                 break
         fb = torch.nonzero(rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_FALLBACK).flatten().to(torch.int32)
         m = int(fb.numel())
+        cnt["pg_fallback"] = m
         if m:
+            ws.pg_fallback = fb   # the dates handed to the per-date kernel (diagnostics)
             polish_w(fb.contiguous(), m, name="polish (fallback, inside polish)")
 
     admm_rounds(None, 0, SS)
@@ -818,7 +821,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
                        status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
-                       admm_launches=launches,
+                       admm_launches=launches, polish_fallbacks=cnt["pg_fallback"],
                        capacitance="group" if gc is not None else ("eig" if eig is not None else
                                                                     ("band" if bd is not None else "direct")))
 

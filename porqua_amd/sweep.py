@@ -38,7 +38,7 @@ EIG_MIN_PER_DATE = 192   # factor='auto': eigen form from this many problems per
 def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0, budget=1.0,
                         geometric=True, settings: engine.Settings | None = None, group=True,
                         factor: str = "auto", gmax: int = engine.GROUP_MAX_DATES,
-                        events: list | None = None):
+                        events: list | None = None, ws: "engine.Workspace | None" = None):
     """Solve min lam x'Sigma_d x - mu_d'x  s.t. 1'x = budget, lb <= x <= ub for every
     rebalance window (rows, tlen: host arrays of engine.window_rows) and every lam.
 
@@ -79,7 +79,7 @@ def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0
         pdate = torch.arange(nd, dtype=torch.int32, device=dev).repeat_interleave(L)
         eig = tl("eig", lambda: engine.EigCap(panel, r_d, t_d, mu_c, qb, pdate, k_ld))
     gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax) if group else None
-    res = engine.solve_lowrank(qb, lr, settings, groups=gp, events=events, eig=eig)
+    res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, events=events, eig=eig)
     meta = {"dates": nd, "lambdas": lam, "grouped": gp is not None and gp.ok,
             "ngroups": None if gp is None else gp.ngroups, "capacitance": res.capacitance,
             "factor": "eig" if eig is not None else "chol",
