@@ -325,10 +325,14 @@ int pq_polish_lr_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* s
  * (ldk/64) 4096), indexed by launch slot (blockIdx: the problem's position in idx[] or
  * its id when idx == NULL).  64 <= ldk <= min(ld, 1024).  A problem whose free set
  * exceeds ldk is left unchanged with out[PQ_OUT_ROUNDS] = -1 unless final_try != 0 (then
- * it is scored at its ADMM point, status PQ_SOLVED_INACCURATE).  Needs lr->dg.          */
+ * it is scored at its ADMM point, status PQ_SOLVED_INACCURATE).  Needs lr->dg.  A free
+ * set beyond ldk is solved in Woodbury form with the T x T capacitance of the free
+ * columns; with band (pq_lr_band_gram's row-band Gram of the panel, rows from r0, pitch
+ * ldo; NULL = none) and every column free, that capacitance is gathered from the band
+ * instead of a T x T x n product.                                                       */
 int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const int32_t* idx,
                         int32_t nidx, const pq_settings* s, int32_t ldk, int32_t final_try,
-                        void* stream);
+                        const double* band, int64_t ldo, int32_t r0, void* stream);
 
 /* K4, grouped pipeline (polish_g.hip): the active-set polish of pq_polish_w_batched as a
  * few throughput kernels per round over every date of a window-path batch -- per-date

@@ -163,6 +163,53 @@ __device__ void form_cwood(const pq_lowrank& lr, int b, int n, const int* fl, in
   __syncthreads();
 }
 
+// The same C from the row-band Gram of the panel (pq_lr_band_gram: band[r - r0][d] =
+// x_r . x_{r-d}) when every column is free: X_F X_F' is then the window's whole Gram, an
+// O(T^2) gather instead of form_cwood's O(T^2 n) product (config 4: n = 3000, every
+// variable free).  Centred windows: Xc Xc' = G - s 1' - 1 s' + (mu.mu) 1 1', s_t = x_t . mu.
+__device__ void form_cwood_band(const pq_lowrank& lr, int b, int n, int nbt, double cdiag, double* Ks,
+                                int64_t ldk, const double* band, int64_t ldo, int r0, double* sx, double* red) {
+  const int T = lr.tlen[b];
+  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  double mm = 0.0;
+  if (mu) {
+    for (int i = w; i < T; i += PW) {
+      const double* row = lr.panel + (int64_t)rws[i] * lr.ldp;
+      double a = 0.0;
+      for (int c = l; c < n; c += 64) a = fma(row[c], mu[c], a);
+      a = wave_sum(a);
+      if (l == 0) sx[i] = a;
+    }
+    double a = 0.0;
+    for (int c = t; c < n; c += PT) a = fma(mu[c], mu[c], a);
+    mm = block_sum(a, red);   // barrier: sx complete
+  }
+  const int ntile = nbt * (nbt + 1) / 2;
+  for (int tile = 0; tile < ntile; ++tile) {
+    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+    while (I * (I + 1) / 2 > tile) --I;
+    const int J = tile - I * (I + 1) / 2;
+    for (int e = t; e < TB * TB; e += PT) {
+      const int gi = I * TB + (e >> 6), gj = J * TB + (e & 63);
+      double v;
+      if (gi < T && gj < T) {
+        const int ri = rws[gi], rj = rws[gj];
+        const int hi = ri > rj ? ri : rj;
+        v = band[(int64_t)(hi - r0) * ldo + (ri > rj ? ri - rj : rj - ri)];
+        if (mu) v += mm - sx[gi] - sx[gj];
+        if (gi == gj) v += cdiag;
+      } else {
+        v = gi == gj ? 1.0 : 0.0;
+      }
+      Ks[(int64_t)gi * ldk + gj] = v;
+    }
+  }
+  __syncthreads();
+}
+
 struct FormRead {   // the lower tiles (diagonal tiles in full) as written
   const double* K;
   int64_t ld;
@@ -285,7 +332,7 @@ __device__ void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k
 
 __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, pq_state st,
                                                  const int32_t* idx, int nidx, pq_settings s, int ldk,
-                                                 int final_try) {
+                                                 int final_try, const double* band, int64_t ldo, int r0) {
   __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS + 2 * KMAX + 15 * 64 + KMAX / 2 + 256];
   double* stg = smem;                  // Cholesky / SYRK stream buffers; S factor; lr_px tree
   double* vec = smem + 4 * STAGE;      // 3 KMAX vectors during refinement; lr_px u
@@ -467,7 +514,8 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       if (t < ma) solL[t] = lamF[Al[t]];
       __syncthreads();
       PQ_STAMP(2);
-      form_cwood(lr, b, n, fl, nbt, dl / psw, K, ldk, smem);
+      if (band && k == n) form_cwood_band(lr, b, n, nbt, dl / psw, K, ldk, band, ldo, r0, smem, red);
+      else form_cwood(lr, b, n, fl, nbt, dl / psw, K, ldk, smem);
       const int info = wg_cholesky(FormRead{K, ldk}, K, ldk, nbt, T, Dt, smem);
       if (info) break;
       PQ_STAMP(3);
@@ -819,7 +867,7 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
 
 extern "C" int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
                                    const int32_t* idx, int32_t nidx, const pq_settings* s, int32_t ldk,
-                                   int32_t final_try, void* stream) {
+                                   int32_t final_try, const double* band, int64_t ldo, int32_t r0, void* stream) {
   PQ_CHECK_ARG(lr && pb && st && s, "pq_polish_w_batched: null argument");
   PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0 && lr->dg,
                "pq_polish_w_batched: window (with its diagonal dg) missing");
@@ -834,7 +882,7 @@ extern "C" int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, p
   const int grid = idx ? nidx : pb->batch;
   if (grid <= 0) return 0;
   hipLaunchKernelGGL(pq::k_polish_w, dim3(grid), dim3(pq::PT), 0, (hipStream_t)stream, *lr, *pb, *st, idx,
-                     nidx, *s, ldk, final_try);
+                     nidx, *s, ldk, final_try, band, ldo, r0);
   PQ_CHECK_LAUNCH("pq_polish_w_batched");
   return 0;
 }

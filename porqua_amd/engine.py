@@ -735,7 +735,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         return lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld, _ptr(idx),
                                       nidx, SS, int(s.max_iter), strm)
 
-    cnt = {"refactors": 0, "launches": 0}
+    cnt = {"refactors": 0, "launches": 0, "pg_fallback": 0}
 
     def admm_rounds(idx, nidx, SSx):
         nonlocal SS
@@ -759,8 +759,9 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         SS = SSp if SSp is not None else SS_main
         kmax = min(qb.ld, 1024)
         final = ldk >= kmax
+        bk = (bd["band"].data_ptr(), bd["ldo"], bd["r0"]) if bd is not None else (None, 0, 0)
         _lib.check(tl(name, lambda: lib.pq_polish_w_batched(L_, P_, S_, _ptr(idx), nidx, SS, ldk, int(final),
-                                                                strm)), "pq_polish_w_batched")
+                                                                *bk, strm)), "pq_polish_w_batched")
         if not final:   # free sets larger than the compact scratch: relaunch those with ldk = kmax
             over = torch.nonzero(ws.out[:, _lib.PQ_OUT_ROUNDS] < 0).flatten().to(torch.int32)
             m = int(over.numel())   # host sync: small vector
@@ -772,7 +773,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                 st2.Dt, st2.Dt_stride = D2.data_ptr(), D2.stride(0)
                 over = over.contiguous()
                 _lib.check(tl(name, lambda: lib.pq_polish_w_batched(L_, P_, ctypes.byref(st2), _ptr(over), m,
-                                                                        SS, kmax, 1, strm)),
+                                                                        SS, kmax, 1, *bk, strm)),
                            "pq_polish_w_batched (relaunch)")
 
     def polish_grouped():
