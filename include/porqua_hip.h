@@ -380,6 +380,14 @@ int pq_simulate_periods(const double* panel, int64_t ldp, int32_t n, const doubl
                         double days_per_year, double* ret, double* wend, int64_t ldwe,
                         double* turnover, int32_t rescale, void* stream);
 
+/* Batched matrix-vector products with the interior-point methods' window matrices
+ * (porqua_amd/ipm_l1.py, the linearised turnover / leverage problem of
+ * src/qp_problems.py:40-157): trans = 0: y[b] = U[b] x[b] (U m x n, row stride ldu, batch
+ * stride su; y m); trans = 1: y[b] = U[b]' x[b] (y n; m <= 8192).  HBM-bound, one read of
+ * U per product.                                                                         */
+int pq_gemv_batched(const double* U, int64_t ldu, int64_t su, int32_t m, int32_t n, int32_t batch,
+                    int32_t trans, const double* x, int64_t sx, double* y, int64_t sy, void* stream);
+
 /* LAD interior-point method (porqua_amd/lad.py; replaces the LP solve behind
  * LAD.model_qpsolvers, src/optimization.py:296-345): out[b] = M[b] V[b], or
  * out[b] = S[b] - M[b] V[b] when S != NULL, for M[b] n x n (row stride ldm, batch stride

@@ -166,6 +166,8 @@ _EXPORTS = {
     "pq_eigcap_form": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                         ctypes.POINTER(PQSettings), c_dp, c_dp, c_dp, c_dp, c_dp, c_int32, c_dp, c_int32, c_dp,
                         c_int64, c_dp, c_dp], c_int32),
+    "pq_gemv_batched": ([c_dp, c_int64, c_int64, c_int32, c_int32, c_int32, c_int32, c_dp, c_int64, c_dp,
+                         c_int64, c_dp], c_int32),
     "pq_workspace_bytes": ([c_int32, c_int32, c_int32, c_int32, c_int32, c_int32], c_int64),
     "pq_simulate_periods": ([c_dp, c_int64, c_int32, c_dp, c_int64, c_dp, c_dp, c_int32, c_dp, c_dp,
                              ctypes.c_double, ctypes.c_double, c_dp, c_dp, c_int64, c_dp, c_int32, c_dp], c_int32),

@@ -55,6 +55,26 @@ class L1Terms:
     lev_budget: float = np.inf
 
 
+def _gemv(U, x, trans: bool = False):
+    """U[b] x[b] (trans: U[b]' x[b]) for U (B, m, n) with unit column stride and x (B, n) or
+    (B, m): the HBM-bound HIP kernel pq_gemv_batched, one read of U per product (a batched
+    GEMM with a single right-hand side ran at ~1 TB/s and dominated the IPM iteration)."""
+    B, m, n = U.shape
+    if U.stride(2) != 1:
+        U = U.contiguous()
+    x = x.contiguous()
+    assert x.shape == (B, m if trans else n), (tuple(x.shape), tuple(U.shape), trans)
+    y = torch.empty((B, n if trans else m), dtype=torch.float64, device=U.device)
+    lib = _lib.load()
+    stream = engine._stream()
+    for s in range(0, B, 65535):   # grid.y limit
+        c = min(B, s + 65535) - s
+        _lib.check(lib.pq_gemv_batched(U[s:].data_ptr(), U.stride(1), U.stride(0), m, n, c, int(trans),
+                                       x[s:].data_ptr(), x.stride(0), y[s:].data_ptr(), y.stride(0), stream),
+                   "pq_gemv_batched")
+    return y
+
+
 def block_k(dx, du, dv, dp, dm):
     """Closed forms of the per-asset elimination (all sums of positive terms):
     det(N'HN) and K = (CN) (N'HN)^-1 (CN)' on the coupling types (x-rows, turnover row,
@@ -121,10 +141,10 @@ class _Coupling:
                        "pq_wgram_batched (l1 coupling)")
         r = k0
         if self.budget:
-            P[:, r, :k0] = torch.bmm(U, K["xt"].unsqueeze(2)).squeeze(2)
+            P[:, r, :k0] = _gemv(U, K["xt"])
             P[:, r, r] = K["tt"].sum(1) + th_st
             r += 1
-        P[:, r, :k0] = torch.bmm(U, K["xL"].unsqueeze(2)).squeeze(2)
+        P[:, r, :k0] = _gemv(U, K["xL"])
         if self.budget:
             P[:, r, r - 1] = K["tL"].sum(1)
         P[:, r, r] = K["LL"].sum(1) + th_sL
@@ -143,7 +163,7 @@ class _Coupling:
 
     def nu(self, yU, yt, yL):
         """(CN)' y per asset: (U'y_U + y_t + y_L, 2 y_t, 2 y_L)."""
-        n1 = torch.bmm(self.U.transpose(1, 2), yU.unsqueeze(2)).squeeze(2) + yL[:, None]
+        n1 = _gemv(self.U, yU, True) + yL[:, None]
         n2 = torch.zeros_like(n1)
         if yt is not None:
             n1 = n1 + yt[:, None]
@@ -154,7 +174,7 @@ class _Coupling:
     def apply(self, y):
         yU, yt, yL = self.split(y)
         w1, w2, w3 = block_solve(self.det, self.cof, *self.nu(yU, yt, yL))
-        out = [torch.bmm(self.U, w1.unsqueeze(2)).squeeze(2) + self.dU * yU]
+        out = [_gemv(self.U, w1) + self.dU * yU]
         if self.budget:
             out.append(((w1 + 2 * w2).sum(1) + self.th_st * yt)[:, None])
         out.append(((w1 + 2 * w3).sum(1) + self.th_sL * yL)[:, None])
@@ -211,7 +231,7 @@ def l1_ipm_batched(UW, pd, q, terms: L1Terms, A=None, b=None, G=None, h=None, lb
     z["v"] = (x0 - z["x"]).clamp(min=0) + 0.1
     z["p"] = z["x"].clamp(min=0) + 0.1
     z["m"] = (-z["x"]).clamp(min=0) + 0.1
-    z["t"] = torch.bmm(UW, z["x"].unsqueeze(2)).squeeze(2)
+    z["t"] = _gemv(UW, z["x"])
     z["sg"] = (hG - z["x"] @ T(np.atleast_2d(G)).T).clamp(min=0.1) if mi else zeros(B, 0)
     z["st"] = ones(B) if budget else zeros(B)
     z["sL"] = ones(B)
@@ -235,13 +255,13 @@ def l1_ipm_batched(UW, pd, q, terms: L1Terms, A=None, b=None, G=None, h=None, lb
     best_it = torch.zeros(B, dtype=torch.int64, device=dev)
 
     def residuals(z, lam, du):
-        Ux = torch.bmm(U, z["x"].unsqueeze(2)).squeeze(2)                 # [UW x; A x; G x]
+        Ux = _gemv(U, z["x"])                 # [UW x; A x; G x]
         rp = {"W": z["t"] - Ux[:, :Tp], "l1": x0 - (z["x"] - z["u"] + z["v"]), "l2": -(z["x"] - z["p"] + z["m"]),
               "L": Lb - (z["p"] + z["m"]).sum(1) - z["sL"]}
         rp["A"] = (bA - Ux[:, Tp:Tp + me]) if me else zeros(B, 0)
         rp["G"] = (hG - Ux[:, Tp + me:] - z["sg"]) if mi else zeros(B, 0)
         rp["t"] = (tau - (z["u"] + z["v"]).sum(1) - z["st"]) if budget else zeros(B)
-        ATl = torch.bmm(U.transpose(1, 2), lam["U"].unsqueeze(2)).squeeze(2) + lam["l1"] + lam["l2"]
+        ATl = _gemv(U, lam["U"], True) + lam["l1"] + lam["l2"]
         lt = lam["t"] if budget else zeros(B)
         rd = {"x": pd[:, None] * z["x"] + q - ATl - du["xl"] + du["xh"],
               "u": c - lt[:, None] + lam["l1"] - du["u"], "v": c - lt[:, None] - lam["l1"] - du["v"],
@@ -316,7 +336,7 @@ def l1_ipm_batched(UW, pd, q, terms: L1Terms, A=None, b=None, G=None, h=None, lb
             a2 = rx["u"] + rx["v"] + dlt["v"] * rp["l1"]
             a3 = rx["p"] + rx["m"] + dlt["m"] * rp["l2"]
             ga1, ga2, ga3 = block_solve(det, cof, a1, a2, a3)
-            Uga = torch.bmm(U, ga1.unsqueeze(2)).squeeze(2)
+            Uga = _gemv(U, ga1)
             gU = torch.cat([rp["W"], rp["A"], rp["G"]], 1) + Uga
             gU[:, :Tp] -= th_t * rx["t"]
             if mi:
@@ -336,7 +356,7 @@ def l1_ipm_batched(UW, pd, q, terms: L1Terms, A=None, b=None, G=None, h=None, lb
             # theta_j -- large for a soft weight).  Each component takes the form that is
             # accurate for it: range space where its weight exceeds the block's geometric mean.
             lt2 = dlt_[:, None] if budget else 0.0
-            yv = {"x": torch.bmm(U.transpose(1, 2), dlU.unsqueeze(2)).squeeze(2) - rx["x"],
+            yv = {"x": _gemv(U, dlU, True) - rx["x"],
                   "u": lt2 - rx["u"], "v": lt2 - rx["v"], "p": dlL[:, None] - rx["p"], "m": dlL[:, None] - rx["m"]}
             th = {"x": 1.0 / dx, "u": 1.0 / dlt["u"], "v": 1.0 / dlt["v"], "p": 1.0 / dlt["p"], "m": 1.0 / dlt["m"]}
             r1 = rp["l1"] - (th["x"] * yv["x"] - th["u"] * yv["u"] + th["v"] * yv["v"])
@@ -363,7 +383,7 @@ def l1_ipm_batched(UW, pd, q, terms: L1Terms, A=None, b=None, G=None, h=None, lb
                 lt2 = dlt_[:, None] if budget else 0.0
                 ru = dlt["u"] * dz["u"] - (lt2 - dlam["l1"]) + rx["u"]
                 rv = dlt["v"] * dz["v"] - (lt2 + dlam["l1"]) + rx["v"]
-                ATd = torch.bmm(U.transpose(1, 2), dlU.unsqueeze(2)).squeeze(2) + dlam["l1"] + dlam["l2"]
+                ATd = _gemv(U, dlU, True) + dlam["l1"] + dlam["l2"]
                 rxx = dx * dz["x"] - ATd + rx["x"]
                 trace.append(("newton", float(ru.abs().max()), float(rv.abs().max()), float(rxx.abs().max()),
                               float(dlt["u"].max()), float(dlt["v"].max())))
@@ -436,7 +456,7 @@ def l1_ipm_batched(UW, pd, q, terms: L1Terms, A=None, b=None, G=None, h=None, lb
     status = torch.full_like(iters, _lib.PQ_MAX_ITER)
     status = torch.where(best_merit < _INACCURATE, torch.full_like(iters, _lib.PQ_SOLVED_INACCURATE), status)
     status = torch.where(best_merit < tol, torch.full_like(iters, _lib.PQ_SOLVED), status)
-    Px = torch.bmm(UW.transpose(1, 2), torch.bmm(UW, best_x.unsqueeze(2))).squeeze(2) + pd[:, None] * best_x
+    Px = _gemv(UW, _gemv(UW, best_x), True) + pd[:, None] * best_x
     obj = 0.5 * (best_x * Px).sum(1) + (q * best_x).sum(1) + c * (best_x - x0).abs().sum(1)
     return LPResult(best_x, lam["U"], status, iters, obj, best_merit)
 

@@ -169,3 +169,19 @@ def test_grouped_window_moments_match_per_date_kernels(device, n, T, stride, off
         X = R[rows[b, :tlen[b]]]
         assert np.abs(mu_b[b] - X.mean(0)).max() <= 1e-14 * scale
         assert np.all(np.abs(dg_b[b] - ((X - X.mean(0)) ** 2).sum(0)) <= 1e-12 * dg_a[b])
+
+
+@pytest.mark.parametrize("m,n,B,trans,offset", [(255, 1000, 37, 0, 0), (255, 1000, 37, 1, 0),
+                                                 (7, 33, 5, 0, 1), (7, 33, 5, 1, 1), (300, 2000, 3, 1, 0)])
+def test_gemv_batched_matches_torch(device, m, n, B, trans, offset):
+    """pq_gemv_batched (ipm_l1's U x / U' x) against torch.bmm in FP64: aligned 16-byte and
+    odd / unaligned scalar paths (offset shifts the base pointer by one double)."""
+    from porqua_amd.ipm_l1 import _gemv
+    g = torch.Generator(device="cpu").manual_seed(m * 7 + n)
+    big = torch.randn(B * m * n + 1, generator=g, dtype=torch.float64).to(device)
+    U = big[offset:offset + B * m * n].view(B, m, n)
+    x = torch.randn((B, m if trans else n), generator=g, dtype=torch.float64).to(device)
+    got = _gemv(U, x, bool(trans))
+    ref = torch.bmm(U.transpose(1, 2) if trans else U, x.unsqueeze(2)).squeeze(2)
+    torch.cuda.synchronize()
+    assert torch.allclose(got, ref, rtol=1e-13, atol=1e-12), float((got - ref).abs().max())

@@ -34,6 +34,11 @@ def test_block_closed_forms_match_projected_inverse():
         assert np.allclose(w, np.linalg.solve(N.T @ H @ N, a), rtol=1e-9, atol=1e-12)
 
 
+def _torch_gemv(U, x, trans=False):
+    """Test scaffolding: the CPU stand-in of pq_gemv_batched (U[b] x[b] / U[b]' x[b])."""
+    return torch.bmm(U.transpose(1, 2) if trans else U, x.unsqueeze(2)).squeeze(2)
+
+
 class _DenseCoupling(ipm_l1._Coupling):
     """Test scaffolding: S formed densely by torch on the CPU, solved by torch.linalg."""
 
@@ -69,6 +74,7 @@ def _reference_qp(P, q, x0, tau, L, lb, ub, tc=None):
 @pytest.mark.parametrize("form", ["budget", "cost"])
 def test_l1_ipm_algebra_matches_oracle(monkeypatch, form):
     monkeypatch.setattr(ipm_l1, "_Coupling", _DenseCoupling)
+    monkeypatch.setattr(ipm_l1, "_gemv", _torch_gemv)
     g = load_golden("msci_mv_shrink")
     n = g["P"].shape[-1]
     rng = np.random.default_rng(3)
@@ -100,6 +106,7 @@ def test_l1_ipm_window_form_matches_oracle(monkeypatch):
     cost form with a leverage budget, long-short box, against the oracle on the reference's
     linearised problem."""
     monkeypatch.setattr(ipm_l1, "_Coupling", _DenseCoupling)
+    monkeypatch.setattr(ipm_l1, "_gemv", _torch_gemv)
     from porqua_amd.synthetic import factor_panel
     n, Tw, B = 120, 60, 2
     _, R, y, _ = factor_panel(200, n, seed=5)
