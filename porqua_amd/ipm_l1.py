@@ -39,7 +39,7 @@ import numpy as np
 import torch
 
 from . import _lib, engine
-from .lad import LPResult, _INACCURATE, _mv, _NormalFactor
+from .lad import LPResult, _INACCURATE, _gemv, _mv, _NormalFactor
 
 F64 = torch.float64
 
@@ -53,26 +53,6 @@ class L1Terms:
     cost: float = 0.0
     to_budget: float | None = None
     lev_budget: float = np.inf
-
-
-def _gemv(U, x, trans: bool = False):
-    """U[b] x[b] (trans: U[b]' x[b]) for U (B, m, n) with unit column stride and x (B, n) or
-    (B, m): the HBM-bound HIP kernel pq_gemv_batched, one read of U per product (a batched
-    GEMM with a single right-hand side ran at ~1 TB/s and dominated the IPM iteration)."""
-    B, m, n = U.shape
-    if U.stride(2) != 1:
-        U = U.contiguous()
-    x = x.contiguous()
-    assert x.shape == (B, m if trans else n), (tuple(x.shape), tuple(U.shape), trans)
-    y = torch.empty((B, n if trans else m), dtype=torch.float64, device=U.device)
-    lib = _lib.load()
-    stream = engine._stream()
-    for s in range(0, B, 65535):   # grid.y limit
-        c = min(B, s + 65535) - s
-        _lib.check(lib.pq_gemv_batched(U[s:].data_ptr(), U.stride(1), U.stride(0), m, n, c, int(trans),
-                                       x[s:].data_ptr(), x.stride(0), y[s:].data_ptr(), y.stride(0), stream),
-                   "pq_gemv_batched")
-    return y
 
 
 def block_k(dx, du, dv, dp, dm):

@@ -91,13 +91,33 @@ class LADProblem:
         rc = w @ self.C.T
         if self.mi:
             rc = rc + torch.cat([torch.zeros_like(rc[:, :self.me]), s], 1)
-        rt = torch.bmm(self.X, w.unsqueeze(2)).squeeze(2) + u - v
+        rt = _gemv(self.X, w) + u - v
         return torch.cat([rc, rt], 1)
 
     def At(self, lam):
         lc, lt = lam[:, :self.mc], lam[:, self.mc:]
-        gw = lc @ self.C + torch.bmm(lt.unsqueeze(1), self.X).squeeze(1)
+        gw = lc @ self.C + _gemv(self.X, lt, True)
         return torch.cat([gw, lt, -lt, lc[:, self.me:]], 1)
+
+
+def _gemv(U, x, trans: bool = False):
+    """U[b] x[b] (trans: U[b]' x[b]) for U (B, m, n) with unit column stride and x (B, n) or
+    (B, m): the HBM-bound HIP kernel pq_gemv_batched, one read of U per product (a batched
+    GEMM with a single right-hand side ran at ~1 TB/s and dominated the IPM iterations)."""
+    B, m, n = U.shape
+    if U.stride(2) != 1:
+        U = U.contiguous()
+    x = x.contiguous()
+    assert x.shape == (B, m if trans else n), (tuple(x.shape), tuple(U.shape), trans)
+    y = torch.empty((B, n if trans else m), dtype=torch.float64, device=U.device)
+    lib = _lib.load()
+    stream = engine._stream()
+    for s in range(0, B, 65535):   # grid.y limit
+        c = min(B, s + 65535) - s
+        _lib.check(lib.pq_gemv_batched(U[s:].data_ptr(), U.stride(1), U.stride(0), m, n, c, int(trans),
+                                       x[s:].data_ptr(), x.stride(0), y[s:].data_ptr(), y.stride(0), stream),
+                   "pq_gemv_batched")
+    return y
 
 
 def _mv(M, V, S=None):
@@ -275,7 +295,7 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
             rx_w, rx_u, rx_v, rx_s = pr.split(rx)
             r_c, r_t = rp[:, :mc], rp[:, mc:]
             g_t = r_t + th_u * rx_u - th_v * rx_v
-            f = -rx_w + torch.bmm((g_t * e_inv).unsqueeze(1), X).squeeze(1)
+            f = -rx_w + _gemv(X, g_t * e_inv, True)
             if mc:
                 g_c = r_c.clone()
                 if pr.mi:
@@ -289,7 +309,7 @@ def lad_ipm_batched(pr: LADProblem, tol: float = 1e-9, max_iter: int = 80, trace
             else:
                 dlc = torch.zeros((B, 0), dtype=F64, device=dev)
                 dw = hsolve(f.unsqueeze(2)).squeeze(2)
-            dlt = (g_t - torch.bmm(X, dw.unsqueeze(2)).squeeze(2)) * e_inv
+            dlt = (g_t - _gemv(X, dw)) * e_inv
             du = th_u * (dlt - rx_u)
             dv = th_v * (-dlt - rx_v)
             ds = th_s * (dlc[:, me:] - rx_s)
