@@ -37,6 +37,8 @@ def main():
                     help="turnover budget TAU and leverage budget L together, long-short box "
                          "[-0.05, 0.1]: the per-asset-block IPM (porqua_amd/ipm_l1.py)")
     ap.add_argument("--chunk", type=int, default=4749)
+    ap.add_argument("--no-gcap", action="store_true", help="per-date capacitances (per-date rho) instead of "
+                    "the group capacitance")
     args = ap.parse_args()
     if args.both:
         return both(args)
@@ -67,7 +69,7 @@ def main():
         ev.clear()
         qb2, lr2, const = split_batch(qb, lr, term, split_panel, np.ones((1, n)), np.ones(1), None, None,
                                       np.zeros(n), np.ones(n))
-        res = engine.solve_lowrank(qb2, lr2, settings, groups=gplan, events=ev)
+        res = engine.solve_lowrank(qb2, lr2, settings, groups=gplan, events=ev, gcap=not args.no_gcap)
         return res, merge_batch(res.x, term)
 
     step()
