@@ -47,18 +47,20 @@ def default_device() -> torch.device:
 class Settings:
     """ADMM / polish settings.  OSQP defaults except a scale-aware initial rho (4 x mean
     diag P, adapted every 60 iterations: no refactorisation on the n = 1000 min-variance
-    windows, tests/engine_model.py) and the polish settings.  ADMM only has to reach an
-    approximate point whose active set the polish can correct: measured on config 3,
-    eps 1e-3 / 1 refinement step gives 21 ADMM iterations + 2.6 polish rounds (95.7k
-    QPs/s) against 26 + 2.3 at eps 1e-4 / 4 steps (85.1k); every answer is still KKT-checked
-    and a rejected polish resumes ADMM to eps_retry.  Passed through ``params`` of the
-    reference API."""
+    windows, tests/engine_model.py), the stopping tolerance and the polish settings.  ADMM
+    only has to reach an approximate point whose active set the polish can correct: measured
+    on config 3 (round 2 kernels, tools/gpu_exp3.sh) eps 2e-3 gives 20 ADMM iterations +
+    2.7 polish rounds against 21 + 2.6 at 1e-3 and 18 + 2.9 at 4e-3 (about 2 % apart; configs
+    2, 4 and 5 also gain), alpha 1.7 / 1.8 trade 10 / 29 more ADMM iterations for 0.7 / 1.5
+    fewer polish rounds and lose; round 1 measured 1e-3 against 1e-4 (95.7k vs 85.1k QPs/s).
+    Every answer is still KKT-checked and a rejected polish resumes ADMM to eps_retry.
+    Passed through ``params`` of the reference API."""
     rho0: float = 0.1
     rho0_rel: float = 4.0      # initial rho = rho0_rel * mean(diag P) (0: use rho0)
     sigma: float = 1e-6
     alpha: float = 1.6
-    eps_abs: float = 1e-3      # ADMM stop before the polish (OSQP's default; the polish
-    eps_rel: float = 1e-3      # identifies the active set and solves the reduced KKT exactly)
+    eps_abs: float = 2e-3      # ADMM stop before the polish (twice OSQP's default; the polish
+    eps_rel: float = 2e-3      # identifies the active set and solves the reduced KKT exactly)
     eps_retry: float = 1e-7    # problems whose polish is rejected resume ADMM to this eps
     rho_min: float = 1e-6
     rho_max: float = 1e6
