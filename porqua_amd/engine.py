@@ -356,7 +356,7 @@ def solve(qb: QPBatch, settings: Settings | None = None, ws: Workspace | None = 
     _rho_floor_q(qb, ws, settings or Settings())
     _lib.check(tl("factor", lambda: lib.pq_factor_batched(P_, S_, None, 0, SS, 1, strm)),
                "pq_factor_batched")
-    cnt = {"refactors": 0, "launches": 0, "pg_fallback": 0}
+    cnt = {"refactors": 0, "launches": 0}
 
     def admm_rounds(idx, nidx, SSx):
         for _ in range(max_rounds):
