@@ -549,9 +549,13 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
         double xt;
         if constexpr (FUSE) {   // x~ = (rhs - X~raw + mu su - Cg' cw) / c, fused with the updates
           double corr = X_h[i] - (mu_h ? su * mu_h[i] : 0.0);
+          if constexpr (MGR > 0) {
 #pragma unroll
-          for (int r = 0; r < MGRA; ++r)
-            if (r < mg) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
+            for (int r = 0; r < MGRA; ++r)
+              if (r < mg) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
+          } else {
+            for (int r = 0; r < mg; ++r) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
+          }
           xt = (rr0 - corr) * g_dinv[g];
         } else {
           xt = X_h[i];
@@ -618,12 +622,23 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
           if (r >= mg) break;
           cvp[r] = hsum(cvp[r]);
         }
-      } else {   // Cg V: written straight to the date's slots (read only by the next symv)
-        for (int r = 0; r < mg; ++r) {
-          double a = 0.0;
-          for (int i = hl; i < n; i += 32) a = fma(Cg_h[(int64_t)r * ld + i], V_h[i], a);
-          a = hsum(a);
-          if (hl == 0) g_cgv[g * MGG + r] = a;
+      } else {   // Cg V: written straight to the date's slots (read only by the next symv);
+                 // four rows per pass over the date's vector (FUSE: V = rhs / c is not stored)
+        const double dv = FUSE ? g_dinv[g] : 1.0;
+        const double* vsrc = FUSE ? R_h : V_h;
+        for (int q0 = 0; q0 < mg; q0 += 4) {
+          double a[4] = {0.0, 0.0, 0.0, 0.0};
+          for (int i = hl; i < n; i += 32) {
+            const double vi = vsrc[i] * dv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (q0 + e < mg) a[e] = fma(Cg_h[(int64_t)(q0 + e) * ld + i], vi, a[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const double v = hsum(a[e]);
+            if (hl == 0 && q0 + e < mg) g_cgv[g * MGG + q0 + e] = v;
+          }
         }
       }
       const int it = g_it[g] + 1;
@@ -723,17 +738,20 @@ extern "C" int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq
                      *st, Minv, k_ld, M_stride, gdates, urows, ucnt, uoff, umax, *s, iters_this_call, pc, ldpc,  \
                      r0, cc)
   const bool small = pb->mg <= pq::MGR_SMALL;
-  const bool fuse = small && pc != nullptr && cc != nullptr;
-  switch (nqk * 4 + (fuse ? 2 : (small ? 0 : 1))) {
+  const bool fuse = pc != nullptr && cc != nullptr;
+  switch (nqk * 4 + (fuse ? (small ? 2 : 3) : (small ? 0 : 1))) {
     case 4: PQ_GRP_CASE(1, pq::MGG_SMALL, pq::MGR_SMALL, false); break;
     case 5: PQ_GRP_CASE(1, pq::MGG_BIG, 0, false); break;
     case 6: PQ_GRP_CASE(1, pq::MGG_SMALL, pq::MGR_SMALL, true); break;
+    case 7: PQ_GRP_CASE(1, pq::MGG_BIG, 0, true); break;
     case 8: PQ_GRP_CASE(2, pq::MGG_SMALL, pq::MGR_SMALL, false); break;
     case 9: PQ_GRP_CASE(2, pq::MGG_BIG, 0, false); break;
     case 10: PQ_GRP_CASE(2, pq::MGG_SMALL, pq::MGR_SMALL, true); break;
+    case 11: PQ_GRP_CASE(2, pq::MGG_BIG, 0, true); break;
     case 12: PQ_GRP_CASE(3, pq::MGG_SMALL, pq::MGR_SMALL, false); break;
     case 13: PQ_GRP_CASE(3, pq::MGG_BIG, 0, false); break;
     case 14: PQ_GRP_CASE(3, pq::MGG_SMALL, pq::MGR_SMALL, true); break;
+    case 15: PQ_GRP_CASE(3, pq::MGG_BIG, 0, true); break;
     default:
       pq::set_error("pq_admm_lr_grouped: unsupported k_ld=%d", k_ld);
       return -1;

@@ -727,7 +727,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             return lib.pq_admm_lr_gcap(L_, P_, S_, ctypes.byref(gc["c"]), SS, int(s.max_iter), bd["pc"].data_ptr(),
                                        bd["pc"].stride(0), bd["r0"], bd["cc"].data_ptr(), strm)
         if grouped:   # every group relaunches; solved dates are skipped inside
-            fz = bd is not None and fuse and qb.mg <= 4   # uniform D + shared Cg: the fused form
+            fz = bd is not None and fuse and qb.mg <= 32   # uniform D + shared Cg: the fused form
             return lib.pq_admm_lr_grouped(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
                                           _ptr(groups.gdates), groups.ngroups, _ptr(groups.urows),
                                           _ptr(groups.ucnt), _ptr(groups.uoff), groups.umax, SS,

@@ -20,27 +20,35 @@ PHASES = ["setup+classify", "free list", "rF/dA", "cholesky", "U+S", "refine", "
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    n, T, D = 1000, 252, int(args[0]) if args else 4749
-    dates, R, _, _ = factor_panel(T - 1 + D, n)
+    cfg4 = "--config4" in sys.argv   # n = 3000 tracking LS with 20 sector caps (tools/bench_configs.py)
+    n, T, D = (3000 if cfg4 else 1000), 252, int(args[0]) if args else (2000 if cfg4 else 4749)
+    dates, R, y, sec = factor_panel(T - 1 + D, n, n_sectors=20 if cfg4 else 10)
     rows, tlen = engine.window_rows(dates, dates[T - 1:T - 1 + D], T)
-    pan = engine.Panel(R)
+    pan = engine.Panel(R, y if cfg4 else None)
     r_d, t_d = pan.rows_to_device(rows, tlen)
-    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
-                                   lb=np.zeros(n), ub=np.ones(n))
+    G = np.stack([(sec == g).astype(float) for g in range(20)]) if cfg4 else None
+    qb = engine.QPBatch.from_dense(None, None, n=n, A=np.ones((1, n)), b=np.ones(1), G=G,
+                                   h=np.full(20, 0.15) if cfg4 else None, lb=np.zeros(n), ub=np.ones(n))
     qb.batch = D
     mu = pan.window_means(r_d, t_d)
     dev = mu.device
     qb.P = None   # window path: P stays in window form
     qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=dev)
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)
-    lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+    if cfg4:
+        xty, _ = pan.gram_xy(r_d, t_d)
+        qb.q = (-2.0 * xty).contiguous()
+        lr = engine.LowRank(pan, r_d, t_d, mu=None)
+    else:
+        lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
     ws = engine.Workspace(qb, dense=False)
     gp = engine.GroupPlan(rows, tlen, dev) if ("--group" in sys.argv or "--gcap" in sys.argv) else None
     off = (9 + ws.mg_pad) * qb.ld   # PQ_WORK_PROF
     for _ in range(2):
         ev = []
         ws.work[:, off + 16:off + 24].zero_()
-        res = engine.solve_lowrank(qb, lr, engine.Settings(), ws, events=ev, groups=gp, gcap="--gcap" in sys.argv)
+        st = engine.Settings.from_params({"rho0_rel": 0.1, "rho0_qrel": 0.0}) if cfg4 else engine.Settings()
+        res = engine.solve_lowrank(qb, lr, st, ws, events=ev, groups=gp, gcap="--gcap" in sys.argv)
         torch.cuda.synchronize()
     ad = ws.work[:, off + 16:off + 24].cpu().numpy() * 10e-3   # wall_clock64 ticks (100 MHz) -> us
     its = res.iters.cpu().numpy().astype(float)
