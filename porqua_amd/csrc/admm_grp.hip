@@ -546,23 +546,31 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       for (int i = hl; i < n; i += 32) {
         const double rb = has_box ? grho(lo_h[i], up_h[i], rho, s) : 0.0;
         const double rr0 = R_h[i];
-        double xt;
-        if constexpr (FUSE) {   // x~ = (rhs - X~raw + mu su - Cg' cw) / c, fused with the updates
-          double corr = X_h[i] - (mu_h ? su * mu_h[i] : 0.0);
-          if constexpr (MGR > 0) {
+        double xt, pxt, cgy = 0.0, cgw = 0.0, cgi[MGRA];
+        if constexpr (MGR == 0) {   // many rows: each Cg entry of asset i read once for all four sums
+          double cwd = 0.0, rgd = 0.0;
+          for (int r = 0; r < mg; ++r) {
+            const double c = Cg_h[(int64_t)r * ld + i];
+            if (FUSE) cwd = fma(g_cw[g * MGG + r], c, cwd);
+            rgd = fma(c, g_rgz[g * MGG + r], rgd);
+            cgy = fma(c, g_yg[g * MGG + r], cgy);
+            cgw = fma(c, g_wg[g * MGG + r], cgw);
+          }
+          // FUSE: x~ = (rhs - X~raw + mu su - Cg' cw) / c, fused with the updates
+          xt = FUSE ? (rr0 - (X_h[i] - (mu_h ? su * mu_h[i] : 0.0) + cwd)) * g_dinv[g] : X_h[i];
+          pxt = rr0 - sigma * xt - rb * xt - rgd;
+          cgi[0] = 0.0;
+        } else {
+          if constexpr (FUSE) {   // x~ = (rhs - X~raw + mu su - Cg' cw) / c, fused with the updates
+            double corr = X_h[i] - (mu_h ? su * mu_h[i] : 0.0);
 #pragma unroll
             for (int r = 0; r < MGRA; ++r)
               if (r < mg) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
+            xt = (rr0 - corr) * g_dinv[g];
           } else {
-            for (int r = 0; r < mg; ++r) corr = fma(g_cw[g * MGG + r], Cg_h[(int64_t)r * ld + i], corr);
+            xt = X_h[i];
           }
-          xt = (rr0 - corr) * g_dinv[g];
-        } else {
-          xt = X_h[i];
-        }
-        double pxt = rr0 - sigma * xt - rb * xt;
-        double cgy = 0.0, cgw = 0.0, cgi[MGRA];
-        if constexpr (MGR > 0) {
+          pxt = rr0 - sigma * xt - rb * xt;
 #pragma unroll
           for (int r = 0; r < MGR; ++r) {
             cgi[r] = r < mg ? Cg_h[(int64_t)r * ld + i] : 0.0;
@@ -571,13 +579,6 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
               cgy = fma(cgi[r], g_yg[g * MGG + r], cgy);
               cgw = fma(cgi[r], g_wg[g * MGG + r], cgw);
             }
-          }
-        } else {
-          for (int r = 0; r < mg; ++r) {
-            const double c = Cg_h[(int64_t)r * ld + i];
-            pxt -= c * g_rgz[g * MGG + r];
-            cgy = fma(c, g_yg[g * MGG + r], cgy);
-            cgw = fma(c, g_wg[g * MGG + r], cgw);
           }
         }
         const double xn = alpha * xt + (1.0 - alpha) * x_h[i];
