@@ -253,7 +253,12 @@ int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
                        int32_t k_ld, int64_t M_stride, const int32_t* gdates, int32_t ngroups,
                        const int32_t* urows, const int32_t* ucnt, const int32_t* uoff, int32_t umax,
                        const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
-                       int32_t r0, const double* cc, void* stream);
+                       int32_t r0, const double* cc, const int32_t* cg_nzr, const double* cg_nzv,
+                       int32_t nzmax, void* stream);
+/* cg_nzr / cg_nzv (nzmax > 0; shared Cg with more than 4 rows): the nonzeros of each column
+ * of Cg, row ids (-1 padded) and values, nzmax per column (e.g. the budget row plus one
+ * sector-membership row per asset: nzmax = 2); the per-asset row sums of the updates then
+ * read nzmax entries instead of mg.                                                      */
 
 /* Group capacitance (admm_gcap.hip): the dates of each slide group (same T, same
  * c = p_scale w_scale, same p_diag, one shared rho grho[g]) share ONE capacitance matrix of

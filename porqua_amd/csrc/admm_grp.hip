@@ -78,7 +78,8 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
                                                  const int32_t* gdates, const int32_t* urows_all,
                                                  const int32_t* ucnt_all, const int32_t* uoff, int umax,
                                                  pq_settings s, int iters_call, const double* pc,
-                                                 int64_t ldpc, int r0, const double* cc) {
+                                                 int64_t ldpc, int r0, const double* cc,
+                                                 const int32_t* cg_nzr, const double* cg_nzv, int nzmax) {
   // pass-1 output W, overwritten in place by the symv with the pass-2 operand Ut (rows outside
   // a date's window zeroed); 2 workgroups fit on a CU
   __shared__ __attribute__((aligned(16))) double WU[(UMAXG + 4) * GMAX];
@@ -549,12 +550,20 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
         double xt, pxt, cgy = 0.0, cgw = 0.0, cgi[MGRA];
         if constexpr (MGR == 0) {   // many rows: each Cg entry of asset i read once for all four sums
           double cwd = 0.0, rgd = 0.0;
-          for (int r = 0; r < mg; ++r) {
-            const double c = Cg_h[(int64_t)r * ld + i];
+          auto row_terms = [&](int r, double c) {
             if (FUSE) cwd = fma(g_cw[g * MGG + r], c, cwd);
             rgd = fma(c, g_rgz[g * MGG + r], rgd);
             cgy = fma(c, g_yg[g * MGG + r], cgy);
             cgw = fma(c, g_wg[g * MGG + r], cgw);
+          };
+          if (nzmax > 0) {   // sparse columns of the shared rows (e.g. budget + sector memberships)
+            for (int e = 0; e < nzmax; ++e) {
+              const int r = cg_nzr[(int64_t)i * nzmax + e];
+              if (r < 0) break;
+              row_terms(r, cg_nzv[(int64_t)i * nzmax + e]);
+            }
+          } else {
+            for (int r = 0; r < mg; ++r) row_terms(r, Cg_h[(int64_t)r * ld + i]);
           }
           // FUSE: x~ = (rhs - X~raw + mu su - Cg' cw) / c, fused with the updates
           xt = FUSE ? (rr0 - (X_h[i] - (mu_h ? su * mu_h[i] : 0.0) + cwd)) * g_dinv[g] : X_h[i];
@@ -719,9 +728,12 @@ extern "C" int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq
                                   const int32_t* gdates, int32_t ngroups, const int32_t* urows,
                                   const int32_t* ucnt, const int32_t* uoff, int32_t umax,
                                   const pq_settings* s, int32_t iters_this_call, const double* pc,
-                                  int64_t ldpc, int32_t r0, const double* cc, void* stream) {
+                                  int64_t ldpc, int32_t r0, const double* cc, const int32_t* cg_nzr,
+                                  const double* cg_nzv, int32_t nzmax, void* stream) {
   PQ_CHECK_ARG(lr && pb && st && s && Minv, "pq_admm_lr_grouped: null argument");
   PQ_CHECK_ARG((pc == nullptr) == (cc == nullptr), "pq_admm_lr_grouped: pc and cc go together");
+  PQ_CHECK_ARG(nzmax == 0 || (cg_nzr && cg_nzv && nzmax > 0 && nzmax <= pb->mg && pb->Cg_stride == 0),
+               "pq_admm_lr_grouped: sparse columns need shared Cg and 0 < nzmax <= mg");
   PQ_CHECK_ARG(pc == nullptr || pb->Cg_stride == 0, "pq_admm_lr_grouped: the fused form needs shared Cg");
   PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0, "pq_admm_lr_grouped: window missing");
   PQ_CHECK_ARG(gdates && urows && ucnt && uoff && umax > 0, "pq_admm_lr_grouped: group plan missing");
@@ -737,7 +749,7 @@ extern "C" int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq
 #define PQ_GRP_CASE(NQKV, MGGV, MGRV, FUSEV)                                                              \
   hipLaunchKernelGGL((pq::k_admm_grp<NQKV, MGGV, MGRV, FUSEV>), dim3(ngroups), dim3(pq::GT), 0, str, *lr, *pb,   \
                      *st, Minv, k_ld, M_stride, gdates, urows, ucnt, uoff, umax, *s, iters_this_call, pc, ldpc,  \
-                     r0, cc)
+                     r0, cc, cg_nzr, cg_nzv, (MGRV) == 0 ? nzmax : 0)
   const bool small = pb->mg <= pq::MGR_SMALL;
   const bool fuse = pc != nullptr && cc != nullptr;
   switch (nqk * 4 + (fuse ? (small ? 2 : 3) : (small ? 0 : 1))) {

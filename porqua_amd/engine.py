@@ -555,6 +555,24 @@ def grouped_applicable(qb: QPBatch, lr: LowRank, groups: "GroupPlan | None", ws:
             and qb.mg <= 32 and k_ld <= 384 and ws.work_stride >= 3 * qb.ld)
 
 
+def _sparse_columns(qb: QPBatch, nz_limit: int = 4):
+    """Column-sparse form of shared general rows (more than 4 rows, at most ``nz_limit``
+    nonzeros per column: the budget row plus 0/1 group memberships, Constraints.add_linear
+    for sector caps) for pq_admm_lr_grouped: (row ids int32 [ld, nzmax] -1 padded, values,
+    nzmax), or (None, None, 0) when the rows are few or dense."""
+    if not qb.shared or qb.mg <= 4:
+        return None, None, 0
+    C = qb.Cg[0, :qb.mg, :]
+    nzc = (C != 0).sum(0)
+    nzmax = int(nzc.max().item())
+    if nzmax == 0 or nzmax > nz_limit:
+        return None, None, 0
+    order = torch.argsort((C == 0).to(torch.int8), dim=0, stable=True)[:nzmax]   # nonzero rows first
+    vals = torch.gather(C, 0, order)
+    rows = torch.where(vals != 0, order, torch.full_like(order, -1)).to(torch.int32)
+    return rows.T.contiguous(), vals.T.contiguous(), nzmax
+
+
 def _uniform_box(qb: QPBatch) -> bool:
     """Every box row of every problem gets the same ADMM rho (pq_lr_capacitance_band)."""
     if qb.lb is None:
@@ -728,15 +746,18 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                                        bd["pc"].stride(0), bd["r0"], bd["cc"].data_ptr(), strm)
         if grouped:   # every group relaunches; solved dates are skipped inside
             fz = bd is not None and fuse and qb.mg <= 32   # uniform D + shared Cg: the fused form
+            nzr, nzv, nzmax = sparse_cols
             return lib.pq_admm_lr_grouped(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
                                           _ptr(groups.gdates), groups.ngroups, _ptr(groups.urows),
                                           _ptr(groups.ucnt), _ptr(groups.uoff), groups.umax, SS,
                                           int(s.max_iter), bd["pc"].data_ptr() if fz else None,
                                           bd["pc"].stride(0) if fz else 0, bd["r0"] if fz else 0,
-                                          bd["cc"].data_ptr() if fz else None, strm)
+                                          bd["cc"].data_ptr() if fz else None, _ptr(nzr), _ptr(nzv), nzmax,
+                                          strm)
         return lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld, _ptr(idx),
                                       nidx, SS, int(s.max_iter), strm)
 
+    sparse_cols = _sparse_columns(qb) if grouped else (None, None, 0)
     cnt = {"refactors": 0, "launches": 0, "pg_fallback": 0}
 
     def admm_rounds(idx, nidx, SSx):

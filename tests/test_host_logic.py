@@ -357,3 +357,27 @@ def test_planners_match_their_contracts_on_random_calendars():
             for d in range(gd[g], gd[g + 1]):
                 t = int(tlen[d])
                 assert np.array_equal(ur[g, uo[d]:uo[d] + t], rows[d, :t])
+
+
+def test_sparse_columns_of_group_rows():
+    """engine._sparse_columns: budget + 0/1 sector rows -> per-column (row, value) lists with
+    -1 padding; dense or few rows -> none (the grouped ADMM then reads Cg densely)."""
+    import torch
+    n = 10
+    sec = np.array([0, 1, 2, 0, 1, 2, 3, 3, 0, 1])
+    G = np.stack([(sec == g).astype(float) for g in range(4)])
+    qb = engine.QPBatch.from_dense(None, None, n=n, A=np.ones((1, n)), b=np.ones(1), G=G, h=np.full(4, 0.5),
+                                   lb=np.zeros(n), ub=np.ones(n), device=torch.device("cpu"))
+    rows, vals, nzmax = engine._sparse_columns(qb)
+    assert nzmax == 2 and rows.shape == (qb.ld, 2)
+    C = qb.Cg[0, :qb.mg, :n].numpy()
+    for i in range(n):
+        dense = np.zeros(qb.mg)
+        for r, v in zip(rows[i].tolist(), vals[i].tolist()):
+            if r >= 0:
+                dense[r] = v
+        assert np.array_equal(dense, C[:, i])
+    assert (rows[n:] == -1).all()
+    qb2 = engine.QPBatch.from_dense(None, None, n=n, A=np.ones((1, n)), b=np.ones(1), G=np.ones((4, n)),
+                                    h=np.full(4, 0.5), lb=np.zeros(n), ub=np.ones(n), device=torch.device("cpu"))
+    assert engine._sparse_columns(qb2)[2] == 0     # 5 nonzeros per column: dense reads
