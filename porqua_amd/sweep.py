@@ -33,6 +33,12 @@ import torch
 from . import engine
 
 EIG_MIN_PER_DATE = 192   # factor='auto': eigen form from this many problems per date
+# |q| floor of the initial rho for the sweep (engine.Settings.rho0_qrel, default 10): its
+# small risk aversions are nearly linear.  Measured at the config-5 shape
+# (tools/gpu_exp5.sh): 3 -> 1826 max ADMM iterations, 10 -> 55, 30 -> 34 (27.8k -> 32.8k
+# QPs/s), 60 -> 26, 100 -> problems fall to the eps_retry ADMM; 30 keeps a factor 3 from both
+# cliffs.  (A single mean-variance backtest at risk aversion 1 is faster at 10.)
+SWEEP_RHO0_QREL = 30.0
 
 
 def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0, budget=1.0,
@@ -79,6 +85,8 @@ def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0
         pdate = torch.arange(nd, dtype=torch.int32, device=dev).repeat_interleave(L)
         eig = tl("eig", lambda: engine.EigCap(panel, r_d, t_d, mu_c, qb, pdate, k_ld))
     gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax) if group else None
+    if settings is None:
+        settings = engine.Settings(rho0_qrel=SWEEP_RHO0_QREL)
     res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, events=events, eig=eig)
     meta = {"dates": nd, "lambdas": lam, "grouped": gp is not None and gp.ok,
             "ngroups": None if gp is None else gp.ngroups, "capacitance": res.capacitance,
