@@ -167,8 +167,15 @@ __device__ void form_cwood(const pq_lowrank& lr, int b, int n, const int* fl, in
 // x_r . x_{r-d}) when every column is free: X_F X_F' is then the window's whole Gram, an
 // O(T^2) gather instead of form_cwood's O(T^2 n) product (config 4: n = 3000, every
 // variable free).  Centred windows: Xc Xc' = G - s 1' - 1 s' + (mu.mu) 1 1', s_t = x_t . mu.
+// A few fixed columns (a later active-set round: k = n - nfix, nfix <= NFIX_MAX, listed in
+// fx) are then downdated, Xc_F Xc_F' = Xc Xc' - sum_{j fixed} xc_j xc_j', from DC-column
+// chunks of the window staged in LDS -- O(T^2 nfix) instead of form_cwood's O(T^2 n).
+constexpr int NFIX_MAX = 128;
+constexpr int DC = 8;
+static_assert(KMAX + DC * KMAX <= CHOL_LDS, "form_cwood_band: sx | column chunk must fit the Cholesky LDS");
 __device__ void form_cwood_band(const pq_lowrank& lr, int b, int n, int nbt, double cdiag, double* Ks,
-                                int64_t ldk, const double* band, int64_t ldo, int r0, double* sx, double* red) {
+                                int64_t ldk, const double* band, int64_t ldo, int r0, const int* fx, int nfix,
+                                double* sx, double* red) {
   const int T = lr.tlen[b];
   const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
@@ -205,6 +212,37 @@ __device__ void form_cwood_band(const pq_lowrank& lr, int b, int n, int nbt, dou
         v = gi == gj ? 1.0 : 0.0;
       }
       Ks[(int64_t)gi * ldk + gj] = v;
+    }
+  }
+  double* cs = sx + KMAX;   // T x DC: centred window columns of a chunk of fixed variables
+  for (int j0 = 0; j0 < nfix; j0 += DC) {
+    const int nc = min(DC, nfix - j0);
+    __syncthreads();
+    for (int e = t; e < T * DC; e += PT) {
+      const int i = e / DC, c = e - i * DC;
+      double v = 0.0;
+      if (c < nc) {
+        const int j = fx[j0 + c];
+        v = lr.panel[(int64_t)rws[i] * lr.ldp + j] - (mu ? mu[j] : 0.0);
+      }
+      cs[e] = v;
+    }
+    __syncthreads();
+    for (int tile = 0; tile < ntile; ++tile) {   // same tile / element map as above
+      int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+      while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+      while (I * (I + 1) / 2 > tile) --I;
+      const int J = tile - I * (I + 1) / 2;
+      for (int e = t; e < TB * TB; e += PT) {
+        const int gi = I * TB + (e >> 6), gj = J * TB + (e & 63);
+        if (gi >= T || gj >= T) continue;
+        const double* a = cs + gi * DC;
+        const double* c = cs + gj * DC;
+        double d = 0.0;
+#pragma unroll
+        for (int q = 0; q < DC; ++q) d = fma(a[q], c[q], d);
+        Ks[(int64_t)gi * ldk + gj] -= d;
+      }
     }
   }
   __syncthreads();
@@ -468,6 +506,7 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
         if (fl[i] == 0) Fl[p++] = i;
     }
     const int nbk = (k + TB - 1) / TB;
+    int px_ready = 0;   // g holds w Xc'Xc xs (uniform)
     int nzb = 0;
     for (int i = t; i < ld; i += PT) {
       const double v = i < n ? (fl[i] == 1 ? lb[i] : (fl[i] == 2 ? ub[i] : 0.0)) : 0.0;
@@ -514,8 +553,23 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       if (t < ma) solL[t] = lamF[Al[t]];
       __syncthreads();
       PQ_STAMP(2);
-      if (band && k == n) form_cwood_band(lr, b, n, nbt, dl / psw, K, ldk, band, ldo, r0, smem, red);
-      else form_cwood(lr, b, n, fl, nbt, dl / psw, K, ldk, smem);
+      const int nfix = n - k;
+      if (band && nfix <= NFIX_MAX) {
+        if (nfix > 0 && w == 0) {   // fixed-column list in Fl (unused in this mode), ascending
+          int base = 0;
+          for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + l;
+            const bool fx = i < n && fl[i] != 0;
+            const unsigned long long m = __ballot(fx);
+            if (fx) Fl[base + __popcll(m & ((1ull << l) - 1ull))] = i;
+            base += __popcll(m);
+          }
+        }
+        __syncthreads();
+        form_cwood_band(lr, b, n, nbt, dl / psw, K, ldk, band, ldo, r0, Fl, nfix, smem, red);
+      } else {
+        form_cwood(lr, b, n, fl, nbt, dl / psw, K, ldk, smem);
+      }
       const int info = wg_cholesky(FormRead{K, ldk}, K, ldk, nbt, T, Dt, smem);
       if (info) break;
       PQ_STAMP(3);
@@ -552,8 +606,10 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       if (tile_potrf_lds(stg, ma)) break;
       PQ_STAMP(4);
       for (int itr = 0; itr < s.refine_iters; ++itr) {
-        // wd = rF - P_FF x_F - C_aF' solL on F ;  rl = dA - C_aF x_F
+        // wd = rF - P_FF x_F - C_aF' solL on F ;  rl = dA - C_aF x_F ;  g = w Xc'Xc x_F
+        // (kept: a converged x_F with x_B = 0 is the final point, whose exact P x this is)
         lr_px(lr, b, n, wx, u, tree, red, [&](int i, double sum) {
+          g[i] = sum;
           double v = 0.0;
           if (fl[i] == 0) {
             v = wr[i] - ps * sum - pd * wx[i];
@@ -576,7 +632,10 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
           double rm = 0.0;
           for (int i = t; i < n; i += PT) rm = fmax(rm, fabs(wd[i]));
           if (t < ma) rm = fmax(rm, fabs(rl[t]));
-          if (block_max(rm, red) <= 1e-13 * sc) break;
+          if (block_max(rm, red) <= 1e-13 * sc) {
+            px_ready = !nzb;
+            break;
+          }
         }
         apply(wd, wt);
         for (int a = w; a < ma; a += PW) {   // wl = C_aF t1 - rl
@@ -752,7 +811,9 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
     }
     __builtin_amdgcn_s_dcache_inv();   // xs was rewritten: no stale scalar-cache reads
     PQ_STAMP(6);
-    if (compact && !nzb) {   // x = x_F exactly: pass 1 gathers the k free columns only
+    if (px_ready) {          // Woodbury mode: the converged refinement's last pass
+      for (int i = t; i < n; i += PT) emit_g(i, g[i]);
+    } else if (compact && !nzb) {   // x = x_F exactly: pass 1 gathers the k free columns only
       lr_pass1_sparse(lr, b, Fl, k, solx, vec, red);
       lr_pass2(lr, b, n, vec, stg, red, [&](int i, double v) { emit_g(i, wsc * v); });
     } else {

@@ -28,7 +28,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from porqua_amd import engine  # noqa: E402
+from porqua_amd import _lib, engine  # noqa: E402
 from porqua_amd.sweep import mean_variance_sweep  # noqa: E402
 from porqua_amd.synthetic import factor_panel  # noqa: E402
 
@@ -46,7 +46,9 @@ def timed(fn, steps):
 def summary(res):
     st = res.status.cpu().numpy()
     return {"status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
-            "mean_iters": float(res.iters.float().mean().item()), "max_iters": int(res.iters.max().item())}
+            "mean_iters": float(res.iters.float().mean().item()), "max_iters": int(res.iters.max().item()),
+            "polish_rounds_mean": float(res.out[:, _lib.PQ_OUT_ROUNDS].mean().item()),
+            "nfree_min": int(res.out[:, _lib.PQ_OUT_NFREE].min().item())}
 
 
 def config4(dates_limit, steps, dev, overrides=None):
