@@ -605,7 +605,11 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       __syncthreads();
       if (tile_potrf_lds(stg, ma)) break;
       PQ_STAMP(4);
-      for (int itr = 0; itr < s.refine_iters; ++itr) {
+      // at least two proximal steps: one step from the ADMM point left config 4's budget row
+      // outside the 1e-10 equality check on every date, and a second active-set round
+      // (new capacitance, Cholesky, Z) cost 1.5x the extra step (33 -> 22 ms per 2000 dates)
+      const int wood_iters = max(s.refine_iters, 2);
+      for (int itr = 0; itr < wood_iters; ++itr) {
         // wd = rF - P_FF x_F - C_aF' solL on F ;  rl = dA - C_aF x_F ;  g = w Xc'Xc x_F
         // (kept: a converged x_F with x_B = 0 is the final point, whose exact P x this is)
         lr_px(lr, b, n, wx, u, tree, red, [&](int i, double sum) {
