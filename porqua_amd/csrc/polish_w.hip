@@ -472,6 +472,12 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
   };
   auto full_px = [&]() { lr_px(lr, b, n, xs, vec, stg, red, emit_g); };
 
+  // At least two proximal refinement steps per round in Woodbury mode: one step from the
+  // ADMM point left config 4's budget row outside the 1e-10 equality check on every date,
+  // and the second active-set round that followed (new capacitance, Cholesky, Z) cost 1.5x
+  // the extra step (polish 33 -> 22 ms per 2000 dates).  A converged step breaks early.
+  // (Compact mode keeps s.refine_iters: it must agree with the grouped polish, polish_g.hip.)
+  const int refine_steps = max(s.refine_iters, 2);
   // Woodbury mode (free set beyond the compact scratch) needs the T x T capacitance to fit
   const bool wood_ok = ((lr.tmax + TB - 1) / TB) * TB <= ldk && lr.tmax <= KMAX;
   int accepted = 0, rounds = 0, nfree = 0, overflow = 0;
@@ -605,11 +611,7 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
       __syncthreads();
       if (tile_potrf_lds(stg, ma)) break;
       PQ_STAMP(4);
-      // at least two proximal steps: one step from the ADMM point left config 4's budget row
-      // outside the 1e-10 equality check on every date, and a second active-set round
-      // (new capacitance, Cholesky, Z) cost 1.5x the extra step (33 -> 22 ms per 2000 dates)
-      const int wood_iters = max(s.refine_iters, 2);
-      for (int itr = 0; itr < wood_iters; ++itr) {
+      for (int itr = 0; itr < refine_steps; ++itr) {
         // wd = rF - P_FF x_F - C_aF' solL on F ;  rl = dA - C_aF x_F ;  g = w Xc'Xc x_F
         // (kept: a converged x_F with x_B = 0 is the final point, whose exact P x this is)
         lr_px(lr, b, n, wx, u, tree, red, [&](int i, double sum) {

@@ -821,7 +821,11 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         cnt["pg_fallback"] = m
         if m:
             ws.pg_fallback = fb   # the dates handed to the per-date kernel (diagnostics)
-            polish_w(fb.contiguous(), m, name="polish (fallback, inside polish)")
+            # two refinement steps per round for the hand-offs (vertex cycling, failed
+            # factorisations): config 5's fallback polish 33 -> 4 ms (tools/gpu_refine_g.sh)
+            sfb = type(s).from_buffer_copy(s)
+            sfb.refine_iters = max(sfb.refine_iters, 2)
+            polish_w(fb.contiguous(), m, ctypes.byref(sfb), name="polish (fallback, inside polish)")
 
     admm_rounds(None, 0, SS)
     SS_main = SS

@@ -48,6 +48,9 @@ def main():
         ev = []
         ws.work[:, off + 16:off + 24].zero_()
         st = engine.Settings.from_params({"rho0_rel": 0.1, "rho0_qrel": 0.0}) if cfg4 else engine.Settings()
+        for a in sys.argv:   # --refine=N: proximal refinement steps per polish round
+            if a.startswith("--refine="):
+                st.refine_iters = int(a.split("=")[1])
         res = engine.solve_lowrank(qb, lr, st, ws, events=ev, groups=gp, gcap="--gcap" in sys.argv)
         torch.cuda.synchronize()
     ad = ws.work[:, off + 16:off + 24].cpu().numpy() * 10e-3   # wall_clock64 ticks (100 MHz) -> us
