@@ -34,7 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from porqua_amd import engine  # noqa: E402
-from porqua_amd.workloads import MinVarianceBacktest  # noqa: E402
+from porqua_amd.workloads import MinVarianceBacktest, TrackingBacktest  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 matrix spec
@@ -42,12 +42,18 @@ FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 matrix spec
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks; without a launcher (no WORLD_SIZE in the environment) bench.py starts "
+                         "them itself, one child process per GPU, before anything touches the GPU")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1000)
+    ap.add_argument("--workload", choices=["config3", "config4"], default="config3",
+                    help="config3: n=1000 long-only min-variance (the metric's configuration); config4: "
+                         "n=3000 tracking LS with 20 sector caps (BASELINE configs[3], 'dates sharded')")
+    ap.add_argument("--n", type=int, default=None, help="assets (config3: 1000, config4: 3000)")
     ap.add_argument("--window", type=int, default=252)
-    ap.add_argument("--dates", type=int, default=4749, help="rebalance dates per rank")
+    ap.add_argument("--dates", type=int, default=None,
+                    help="rebalance dates per rank (--strong: in total); config3: 4749, config4: 9749")
     ap.add_argument("--path", choices=["auto", "dense", "lowrank"], default="auto",
                     help="dense K^-1 (K2 n^3 + K3 n^2 stream) or Woodbury low-rank (T + mg < n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -68,8 +74,61 @@ def parse():
     return ap.parse_args()
 
 
+def launch_plan(gpus: int, env: dict):
+    """Environments of the rank processes ``bench.py --gpus N`` starts itself when no
+    launcher did (no WORLD_SIZE): ranks 0..N-1 on 127.0.0.1, one per GPU (LOCAL_RANK = RANK).
+    None when this process is already a rank (torchrun, or one of our children) or N <= 1."""
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    port = env.get("MASTER_PORT")
+    if not port:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = str(s.getsockname()[1])
+    return [dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=port) for r in range(gpus)]
+
+
+def run_ranks(envs, argv, script=None) -> int:
+    """Start one child per rank (this process never touches the GPU) and wait for all; if a
+    rank fails, the others are terminated (by their own PIDs) so none blocks in a collective."""
+    import subprocess
+    script = script or os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e) for e in envs]
+    rc = 0
+    while procs:
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0:
+                rc = rc or r
+                for o in procs:
+                    o.terminate()
+                for o in procs:
+                    try:
+                        o.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        o.kill()
+                        o.wait()
+                procs = []
+                break
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse()
+    plan = launch_plan(args.gpus, os.environ)
+    if plan is not None:
+        sys.exit(run_ranks(plan, sys.argv[1:]))
+    cfg4 = args.workload == "config4"
+    if args.n is None:
+        args.n = 3000 if cfg4 else 1000
+    if args.dates is None:
+        args.dates = 9749 if cfg4 else 4749
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -78,7 +137,7 @@ def main():
     # CPU baseline first, in a child process, before this process touches the GPU (its
     # process pool forks; bench.py itself never forks after HIP initialisation)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg4:
         import subprocess
         cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--n", str(args.n), "--window", str(args.window),
                "--dates", str(args.dates), "--budget", str(args.cpu_budget)]
@@ -96,10 +155,17 @@ def main():
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     n, T = args.n, args.window
-    settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))
-    wl = MinVarianceBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
-                             path=args.path, group=not args.no_group, slide=not args.no_slide,
-                             with_cov=args.with_cov, strong=args.strong)
+    if cfg4:
+        settings = engine.Settings.from_params(dict({"rho0_rel": 0.1, "rho0_qrel": 0.0},
+                                                    **dict(kv.split("=", 1) for kv in args.set)))
+        wl = TrackingBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
+                              strong=args.strong)
+    else:
+        settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))
+        wl = MinVarianceBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
+                                 path=args.path, group=not args.no_group, slide=not args.no_slide,
+                                 with_cov=args.with_cov, strong=args.strong)
+    gloo = dist is not None and dist.get_backend() != "nccl"
     D = wl.D                                            # dates of this rank
     D_all = wl.global_dates                             # dates of the whole job
     R_rank, y_rank, ends_local, pan = wl.R_rank, wl.y_rank, wl.ends_local, wl.pan
@@ -128,6 +194,13 @@ def main():
         x_stage[k][:D].copy_(res.x[:, :n])
         ready = torch.cuda.Event()
         ready.record(main)
+        if gloo:   # rehearsal backend (CPU collectives): gather through host memory, synchronously
+            ready.synchronize()
+            parts = [torch.empty((Dpad, n), dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, x_stage[k].cpu())
+            if rank == 0:
+                w_host[k].copy_(torch.cat(parts))
+            return res
         with torch.cuda.stream(side):
             side.wait_event(ready)
             if world > 1:
@@ -157,7 +230,8 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        red_dev = torch.device("cpu") if gloo else dev
+        t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -166,10 +240,10 @@ def main():
     cert = wl.certificate(res)
     if dist:
         cv = torch.tensor([cert["max_violation"], cert["max_rel_stationarity"],
-                           cert["max_rel_complementarity"]], dtype=torch.float64, device=dev)
+                           cert["max_rel_complementarity"]], dtype=torch.float64, device=red_dev)
         dist.all_reduce(cv, op=dist.ReduceOp.MAX)
         cert["max_violation"], cert["max_rel_stationarity"], cert["max_rel_complementarity"] = cv.tolist()
-        st_all = torch.bincount((res.status.long() + 8).clamp(0, 15), minlength=16).to(dev)
+        st_all = torch.bincount((res.status.long() + 8).clamp(0, 15), minlength=16).to(red_dev)
         dist.all_reduce(st_all)
         cert["status_counts"] = {str(i - 8): int(v) for i, v in enumerate(st_all.tolist()) if v}
     # ---- per-kernel timing (HIP events on the launch stream) ------------------------------
@@ -275,8 +349,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (factor-model panel, seed 20240314; usa_returns absent)",
-        "config": {"workload": "config3: long-only min-variance (P=2*Pearson cov, budget + box [0,1]), "
-                               "daily rebalance", "n_assets": n, "window": T,
+        "config": {"workload": ("config4: tracking-error LS (P=2 X'X, q=-2 X'y), budget + box [0,1] + 20 sector "
+                                "caps <= 0.15, daily rebalance" if cfg4 else
+                                "config3: long-only min-variance (P=2*Pearson cov, budget + box [0,1]), "
+                                "daily rebalance"), "n_assets": n, "window": T,
                    "dates_per_gpu": D, "global_batch": D_all, "parallelism": f"dates-sharded x{world}"},
         "roofline": {"bound": "hbm", "kernel": kern + (" (K3, grouped low-rank)" if grouped else " (K3)"),
                      "achieved": admm_gbs,
@@ -330,6 +406,12 @@ def main():
                                                    "from the panel rows (torch), not by the engine")},
         "cpu_baseline": None,
     }
+    if cfg4:   # the next-row and drop-in legs below are config-3 (n = 1000 min-variance) lines
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     # ---- next row, outside the timed region: Strategy.simulate of
     # the solved weights, one holding period per rebalance date (float, level, turnover) ----
     wx = res.x[:, :n]

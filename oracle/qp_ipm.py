@@ -97,29 +97,58 @@ def _as2d(M, n):
     return M.reshape(-1, n)
 
 
-def _kkt_solve(H, A, r1, r2, reg=0.0):
-    n = H.shape[0]
-    if A is None or A.shape[0] == 0:
-        M = H + reg * np.eye(n)
-        try:
-            return sla.solve(M, r1, assume_a="sym"), np.zeros(0)
-        except (sla.LinAlgError, ValueError):
-            return np.linalg.lstsq(M, r1, rcond=None)[0], np.zeros(0)
-    me = A.shape[0]
-    K = np.zeros((n + me, n + me))
-    K[:n, :n] = H + reg * np.eye(n)
-    K[:n, n:] = A.T
-    K[n:, :n] = A
-    if reg:
-        K[n:, n:] = -reg * np.eye(me)
-    rhs = np.concatenate([r1, r2])
+class SingularKKT(Exception):
+    """The (1,1) block is not numerically positive definite (Cholesky breakdown)."""
+
+
+def _chol(M):
     try:
-        sol = sla.solve(K, rhs)
-        if not np.all(np.isfinite(sol)):
-            raise sla.LinAlgError
-    except (sla.LinAlgError, ValueError):
-        sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
-    return sol[:n], sol[n:]
+        c = sla.cho_factor(M, lower=True, check_finite=False)
+    except sla.LinAlgError:
+        raise SingularKKT from None
+    if not np.all(np.isfinite(c[0].diagonal())) or np.min(c[0].diagonal()) <= 0.0:
+        raise SingularKKT
+    return c
+
+
+def _kkt_solve(H, A, r1, r2, reg=0.0, shift=True):
+    """[H + reg I, A'; A, -reg I] [x; y] = [r1; r2] by the Cholesky of H + reg I and the
+    Schur complement S = A (H + reg I)^-1 A' of the equality rows -- cvxopt's 'chol2' KKT
+    solver family (coneqp factors P + G'W^-2 G, PD whenever the stacked [P; A; G] has full
+    column rank; with a finite box every column is in G).  One step of iterative refinement on
+    the full system.  When the Cholesky breaks down (an interior-point H whose barrier weights
+    span ~1e24 can lose definiteness in rounding) and ``shift`` is set, it is retried on
+    H + 1e-14 max|diag H| I: an inexact Newton direction, harmless to a path-following method
+    whose residuals are recomputed from the iterate every iteration.  ``shift=False`` raises
+    SingularKKT instead (exact solves only)."""
+    n = H.shape[0]
+    me = 0 if A is None else A.shape[0]
+    if n == 0:   # every variable fixed: no primal unknowns, the multipliers stay undetermined (0)
+        return np.zeros(0), np.zeros(me)
+    M = H + reg * np.eye(n) if reg else H
+    try:
+        c = _chol(M)
+    except SingularKKT:
+        if not shift:
+            raise
+        M = M + 1e-14 * max(float(np.max(np.abs(np.diag(H)))), 1e-300) * np.eye(n)
+        c = _chol(M)
+
+    def solve(f, g):
+        hf = sla.cho_solve(c, f, check_finite=False)
+        if not me:
+            return hf, np.zeros(0)
+        dy = np.linalg.solve(S, A @ hf - g)
+        return hf - HiA @ dy, dy
+
+    if me:
+        HiA = sla.cho_solve(c, A.T, check_finite=False)
+        S = A @ HiA + (reg * np.eye(me) if reg else 0.0)
+    x, y = solve(r1, r2)
+    e1 = r1 - (H @ x + reg * x + (A.T @ y if me else 0.0))
+    e2 = (r2 - (A @ x - reg * y)) if me else np.zeros(0)
+    cx, cy = solve(e1, e2)
+    return x + cx, (y + cy if me else np.zeros(0))
 
 
 def solve_qp(P, q, G=None, h=None, A=None, b=None, lb=None, ub=None,
@@ -295,7 +324,12 @@ def _refine_active_set(sol: OracleSolution, max_rounds: int = 30):
         d = np.concatenate(rhsC) if rhsC else np.zeros(0)
         rF = -q[F] - (P[np.ix_(F, Bi)] @ xb[Bi] if len(Bi) else 0.0)
         dF = d - (C[:, Bi] @ xb[Bi] if len(Bi) else 0.0)
-        xF, lam = _kkt_solve(P[np.ix_(F, F)], C[:, F] if C.shape[0] else None, rF, dF)
+        try:   # exact solves only: a singular P_FF means the optimal face is not a point
+            xF, lam = _kkt_solve(P[np.ix_(F, F)], C[:, F] if C.shape[0] else None, rF, dF, shift=False)
+        except SingularKKT:
+            sol.extras["refined"] = False
+            sol.extras["refine_skipped"] = "P_FF singular on the detected face (non-unique optimum)"
+            return
         xn = xb.copy()
         xn[F] = xF
         y = lam[:me] if me else None

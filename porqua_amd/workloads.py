@@ -116,47 +116,158 @@ class MinVarianceBacktest:
                                   b=1.0, lb=lb, ub=ub, chunk=chunk)
 
 
-def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_row, b, lb, ub,
-                       chunk: int = 256) -> dict:
-    """KKT residuals of every solution of a window-path batch with one equality row
-    ``A_row' x = b`` and a box, P_d = scale_d * Xc_d' Xc_d (Xc = window rows minus ``mu``;
-    ``mu`` None = uncentred).  P x is recomputed here with torch from the panel rows.
+class TrackingBacktest:
+    """Config 4 on one device (BASELINE.json configs[3]): a synthetic factor panel with 20
+    sectors, n = 3000 assets, 252-day windows, daily rebalancing, tracking-error least
+    squares P = 2 X'X (uncentred), q = -2 X'y (LeastSquares.set_objective,
+    src/optimization.py:206-226) with budget 1'x = 1, long-only box [0, 1] and 20 sector
+    caps G x <= 0.15 (Constraints.add_linear / to_GhAb, src/constraints.py:66-94, 114-167):
+    21 shared general rows.  ``strong``: ``D`` dates in total, contiguous block per rank;
+    otherwise ``D`` dates per rank of one longer panel.  q is formed inside ``step`` (the
+    X'y window products are part of the per-date objective)."""
+
+    N_SECTORS = 20
+    CAP = 0.15
+
+    def __init__(self, n: int = 3000, T: int = 252, D: int = 9749, rank: int = 0, world: int = 1,
+                 device=None, settings: engine.Settings | None = None, strong: bool = False):
+        self.n, self.T = n, T
+        self.device = dev = device or engine.default_device()
+        if strong:
+            per = -(-D // world)
+            lo = rank * per
+            self.D = max(0, min(D, lo + per) - lo)
+            d_total = T - 1 + D
+        else:
+            lo = rank * D
+            self.D = D
+            d_total = T - 1 + D * world
+        self.global_dates = D if strong else D * world
+        D = self.D
+        dates, R, y, sec = factor_panel(d_total, n, n_sectors=self.N_SECTORS)
+        self.R_rank = R[lo:lo + T - 1 + D]
+        self.y_rank = y[lo:lo + T - 1 + D]
+        self.ends_local = np.arange(T - 1, T - 1 + D)
+        self.row_offset = lo
+        sl_dates = dates[lo:lo + T - 1 + D]
+        self.dates_rank = sl_dates
+        self.rows, self.tlen = engine.window_rows(sl_dates, sl_dates[self.ends_local], T)
+        self.pan = engine.Panel(self.R_rank, self.y_rank, device=dev)
+        self.rows_d, self.tlen_d = self.pan.rows_to_device(self.rows, self.tlen)
+        self.G = np.stack([(sec == g).astype(float) for g in range(self.N_SECTORS)])
+        qb = engine.QPBatch.from_dense(None, None, A=np.ones((1, n)), b=np.ones(1), G=self.G,
+                                       h=np.full(self.N_SECTORS, self.CAP), lb=np.zeros(n), ub=np.ones(n),
+                                       device=dev, n=n)
+        qb.batch = D
+        qb.q = torch.zeros((D, qb.ld), dtype=F64, device=dev)
+        qb.p_scale = torch.full((D,), 2.0, dtype=F64, device=dev)
+        self.qb = qb
+        self.plan = None
+        self.mu = None
+        self.gplan = engine.GroupPlan(self.rows, self.tlen, dev)
+        self.lr = engine.LowRank(self.pan, self.rows_d, self.tlen_d, mu=None)
+        self.use_lr, self.with_cov = True, False
+        # tracking objectives start at a small rho (engine.Settings docs; tools/bench_configs.py)
+        self.settings = settings or engine.Settings(rho0_rel=0.1, rho0_qrel=0.0)
+        self.ws = engine.Workspace(qb, dense=False)
+
+    @property
+    def grouped(self) -> bool:
+        return engine.grouped_applicable(self.qb, self.lr, self.gplan, self.ws)
+
+    def step(self, events: list | None = None) -> engine.BatchResult:
+        if events is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        xty, _ = self.pan.gram_xy(self.rows_d, self.tlen_d)
+        torch.mul(xty, -2.0, out=self.qb.q)
+        self.lr.refresh()
+        if events is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            events.append(("moments", e0, e1))
+        return engine.solve_lowrank(self.qb, self.lr, self.settings, self.ws, events=events, groups=self.gplan)
+
+    def certificate(self, res: engine.BatchResult, chunk: int = 128) -> dict:
+        qb, n = self.qb, self.n
+        return window_certificate(self.pan.R, self.rows_d, self.tlen_d, None, self.qb.p_scale, qb.q[:, :n], res,
+                                  lb=torch.zeros(n, dtype=F64, device=self.device),
+                                  ub=torch.ones(n, dtype=F64, device=self.device), chunk=chunk,
+                                  C=qb.Cg[0, :qb.mg, :n], lg=qb.lg[0, :qb.mg], ug=qb.ug[0, :qb.mg])
+
+
+def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_row=None, b=None, lb=None, ub=None,
+                       chunk: int = 256, C=None, lg=None, ug=None, rows_of=None) -> dict:
+    """KKT residuals of every solution of a window-path batch, P_p = scale_p * Xc_p' Xc_p
+    (Xc = window rows minus ``mu``; ``mu`` None = uncentred).  P x is recomputed here with
+    torch from the panel rows, not by the engine's kernels.
+
+    General rows: ``C`` (mg, n) with bounds ``lg <= C x <= ug`` (equalities lg == ug, as the
+    engine stores them: equality rows first) and multipliers ``res.y`` (mg); the legacy form
+    ``A_row' x = b`` is one equality row.  Box ``lb <= x <= ub`` with multipliers
+    ``res.z_box``.  ``rows_of`` (optional int64 device tensor, one entry per problem) maps
+    problem p to its window / moments row in ``rows``, ``tlen``, ``mu`` (e.g. the date of a
+    risk-aversion sweep problem).
 
     Returns the maxima over the batch of
-      * ``max_violation``: max(|A x - b|, [lb - x]+, [x - ub]+) (absolute, the BASELINE bar);
-      * ``max_rel_stationarity``: ||P x + q + A'y + z_box||inf /
-        max(||P x||inf, ||q||inf, ||A'y||inf, ||z_box||inf)  (OSQP-style relative);
-      * ``max_rel_complementarity``: max |z_box^- (x - lb)|, |z_box^+ (ub - x)| over the
-        same scale;
+      * ``max_violation``: max(|C x - b| on equality rows, [C x - ug]+, [lg - C x]+,
+        [lb - x]+, [x - ub]+) (absolute, the BASELINE bar);
+      * ``max_rel_stationarity``: ||P x + q + C'y + z_box||inf /
+        max(||P x||inf, ||q||inf, ||C'y||inf, ||z_box||inf)  (OSQP-style relative);
+      * ``max_rel_complementarity``: the multipliers' complementarity products (box and
+        inequality rows) over the same scale; plus ``max_dual_sign``: the largest wrong-sign
+        multiplier of an inequality row over the scale;
     and the status histogram."""
     B, n = res.x.shape
+    dev = R.device
     tmax = rows.shape[1]
-    viol = torch.zeros((), dtype=F64, device=R.device)
-    stat = torch.zeros((), dtype=F64, device=R.device)
-    comp = torch.zeros((), dtype=F64, device=R.device)
-    ar = torch.arange(tmax, device=R.device)
+    if C is None:
+        C = A_row.reshape(1, n)
+        lg = ug = torch.full((1,), float(b), dtype=F64, device=dev)
+    C = C.to(dev, F64)
+    lg = lg.to(dev, F64)
+    ug = ug.to(dev, F64)
+    mg = C.shape[0]
+    eq = lg == ug
+    viol = torch.zeros((), dtype=F64, device=dev)
+    stat = torch.zeros((), dtype=F64, device=dev)
+    comp = torch.zeros((), dtype=F64, device=dev)
+    dsign = torch.zeros((), dtype=F64, device=dev)
+    ar = torch.arange(tmax, device=dev)
     for s in range(0, B, chunk):
         e = min(B, s + chunk)
         x = res.x[s:e]
-        X = R[rows[s:e].long()]                                         # (b, tmax, n)
-        valid = (ar[None, :] < tlen[s:e, None]).to(F64)
+        ri = torch.arange(s, e, device=dev) if rows_of is None else rows_of[s:e]
+        X = R[rows[ri].long()]                                          # (b, tmax, n)
+        valid = (ar[None, :] < tlen[ri, None]).to(F64)
         if mu is not None:
-            X = X - mu[s:e, None, :n]
+            X = X - mu[ri, None, :n]
         X = X * valid[:, :, None]
         v = torch.bmm(X, x[:, :, None])                                 # (b, tmax, 1)
         Px = scale[s:e, None] * torch.bmm(X.transpose(1, 2), v)[:, :, 0]
-        y = res.y[s:e, :1]
+        y = res.y[s:e, :mg]
         zb = res.z_box[s:e]
-        Aty = y * A_row[None, :]
-        r = Px + q[s:e] + Aty + zb
-        sc = torch.stack([Px.abs().amax(1), q[s:e].abs().amax(1), Aty.abs().amax(1), zb.abs().amax(1)]).amax(0)
+        Cty = y @ C
+        r = Px + q[s:e] + Cty + zb
+        sc = torch.stack([Px.abs().amax(1), q[s:e].abs().amax(1), Cty.abs().amax(1), zb.abs().amax(1)]).amax(0)
         sc = torch.clamp(sc, min=torch.finfo(F64).tiny)
         stat = torch.maximum(stat, (r.abs().amax(1) / sc).max())
-        pv = torch.stack([(x @ A_row - b).abs(), (lb - x).clamp(min=0).amax(1), (x - ub).clamp(min=0).amax(1)])
+        cx = x @ C.T                                                    # (b, mg)
+        gv = torch.maximum((cx - ug).clamp(min=0), (lg - cx).clamp(min=0))
+        pv = torch.stack([gv.amax(1), (lb - x).clamp(min=0).amax(1), (x - ub).clamp(min=0).amax(1)])
         viol = torch.maximum(viol, pv.max())
         cp = torch.maximum((zb.clamp(max=0) * (x - lb)).abs().amax(1), (zb.clamp(min=0) * (ub - x)).abs().amax(1))
+        if bool((~eq).any()):
+            ye = y[:, ~eq]
+            cg = torch.maximum((ye.clamp(min=0) * (ug[~eq] - cx[:, ~eq])).abs(),
+                               (ye.clamp(max=0) * (cx[:, ~eq] - lg[~eq])).abs()).amax(1)
+            cp = torch.maximum(cp, cg)
+            # a one-sided row (lg = -inf) must carry y >= 0, (ug = +inf) y <= 0
+            ws = torch.maximum((-ye).clamp(min=0) * torch.isinf(lg[~eq]), ye.clamp(min=0) * torch.isinf(ug[~eq]))
+            dsign = torch.maximum(dsign, (ws.amax(1) / sc).max())
         comp = torch.maximum(comp, (cp / sc).max())
     st = res.status.cpu().numpy()
     return {"max_violation": float(viol.item()), "max_rel_stationarity": float(stat.item()),
-            "max_rel_complementarity": float(comp.item()),
+            "max_rel_complementarity": float(comp.item()), "max_dual_sign": float(dsign.item()),
+            "problems": int(B),
             "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
