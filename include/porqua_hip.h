@@ -202,6 +202,17 @@ int pq_init_state_lr(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, c
 int pq_factor_batched(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
                       const pq_settings* s, int32_t invert, void* stream);
 
+/* K2L: pq_factor_batched for LARGE problems (the per-QP drop-in at thousands of assets:
+ * QuadraticProgram.solve with a dense n x n P, src/qp_problems.py:184-216, called per date by
+ * the serial Backtest.run, src/backtest.py:185-199).  Same K formation, info[] / status and
+ * invert semantics, but each problem is spread over many workgroups (one 64 x 64 tile each):
+ * right-looking blocked potrf (diagonal block, panel, trailing update launches per block
+ * column), then trtri into `scratch` (L^-1, ld x ld per launch slot: problem idx[i] uses
+ * scratch + i * scratch_stride) and lauum back into K.  scratch may be NULL when invert = 0. */
+int pq_factor_large(const pq_problem* pb, pq_state* st, const int32_t* idx, int32_t nidx,
+                    const pq_settings* s, int32_t invert, double* scratch, int64_t scratch_stride,
+                    void* stream);
+
 /* K3: up to `iters_this_call` OSQP-style ADMM iterations per problem idx[] (stops a
  * problem at convergence, at settings.max_iter, or when adaptive rho requests a
  * refactorisation: status PQ_NEED_REFACTOR and rho[] already updated).
@@ -396,7 +407,7 @@ int pq_gemv_batched(const double* U, int64_t ldu, int64_t su, int32_t m, int32_t
 /* LAD interior-point method (porqua_amd/lad.py; replaces the LP solve behind
  * LAD.model_qpsolvers, src/optimization.py:296-345): out[b] = M[b] V[b], or
  * out[b] = S[b] - M[b] V[b] when S != NULL, for M[b] n x n (row stride ldm, batch stride
- * sm) and V, S, out n x k row-major (batch strides sv, ss, so).  n <= 1024, 1 <= k <= 4.
+ * sm) and V, S, out n x k row-major (batch strides sv, ss, so).  1 <= k <= 4 (V in LDS for n <= 1024, read through L2 beyond).
  * Applies the K2-inverted normal matrix H^-1 and H itself to the IPM right-hand sides.   */
 int pq_lad_mv_batched(const double* M, int64_t ldm, int64_t sm, int32_t n, int32_t batch,
                       const double* V, int64_t sv, int32_t k, const double* S, int64_t ss,

@@ -111,44 +111,58 @@ def _chol(M):
     return c
 
 
-def _kkt_solve(H, A, r1, r2, reg=0.0, shift=True):
-    """[H + reg I, A'; A, -reg I] [x; y] = [r1; r2] by the Cholesky of H + reg I and the
-    Schur complement S = A (H + reg I)^-1 A' of the equality rows -- cvxopt's 'chol2' KKT
-    solver family (coneqp factors P + G'W^-2 G, PD whenever the stacked [P; A; G] has full
-    column rank; with a finite box every column is in G).  One step of iterative refinement on
-    the full system.  When the Cholesky breaks down (an interior-point H whose barrier weights
-    span ~1e24 can lose definiteness in rounding) and ``shift`` is set, it is retried on
-    H + 1e-14 max|diag H| I: an inexact Newton direction, harmless to a path-following method
-    whose residuals are recomputed from the iterate every iteration.  ``shift=False`` raises
-    SingularKKT instead (exact solves only)."""
-    n = H.shape[0]
-    me = 0 if A is None else A.shape[0]
-    if n == 0:   # every variable fixed: no primal unknowns, the multipliers stay undetermined (0)
-        return np.zeros(0), np.zeros(me)
-    M = H + reg * np.eye(n) if reg else H
-    try:
-        c = _chol(M)
-    except SingularKKT:
-        if not shift:
-            raise
-        M = M + 1e-14 * max(float(np.max(np.abs(np.diag(H)))), 1e-300) * np.eye(n)
-        c = _chol(M)
+class _KKT:
+    """Factor of [H + reg I, A'; A, -(D + reg I)] for repeated solves: the Cholesky of
+    H + reg I and the Schur complement S = A (H + reg I)^-1 A' + D + reg I of the bordered
+    rows -- cvxopt's 'chol2' KKT solver family.  Each solve takes one step of iterative
+    refinement on the full system.  The multipliers of linearly dependent rows are not unique:
+    S is solved in the minimum-norm sense.  When the Cholesky breaks down and ``shift`` is set,
+    it is retried on H + 1e-14 max|diag H| I (an inexact Newton direction, harmless to a
+    path-following method whose residuals are recomputed from the iterate every iteration);
+    ``shift=False`` raises SingularKKT instead (exact solves only)."""
 
-    def solve(f, g):
-        hf = sla.cho_solve(c, f, check_finite=False)
-        if not me:
+    def __init__(self, H, A, reg=0.0, shift=True, D=None):
+        n = H.shape[0]
+        self.H, self.A, self.reg = H, A, reg
+        self.me = me = 0 if A is None else A.shape[0]
+        self.n = n
+        if n == 0:
+            return
+        M = H + reg * np.eye(n) if reg else H
+        try:
+            self.c = _chol(M)
+        except SingularKKT:
+            if not shift:
+                raise
+            M = M + 1e-14 * max(float(np.max(np.abs(np.diag(H)))), 1e-300) * np.eye(n)
+            self.c = _chol(M)
+        Dv = np.zeros(me) if D is None else np.asarray(D, dtype=np.float64)
+        self.Dv = Dv + reg if reg else Dv
+        if me:
+            self.HiA = sla.cho_solve(self.c, A.T, check_finite=False)
+            self.S = A @ self.HiA + np.diag(self.Dv)
+
+    def _solve1(self, f, g):
+        hf = sla.cho_solve(self.c, f, check_finite=False)
+        if not self.me:
             return hf, np.zeros(0)
-        dy = np.linalg.solve(S, A @ hf - g)
-        return hf - HiA @ dy, dy
+        dy = np.linalg.lstsq(self.S, self.A @ hf - g, rcond=1e-13)[0]
+        return hf - self.HiA @ dy, dy
 
-    if me:
-        HiA = sla.cho_solve(c, A.T, check_finite=False)
-        S = A @ HiA + (reg * np.eye(me) if reg else 0.0)
-    x, y = solve(r1, r2)
-    e1 = r1 - (H @ x + reg * x + (A.T @ y if me else 0.0))
-    e2 = (r2 - (A @ x - reg * y)) if me else np.zeros(0)
-    cx, cy = solve(e1, e2)
-    return x + cx, (y + cy if me else np.zeros(0))
+    def solve(self, r1, r2):
+        if self.n == 0:   # every variable fixed: no primal unknowns, the multipliers stay undetermined (0)
+            return np.zeros(0), np.zeros(self.me)
+        A, me = self.A, self.me
+        x, y = self._solve1(r1, r2)
+        e1 = r1 - (self.H @ x + self.reg * x + (A.T @ y if me else 0.0))
+        e2 = (r2 - (A @ x - self.Dv * y)) if me else np.zeros(0)
+        cx, cy = self._solve1(e1, e2)
+        return x + cx, (y + cy if me else np.zeros(0))
+
+
+def _kkt_solve(H, A, r1, r2, reg=0.0, shift=True, D=None):
+    """One solve with a fresh _KKT factor."""
+    return _KKT(H, A, reg=reg, shift=shift, D=D).solve(r1, r2)
 
 
 def solve_qp(P, q, G=None, h=None, A=None, b=None, lb=None, ub=None,
@@ -240,13 +254,42 @@ def _solve_qp_scaled(P, q, G, h, A, b, lb, ub, tol, max_iter, refine) -> OracleS
                 x, y, s, z = best[1]
                 break
         w = z / s if m else np.zeros(0)
-        H = P + (Gh.T * w) @ Gh
-        reg = 0.0
+        # Newton system, box rows (unit rows of Gh) folded into H as a diagonal.  The general
+        # rows G are folded too (H + G'diag(w_G)G, as coneqp's chol2 does) unless that
+        # Cholesky breaks down: an active row's weight z/s reaches ~1e23 and leaves a rank-mi
+        # spike FP64 cannot resolve; then they stay bordered, C = [A; G], D = [0; s_G/z_G],
+        # where the spike is the harmless entry s/z ~ 1e-23.
+        Hd = P.copy()
+        dg = np.zeros(n)
+        np.add.at(dg, Lidx, w[mi:mi + len(Lidx)])
+        np.add.at(dg, Uidx, w[mi + len(Lidx):])
+        Hd[np.diag_indices(n)] += dg
+        kkt, bordered = None, False
+        if mi:
+            try:
+                kkt = _KKT(Hd + (G.T * w[:mi]) @ G, A if me else None, shift=False)
+            except SingularKKT:
+                C = np.vstack([A if me else np.zeros((0, n)), G])
+                kkt = _KKT(Hd, C, D=np.concatenate([np.zeros(me), s[:mi] / z[:mi]]))
+                bordered = True
+        else:
+            kkt = _KKT(Hd, A if me else None)
 
         def newton(rc):
-            # ds = -ri - Gh dx ; dz = (-rc + z*ri)/s + w*(Gh dx)
-            r1 = -rd - Gh.T @ ((-rc + z * ri) / s) if m else -rd
-            dx, dy = _kkt_solve(H, A, r1, -rp, reg=reg)
+            # ds = -ri - Gh dx ; dz = (-rc - z ds) / s   (all rows); box rows eliminated:
+            #   H dx + A'dy + G'dz_G = -rd - E'((-rc_b + z_b ri_b)/s_b),  A dx = -rp,
+            # and the general rows either folded (dz_G = ((-rc_G + z_G ri_G) + z_G G dx)/s_G)
+            # or bordered:  G dx - (s_G/z_G) dz_G = -(-rc_G + z_G ri_G)/z_G
+            vb = (-rc[mi:] + z[mi:] * ri[mi:]) / s[mi:]
+            r1 = -rd - Gh[mi:].T @ vb if m > mi else -rd
+            vg = (-rc[:mi] + z[:mi] * ri[:mi])
+            if bordered:
+                dx, dl = kkt.solve(r1, np.concatenate([-rp, -vg / z[:mi]]))
+                dy = dl[:me]
+            else:
+                if mi:
+                    r1 = r1 - G.T @ (vg / s[:mi])
+                dx, dy = kkt.solve(r1, -rp)
             ds = -ri - Gh @ dx
             dz = (-rc - z * ds) / s if m else np.zeros(0)
             return dx, dy, ds, dz

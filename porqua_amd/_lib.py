@@ -131,6 +131,8 @@ _EXPORTS = {
                        ctypes.POINTER(PQSettings), c_dp], c_int32),
     "pq_factor_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
                            ctypes.POINTER(PQSettings), c_int32, c_dp], c_int32),
+    "pq_factor_large": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
+                         ctypes.POINTER(PQSettings), c_int32, c_dp, c_int64, c_dp], c_int32),
     "pq_admm_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
                          ctypes.POINTER(PQSettings), c_int32, c_dp], c_int32),
     "pq_polish_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,

@@ -113,6 +113,45 @@ __device__ void tile_trinv(const double* T, double* X, int nvalid) {
 }
 
 
+// KKT matrix K = ps P + pd I + sigma I + Cg' R Cg + R_box, element by element (K2 / K2L)
+struct FormCtx {
+  const double* P;
+  int64_t ld;
+  int n, mg;
+  double ps, pd, sigma;
+  const double* Cg;
+  const double* lg;   // general-row bounds (rho of each row derived on the fly)
+  const double* ug;
+  const double* lb;
+  const double* ub;
+  double rho, rho_min, eq_scale;
+};
+
+__device__ __forceinline__ double rho_for(double l, double u, double rho, double rho_min,
+                                          double eq_scale) {
+  if (l == u) return rho * eq_scale;
+  if (isinf(l) && isinf(u)) return rho_min;
+  return rho;
+}
+
+__device__ __forceinline__ double form_elem(const FormCtx& f, int gi, int gj) {
+  if (gi >= f.n || gj >= f.n) return gi == gj ? 1.0 : 0.0;
+  double v = f.ps * f.P[(int64_t)gi * f.ld + gj];
+  for (int r = 0; r < f.mg; ++r)
+    v += rho_for(f.lg[r], f.ug[r], f.rho, f.rho_min, f.eq_scale) * f.Cg[(int64_t)r * f.ld + gi] *
+         f.Cg[(int64_t)r * f.ld + gj];
+  if (gi == gj) {
+    v += f.pd + f.sigma;
+    if (f.lb != nullptr) v += rho_for(f.lb[gi], f.ub[gi], f.rho, f.rho_min, f.eq_scale);
+  }
+  return v;
+}
+
+struct FormOp {
+  const FormCtx* f;
+  __device__ __forceinline__ double operator()(int gi, int gj) const { return form_elem(*f, gi, gj); }
+};
+
 // LDS needed by wg_cholesky: 4*STAGE (stream buffers / W image / diag tile) + TB*LDW.
 constexpr int CHOL_LDS = 4 * STAGE + TB * LDW;
 

@@ -3,26 +3,31 @@
 // n x k row-major (k <= 4).  Each LAD iteration applies H^-1 (from K2) and H to a handful of
 // right-hand sides; the product is HBM-bound on M (8 n^2 bytes per date), so one wave
 // streams whole rows of M with coalesced (16-B when aligned) loads while V sits in LDS, and the k dot products
-// of a row share every load of M.
+// of a row share every load of M.  Beyond 1024 columns (the large-n IPM of
+// porqua_amd/ipm.py behind the per-QP drop-in) V is read from global memory instead of LDS:
+// it is n k doubles, a few hundred KB at most, and stays in L2 across the row blocks.
 #include "capi_util.h"
 
 namespace {
 
 constexpr int kWG = 256;          // 4 waves
 constexpr int kRowsPerWG = 16;    // 4 rows per wave
-constexpr int kMaxN = 1024;
+constexpr int kMaxN = 1024;       // V staged in LDS up to here
 constexpr int kMaxK = 4;
 
-template <int K, bool VEC>
+template <int K, bool VEC, bool LDSV>
 __global__ __launch_bounds__(kWG) void k_lad_mv(const double* __restrict__ M, int64_t ldm, int64_t sm,
                                                 int n, const double* __restrict__ V, int64_t sv,
                                                 const double* __restrict__ S, int64_t ss,
                                                 double* __restrict__ out, int64_t so) {
-  __shared__ double v[kMaxN * K];
+  __shared__ double vl[LDSV ? kMaxN * K : 1];
   const int b = blockIdx.y;
   const double* Vb = V + (int64_t)b * sv;
-  for (int i = threadIdx.x; i < n * K; i += kWG) v[i] = Vb[i];
-  __syncthreads();
+  if (LDSV) {
+    for (int i = threadIdx.x; i < n * K; i += kWG) vl[i] = Vb[i];
+    __syncthreads();
+  }
+  const double* v = LDSV ? vl : Vb;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const double* Mb = M + (int64_t)b * sm;
   for (int rr = 0; rr < kRowsPerWG / 4; ++rr) {
@@ -67,10 +72,17 @@ void launch(const double* M, int64_t ldm, int64_t sm, int n, int batch, const do
             const double* S, int64_t ss, double* out, int64_t so, hipStream_t st) {
   dim3 grid((n + kRowsPerWG - 1) / kRowsPerWG, batch);
   const bool vec = (n % 2 == 0) && (ldm % 2 == 0) && (sm % 2 == 0) && ((uintptr_t)M % 16 == 0);
-  if (vec)
-    hipLaunchKernelGGL((k_lad_mv<K, true>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
-  else
-    hipLaunchKernelGGL((k_lad_mv<K, false>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
+  if (n <= kMaxN) {
+    if (vec)
+      hipLaunchKernelGGL((k_lad_mv<K, true, true>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
+    else
+      hipLaunchKernelGGL((k_lad_mv<K, false, true>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL((k_lad_mv<K, true, false>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
+    else
+      hipLaunchKernelGGL((k_lad_mv<K, false, false>), grid, dim3(kWG), 0, st, M, ldm, sm, n, V, sv, S, ss, out, so);
+  }
 }
 
 }  // namespace
@@ -79,7 +91,7 @@ extern "C" int pq_lad_mv_batched(const double* M, int64_t ldm, int64_t sm, int32
                                  const double* V, int64_t sv, int32_t k, const double* S, int64_t ss,
                                  double* out, int64_t so, void* stream) {
   PQ_CHECK_ARG(M && V && out, "pq_lad_mv_batched: null pointer");
-  PQ_CHECK_ARG(n > 0 && n <= kMaxN && ldm >= n && batch >= 0, "pq_lad_mv_batched: bad n / ldm (n=%d)", n);
+  PQ_CHECK_ARG(n > 0 && ldm >= n && batch >= 0 && batch <= 65535, "pq_lad_mv_batched: bad n / ldm / batch (n=%d)", n);
   PQ_CHECK_ARG(k >= 1 && k <= kMaxK, "pq_lad_mv_batched: k must be in [1, 4] (k=%d)", k);
   PQ_CHECK_ARG(sv >= (int64_t)n * k && so >= (int64_t)n * k && (!S || ss >= (int64_t)n * k),
                "pq_lad_mv_batched: bad vector strides");

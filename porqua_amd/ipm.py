@@ -1,4 +1,5 @@
-"""Dense QPs with many general rows on the device: a batched primal-dual IPM.
+"""Dense QPs with many general rows, or more than 1024 assets, on the device: a batched
+primal-dual IPM.
 
 The ADMM engine (K2-K4) keeps at most 64 general rows in LDS.  The reference's linearised
 l1 forms can exceed that: with both a turnover term and a leverage constraint,
@@ -12,7 +13,9 @@ Mehrotra predictor-corrector on the same machinery as the LAD LP (porqua_amd/lad
 slacks of G are eliminated exactly, leaving H = P + diag(z/s) + G' diag(z_G/s_G) G (N x N,
 one batched GEMM), factored and inverted on K2 (``pq_factor_batched``, invert = 2), applied
 by ``pq_lad_mv_batched`` with refinement, and bordered by the equality rows through a
-small Schur system.  N <= 1024.
+small Schur system.  Beyond 1024 variables (the per-QP drop-in at thousands of assets,
+src/qp_problems.py:184-216) the normal matrix is factored and inverted on K2L
+(``pq_factor_large``: many workgroups per matrix) instead of K2.
 """
 from __future__ import annotations
 
@@ -60,6 +63,9 @@ def qp_ipm_batched(P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, tol: 
     done = torch.zeros(B, dtype=torch.bool, device=dev)
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
     best_x = x.clone()
+    best_ya = ya.clone()
+    best_zs = zs.clone()
+    best_zb = zh - zl
     best_merit = torch.full((B,), np.inf, dtype=F64, device=dev)
     best_it = torch.zeros(B, dtype=torch.int64, device=dev)
 
@@ -82,6 +88,9 @@ def qp_ipm_batched(P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, tol: 
         merit = torch.where(torch.isnan(merit), torch.full_like(merit, np.inf), merit)
         better = (merit < best_merit) & ~done
         best_x = torch.where(better[:, None], x, best_x)
+        best_ya = torch.where(better[:, None], ya, best_ya)
+        best_zs = torch.where(better[:, None], zs, best_zs)
+        best_zb = torch.where(better[:, None], zh - zl, best_zb)
         best_it = torch.where(better, torch.full_like(best_it, it), best_it)
         best_merit = torch.where(better, merit, best_merit)
         done = done | (merit < tol) | ((it - best_it > 6) & (best_merit < _INACCURATE))
@@ -180,4 +189,10 @@ def qp_ipm_batched(P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, tol: 
     status = torch.where(best_merit < _INACCURATE, torch.full_like(iters, _lib.PQ_SOLVED_INACCURATE), status)
     status = torch.where(best_merit < tol, torch.full_like(iters, _lib.PQ_SOLVED), status)
     Pb = _mv(P, best_x.unsqueeze(2)).squeeze(2)
-    return LPResult(best_x, ya, status, iters, 0.5 * (best_x * Pb).sum(1) + (q * best_x).sum(1), best_merit)
+    res = LPResult(best_x, best_ya, status, iters, 0.5 * (best_x * Pb).sum(1) + (q * best_x).sum(1), best_merit)
+    # multipliers at the returned iterate in qpsolvers' signs (P x + q + A'y + G'z + z_box = 0):
+    # y = -ya, z = zs (>= 0), z_box = zh - zl (upper bounds positive, lower negative)
+    res.z = best_zs if mi else None
+    res.z_box = best_zb
+    res.Px = Pb
+    return res

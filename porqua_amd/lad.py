@@ -124,8 +124,9 @@ def _mv(M, V, S=None):
     """M V, or S - M V, for M (B, n, n) with unit column stride and V (B, n, k): the HIP
     kernel pq_lad_mv_batched for k <= 4 (one pass over M), a batched GEMM otherwise."""
     B, n, k = V.shape
-    if k > 4 or n > 1024:
-        return torch.bmm(M, V) if S is None else S - torch.bmm(M, V)
+    if k > 4:   # several passes over M, four right-hand sides each
+        parts = [_mv(M, V[:, :, c:c + 4], None if S is None else S[:, :, c:c + 4]) for c in range(0, k, 4)]
+        return torch.cat(parts, 2)
     assert M.stride(2) == 1 and M.shape[1] == n and M.shape[2] == n
     V = V.contiguous()
     S = None if S is None else S.contiguous()
@@ -141,10 +142,14 @@ class _NormalFactor:
     """H = diag(1/theta_w) + X' diag(1/(theta_u + theta_v)) X per window (n x n), factored
     and inverted on K2 (pq_factor_batched, invert = 2: Cholesky, trtri, lauum)."""
 
+    LARGE = 1024   # beyond: K2L (pq_factor_large, many workgroups per matrix)
+
     def __init__(self, B, m, dev):
         self.m = m
         self.qb = engine.QPBatch(m, B, 0, device=dev, has_box=False)
         self.ws = engine.Workspace(self.qb)
+        self.scratch = (torch.empty((B, self.qb.ld, self.qb.ld), dtype=F64, device=dev)
+                        if m > self.LARGE else None)
         self.s = engine.Settings(sigma=0.0).to_c()
         self.pb = self.qb.c_struct()
         self.st = self.ws.c_struct()
@@ -165,8 +170,13 @@ class _NormalFactor:
         for attempt in range(retries + 1):
             P[:, :m, :m].copy_(H)
             P.diagonal(dim1=1, dim2=2)[:, :m].add_(shift)
-            _lib.check(lib.pq_factor_batched(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
-                                             ctypes.byref(self.s), 2, engine._stream()), "pq_factor_batched (LP)")
+            if self.scratch is not None:
+                _lib.check(lib.pq_factor_large(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
+                                               ctypes.byref(self.s), 2, self.scratch.data_ptr(),
+                                               self.scratch.stride(0), engine._stream()), "pq_factor_large")
+            else:
+                _lib.check(lib.pq_factor_batched(ctypes.byref(self.pb), ctypes.byref(self.st), None, 0,
+                                                 ctypes.byref(self.s), 2, engine._stream()), "pq_factor_batched (LP)")
             bad = self.ws.info != 0
             if attempt == retries or not bool(bad.any()):     # host sync: one small flag
                 break

@@ -246,7 +246,7 @@ def solve_batch(qps, settings=None, device=None):
         h = np.broadcast_to(h, (len(qps), h.size)).copy()
     me = 0 if A is None else A.shape[-2]
     mi = 0 if G is None else G.shape[-2]
-    if me + mi > IPM_ROWS:
+    if me + mi > IPM_ROWS or n > DENSE_ADMM_MAX_N:
         return _solve_batch_ipm(P, q, A, b, G, h, lb, ub, device)
     qb = engine.QPBatch.from_dense(P, q, A=A, b=b, G=G, h=h, lb=lb, ub=ub, device=device)
     res = engine.solve(qb, settings)
@@ -254,19 +254,31 @@ def solve_batch(qps, settings=None, device=None):
 
 
 IPM_ROWS = 64    # general rows the ADMM engine keeps in LDS; beyond: the device IPM
+# the dense ADMM (K3) keeps its n-vectors in LDS up to 1024 assets; larger dense QPs (the
+# per-QP drop-in at configs 4/5 sizes: QuadraticProgram.solve with a 3000 x 3000 or 5000 x
+# 5000 P, src/qp_problems.py:184-216) go to the device IPM on K2L (pq_factor_large)
+DENSE_ADMM_MAX_N = 1024
 
 
 def _solve_batch_ipm(P, q, A, b, G, h, lb, ub, device=None):
     """More than IPM_ROWS general rows (e.g. the reference's linearised turnover + leverage
-    rows together, src/qp_problems.py:40-118): porqua_amd.ipm.qp_ipm_batched (K2-factored
-    normal equations, N <= 1024, constraint matrices shared by the batch)."""
+    rows together, src/qp_problems.py:40-118) or more than DENSE_ADMM_MAX_N assets:
+    porqua_amd.ipm.qp_ipm_batched (Mehrotra predictor-corrector, the algorithm family of the
+    reference's default cvxopt backend; normal matrices factored and inverted on K2, or on the
+    multi-workgroup K2L beyond 1024 assets).  Problems with their own constraint matrices are
+    solved one at a time."""
     import torch
     from . import _lib, engine
     from .ipm import qp_ipm_batched
-    if (A is not None and A.ndim == 3) or (G is not None and G.ndim == 3):
-        raise NotImplementedError("more than 64 general rows with per-problem constraint matrices")
-    if P.shape[-1] > 1024:
-        raise NotImplementedError("more than 64 general rows with n > 1024")
+    if ((A is not None and A.ndim == 3) or (G is not None and G.ndim == 3)
+            or (lb is not None and np.ndim(lb) == 2) or (ub is not None and np.ndim(ub) == 2)):
+        B = P.shape[0]
+        out = []
+        for i in range(B):
+            pick = lambda v, nd: None if v is None else (v[i] if np.asarray(v).ndim == nd else v)
+            out += _solve_batch_ipm(P[i:i + 1], q[i:i + 1], pick(A, 3), pick(b, 2), pick(G, 3), pick(h, 2),
+                                    pick(lb, 2), pick(ub, 2), device)
+        return out
     dev = device or engine.default_device()
     B, n = q.shape
     T = lambda v: None if v is None else torch.from_numpy(np.array(v, dtype=np.float64)).to(dev)
@@ -283,19 +295,56 @@ def _solve_batch_ipm(P, q, A, b, G, h, lb, ub, device=None):
     obj = res.obj.cpu().numpy()
     merit = res.merit.cpu().numpy()
     ya = res.lam.cpu().numpy()
+    zs = res.z.cpu().numpy() if res.z is not None else None
+    zb = res.z_box.cpu().numpy()
+    # qpsolvers' residuals of the returned point (src/helper_functions.py:69-80;
+    # example/compare_solver.ipynb:212-216), from the device P x
+    Px = res.Px.cpu().numpy()
+    prim, dual, gap = _residuals(x, Px, q, A, bb, G, hh, lb, ub, -ya if A is not None else None, zs, zb)
     sols = []
     for i in range(B):
         s = Solution(x=x[i].copy(), status=int(st[i]), iterations=int(it[i]))
         s.found = int(st[i]) in (_lib.PQ_SOLVED, _lib.PQ_SOLVED_INACCURATE)
         s.y = -ya[i].copy() if A is not None else None      # qpsolvers sign: Px + q + A'y + ... = 0
-        s.z = s.z_box = None
+        s.z = zs[i].copy() if zs is not None else None
+        s.z_box = zb[i].copy() if (lb is not None or ub is not None) else None
         s.obj = float(obj[i]) if s.found else None
-        s._prim = s._dual = s._gap = float(merit[i])
-        s.extras = {"solver": "device IPM (more than 64 general rows)"}
+        s._prim, s._dual, s._gap = float(prim[i]), float(dual[i]), float(gap[i])
+        s.extras = {"solver": "device IPM" + (" (K2L, n > 1024)" if n > DENSE_ADMM_MAX_N else
+                                             " (more than 64 general rows)"), "merit": float(merit[i])}
         if not s.found:
             s.x = None
         sols.append(s)
     return sols
+
+
+def _residuals(x, Px, q, A, b, G, h, lb, ub, y, z, zb):
+    """Per problem: primal residual max(|Ax - b|, [Gx - h]+, [lb - x]+, [x - ub]+), dual
+    residual |Px + q + A'y + G'z + z_box|inf and duality gap |x'Px + q'x + b'y + h'z +
+    lb'min(z_box, 0) + ub'max(z_box, 0)| (qpsolvers Solution semantics)."""
+    B = x.shape[0]
+    prim = np.zeros(B)
+    g = Px + q
+    gap = (x * Px).sum(1) + (q * x).sum(1)
+    if A is not None:
+        prim = np.maximum(prim, np.abs(x @ A.T - b).max(1))
+        g = g + y @ A
+        gap = gap + (b * y).sum(1)
+    if G is not None:
+        prim = np.maximum(prim, np.maximum(x @ G.T - h, 0.0).max(1))
+        g = g + z @ G
+        gap = gap + (h * z).sum(1)
+    if lb is not None:
+        lo = np.broadcast_to(lb, x.shape)
+        prim = np.maximum(prim, np.maximum(lo - x, 0.0).max(1))
+        gap = gap + (np.where(np.isfinite(lo), lo, 0.0) * np.minimum(zb, 0.0)).sum(1)
+    if ub is not None:
+        up = np.broadcast_to(ub, x.shape)
+        prim = np.maximum(prim, np.maximum(x - up, 0.0).max(1))
+        gap = gap + (np.where(np.isfinite(up), up, 0.0) * np.maximum(zb, 0.0)).sum(1)
+    if lb is not None or ub is not None:
+        g = g + zb
+    return prim, np.abs(g).max(1), np.abs(gap)
 
 
 def batch_result_to_solutions(res, qb):

@@ -94,5 +94,7 @@ def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0
             # factorisations: one eigendecomposition per date (eig) or one Cholesky per
             # problem and per adaptive-rho change (chol; the eig form re-forms instead)
             "factorizations": nd if eig is not None else
-            ((gp.ngroups if res.capacitance == "group" else B) + res.refactors)}
+            ((gp.ngroups if res.capacitance == "group" else B) + res.refactors),
+            # the batch as solved (certificates: workloads.window_certificate)
+            "qb": qb, "lr": lr}
     return res, meta

@@ -61,3 +61,20 @@ def usa_panel(sptr_days: np.ndarray, sptr: np.ndarray, n_assets: int = 494, n_ro
     eps = rng.normal(0.0, 0.015, size=(n_rows, n_assets))
     R = np.ascontiguousarray(y[:, None] * beta[None, :] + g[:, sector] + eps)
     return days.astype("datetime64[D]"), R, y
+
+
+def dense_qp(n: int = 2000, T: int = 300, seed: int = 20240315, n_groups: int = 3):
+    """A well-posed dense QP of the kind QuadraticProgram.solve receives (src/qp_problems.py:
+    184-216), for the per-QP drop-in beyond 1024 assets: P = 2 (Sigma + 0.05 mean(diag Sigma)
+    I) (linear_shrinkage, src/covariance.py:71-84, so P is PD and the optimum unique),
+    q = -mu, budget 1'x = 1, box [0, 0.05], and ``n_groups`` group caps G x <= 0.36 (3 groups: feasible, binding).
+    Returns dict(P, q, A, b, G, h, lb, ub)."""
+    rng = np.random.default_rng(seed)
+    X = rng.normal(3e-4, 0.02, size=(T, n)) + rng.normal(0.0, 0.01, size=(T, 1))
+    Xc = X - X.mean(0)
+    S = Xc.T @ Xc / (T - 1)
+    S += 0.05 * np.mean(np.diag(S)) * np.eye(n)
+    grp = rng.integers(0, n_groups, size=n)
+    G = np.stack([(grp == g).astype(float) for g in range(n_groups)])
+    return {"P": 2.0 * S, "q": -X.mean(0), "A": np.ones((1, n)), "b": np.ones(1), "G": G,
+            "h": np.full(n_groups, 0.36), "lb": np.zeros(n), "ub": np.full(n, 0.05)}

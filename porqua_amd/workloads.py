@@ -271,3 +271,14 @@ def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_r
             "max_rel_complementarity": float(comp.item()), "max_dual_sign": float(dsign.item()),
             "problems": int(B),
             "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}
+
+
+def sweep_certificate(panel, res: engine.BatchResult, meta: dict, chunk: int = 128) -> dict:
+    """window_certificate of a porqua_amd.sweep.mean_variance_sweep batch (P = 2 lam Sigma_d,
+    q = -mu_d, budget + box), from the batch as it was solved (``meta['qb']``, ``meta['lr']``)."""
+    qb, lr = meta["qb"], meta["lr"]
+    n, mg = qb.n, qb.mg
+    scale = qb.p_scale * lr.w_scale
+    return window_certificate(panel.R, lr.rows, lr.tlen, lr.mu, scale, qb.q[:, :n], res,
+                              lb=qb.lb[0, :n], ub=qb.ub[0, :n], chunk=chunk, C=qb.Cg[0, :mg, :n],
+                              lg=qb.lg[0, :mg], ug=qb.ug[0, :mg])

@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 from porqua_amd import _lib, engine  # noqa: E402
 from porqua_amd.sweep import mean_variance_sweep  # noqa: E402
 from porqua_amd.synthetic import factor_panel  # noqa: E402
+from porqua_amd.workloads import TrackingBacktest, sweep_certificate  # noqa: E402
 
 
 def timed(fn, steps):
@@ -52,37 +53,21 @@ def summary(res):
 
 
 def config4(dates_limit, steps, dev, overrides=None):
-    n, T, ns, cap = 3000, 252, 20, 0.15
-    dates, R, y, sec = factor_panel(10000, n, n_sectors=ns)
-    ends = np.arange(T - 1, 10000)[:dates_limit]
-    rows, tlen = engine.window_rows(dates, dates[ends], T)
-    pan = engine.Panel(R, y, device=dev)
-    r_d, t_d = pan.rows_to_device(rows, tlen)
-    B = len(ends)
-    G = np.stack([(sec == g).astype(float) for g in range(ns)])
-    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
-                                   G=G, h=np.full(ns, cap), lb=np.zeros(n), ub=np.ones(n), device=dev)
-    qb.batch, qb.P = B, None
-    qb.p_scale = torch.full((B,), 2.0, dtype=torch.float64, device=dev)
-    lr = engine.LowRank(pan, r_d, t_d, mu=None)
-    gp = engine.GroupPlan(rows, tlen, dev)
-    ws = engine.Workspace(qb, dense=False)
+    """The config-4 workload exactly as bench.py --workload config4 and
+    tests/test_full_configs_gpu.py build it (workloads.TrackingBacktest)."""
     settings = engine.Settings.from_params(dict({"rho0_rel": 0.1, "rho0_qrel": 0.0}, **(overrides or {})))
-
+    wl = TrackingBacktest(D=dates_limit, device=dev, settings=settings)
     ev = []
 
     def run():
         ev.clear()
-        xty, _ = pan.gram_xy(r_d, t_d)                 # q = -2 X'y per date, inside the step
-        qb.q = (-2.0 * xty).contiguous()
-        lr.refresh()
-        return engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, events=ev)
+        return wl.step(events=ev)     # q = -2 X'y per date (window products) inside the step
 
     res, dt = timed(run, steps)
     torch.cuda.synchronize()
     return dict({"config": "config4: n=3000 tracking LS, budget + box + 20 sector caps, daily",
-                 "qps": B / dt, "ms_per_step": dt * 1e3, "dates": B, "stage_ms": stage_ms(ev)},
-                **summary(res))
+                 "qps": wl.D / dt, "ms_per_step": dt * 1e3, "dates": wl.D, "stage_ms": stage_ms(ev)},
+                **summary(res), certificate=wl.certificate(res))
 
 
 def stage_ms(events):
@@ -110,7 +95,9 @@ def config5(steps, dev, settings=None, factor="auto"):
         return r
     res, dt = timed(run, steps)
     torch.cuda.synchronize()
+    cert = sweep_certificate(pan, res, meta)
     return dict({"config": "config5: n=5000 mean-variance, 64 monthly dates x 64 risk aversions",
+                 "certificate": cert,
                  "qps": nd * L / dt, "ms_per_step": dt * 1e3, "qps_per_step": nd * L,
                  "capacitance": meta.get("capacitance"), "factorizations_per_step": meta.get("factorizations"),
                  "factor": meta.get("factor"), "stage_ms": stage_ms(ev)}, **summary(res))
