@@ -434,6 +434,30 @@ int pq_wgram_batched(const double* U, int64_t ldu, int64_t su, int32_t k, int32_
  * Replaces nothing in the reference (qpsolvers allocates internally); SURVEY.md §8(b).   */
 int64_t pq_workspace_bytes(int32_t n, int32_t batch, int32_t mg, int32_t path, int32_t tmax, int32_t ldk);
 
+
+/* Batched symmetric eigensolver (two-sided block Jacobi, FP64): the eigendecomposition behind
+ * nearestPD's projection (src/helper_functions.py:42-45: for symmetric B the SVD gives
+ * H = Q |L| Q', so (B + H)/2 = Q max(L, 0) Q') and behind its shift loop's
+ * np.linalg.eigvals (:51-56).  A (ld x ld per matrix, symmetric, overwritten: diagonalised),
+ * entries beyond n ignored (zeroed); V (may be NULL) receives the eigenvectors (columns);
+ * evals[b][0..ld) = diag of the diagonalised A (unsorted; 0 beyond n).  work:
+ * pq_sym_eig_work_doubles(ld) doubles per matrix.  Sweeps of 64 x 64 subproblems (one
+ * workgroup each, cyclic Jacobi in LDS) and MFMA tile updates, until a sweep rotates nothing
+ * (at most max_sweeps; rotation threshold |a_pq| > tol sqrt|a_pp a_qq|).                  */
+int64_t pq_sym_eig_work_doubles(int32_t ld);
+int pq_sym_eig_batched(double* A, int32_t ld, int64_t a_stride, int32_t n, int32_t batch, double* V,
+                       int64_t v_stride, double* evals, int64_t e_stride, double* work, int64_t w_stride,
+                       int32_t max_sweeps, double tol, void* stream);
+
+/* out = V diag(max(evals, 0)) V' (full ld x ld, columns k >= n of V ignored): the PSD
+ * projection A2 of nearestPD (src/helper_functions.py:43-44) on FP64 MFMA.               */
+int pq_psd_form_batched(const double* V, int64_t v_stride, const double* evals, int64_t e_stride, int32_t ld,
+                        int32_t n, int32_t batch, double* out, int64_t o_stride, void* stream);
+
+/* C = op(A) op(B) for ld x ld matrices (ta / tb != 0: transposed), FP64 MFMA tiles.      */
+int pq_tile_gemm_batched(const double* A, int64_t sa, int32_t ta, const double* B, int64_t sb, int32_t tb,
+                         double* C, int64_t sc, int32_t ld, int32_t batch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -133,6 +133,12 @@ _EXPORTS = {
                            ctypes.POINTER(PQSettings), c_int32, c_dp], c_int32),
     "pq_factor_large": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
                          ctypes.POINTER(PQSettings), c_int32, c_dp, c_int64, c_dp], c_int32),
+    "pq_sym_eig_work_doubles": ([c_int32], c_int64),
+    "pq_sym_eig_batched": ([c_dp, c_int32, c_int64, c_int32, c_int32, c_dp, c_int64, c_dp, c_int64, c_dp, c_int64,
+                            c_int32, ctypes.c_double, c_dp], c_int32),
+    "pq_psd_form_batched": ([c_dp, c_int64, c_dp, c_int64, c_int32, c_int32, c_int32, c_dp, c_int64, c_dp], c_int32),
+    "pq_tile_gemm_batched": ([c_dp, c_int64, c_int32, c_dp, c_int64, c_int32, c_dp, c_int64, c_int32, c_int32,
+                              c_dp], c_int32),
     "pq_admm_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,
                          ctypes.POINTER(PQSettings), c_int32, c_dp], c_int32),
     "pq_polish_batched": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,

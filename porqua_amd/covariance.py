@@ -116,7 +116,7 @@ def _pairwise_batch(panel, rows, tlen, out, method, lam_raw, check_pd):
     and nearestPD repair for the dates that need it (src/covariance.py:50-54) -> (S, 0, None,
     None); None when some pair has fewer than 2 common rows (the reference fails there too)."""
     import torch
-    from .helper_functions import nearestPD, pd_info
+    from .helper_functions import nearestPD_device, pd_info_device
     S = panel.cov_pairwise(rows, tlen, out=out)
     n = panel.n
     if bool(torch.isnan(S[:, :n, :n]).any().item()):
@@ -128,12 +128,10 @@ def _pairwise_batch(panel, rows, tlen, out, method, lam_raw, check_pd):
         if lam > 0:
             md = torch.diagonal(S, dim1=1, dim2=2)[:, :n].mean(dim=1)
             S[:, idx, idx] += (lam * md)[:, None]
-    if check_pd:
-        Sn = S[:, :n, :n].cpu().numpy()
-        bad = np.flatnonzero(pd_info(Sn, S.device) != 0)
-        if bad.size:
-            fixed = nearestPD(Sn[bad], S.device)
-            S[torch.from_numpy(bad).to(S.device), :n, :n] = torch.from_numpy(np.ascontiguousarray(fixed)).to(S.device)
+    if check_pd:   # on the device: K2 info for every date, the repair for the failing ones only
+        bad = torch.nonzero(pd_info_device(S, n) != 0).flatten()
+        if bad.numel():
+            S[bad, :n, :n] = nearestPD_device(S[bad], n)[:, :n, :n]
     return S, torch.zeros(B, dtype=torch.float64, device=S.device), None, None
 
 

@@ -6,18 +6,27 @@
 """PD test / repair and small helpers (mirror of src/helper_functions.py:29-83).
 
 ``isPD`` is the batched device Cholesky (K2) info flag.  ``nearestPD`` is the reference's
-Higham / D'Errico repair (src/helper_functions.py:29-58) on the device for a whole batch:
-symmetrise, SVD polar projection onto the PSD cone, and -- while the K2 Cholesky still
-fails -- the shift A3 += I (-lambda_min k^2 + spacing(||A||_F)), k = 1, 2, ...  The SVD and
-the eigenvalues run on the GPU through rocSOLVER (torch.linalg; the repair is a library
-factorisation, not a hot-path kernel), the PD tests on K2.  ``nearestPD_shift`` is the
-cheaper repair used before (a spacing-scaled diagonal shift grown x4 until K2 succeeds);
-for the covariance / Gram inputs on this path both agree to ~1e-15 relative.
+Higham / D'Errico repair (src/helper_functions.py:29-58) on the device for a whole batch,
+entirely in hand-written kernels and without host copies of the matrices:
+  * B = (A + A')/2; the SVD projection H = V' diag(s) V, A2 = (B + H)/2 equals
+    Q max(L, 0) Q' for the symmetric eigendecomposition B = Q L Q' (s = |L|), computed by the
+    batched block-Jacobi eigensolver (pq_sym_eig_batched) and one MFMA product
+    (pq_psd_form_batched); A3 = (A2 + A2')/2;
+  * while K2's Cholesky of A3 fails: A3 += I (-lambda_min k^2 + spacing(||A||_F)), k = 1, 2, ...
+    with lambda_min the smallest eigenvalue of the formed A3 (np.linalg.eigvals in the
+    reference), from the Jacobi eigensolver on Q' A3 Q (warm: nearly diagonal).
+The only host traffic is the per-matrix Cholesky info vector of each loop pass.
+``nearestPD_shift`` is the cheaper repair used before (a spacing-scaled diagonal shift grown
+x4 until K2 succeeds).
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
+
+F64 = torch.float64
 
 
 def to_numpy(data):
@@ -30,14 +39,41 @@ def _as_batch(A):
     return (A[None] if A.ndim == 2 else A), A.ndim == 2
 
 
+def pd_info_device(S: torch.Tensor, n: int, chunk: int = 1024) -> torch.Tensor:
+    """Cholesky info per matrix (0 = positive definite) of the device batch S (B, ld, ld)
+    (symmetric, the lower triangle is read), computed by K2 in chunks of ``chunk`` matrices
+    (the factor workspace is chunk x ld x ld) -> int32 device tensor (B,)."""
+    from . import _lib, engine
+    B = S.shape[0]
+    info = torch.zeros(B, dtype=torch.int32, device=S.device)
+    lib = _lib.load()
+    st = engine.Settings(sigma=0.0).to_c()
+    for s0 in range(0, B, chunk):
+        e0 = min(B, s0 + chunk)
+        qb = engine.QPBatch(n, e0 - s0, 0, device=S.device, has_box=False, P=S[s0:e0])
+        if S.shape[-1] != qb.ld or S.stride(1) != qb.ld:
+            Pp = torch.zeros((e0 - s0, qb.ld, qb.ld), dtype=F64, device=S.device)
+            Pp[:, :n, :n] = S[s0:e0, :n, :n]
+            qb.P = Pp
+        ws = engine.Workspace(qb)
+        pb, sw = qb.c_struct(), ws.c_struct()
+        pb.lb = pb.ub = None
+        strm = engine._stream()
+        _lib.check(lib.pq_init_state(ctypes.byref(pb), ctypes.byref(sw), None, 0, ctypes.byref(st), strm), "init")
+        _lib.check(lib.pq_factor_batched(ctypes.byref(pb), ctypes.byref(sw), None, 0, ctypes.byref(st), 0, strm),
+                   "pq_factor_batched (isPD)")
+        info[s0:e0] = ws.info
+    return info
+
+
 def pd_info(A, device=None) -> np.ndarray:
     """Cholesky info per matrix (0 = positive definite), computed by K2 on the device."""
     from . import engine
     Ab, _ = _as_batch(A)
+    dev = device or engine.default_device()
     n = Ab.shape[-1]
-    qb = engine.QPBatch.from_dense(0.5 * (Ab + np.swapaxes(Ab, 1, 2)), np.zeros(Ab.shape[:2]), device=device)
-    _, info = engine.factor_only(qb)
-    return info.cpu().numpy()[: Ab.shape[0]]
+    S = torch.from_numpy(np.ascontiguousarray(0.5 * (Ab + np.swapaxes(Ab, 1, 2)))).to(dev)
+    return pd_info_device(S, n).cpu().numpy()
 
 
 def isPD(B, device=None) -> bool:
@@ -45,30 +81,89 @@ def isPD(B, device=None) -> bool:
     return bool(np.all(pd_info(B, device) == 0))
 
 
+def sym_eig(A: torch.Tensor, n: int, vectors: bool = True, max_sweeps: int = 30, tol: float = 1e-14):
+    """Symmetric eigendecomposition of the device batch A (B, ld, ld), ld a multiple of 64,
+    by the hand-written block-Jacobi kernels (pq_sym_eig_batched).  A is overwritten
+    (diagonalised).  Returns (evals (B, ld): eigenvalue j of matrix b at evals[b, j], j < n,
+    unsorted; V (B, ld, ld) with the eigenvectors as columns, or None)."""
+    from . import _lib, engine
+    lib = _lib.load()
+    B, ld = A.shape[0], A.shape[-1]
+    if ld % 64 or A.stride(2) != 1 or A.stride(1) != ld:
+        raise ValueError("sym_eig: contiguous (B, ld, ld) with ld a multiple of 64 expected")
+    dev = A.device
+    w = int(lib.pq_sym_eig_work_doubles(ld))
+    work = torch.empty((B, w), dtype=F64, device=dev)
+    V = torch.empty((B, ld, ld), dtype=F64, device=dev) if vectors else None
+    ev = torch.empty((B, ld), dtype=F64, device=dev)
+    for s0 in range(0, B, 65535):
+        e0 = min(B, s0 + 65535)
+        _lib.check(lib.pq_sym_eig_batched(A[s0:].data_ptr(), ld, A.stride(0), n, e0 - s0,
+                                          None if V is None else V[s0:].data_ptr(), ld * ld, ev[s0:].data_ptr(),
+                                          ld, work[s0:].data_ptr(), w, max_sweeps, tol, engine._stream()),
+                   "pq_sym_eig_batched")
+    return ev, V
+
+
+def _tile_gemm(A, ta, B, tb):
+    from . import _lib, engine
+    C = torch.empty_like(A)
+    ld = A.shape[-1]
+    _lib.check(_lib.load().pq_tile_gemm_batched(A.data_ptr(), A.stride(0), int(ta), B.data_ptr(), B.stride(0),
+                                                int(tb), C.data_ptr(), C.stride(0), ld, A.shape[0],
+                                                engine._stream()), "pq_tile_gemm_batched")
+    return C
+
+
+def _spacing(x: torch.Tensor) -> torch.Tensor:
+    """np.spacing for positive finite FP64 values, on the device."""
+    _, e = torch.frexp(x)
+    return torch.ldexp(torch.ones_like(x), (e - 53).to(torch.int32))
+
+
+def nearestPD_device(A: torch.Tensor, n: int, max_attempts: int = 60) -> torch.Tensor:
+    """src/helper_functions.py:29-58 for the device batch A (B, n, n) or (B, ld, ld) (entries
+    beyond n ignored) -> (B, ld, ld) device tensor, ld = round_up(n, 64), zero padded."""
+    from . import _lib, engine
+    B = A.shape[0]
+    ld = engine.round_up(n, 64)
+    dev = A.device
+    An = A[:, :n, :n]
+    Bm = torch.zeros((B, ld, ld), dtype=F64, device=dev)
+    Bm[:, :n, :n] = 0.5 * (An + An.transpose(1, 2))                       # :40
+    spacing = _spacing(torch.linalg.matrix_norm(An, ord="fro"))          # :48 np.spacing(norm(A))
+    W = Bm.clone()
+    ev, V = sym_eig(W, n)                                                # :42 (B = Q L Q')
+    A2 = torch.empty_like(Bm)
+    _lib.check(_lib.load().pq_psd_form_batched(V.data_ptr(), V.stride(0), ev.data_ptr(), ev.stride(0), ld, n, B,
+                                                A2.data_ptr(), A2.stride(0), engine._stream()),
+               "pq_psd_form_batched")                                    # :43-44 (B + H)/2
+    A3 = 0.5 * (A2 + A2.transpose(1, 2))                                 # :45
+    todo = torch.nonzero(pd_info_device(A3, n) != 0).flatten()          # :47 isPD
+    diag = torch.arange(n, device=dev)
+    k = 1
+    while todo.numel() and k <= max_attempts:                            # :51-56
+        At, Vt = A3[todo].contiguous(), V[todo].contiguous()
+        M = _tile_gemm(Vt, 1, _tile_gemm(At, 0, Vt, 0), 0)              # Q' A3 Q: eigvals(A3)
+        M = 0.5 * (M + M.transpose(1, 2))
+        evm, _ = sym_eig(M, n, vectors=False)
+        mineig = evm[:, :n].amin(1)
+        A3[todo[:, None], diag[None, :], diag[None, :]] += (-mineig * k ** 2 + spacing[todo])[:, None]
+        k += 1
+        ok = pd_info_device(A3[todo], n) == 0
+        todo = todo[~ok]
+    return A3
+
+
 def nearestPD(A, device=None, max_attempts: int = 60):
-    """src/helper_functions.py:29-58 on the device, for one matrix or a batch."""
+    """src/helper_functions.py:29-58 on the device, for one matrix or a batch (host arrays
+    in and out; nearestPD_device keeps them on the device)."""
     from . import engine
     Ab, single = _as_batch(A)
     dev = device or engine.default_device()
-    At = torch.from_numpy(np.ascontiguousarray(Ab)).to(dev)
-    B = 0.5 * (At + At.transpose(1, 2))
-    _, s, Vh = torch.linalg.svd(B)                                   # :42
-    H = Vh.transpose(1, 2) @ (s[:, :, None] * Vh)                      # :43  V' diag(s) V
-    A2 = 0.5 * (B + H)                                                 # :44
-    A3 = 0.5 * (A2 + A2.transpose(1, 2))                               # :45
     n = Ab.shape[-1]
-    eye = torch.eye(n, dtype=torch.float64, device=dev)
-    spacing = torch.from_numpy(np.array([np.spacing(np.linalg.norm(Ab[i])) for i in range(len(Ab))])).to(dev)
-    todo = np.flatnonzero(pd_info(A3.cpu().numpy(), dev) != 0)         # :47 isPD
-    k = 1
-    while todo.size and k <= max_attempts:                             # :51-56
-        t = torch.from_numpy(todo).to(dev)
-        mineig = torch.linalg.eigvalsh(A3[t]).amin(1)                  # symmetric: eigvals are real
-        A3[t] += eye[None] * (-mineig * k ** 2 + spacing[t])[:, None, None]
-        k += 1
-        ok = pd_info(A3[t].cpu().numpy(), dev) == 0
-        todo = todo[~ok]
-    out = A3.cpu().numpy()
+    A3 = nearestPD_device(torch.from_numpy(np.ascontiguousarray(Ab)).to(dev), n, max_attempts)
+    out = A3[:, :n, :n].cpu().numpy()
     return out[0] if single else out
 
 

@@ -196,3 +196,88 @@ def qp_ipm_batched(P, q, A=None, b=None, G=None, h=None, lb=None, ub=None, tol: 
     res.z_box = best_zb
     res.Px = Pb
     return res
+
+
+def active_set_polish(P, q, A, b, G, h, lb, ub, x, y, z, zb, rounds: int = 8):
+    """Exact solve on the active set detected at an interior-point answer, for ONE problem
+    (device tensors; y, z, zb in qpsolvers' signs: P x + q + A'y + G'z + z_box = 0).  The
+    interior-point iterate stops at merit ~1e-9 with its weights accurate to ~1e-4 near
+    degenerate faces; the reduced system [P_FF C_F'; C_F 0] on the free set F and the active
+    rows C = [A; G_act] (P_FF factored and inverted on K2 / K2L, the rows bordered by a small
+    Schur system, one step of iterative refinement) gives the optimum to rounding.  A short
+    primal-dual active-set loop corrects the classification (the oracle's refinement,
+    oracle/qp_ipm.py).  Returns (x, y, z, z_box, ok); ok False (P_FF not PD: the optimal
+    face is not a point, or no consistent active set within ``rounds``) leaves the caller's
+    iterate in place."""
+    dev = q.device
+    n = q.numel()
+    me = 0 if A is None else A.shape[0]
+    mi = 0 if G is None else G.shape[0]
+    sc = float(max(P.abs().max().item(), q.abs().max().item(), 1e-300))
+    Ps, qs = P / sc, q / sc
+    inf = torch.full((n,), np.inf, dtype=F64, device=dev)
+    lo = -inf if lb is None else lb
+    up = inf if ub is None else ub
+    at_lo = torch.isfinite(lo) & ((x - lo) < -zb)
+    at_up = torch.isfinite(up) & ((up - x) < zb) & ~at_lo
+    act = ((h - G @ x) < z) if mi else torch.zeros(0, dtype=torch.bool, device=dev)
+    tol = 1e-12 * (1.0 + float(qs.abs().max().item()))
+    for _ in range(rounds):
+        fixed = at_lo | at_up
+        xb = torch.where(at_lo, lo, torch.where(at_up, up, torch.zeros_like(x)))
+        F = torch.nonzero(~fixed).flatten()
+        nF = int(F.numel())
+        C = torch.cat([A if me else torch.zeros((0, n), dtype=F64, device=dev),
+                       G[act] if mi else torch.zeros((0, n), dtype=F64, device=dev)])
+        d = torch.cat([b if me else torch.zeros(0, dtype=F64, device=dev),
+                       h[act] if mi else torch.zeros(0, dtype=F64, device=dev)])
+        m = C.shape[0]
+        if nF == 0:
+            return x, y, z, zb, False
+        PFF = Ps[F][:, F].contiguous()
+        rF = -(qs + Ps @ xb)[F]
+        dF = d - C @ xb
+        CF = C[:, F].contiguous()
+        fac = _NormalFactor(1, nF, dev)
+        if bool(fac.factor(PFF[None], 0.0, retries=0).any()):
+            return x, y, z, zb, False
+        HiC = fac.solve_mat(CF.T[None].contiguous())[0] if m else None
+
+        def solve(f, g):
+            hf = fac.solve_mat(f[None, :, None].contiguous())[0, :, 0]
+            if not m:
+                return hf, torch.zeros(0, dtype=F64, device=dev)
+            S = (CF @ HiC).cpu().numpy()
+            lam = np.linalg.lstsq(S, (CF @ hf - g).cpu().numpy(), rcond=1e-13)[0]
+            lam = torch.from_numpy(lam).to(dev)
+            return hf - HiC @ lam, lam
+
+        xF, lam = solve(rF, dF)
+        e1 = rF - (PFF @ xF + (CF.T @ lam if m else 0.0))
+        e2 = dF - CF @ xF if m else dF
+        cx, cl = solve(e1, e2)
+        xF, lam = xF + cx, lam + cl
+        xn = xb.clone()
+        xn[F] = xF
+        g = Ps @ xn + qs + (C.T @ lam if m else 0.0)
+        zbn = torch.where(fixed, -g, torch.zeros_like(g))
+        viol_lo = ~fixed & (xn < lo - 1e-13)
+        viol_up = ~fixed & (xn > up + 1e-13)
+        bad_lo = at_lo & (zbn > tol)
+        bad_up = at_up & (zbn < -tol)
+        zG = torch.zeros(mi, dtype=F64, device=dev)
+        if mi:
+            zG[act] = lam[me:]
+            viol_G = ~act & ((G @ xn - h) > 1e-13)
+            bad_G = act & (zG < -tol)
+        else:
+            viol_G = bad_G = torch.zeros(0, dtype=torch.bool, device=dev)
+        flags = torch.stack([v.any() for v in (viol_lo, viol_up, bad_lo, bad_up)] +
+                            ([viol_G.any(), bad_G.any()] if mi else []))
+        if not bool(flags.any()):
+            return xn, lam[:me] * sc, zG * sc, zbn * sc, True
+        at_lo = (at_lo & ~bad_lo) | viol_lo
+        at_up = (at_up & ~bad_up) | viol_up
+        if mi:
+            act = (act & ~bad_G) | viol_G
+    return x, y, z, zb, False

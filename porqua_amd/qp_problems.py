@@ -288,7 +288,30 @@ def _solve_batch_ipm(P, q, A, b, G, h, lb, ub, device=None):
 
     bb = None if A is None else rows(b, A.shape[0])
     hh = None if G is None else rows(h, G.shape[0])
-    res = qp_ipm_batched(T(P), T(q), T(A), T(bb), T(G), T(hh), T(lb), T(ub))
+    Pd, qd, Ad, bd, Gd, hd, lbd, ubd = T(P), T(q), T(A), T(bb), T(G), T(hh), T(lb), T(ub)
+    res = qp_ipm_batched(Pd, qd, Ad, bd, Gd, hd, lbd, ubd)
+    # active-set polish of every answer (exact on the detected face when P_FF is PD)
+    from .ipm import active_set_polish
+    polished = np.zeros(B, dtype=bool)
+    if res.z is None:
+        res.z = torch.zeros((B, 0), dtype=torch.float64, device=dev)
+    for i in range(B):
+        if int(res.status[i]) not in (_lib.PQ_SOLVED, _lib.PQ_SOLVED_INACCURATE):
+            continue
+        xi, yi, zi, zbi, ok = active_set_polish(Pd[i], qd[i], Ad, None if bd is None else bd[i], Gd,
+                                                None if hd is None else hd[i], lbd, ubd, res.x[i], -res.lam[i],
+                                                res.z[i], res.z_box[i])
+        if ok:
+            polished[i] = True
+            res.x[i], res.lam[i], res.z_box[i] = xi, -yi, zbi
+            if Gd is not None:
+                res.z[i] = zi
+            res.status[i] = _lib.PQ_SOLVED
+            Pxi = Pd[i] @ xi
+            res.Px[i] = Pxi
+            res.obj[i] = 0.5 * (xi @ Pxi) + qd[i] @ xi
+    if Gd is None:
+        res.z = None
     x = res.x.cpu().numpy()
     st = res.status.cpu().numpy()
     it = res.iters.cpu().numpy()
@@ -311,7 +334,8 @@ def _solve_batch_ipm(P, q, A, b, G, h, lb, ub, device=None):
         s.obj = float(obj[i]) if s.found else None
         s._prim, s._dual, s._gap = float(prim[i]), float(dual[i]), float(gap[i])
         s.extras = {"solver": "device IPM" + (" (K2L, n > 1024)" if n > DENSE_ADMM_MAX_N else
-                                             " (more than 64 general rows)"), "merit": float(merit[i])}
+                                             " (more than 64 general rows)"), "merit": float(merit[i]),
+                    "active_set_polish": bool(polished[i])}
         if not s.found:
             s.x = None
         sols.append(s)

@@ -210,8 +210,8 @@ def test_backtest_lowrank_path_matches_oracle(device, kind):
 
 
 def test_nearest_pd_higham_on_device_matches_reference(device):
-    """nearestPD (src/helper_functions.py:29-58) on the device: the SVD polar projection and
-    the eigenvalue shifts run through rocSOLVER, the PD tests on K2.  Checked against the
+    """nearestPD (src/helper_functions.py:29-58) on the device: the projection and the
+    eigenvalue shifts on the hand-written block-Jacobi eigensolver, the PD tests on K2.  Checked against the
     reference's repaired covariance (golden) and against the oracle restatement on
     genuinely indefinite matrices, where the projection and several shifts act."""
     g = load_golden("cov_cases")
