@@ -476,7 +476,9 @@ __global__ __launch_bounds__(PT) void k_polish_w(pq_lowrank lr, pq_problem pb, p
   // ADMM point left config 4's budget row outside the 1e-10 equality check on every date,
   // and the second active-set round that followed (new capacitance, Cholesky, Z) cost 1.5x
   // the extra step (polish 33 -> 22 ms per 2000 dates).  A converged step breaks early.
-  // (Compact mode keeps s.refine_iters: it must agree with the grouped polish, polish_g.hip.)
+  // Compact mode takes s.refine_iters steps as given: the caller chooses them (the grouped
+  // polish's own dates take 1; the dates it hands to this kernel are relaunched with at least
+  // 2, engine.solve_lowrank polish_grouped, so those may take more steps than grouped dates).
   const int refine_steps = max(s.refine_iters, 2);
   // Woodbury mode (free set beyond the compact scratch) needs the T x T capacitance to fit
   const bool wood_ok = ((lr.tmax + TB - 1) / TB) * TB <= ldk && lr.tmax <= KMAX;

@@ -49,7 +49,7 @@ class Settings:
     diag P, adapted every 60 iterations: no refactorisation on the n = 1000 min-variance
     windows, tests/engine_model.py), the stopping tolerance and the polish settings.  ADMM
     only has to reach an approximate point whose active set the polish can correct: measured
-    on config 3 (round 2 kernels, tools/gpu_exp3.sh) eps 2e-3 gives 20 ADMM iterations +
+    on config 3 (round 2 kernels, bench.py --set eps_abs=... eps_rel=...) eps 2e-3 gives 20 ADMM iterations +
     2.7 polish rounds against 21 + 2.6 at 1e-3 and 18 + 2.9 at 4e-3 (about 2 % apart; configs
     2, 4 and 5 also gain), alpha 1.7 / 1.8 trade 10 / 29 more ADMM iterations for 0.7 / 1.5
     fewer polish rounds and lose; round 1 measured 1e-3 against 1e-4 (95.7k vs 85.1k QPs/s).
@@ -822,7 +822,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         if m:
             ws.pg_fallback = fb   # the dates handed to the per-date kernel (diagnostics)
             # two refinement steps per round for the hand-offs (vertex cycling, failed
-            # factorisations): config 5's fallback polish 33 -> 4 ms (tools/gpu_refine_g.sh)
+            # factorisations): config 5's fallback polish 31.3 -> 7.5 ms
+            # (profiles/r02k_bench_config5_qrel30.log -> r02l_bench_config5_fallback_refine2.log)
             sfb = type(s).from_buffer_copy(s)
             sfb.refine_iters = max(sfb.refine_iters, 2)
             polish_w(fb.contiguous(), m, ctypes.byref(sfb), name="polish (fallback, inside polish)")

@@ -131,8 +131,25 @@ class _Coupling:
         nf = self.nf
         _lib.check(lib.pq_factor_batched(ctypes.byref(nf.pb), ctypes.byref(nf.st), None, 0,
                                          ctypes.byref(nf.s), 2, stream), "pq_factor_batched (l1 coupling)")
+        # a breakdown (rounding, barrier weights spread over ~1e24) is refactored with a
+        # growing diagonal shift, like the LAD / Woodbury normal matrices (lad._NormalFactor,
+        # woodbury.NormalM): the shifted inverse is only the preconditioner of ``solve``,
+        # which refines against the exact S, so the direction stays exact
+        bad = nf.ws.info != 0
+        kk = torch.arange(self.k, device=P.device)
+        for attempt in range(3):
+            if not bool(bad.any()):          # host sync: one small flag
+                break
+            idx = torch.nonzero(bad).flatten()
+            d = P[idx[:, None], kk[None, :], kk[None, :]]
+            P[idx[:, None], kk[None, :], kk[None, :]] = d + (1e-12 * 1e4 ** attempt) * d.abs().amax(1, keepdim=True).clamp(min=1e-300)
+            idx32 = idx.to(torch.int32).contiguous()
+            _lib.check(lib.pq_factor_batched(ctypes.byref(nf.pb), ctypes.byref(nf.st), idx32.data_ptr(),
+                                             int(idx32.numel()), ctypes.byref(nf.s), 2, stream),
+                       "pq_factor_batched (l1 coupling, shifted)")
+            bad[idx] = nf.ws.info[idx] != 0
         self.Minv = nf.ws.K[:, :self.k, :self.k]
-        return nf.ws.info != 0
+        return bad
 
     def split(self, y):
         k0 = self.k0

@@ -135,9 +135,13 @@ def term_from_model(constraints, params, universe):
         x_init = np.array([x0.get(a, 0) for a in universe], dtype=np.float64)
         tc = params.get("transaction_cost")
         if tc is not None and tocon and not tc:
-            # the reference applies BOTH linearisations here (tc is not None, and `not 0` is
-            # True, src/optimization.py:131-137): a zero-cost term plus the budget -- the
-            # budget form's optimum
+            # INTENTIONAL DIFFERENCE from the reference: with transaction_cost == 0 it applies
+            # BOTH linearisations (tc is not None, and `not 0` is True,
+            # src/optimization.py:131-137); the second one sizes its rows for the already
+            # extended 2N variables (src/qp_problems.py:40-59), leaving G with m + 6N + 1 rows
+            # against h with m + 4N + 1 entries, which qpsolvers rejects -- the reference has
+            # no answer here.  The engine solves the intended problem: the turnover budget
+            # with a zero cost (the budget form)
             term = L1Split("budget", x_init, tocon["rhs"])
         elif tc is not None:
             term = L1Split("cost", x_init, tc)

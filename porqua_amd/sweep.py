@@ -35,7 +35,7 @@ from . import engine
 EIG_MIN_PER_DATE = 192   # factor='auto': eigen form from this many problems per date
 # |q| floor of the initial rho for the sweep (engine.Settings.rho0_qrel, default 10): its
 # small risk aversions are nearly linear.  Measured at the config-5 shape
-# (tools/gpu_exp5.sh): 3 -> 1826 max ADMM iterations, 10 -> 55, 30 -> 34 (27.8k -> 32.8k
+# (tools/bench_configs.py --only 5 --set rho0_qrel=...): 3 -> 1826 max ADMM iterations, 10 -> 55, 30 -> 34 (27.8k -> 32.8k
 # QPs/s), 60 -> 26, 100 -> problems fall to the eps_retry ADMM; 30 keeps a factor 3 from both
 # cliffs.  (A single mean-variance backtest at risk aversion 1 is faster at 10.)
 SWEEP_RHO0_QREL = 30.0
