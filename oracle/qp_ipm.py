@@ -160,6 +160,34 @@ class _KKT:
         return x + cx, (y + cy if me else np.zeros(0))
 
 
+def _kkt_solve_indefinite(H, A, r1, r2):
+    """[H A'; A 0] [x; y] = [r1; r2] by LAPACK's symmetric-indefinite solver (sysv), raising
+    (LinAlgError / LinAlgWarning) instead of returning an ill-conditioned answer."""
+    import warnings
+    n, me = H.shape[0], A.shape[0]
+    K = np.zeros((n + me, n + me))
+    K[:n, :n] = H
+    K[:n, n:] = A.T
+    K[n:, :n] = A
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", sla.LinAlgWarning)
+        sol = sla.solve(K, np.concatenate([r1, r2]), assume_a="sym")
+    if not np.all(np.isfinite(sol)):
+        raise sla.LinAlgError("non-finite KKT solution")
+    return sol[:n], sol[n:]
+
+
+def _kkt_solve_lstsq(H, A, r1, r2):
+    """Minimum-norm least-squares solution of [H A'; A 0] [x; y] = [r1; r2] (SVD-based)."""
+    n, me = H.shape[0], A.shape[0]
+    K = np.zeros((n + me, n + me))
+    K[:n, :n] = H
+    K[:n, n:] = A.T
+    K[n:, :n] = A
+    sol = np.linalg.lstsq(K, np.concatenate([r1, r2]), rcond=None)[0]
+    return sol[:n], sol[n:]
+
+
 def _kkt_solve(H, A, r1, r2, reg=0.0, shift=True, D=None):
     """One solve with a fresh _KKT factor."""
     return _KKT(H, A, reg=reg, shift=shift, D=D).solve(r1, r2)
@@ -367,12 +395,20 @@ def _refine_active_set(sol: OracleSolution, max_rounds: int = 30):
         d = np.concatenate(rhsC) if rhsC else np.zeros(0)
         rF = -q[F] - (P[np.ix_(F, Bi)] @ xb[Bi] if len(Bi) else 0.0)
         dF = d - (C[:, Bi] @ xb[Bi] if len(Bi) else 0.0)
-        try:   # exact solves only: a singular P_FF means the optimal face is not a point
+        try:   # exact solves only
             xF, lam = _kkt_solve(P[np.ix_(F, F)], C[:, F] if C.shape[0] else None, rF, dF, shift=False)
         except SingularKKT:
-            sol.extras["refined"] = False
-            sol.extras["refine_skipped"] = "P_FF singular on the detected face (non-unique optimum)"
-            return
+            # P_FF singular: the bordered system can still be nonsingular when the active rows
+            # pin the null directions down (e.g. the auxiliary variables of the l1
+            # linearisations, P = 0 on them); solved by a symmetric-indefinite factorisation.
+            # If that is singular too, the optimal face is not a point (e.g. x+ and x- of the
+            # leverage split both positive for an asset): the minimum-norm least-squares
+            # solution of the consistent system is one exact point of the face.  Either way
+            # the candidate is kept only if it improves the KKT residuals (below).
+            try:
+                xF, lam = _kkt_solve_indefinite(P[np.ix_(F, F)], C[:, F], rF, dF)
+            except (sla.LinAlgError, sla.LinAlgWarning, ValueError):
+                xF, lam = _kkt_solve_lstsq(P[np.ix_(F, F)], C[:, F], rF, dF)
         xn = xb.copy()
         xn[F] = xF
         y = lam[:me] if me else None

@@ -259,8 +259,11 @@ def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_r
         cp = torch.maximum((zb.clamp(max=0) * (x - lb)).abs().amax(1), (zb.clamp(min=0) * (ub - x)).abs().amax(1))
         if bool((~eq).any()):
             ye = y[:, ~eq]
-            cg = torch.maximum((ye.clamp(min=0) * (ug[~eq] - cx[:, ~eq])).abs(),
-                               (ye.clamp(max=0) * (cx[:, ~eq] - lg[~eq])).abs()).amax(1)
+            ugf = torch.where(torch.isfinite(ug[~eq]), ug[~eq], torch.zeros_like(ug[~eq]))
+            lgf = torch.where(torch.isfinite(lg[~eq]), lg[~eq], torch.zeros_like(lg[~eq]))
+            # a multiplier of the right sign at an infinite bound is caught by max_dual_sign
+            cg = torch.maximum((ye.clamp(min=0) * (ugf - cx[:, ~eq]) * torch.isfinite(ug[~eq])).abs(),
+                               (ye.clamp(max=0) * (cx[:, ~eq] - lgf) * torch.isfinite(lg[~eq])).abs()).amax(1)
             cp = torch.maximum(cp, cg)
             # a one-sided row (lg = -inf) must carry y >= 0, (ug = +inf) y <= 0
             ws = torch.maximum((-ye).clamp(min=0) * torch.isinf(lg[~eq]), ye.clamp(min=0) * torch.isinf(ug[~eq]))

@@ -58,4 +58,4 @@ def test_psd_projection_of_rank_deficient_covariance(device):
                                                 out.data_ptr(), out.stride(0), engine._stream()), "psd_form")
     L, Q = np.linalg.eigh(S)
     ref = (Q * np.maximum(L, 0)) @ Q.T
-    assert np.abs(out[0, :n, :n].cpu().numpy() - ref).max() <= 1e-12 * np.abs(S).max()
+    assert np.abs(out[0, :n, :n].cpu().numpy() - ref).max() <= 5e-13 * (ld // 32) * np.abs(S).max()
