@@ -356,7 +356,13 @@ def test_device_backtest_turnover_and_leverage_window_path():
         qp.linearize_leverage_constraint(N=n, leverage_budget=1.2)
         o = solve_qp(qp["P"], qp["q"], G=qp["G"], h=qp["h"], A=qp["A"], b=qp["b"], lb=qp["lb"], ub=qp["ub"])
         f = lambda x: 0.5 * x @ P @ x + q @ x                # noqa: E731
-        assert abs(f(W[i]) - f(o.x[:n])) <= 1e-7 * max(abs(f(o.x[:n])), 1e-6), (i, f(W[i]), f(o.x[:n]))
+        # the linearised problem's optimal face is not a point (auxiliary variables), and the
+        # oracle IPM's duality gap floors near 1e-7 relative there (its active-set refinement
+        # does not apply): the device answer (feasible, checked below) may only be LOWER than
+        # the oracle's by more than 1e-7, and sits within the north_star's 1e-6 bar either way
+        fo, fw = f(o.x[:n]), f(W[i])
+        assert fw - fo <= 1e-7 * max(abs(fo), 1e-6), (i, fw, fo)
+        assert abs(fw - fo) <= 1e-6 * max(abs(fo), 1e-6), (i, fw, fo)
         assert np.abs(W[i] - o.x[:n]).max() < 1e-6, (i, np.abs(W[i] - o.x[:n]).max())
         assert np.abs(W[i]).sum() <= 1.2 + 1e-7 and np.abs(W[i] - w0).sum() <= 0.5 + 1e-7
         assert abs(W[i].sum() - 1) < 1e-8 and W[i].min() > -0.02 - 1e-8 and W[i].max() < 0.05 + 1e-8
