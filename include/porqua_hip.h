@@ -286,7 +286,10 @@ int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
  *                      per-date M_b^-1 symv replaced by one MFMA GEMM with M_U^-1 per
  *                      group plus the small per-date correction.  Adaptive rho is decided
  *                      per group (NEED_REFACTOR for all its running dates, grho updated).
- * Centred windows (lr->mu != NULL), shared general rows (mg <= 4), uniform ADMM diagonal.
+ * Centred windows (lr->mu != NULL: MeanVariance) or uncentred (lr->mu == NULL: the
+ * LeastSquares tracking of src/optimization.py:206-226, no mean column), shared general rows
+ * (mg <= 4 register-resident; 4 < mg <= 24 in the column-sparse form cg_nzr / cg_nzv with
+ * nzmax <= 4, as for pq_admm_lr_grouped; U + mg <= 320), uniform ADMM diagonal.
  * Replaces qpsolvers.solve_problem (src/qp_problems.py:211-214) for the batched backtest. */
 typedef struct pq_gcap {
   const int32_t* gdates; int32_t ngroups;
@@ -305,7 +308,7 @@ int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, co
                     int32_t r0, const double* pc, int64_t ldpc, void* stream);
 int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
                     const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc, int32_t r0,
-                    const double* cc, void* stream);
+                    const double* cc, const int32_t* cg_nzr, const double* cg_nzv, int32_t nzmax, void* stream);
 
 /* K2, eigen form (the risk-aversion x date sweep, BASELINE configs[4]): M_b^-1 of every
  * problem b (or idx[0..nidx)) of the window path from ONE symmetric eigendecomposition per

@@ -171,7 +171,7 @@ _EXPORTS = {
                          c_dp, c_int64, c_dp], c_int32),
     "pq_admm_lr_gcap": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                          ctypes.POINTER(PQGcap), ctypes.POINTER(PQSettings), c_int32, c_dp, c_int64, c_int32, c_dp,
-                         c_dp], c_int32),
+                         c_dp, c_dp, c_int32, c_dp], c_int32),
     "pq_eigcap_form": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                         ctypes.POINTER(PQSettings), c_dp, c_dp, c_dp, c_dp, c_dp, c_int32, c_dp, c_int32, c_dp,
                         c_int64, c_dp, c_dp], c_int32),

@@ -40,7 +40,10 @@ constexpr int CTP2 = 6;        // GEMM row tiles per wave (U + mg <= 324: 21 til
 constexpr int CG_MAX = 16;     // dates per group (MFMA N)
 constexpr int CU_MAX = 320;    // union rows per group
 constexpr int CMG = 4;         // general rows (register-resident, fused form)
-constexpr int CK_MAX = CU_MAX + CMG;   // capacitance rows
+constexpr int CMGW = 24;       // general rows, wide form: column-sparse Cg (budget + sector caps)
+constexpr int CNZ = 4;         // wide form: nonzeros per Cg column
+constexpr int CP1_ROWS = 16 * CNW * CTP1;   // pass-1 MFMA rows: U + mg <= 320
+constexpr int CK_MAX = CP1_ROWS + 4;     // capacitance rows (U + mg <= 320)
 constexpr int CH_MAX = 64;     // m + 1 = U - T + 1 <= 64
 
 #ifdef PQ_PROFILE
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(256) void k_gcap_assemble(pq_lowrank lr, pq_problem
                                                        const double* band, int64_t ldo, int r0, const double* pc,
                                                        int64_t ldpc, const double* cc) {
   __shared__ int s_w[CU_MAX];
-  __shared__ double s_sr[CMG];
+  __shared__ double s_sr[CMGW];
   const int grp = blockIdx.x;
   const int d0 = gc.gdates[grp];
   const int U = gc.ucnt[grp], mg = pb.mg, k_ld = gc.k_ld;
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(PT_PREP) void k_gcap_prep(pq_lowrank lr, pq_problem
   constexpr int HP = CH_MAX + 1;
   __shared__ double H[CH_MAX * HP];
   __shared__ double X[CH_MAX * CH_MAX];
-  __shared__ double s_mm[CG_MAX], s_aq[CG_MAX], s_sr[CMG];
+  __shared__ double s_mm[CG_MAX], s_aq[CG_MAX], s_sr[CMGW];
   __shared__ int s_off[CG_MAX], s_T[CG_MAX];
   const int slot = xcd_slot(blockIdx.x, gridDim.x);
   const int grp = idx ? idx[slot] : slot;
@@ -164,8 +167,11 @@ __global__ __launch_bounds__(PT_PREP) void k_gcap_prep(pq_lowrank lr, pq_problem
   const int ktile = (kU + 15) >> 4;
   for (int e = t; e < (CK_MAX + 16) * CG_MAX; e += PT_PREP) s_a[e] = 0.0;
   __syncthreads();
-  // ---- A: a_b for every date (wave per union row; the row of G_U in registers) ------------
-  for (int u = w; u < U; u += PW_PREP) {
+  // ---- A: a_b for every date (wave per union row; the row of G_U in registers).  Uncentred
+  //      windows (lr.mu null, LeastSquares): no mean column, a_b = q_b = 0 and H_b's last
+  //      row / column is the unit vector ------------------------------------------------------
+  const bool centred = lr.mu != nullptr;
+  for (int u = w; centred && u < U; u += PW_PREP) {
     double gv[CU_MAX / 64];
 #pragma unroll
     for (int j = 0; j < CU_MAX / 64; ++j) {
@@ -184,7 +190,7 @@ __global__ __launch_bounds__(PT_PREP) void k_gcap_prep(pq_lowrank lr, pq_problem
       if (l == 0) s_a[u * CG_MAX + gg] = g.sqc * sum / s_T[gg];
     }
   }
-  for (int e = w; e < mg * G; e += PW_PREP) {   // general rows: sqrt(R_r) Cg_r mu_b = sqrt(R_r) (1/T) sum PC
+  for (int e = w; centred && e < mg * G; e += PW_PREP) {   // general rows: sqrt(R_r) Cg_r mu_b = sqrt(R_r) (1/T) sum PC
     const int r = e / G, gg = e % G;
     double sum = 0.0;
     for (int tt = l; tt < s_T[gg]; tt += 64) sum += pc[(int64_t)s_w[s_off[gg] + tt] * ldpc + r];
@@ -229,9 +235,11 @@ __global__ __launch_bounds__(PT_PREP) void k_gcap_prep(pq_lowrank lr, pq_problem
     A[k_ld + u] = u < kU ? s_q[u * CG_MAX + gg] : 0.0;
   }
   for (int gg = w; gg < G; gg += PW_PREP) {
-    const double* mu = lr.mu + (int64_t)(d0 + gg) * lr.mu_stride;
     double mm = 0.0, aq = 0.0;
-    for (int i = l; i < n; i += 64) mm = fma(mu[i], mu[i], mm);
+    if (centred) {
+      const double* mu = lr.mu + (int64_t)(d0 + gg) * lr.mu_stride;
+      for (int i = l; i < n; i += 64) mm = fma(mu[i], mu[i], mm);
+    }
     for (int u = l; u < kU; u += 64) aq = fma(s_a[u * CG_MAX + gg], s_q[u * CG_MAX + gg], aq);
     mm = wave_sum(mm);
     aq = wave_sum(aq);
@@ -336,12 +344,17 @@ __global__ __launch_bounds__(PT_PREP) void k_gcap_prep(pq_lowrank lr, pq_problem
 }
 
 // ---- the ADMM iterations -------------------------------------------------------------------
-// MGC: general rows compiled in (0 for box-only problems: no Cg registers in the epilogue)
+// MGC: general rows compiled in (0 for box-only problems: no Cg registers in the epilogue;
+// CMGW: the wide form, up to 24 shared rows read column-sparse -- cg_nzr / cg_nzv, nzmax <= CNZ
+// nonzeros per asset, e.g. the budget plus one 0/1 sector membership -- instead of as
+// register-resident columns)
 template <int MGC>
 __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
                                                   pq_settings s, int iters_call, const double* pc, int64_t ldpc,
-                                                  int r0, const double* cc) {
-  constexpr int MGG = 8;
+                                                  int r0, const double* cc, const int32_t* cg_nzr,
+                                                  const double* cg_nzv, int nzmax) {
+  constexpr bool WIDE = MGC > CMG;
+  constexpr int MGG = WIDE ? CMGW : 8;
   __shared__ __attribute__((aligned(16))) double WU[(CU_MAX + 4) * CG_MAX];
   double* const UT = WU;
   __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX], g_qmax[CG_MAX], g_coef[CG_MAX];
@@ -349,12 +362,14 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   constexpr int NPART = 5;                    // per wave and date: 4 maxima, mu.V
   __shared__ double g_part[CNW * CG_MAX * NPART];
   __shared__ double g_gm[CG_MAX * 3];
-  __shared__ double g_zg[CG_MAX * MGG], g_yg[CG_MAX * MGG], g_rg[CG_MAX * MGG], g_lg[CG_MAX * MGG],
-      g_ug[CG_MAX * MGG], g_cgv[CG_MAX * MGG], g_cgx[CG_MAX * MGG], g_wg[CG_MAX * MGG],
-      g_cw[CG_MAX * MGG], g_zt[CG_MAX * MGG], g_rgz[CG_MAX * MGG], g_cmu[CG_MAX * MGG];
+  // per (date, row); the rows' bounds and rho are shared by the group's dates
+  __shared__ double g_zg[CG_MAX * MGG], g_yg[CG_MAX * MGG], g_cgv[CG_MAX * MGG], g_cgx[CG_MAX * MGG],
+      g_wg[CG_MAX * MGG], g_cw[CG_MAX * MGG], g_rgz[CG_MAX * MGG], g_cmu[CG_MAX * MGG];
+  __shared__ double g_rg[MGG], g_lg[MGG], g_ug[MGG];
+  double* const g_zt = g_rgz;   // Cg x~ of (date, row): read, then overwritten by rho z~, by one lane
   __shared__ int g_act[CG_MAX], g_it[CG_MAX], g_end[CG_MAX], g_stat[CG_MAX], g_off[CG_MAX], g_T[CG_MAX];
   __shared__ int s_urow[CU_MAX];
-  __shared__ double s_sr[CMG];
+  __shared__ double s_sr[MGG];
   __shared__ double s_rho;
   __shared__ int s_any;
 
@@ -366,6 +381,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int n = pb.n, ld = pb.ld, mg = pb.mg, k_ld = gc.k_ld;
   const int kU = U + mg;
   const bool has_box = pb.lb != nullptr;
+  const bool centred = lr.mu != nullptr;   // null: uncentred windows (mu = 0 throughout)
   const double sigma = s.sigma, alpha = s.alpha;
   const double* Mi = gc.Minv + (int64_t)grp * gc.M_stride;
 #ifdef PQ_PROFILE
@@ -399,20 +415,20 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
   for (int e = t; e < CG_MAX * MGG; e += CT) {
     const int g = e / MGG, r = e % MGG;
-    double zg = 0, yg = 0, lgv = 0, ugv = 0, rg = 0;
+    double zg = 0, yg = 0;
     if (g < G && r < mg) {
       const int b = d0 + g;
       zg = st.z[(int64_t)b * st.m_ld + r];
       yg = st.y[(int64_t)b * st.m_ld + r];
-      lgv = pb.lg[r];
-      ugv = pb.ug[r];
-      rg = crho(lgv, ugv, rho, s);
     }
     g_zg[e] = zg;
     g_yg[e] = yg;
-    g_lg[e] = lgv;
-    g_ug[e] = ugv;
-    g_rg[e] = rg;
+  }
+  if (t < MGG) {
+    const bool ok = t < mg;
+    g_lg[t] = ok ? pb.lg[t] : 0.0;
+    g_ug[t] = ok ? pb.ug[t] : 0.0;
+    g_rg[t] = ok ? crho(pb.lg[t], pb.ug[t], rho, s) : 0.0;
   }
   __syncthreads();
 
@@ -423,7 +439,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const double* __restrict__ lo_h = has_box ? pb.lb + (int64_t)hb * pb.box_stride : nullptr;  \
   const double* __restrict__ up_h = has_box ? pb.ub + (int64_t)hb * pb.box_stride : nullptr;  \
   const double* __restrict__ Cg_h = mg ? pb.Cg : nullptr;                                     \
-  const double* __restrict__ mu_h = lr.mu + (int64_t)hb * lr.mu_stride;                       \
+  const double* __restrict__ mu_h = centred ? lr.mu + (int64_t)hb * lr.mu_stride : nullptr;   \
   double* __restrict__ x_h = st.x + (int64_t)hb * ld;                                         \
   double* __restrict__ Px_h = st.Px + (int64_t)hb * ld;                                       \
   double* __restrict__ zb_h = st.z + (int64_t)hb * st.m_ld + st.mg_pad;                       \
@@ -443,7 +459,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       double a = 0.0, am = 0.0;
       for (int i = hl; i < n; i += 32) {
         a = fma(Cg_h[(int64_t)r * ld + i], x_h[i], a);
-        am = fma(Cg_h[(int64_t)r * ld + i], mu_h[i], am);
+        if (centred) am = fma(Cg_h[(int64_t)r * ld + i], mu_h[i], am);
       }
       a = csum32(a);
       am = csum32(am);
@@ -452,22 +468,32 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         g_cmu[g * MGG + r] = am;
       }
     }
-    if (hl < mg) g_wg[g * MGG + hl] = g_rg[g * MGG + hl] * g_zg[g * MGG + hl] - g_yg[g * MGG + hl];
+    if (hl < mg) g_wg[g * MGG + hl] = g_rg[hl] * g_zg[g * MGG + hl] - g_yg[g * MGG + hl];
+    __builtin_amdgcn_wave_barrier();
     double muv = 0.0, cvp[CMG] = {0.0, 0.0, 0.0, 0.0}, qmax = 0.0;
     for (int i = hl; i < n; i += 32) {
       qmax = fmax(qmax, fabs(q_h[i]));
       const double rb = has_box ? crho(lo_h[i], up_h[i], rho, s) : 0.0;
       double rr = sigma * x_h[i] - q_h[i];
       if (has_box) rr += rb * zb_h[i] - yb_h[i];
+      if constexpr (WIDE) {   // column-sparse rows (Cg V of the first iteration: pass 1)
+        for (int e = 0; e < nzmax; ++e) {
+          const int r = cg_nzr[(int64_t)i * nzmax + e];
+          if (r >= 0) rr += cg_nzv[(int64_t)i * nzmax + e] * g_wg[g * MGG + r];
+        }
+      } else {
 #pragma unroll
-      for (int r = 0; r < CMG; ++r)
-        if (r < mg) rr += Cg_h[(int64_t)r * ld + i] * g_wg[g * MGG + r];
+        for (int r = 0; r < CMG; ++r)
+          if (r < mg) rr += Cg_h[(int64_t)r * ld + i] * g_wg[g * MGG + r];
+      }
       const double v = rr * dinv;
       R_h[i] = rr;
-      muv = fma(mu_h[i], v, muv);
+      if (centred) muv = fma(mu_h[i], v, muv);
+      if constexpr (!WIDE) {
 #pragma unroll
-      for (int r = 0; r < CMG; ++r)
-        if (r < mg) cvp[r] = fma(Cg_h[(int64_t)r * ld + i], v, cvp[r]);
+        for (int r = 0; r < CMG; ++r)
+          if (r < mg) cvp[r] = fma(Cg_h[(int64_t)r * ld + i], v, cvp[r]);
+      }
     }
     muv = csum32(muv);
     qmax = cmax32(qmax);
@@ -476,7 +502,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (hl == 0) {
       g_muv[g] = muv;
       g_qmax[g] = qmax;   // |q| (dual scale) is fixed over the iterations
-      for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
+      if constexpr (!WIDE)
+        for (int r = 0; r < mg; ++r) g_cgv[g * MGG + r] = cvp[r];
     }
   }
   if (t == 0) {
@@ -743,9 +770,9 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         double gm[3] = {0.0, 0.0, 0.0};   // |Cx - z| |Cx| |z| of the general rows
         if (hl < mg) {
           const int e = g * MGG + hl;
-          const double rg = g_rg[e], zt = g_zt[e];
+          const double rg = g_rg[hl], zt = g_zt[e];
           const double zh = alpha * zt + (1.0 - alpha) * g_zg[e];
-          const double zn = fmin(fmax(zh + g_yg[e] / rg, g_lg[e]), g_ug[e]);
+          const double zn = fmin(fmax(zh + g_yg[e] / rg, g_lg[hl]), g_ug[hl]);
           const double yn = g_yg[e] + rg * (zh - zn);
           const double cx = alpha * zt + (1.0 - alpha) * g_cgx[e];
           gm[0] = fabs(cx - zn);
@@ -826,10 +853,25 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
         if (!cin) continue;
         // per-asset data, shared by the lane's dates
-        double2 cg2[MGC > 0 ? MGC : 1];
+        constexpr int MGR = WIDE ? 1 : (MGC > 0 ? MGC : 1);   // register-resident columns
+        double2 cg2[MGR];
+        if constexpr (!WIDE) {
 #pragma unroll
-        for (int c = 0; c < MGC; ++c)
-          cg2[c] = c < mg ? *reinterpret_cast<const double2*>(pb.Cg + (int64_t)c * ld + i) : double2{0.0, 0.0};
+          for (int c = 0; c < MGC; ++c)
+            cg2[c] = c < mg ? *reinterpret_cast<const double2*>(pb.Cg + (int64_t)c * ld + i) : double2{0.0, 0.0};
+        }
+        int nzr2[2][WIDE ? CNZ : 1];   // wide form: the pair's nonzero rows (-1: none) and values
+        double nzv2[2][WIDE ? CNZ : 1];
+        if constexpr (WIDE) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int e = 0; e < CNZ; ++e) {
+              const bool ok = e < nzmax;
+              nzr2[h][e] = ok ? cg_nzr[(int64_t)(i + h) * nzmax + e] : -1;
+              nzv2[h][e] = ok ? cg_nzv[(int64_t)(i + h) * nzmax + e] : 0.0;
+            }
+        }
         double2 lo2 = double2{0.0, 0.0}, up2 = double2{0.0, 0.0}, rb2 = double2{0.0, 0.0};
         if (has_box && box_shared) {
           lo2 = *reinterpret_cast<const double2*>(pb.lb + i);
@@ -855,7 +897,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           double* zb_m = st.z + (int64_t)bm * st.m_ld + st.mg_pad + i;
           double* yb_m = st.y + (int64_t)bm * st.m_ld + st.mg_pad + i;
           const double2 rr2 = *reinterpret_cast<const double2*>(R_m);
-          const double2 mu2 = *reinterpret_cast<const double2*>(lr.mu + (int64_t)bm * lr.mu_stride + i);
+          const double2 mu2 = centred ? *reinterpret_cast<const double2*>(lr.mu + (int64_t)bm * lr.mu_stride + i)
+                                      : double2{0.0, 0.0};
           const double2 x2 = *reinterpret_cast<const double2*>(x_m);
           const double2 px2 = *reinterpret_cast<const double2*>(Px_m);
           const double2 q2 = *reinterpret_cast<const double2*>(pb.q + (int64_t)bm * pb.q_stride + i);
@@ -864,10 +907,10 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             z2 = *reinterpret_cast<const double2*>(zb_m);
             y2 = *reinterpret_cast<const double2*>(yb_m);
           }
-          double cwm[MGC > 0 ? MGC : 1], rgzm[MGC > 0 ? MGC : 1], ygm[MGC > 0 ? MGC : 1], wgm[MGC > 0 ? MGC : 1];
+          double cwm[MGR], rgzm[MGR], ygm[MGR], wgm[MGR];
 #pragma unroll
-          for (int c = 0; c < MGC; ++c) {
-            const bool ok = c < mg;
+          for (int c = 0; c < MGR; ++c) {
+            const bool ok = !WIDE && c < mg;
             cwm[c] = ok ? g_cw[m * MGG + c] : 0.0;
             rgzm[c] = ok ? g_rgz[m * MGG + c] : 0.0;
             ygm[c] = ok ? g_yg[m * MGG + c] : 0.0;
@@ -877,18 +920,33 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           auto one = [&](double xr, double rr0, double mui, double xi, double pxi, double qi, double zi, double yi,
                          double loi, double upi, double rbi, int sel, double& xn_o, double& pxn_o, double& zn_o,
                          double& yn_o, double& rr_o) {
-            double corr = xr - su * mui;
-            double cgi[MGC > 0 ? MGC : 1];
+            // wide form: the sums over the asset's nonzero rows (Cg' cw, Cg' rho z~, Cg' y, Cg' w)
+            double gcw = 0.0, grgz = 0.0, cgy = 0.0, cgw = 0.0;
+            if constexpr (WIDE) {
 #pragma unroll
-            for (int c = 0; c < MGC; ++c) {
+              for (int e = 0; e < CNZ; ++e) {
+                const int rw = sel ? nzr2[1][e] : nzr2[0][e];
+                if (rw >= 0) {
+                  const double v = sel ? nzv2[1][e] : nzv2[0][e];
+                  const int o = m * MGG + rw;
+                  gcw = fma(g_cw[o], v, gcw);
+                  grgz = fma(v, g_rgz[o], grgz);
+                  cgy = fma(v, g_yg[o], cgy);
+                  cgw = fma(v, g_wg[o], cgw);
+                }
+              }
+            }
+            double corr = xr - su * mui + gcw;
+            double cgi[MGR];
+#pragma unroll
+            for (int c = 0; c < MGR && !WIDE; ++c) {
               cgi[c] = sel ? cg2[c].y : cg2[c].x;
               corr = fma(cwm[c], cgi[c], corr);
             }
             const double xt = (rr0 - corr) * dinv;
-            double pxt = rr0 - sigma * xt - rbi * xt;
-            double cgy = 0.0, cgw = 0.0;
+            double pxt = rr0 - sigma * xt - rbi * xt - grgz;
 #pragma unroll
-            for (int c = 0; c < MGC; ++c) {
+            for (int c = 0; c < MGR && !WIDE; ++c) {
               pxt -= cgi[c] * rgzm[c];
               cgy = fma(cgi[c], ygm[c], cgy);
               cgw = fma(cgi[c], wgm[c], cgw);
@@ -1050,12 +1108,11 @@ static int gcap_check(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap*
   PQ_CHECK_ARG(gc->gdates && gc->urows && gc->ucnt && gc->uoff && gc->gidx && gc->grho && gc->ngroups > 0,
                "%s: group plan missing", who);
   PQ_CHECK_ARG(gc->umax > 0 && gc->umax <= pq::CU_MAX, "%s: umax must be in (0, %d]", who, pq::CU_MAX);
-  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::CMG && pb->Cg_stride == 0 && pb->g_stride == 0,
-               "%s: needs shared general rows, mg <= %d", who, pq::CMG);
+  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::CMGW && pb->Cg_stride == 0 && pb->g_stride == 0,
+               "%s: needs shared general rows, mg <= %d", who, pq::CMGW);
   // (the caller guarantees ucnt[g] + mg <= k_ld for every group; U <= umax <= 320)
   PQ_CHECK_ARG(gc->k_ld % 64 == 0 && gc->k_ld >= 64 && gc->k_ld <= 384,
                "%s: need 64 <= k_ld <= 384, a multiple of 64 (k_ld=%d)", who, gc->k_ld);
-  PQ_CHECK_ARG(lr->mu != nullptr, "%s: the group form needs the window means (centred covariance)", who);
   return 0;
 }
 
@@ -1079,7 +1136,7 @@ extern "C" int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(gc->aq_stride >= 2 * (int64_t)gc->k_ld && gc->ldh > 0 && gc->ldh <= pq::CH_MAX,
                "pq_gcap_prepare: aq needs 2 k_ld per date, ldh <= %d", pq::CH_MAX);
   PQ_CHECK_ARG(pb->mg == 0 || pc, "pq_gcap_prepare: general rows need pc");
-  PQ_CHECK_ARG(gc->umax <= pq::CU_MAX && pb->mg <= pq::CMG, "pq_gcap_prepare: union or general rows too many");
+  PQ_CHECK_ARG(gc->umax <= pq::CU_MAX && pb->mg <= pq::CMGW, "pq_gcap_prepare: union or general rows too many");
   const int grid = idx ? nidx : gc->ngroups;   // one workgroup per group (idx: group subset)
   if (grid <= 0) return 0;
   hipLaunchKernelGGL(pq::k_gcap_prep, dim3(grid), dim3(pq::PT_PREP), 0, (hipStream_t)stream, *lr, *pb, *st, *gc, *s, idx,
@@ -1090,7 +1147,8 @@ extern "C" int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_st
 
 extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
                                const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
-                               int32_t r0, const double* cc, void* stream) {
+                               int32_t r0, const double* cc, const int32_t* cg_nzr, const double* cg_nzv,
+                               int32_t nzmax, void* stream) {
   if (gcap_check(lr, pb, gc, "pq_admm_lr_gcap")) return -1;
   PQ_CHECK_ARG(st && s && gc->Minv && gc->aq && gc->hinv, "pq_admm_lr_gcap: null argument");
   PQ_CHECK_ARG(pb->mg == 0 || (pc && cc), "pq_admm_lr_gcap: general rows need pc and cc");
@@ -1100,15 +1158,21 @@ extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(pb->ld % 2 == 0 && st->work_stride % 2 == 0 && st->m_ld % 2 == 0 && st->mg_pad % 2 == 0 &&
                    pb->q_stride % 2 == 0 && pb->box_stride % 2 == 0 && lr->mu_stride % 2 == 0,
                "pq_admm_lr_gcap: strides must be even");
+  PQ_CHECK_ARG(pb->mg <= pq::CMG || (cg_nzr && cg_nzv && nzmax > 0 && nzmax <= pq::CNZ),
+               "pq_admm_lr_gcap: more than %d general rows need their column-sparse form (nzmax <= %d)", pq::CMG,
+               pq::CNZ);
   if (pb->mg == 0)
     hipLaunchKernelGGL(pq::k_admm_gcap<0>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
-                       *gc, *s, iters_this_call, pc, ldpc, r0, cc);
+                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
   else if (pb->mg == 1)   // the budget row alone (the usual case): one general row in registers
     hipLaunchKernelGGL(pq::k_admm_gcap<1>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
-                       *gc, *s, iters_this_call, pc, ldpc, r0, cc);
-  else
+                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
+  else if (pb->mg <= pq::CMG)
     hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMG>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
-                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc);
+                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
+  else   // budget + sector caps: column-sparse rows
+    hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMGW>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
+                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, cg_nzr, cg_nzv, nzmax);
   PQ_CHECK_LAUNCH("pq_admm_lr_gcap");
   return 0;
 }

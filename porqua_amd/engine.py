@@ -716,8 +716,12 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         _lib.check(lib.pq_factor_batched(PM_, SM_, _ptr(idx), nidx, SSM, 1, strm), "pq_factor_batched(M)")
 
     grouped = grouped_applicable(qb, lr, groups, ws)
-    gcap_try = (gcap and eig is None and grouped and fuse and qb.mg <= 4 and lr.mu is not None and qb.shared
-                and groups.ucnt_max + qb.mg <= 384 and groups.corr_max <= 64)
+    sparse_cols = _sparse_columns(qb) if grouped else (None, None, 0)
+    # group capacitance: shared rows, register-resident (mg <= 4) or column-sparse (mg <= 24,
+    # <= 4 nonzeros per asset); pass 1 of admm_gcap.hip covers U + mg <= 320 rows
+    gcap_try = (gcap and eig is None and grouped and fuse and qb.shared
+                and (qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
+                and groups.ucnt_max + qb.mg <= 320 and groups.corr_max <= 64)
     if band:
         bd = tl("gram", lambda: _band_setup(qb, lr, strm, w_min=groups.span_max if gcap_try else 0))
     gc = _gcap_setup(qb, lr, ws, groups, settings or Settings()) if (gcap_try and bd is not None) else None
@@ -742,8 +746,10 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
 
     def admm(idx, nidx):
         if gc is not None:   # group capacitance (admm_gcap.hip)
+            nzr, nzv, nzmax = sparse_cols if qb.mg > 4 else (None, None, 0)
             return lib.pq_admm_lr_gcap(L_, P_, S_, ctypes.byref(gc["c"]), SS, int(s.max_iter), bd["pc"].data_ptr(),
-                                       bd["pc"].stride(0), bd["r0"], bd["cc"].data_ptr(), strm)
+                                       bd["pc"].stride(0), bd["r0"], bd["cc"].data_ptr(), _ptr(nzr), _ptr(nzv),
+                                       nzmax, strm)
         if grouped:   # every group relaunches; solved dates are skipped inside
             fz = bd is not None and fuse and qb.mg <= 32   # uniform D + shared Cg: the fused form
             nzr, nzv, nzmax = sparse_cols
@@ -757,7 +763,6 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         return lib.pq_admm_lr_batched(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld, _ptr(idx),
                                       nidx, SS, int(s.max_iter), strm)
 
-    sparse_cols = _sparse_columns(qb) if grouped else (None, None, 0)
     cnt = {"refactors": 0, "launches": 0, "pg_fallback": 0}
 
     def admm_rounds(idx, nidx, SSx):

@@ -8,6 +8,8 @@ per-date low-rank Woodbury correction, against the per-date capacitance path it 
   reach the same optimum.
 * Adaptive rho: a group-level refactorisation (every 5 iterations, tight eps) still ends at
   the same optimum.
+* Uncentred windows (LeastSquares tracking, P = 2 X'X, q = -2 X'y, src/optimization.py:206-226):
+  the group form without the mean column, against the per-date path.
 """
 import numpy as np
 import pytest
@@ -19,11 +21,11 @@ from porqua_amd.synthetic import factor_panel
 pytestmark = pytest.mark.gpu
 
 
-def _problem(device, n, T, D, ub, stride=1):
+def _problem(device, n, T, D, ub, stride=1, centred=True):
     ends = list(range(T + 5, T + 5 + D * stride, stride))
     dates, R, y, sec = factor_panel(max(ends) + 1, n)
     rows, tlen = engine.window_rows(dates, dates[ends], T)
-    pan = engine.Panel(R, device=device)
+    pan = engine.Panel(R, y, device=device)
     r_d, t_d = pan.rows_to_device(rows, tlen)
     qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
                                    lb=np.zeros(n), ub=np.full(n, ub), device=device)
@@ -31,8 +33,13 @@ def _problem(device, n, T, D, ub, stride=1):
     qb.P = None
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=device)
     qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=device)
-    mu = pan.window_means(r_d, t_d)
-    lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+    if centred:
+        mu = pan.window_means(r_d, t_d)
+        lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=1.0 / (t_d.to(torch.float64) - 1.0))
+    else:   # tracking least squares: P = 2 X'X, q = -2 X'y
+        xty, _ = pan.gram_xy(r_d, t_d)
+        qb.q = (-2.0 * xty).contiguous()
+        lr = engine.LowRank(pan, r_d, t_d, mu=None)
     gp = engine.GroupPlan(rows, tlen, device)
     return qb, lr, gp
 
@@ -76,3 +83,25 @@ def test_gcap_group_rho_adaptation(device):
     assert cap == "group" and refactors > 0
     assert np.all(sb == _lib.PQ_SOLVED), sb
     assert np.abs(xa - xb).max() <= 1e-8
+
+
+@pytest.mark.parametrize("n,T,D,ub,stride", [(1000, 252, 48, 1.0, 1), (494, 252, 40, 1.0, 1), (300, 60, 30, 0.2, 3)])
+def test_gcap_uncentred_same_iterates_with_one_rho(device, n, T, D, ub, stride):
+    qb, lr, gp = _problem(device, n, T, D, ub, stride, centred=False)
+    st = engine.Settings(rho0_rel=0.0, rho0=0.05, rho0_qrel=0.0, adapt_interval=0)
+    xa, sa, ia, cap_a, _ = _run(qb, lr, gp, False, st)
+    xb, sb, ib, cap_b, _ = _run(qb, lr, gp, True, st)
+    assert cap_a == "band" and cap_b == "group"
+    assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED), (sa, sb)
+    assert np.abs(ia - ib).max() <= 1, (ia, ib)
+    assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()
+
+
+def test_gcap_uncentred_tracking_default_settings(device):
+    qb, lr, gp = _problem(device, 1000, 252, 64, 1.0, centred=False)
+    st = engine.Settings(rho0_rel=0.1, rho0_qrel=0.0)   # the tracking workloads' settings
+    xa, sa, _, _, _ = _run(qb, lr, gp, False, st)
+    xb, sb, _, cap, _ = _run(qb, lr, gp, True, st)
+    assert cap == "group"
+    assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED)
+    assert np.abs(xa - xb).max() <= 1e-8, np.abs(xa - xb).max()
