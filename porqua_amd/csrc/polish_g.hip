@@ -544,43 +544,6 @@ __device__ void w_bwd(const double* Lp, int k, double* y, double* xo) {
   }
 }
 
-// rows a0 .. a0 + m - 1 of Ub (stride ustr) <- L^-1 e_{pos[a]}: columns of L^-1 for the unit
-// rows of a Schur-update round, all m in one blocked forward pass (one wave; yo: LDS, 16 x PG_MB)
-__device__ void w_fwd_units(const double* Lp, int k, double* Ub, int64_t ustr, int a0, int m, const int* pos,
-                            double* yo) {
-  const int l = lane_id();
-  for (int e = l; e < m * k; e += 64) {
-    const int a = e / k, p = e - a * k;
-    Ub[(int64_t)(a0 + a) * ustr + p] = (p == pos[a]) ? 1.0 : 0.0;
-  }
-  WSYNC();
-  for (int p0 = 0; p0 < k; p0 += 16) {
-    const int nb = min(16, k - p0);
-    for (int e = l; e < nb * m; e += 64) {   // yo[i][a] = (L11^-1 y_block)[i][a]
-      const int i = e / m, a = e - i * m;
-      const double* y = Ub + (int64_t)(a0 + a) * ustr + p0;
-      double v = 0.0;
-      for (int j = 0; j <= i; ++j) v = fma(Lp[pk(p0 + i, p0 + j)], y[j], v);
-      yo[i * PG_MB + a] = v;
-    }
-    WSYNC();
-    for (int e = l; e < nb * m; e += 64) {
-      const int i = e / m, a = e - i * m;
-      Ub[(int64_t)(a0 + a) * ustr + p0 + i] = yo[i * PG_MB + a];
-    }
-    for (int e = l; e < (k - p0 - nb) * m; e += 64) {   // rows below: y_r -= L_r,blk yo
-      const int rr = e / m, a = e - rr * m;
-      const int r = p0 + nb + rr;
-      double* y = Ub + (int64_t)(a0 + a) * ustr + r;
-      double v = *y;
-      const double* lr_ = Lp + pk(r, p0);
-      for (int j = 0; j < nb; ++j) v = fma(-lr_[j], yo[j * PG_MB + a], v);
-      *y = v;
-    }
-    WSYNC();
-  }
-}
-
 template <int KS>
 __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
                                                  int klo, int upd_ok) {
@@ -589,7 +552,6 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   __shared__ double xF[KS], t1[KS], t2[KS], rx[KS];
   __shared__ double Sm[PG_MB * PG_MB], lamv[PG_MB], wl[PG_MB], rl[PG_MB], dAv[PG_MB];
   __shared__ int s_al[PG_MB];   // bordered row a: general row s_al[a] (a < ma) or F-position (a >= ma)
-  __shared__ double yo[16 * PG_MB];
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING) return;
@@ -675,32 +637,27 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   // U = L^-1 C_b' (row a: general row s_al[a], or the unit vector of position s_al[a]),
   // S = U'U + delta I (the bordered unit rows carry no delta: they are exact)
   WSYNC();
-  for (int a = 0; a < ma; ++a) {
-    const double* cr = Cg + (int64_t)s_al[a] * ld;
-    for (int p = l; p < k; p += 64) t1[p] = cr[wk.Fl[p]];
+  for (int a = 0; a < mb; ++a) {
+    if (a < ma) {
+      const double* cr = Cg + (int64_t)s_al[a] * ld;
+      for (int p = l; p < k; p += 64) t1[p] = cr[wk.Fl[p]];
+    } else {
+      for (int p = l; p < k; p += 64) t1[p] = (p == s_al[a]) ? 1.0 : 0.0;
+    }
     WSYNC();
     w_fwd(Lp, k, t1, t2);
     for (int p = l; p < k; p += 64) Ub[(int64_t)a * ustr + p] = t2[p];
   }
-  if (nd) w_fwd_units(Lp, k, Ub, ustr, ma, nd, s_al + ma, yo);
   WSYNC();
-  if (mb == 1) {
+  for (int e = 0; e < mb * mb; ++e) {
+    const int ii = e / mb, jj = e % mb;
+    if (jj > ii) continue;
+    const double* ui = Ub + (int64_t)ii * ustr;
+    const double* uj = Ub + (int64_t)jj * ustr;
     double sum = 0.0;
-    for (int p = l; p < k; p += 64) sum += Ub[p] * Ub[p];
+    for (int p = l; p < k; p += 64) sum += ui[p] * uj[p];
     sum = wave_sum(sum);
-    if (l == 0) Sm[0] = sum + (ma ? delta : 0.0);
-  } else {   // one lane per entry of the lower triangle
-    for (int e = l; e < mb * (mb + 1) / 2; e += 64) {
-      int ii = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-      while ((ii + 1) * (ii + 2) / 2 <= e) ++ii;
-      while (ii * (ii + 1) / 2 > e) --ii;
-      const int jj = e - ii * (ii + 1) / 2;
-      const double* ui = Ub + (int64_t)ii * ustr;
-      const double* uj = Ub + (int64_t)jj * ustr;
-      double sum = 0.0;
-      for (int p = 0; p < k; ++p) sum = fma(ui[p], uj[p], sum);
-      Sm[ii * PG_MB + jj] = sum + (ii == jj && ii < ma ? delta : 0.0);
-    }
+    if (l == 0) Sm[ii * PG_MB + jj] = sum + (ii == jj && ii < ma ? delta : 0.0);
   }
   WSYNC();
   int sbad = 0;
@@ -725,7 +682,9 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   }
   WSTAMP(2);
   // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------
-  const int nref = s.refine_iters;
+  // an update round refines at least twice: its start (the previous round's x_F) is further
+  // from the new point than the ADMM point of a first round
+  const int nref = upd ? max(s.refine_iters, 2) : s.refine_iters;
   for (int itr = 0; itr < nref; ++itr) {
     // rx = rF - P_FF x - C_aF' lam - sum_unit e_p lam  (lane per row, P_FF from the K scratch)
     for (int p = l; p < k; p += 64) {   // P_FF is symmetric in K: column p, coalesced over lanes
