@@ -369,7 +369,7 @@ int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st
  * window passes of a group run split over 4 workgroups (column slices), with
  * pass_scratch = ngroups * PQ_PG_PASS_SCRATCH doubles for their partial products.
  * Replaces, with pq_polish_w_batched, the accuracy of qpsolvers (src/qp_problems.py:211-214). */
-#define PQ_PG_RECORD 392
+#define PQ_PG_RECORD 320
 #define PQ_PG_PASS_SCRATCH 20816   /* doubles per group: 4 x 324 x 16 + 4 x 16 + 16 */
 #define PQ_PG_PENDING 0
 #define PQ_PG_DONE 1

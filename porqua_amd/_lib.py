@@ -25,7 +25,7 @@ PQ_PRIMAL_INFEASIBLE = -3
 PQ_DUAL_INFEASIBLE = -4
 PQ_NON_CONVEX = -5
 
-PQ_PG_RECORD = 392                   # doubles per problem of the grouped polish record
+PQ_PG_RECORD = 320                   # doubles per problem of the grouped polish record
 PQ_PG_PASS_SCRATCH = 20816           # doubles per slide group of the split polish window passes
 PQ_PG_PENDING, PQ_PG_DONE, PQ_PG_FALLBACK, PQ_PG_SKIP = range(4)
 PQ_PG_STATE = 3                      # record field holding the state

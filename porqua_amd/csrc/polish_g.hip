@@ -37,23 +37,10 @@ namespace pq {
 constexpr int PGR = PQ_PG_RECORD;
 enum : int {
   R_K = 0, R_MA = 1, R_NZB = 2, R_STATE = 3, R_ROUNDS = 4, R_SC = 5,
-  R_ACT = 64, R_LAM = 128, R_DA = 192, R_SOL = 256, R_AL = 288,
-  // Schur-update rounds: R_MODE 1 = this round reuses the saved factor of P_FF (R_LSV: the
-  // factor of the current free list is saved in the K scratch), with R_ND free variables of
-  // that list fixed again as bordered unit rows (positions R_DP, values R_DV)
-  R_MODE = 320, R_ND = 321, R_LSV = 322, R_DP = 328, R_DV = 360
+  R_ACT = 64, R_LAM = 128, R_DA = 192, R_SOL = 256, R_AL = 288
 };
 constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
 constexpr int PG_MGMAX = 32;   // general rows
-constexpr int PG_MB = 24;      // bordered rows of a Schur-update round: active general rows + unit rows
-constexpr int PG_NPMAX = PG_KMAX * (PG_KMAX + 1) / 2;   // packed factor of the largest free set
-static_assert(R_DV + 32 <= PQ_PG_RECORD, "PQ_PG_RECORD too small");
-// K scratch of a date (ldk x ldk): P_FF in rows [0, k); from row PG_KMAX the saved packed
-// factor (PG_NPMAX doubles) and the bordered rows' U = L^-1 C' (PG_MB x PG_KMAX) -- when it
-// fits (ldk >= 256); otherwise no Schur-update rounds and U in the work buffer
-__host__ __device__ constexpr bool pg_update_ok(int ldk) {
-  return (int64_t)ldk * ldk >= (int64_t)PG_KMAX * ldk + PG_NPMAX + PG_MB * PG_KMAX;
-}
 
 struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
   double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;
@@ -138,9 +125,6 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
     R[R_SC] = sc;
     R[R_K] = 0;
     R[R_NZB] = 0;
-    R[R_MODE] = 0;
-    R[R_ND] = 0;
-    R[R_LSV] = 0;
   }
 #ifdef PQ_PROFILE
   if (t >= 8 && t < 20) R[t] = 0.0;
@@ -150,7 +134,7 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
 // ---------------------------------------------------------------------------------------
 // setup: free list, active rows, x_B, dA, the starting point of the refinement
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, double* rec, int kmax, int upd_ok) {
+__global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, double* rec, int kmax) {
   __shared__ int wcnt[PW];
   __shared__ int s_al[PG_MGMAX + 1];
   __shared__ double red[16];
@@ -167,7 +151,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
   const double* lb = has_box ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
   const double* ub = has_box ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
   PGWork wk(st, b, ld);
-  // ---- count of the free variables: wave w owns a contiguous index range ------------------
+  // ---- stable compaction of the free variables: wave w owns a contiguous index range ----
   const int seg = ((n + PW * 64 - 1) / (PW * 64)) * 64;
   const int lo = w * seg, hi = min(n, lo + seg);
   int c = 0;
@@ -189,75 +173,31 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     k += wcnt[ww];
   }
   const int ma = s_al[PG_MGMAX];
-  // ---- Schur-update round?  The previous round's factor of P_FF (free list F1, saved by the
-  // solve) is reused when every free variable is still in F1: the variables of F1 fixed since
-  // become bordered unit rows (x_p = bound) instead of a new P_FF and Cholesky.  A released
-  // variable (outside F1) needs the full round. ---------------------------------------------
-  const int k1 = (int)R[R_K];
-  bool upd = false;
-  int nd = 0;
-  if (upd_ok && R[R_LSV] == 1.0 && k1 > 0 && ma <= 8) {
-    double c1 = 0.0;
-    for (int p = t; p < k1; p += PT) c1 += (wk.fl[wk.Fl[p]] == 0) ? 1.0 : 0.0;
-    const int c1i = (int)(block_sum(c1, red) + 0.5);
-    nd = k1 - c1i;
-    upd = (c1i == k) && nd > 0 && nd < k1 && ma + nd <= PG_MB;   // uniform
+  // every variable at a bound (a vertex, e.g. nearly linear objectives): x = x_B, and the
+  // multiplier of at most one active equality row is chosen in the post from the dual
+  // feasibility interval of the bound variables (k_pg_post); otherwise the per-date kernel
+  const bool vertex_ok = ma == 0 || (ma == 1 && lg[s_al[0]] == ug[s_al[0]]);
+  if ((k == 0 && !vertex_ok) || k > kmax || ma > PG_MGMAX) {   // uniform
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
   }
-  if (upd) {
-    if (w == 0) {   // deleted positions of F1 (ascending) and their bound values
-      int nb = 0;
-      for (int p0 = 0; p0 < k1; p0 += 64) {
-        const int p = p0 + l;
-        const int i = p < k1 ? wk.Fl[p] : 0;
-        const int f = p < k1 ? wk.fl[i] : 0;
-        const unsigned long long m = __ballot(f != 0);
-        if (f != 0) {
-          const int j = nb + __popcll(m & ((1ull << l) - 1ull));
-          R[R_DP + j] = p;
-          R[R_DV + j] = f == 1 ? lb[i] : ub[i];
-        }
-        nb += __popcll(m);
-      }
-    }
-    // x_B over the complement of F1 (unchanged since the factored round), 0 on F1
-    for (int i = t; i < ld; i += PT) {
-      const int f = wk.fl[i];
-      wk.xb[i] = i < n ? (f == 1 ? lb[i] : (f == 2 ? ub[i] : 0.0)) : 0.0;
-    }
-    __syncthreads();
-    for (int j = t; j < nd; j += PT) {
-      const int pp = (int)R[R_DP + j];
-      wk.xb[wk.Fl[pp]] = 0.0;
-      wk.solx[pp] = R[R_DV + j];   // the refinement starts on the unit rows
-    }
-    __syncthreads();
-  } else {
-    // every variable at a bound (a vertex, e.g. nearly linear objectives): x = x_B, and the
-    // multiplier of at most one active equality row is chosen in the post from the dual
-    // feasibility interval of the bound variables (k_pg_post); otherwise the per-date kernel
-    const bool vertex_ok = ma == 0 || (ma == 1 && lg[s_al[0]] == ug[s_al[0]]);
-    if ((k == 0 && !vertex_ok) || k > kmax || ma > PG_MGMAX) {   // uniform
-      if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
-      return;
-    }
-    for (int i0 = lo; i0 < hi; i0 += 64) {
-      const int i = i0 + l;
-      const bool f = i < hi && wk.fl[i] == 0;
-      const unsigned long long m = __ballot(f);
-      if (f) wk.Fl[base + __popcll(m & ((1ull << l) - 1ull))] = i;
-      base += __popcll(m);
-    }
-    // ---- fixed values -------------------------------------------------------------------------
-    for (int i = t; i < ld; i += PT) {
-      const int f = wk.fl[i];
-      const double v = i < n ? (f == 1 ? lb[i] : (f == 2 ? ub[i] : 0.0)) : 0.0;
-      wk.xb[i] = v;
-      if (k == 0) wk.xs[i] = v;
-    }
+  for (int i0 = lo; i0 < hi; i0 += 64) {
+    const int i = i0 + l;
+    const bool f = i < hi && wk.fl[i] == 0;
+    const unsigned long long m = __ballot(f);
+    if (f) wk.Fl[base + __popcll(m & ((1ull << l) - 1ull))] = i;
+    base += __popcll(m);
   }
+  // ---- fixed values, nzb -------------------------------------------------------------------
   int nzb = 0;
-  for (int i = t; i < ld; i += PT) nzb |= (wk.xb[i] != 0.0);
-  nzb = block_or(nzb, red);   // barrier: Fl and xb complete below
+  for (int i = t; i < ld; i += PT) {
+    const int f = wk.fl[i];
+    const double v = i < n ? (f == 1 ? lb[i] : (f == 2 ? ub[i] : 0.0)) : 0.0;
+    wk.xb[i] = v;
+    if (k == 0) wk.xs[i] = v;
+    nzb |= (v != 0.0);
+  }
+  nzb = block_or(nzb, red);   // barrier: Fl complete below
   // ---- d_a = rhs_a - C_aB x_B ----------------------------------------------------------------
   for (int a = w; a < ma; a += PW) {
     const int r = s_al[a];
@@ -267,25 +207,20 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     sum = wave_sum(sum);
     if (l == 0) R[R_DA + a] = (R[R_ACT + r] == 1.0 ? lg[r] : ug[r]) - sum;
   }
-  if (!upd) {   // an update round keeps rF (-q_F - P_FB x_B of the factored round) and solx
-    const int kp = (k + 15) & ~15;
-    for (int p = t; p < kp; p += PT) {
-      const int i = p < k ? wk.Fl[p] : 0;
-      wk.solx[p] = p < k ? wk.xs[i] : 0.0;
-      wk.rF[p] = p < k ? -q[i] : 0.0;
-    }
+  const int kp = (k + 15) & ~15;
+  for (int p = t; p < kp; p += PT) {
+    const int i = p < k ? wk.Fl[p] : 0;
+    wk.solx[p] = p < k ? wk.xs[i] : 0.0;
+    wk.rF[p] = p < k ? -q[i] : 0.0;
   }
   if (t < ma) {
     R[R_AL + t] = s_al[t];
     R[R_SOL + t] = R[R_LAM + s_al[t]];
   }
   if (t == 0) {
-    R[R_K] = upd ? k1 : k;
+    R[R_K] = k;
     R[R_MA] = ma;
     R[R_NZB] = nzb;
-    R[R_MODE] = upd ? 1.0 : 0.0;
-    R[R_ND] = upd ? nd : 0;
-    if (!upd) R[R_LSV] = 0.0;   // the solve saves the new factor
     R[R_ROUNDS] += 1.0;
   }
 }
@@ -307,7 +242,7 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPIT];
   const int b = blockIdx.x;
   const double* R = rec + (int64_t)b * PGR;
-  if (R[R_STATE] != PQ_PG_PENDING || R[R_MODE] != 0.0) return;   // update rounds keep P_FF
+  if (R[R_STATE] != PQ_PG_PENDING) return;
   const int k = (int)R[R_K];
   if (k > PG_KMAX || k == 0) return;
   const int ld = pb.ld;
@@ -546,12 +481,12 @@ __device__ void w_bwd(const double* Lp, int k, double* y, double* xo) {
 
 template <int KS>
 __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
-                                                 int klo, int upd_ok) {
+                                                 int klo) {
   constexpr int NP = KS * (KS + 1) / 2;
   __shared__ double Lp[NP];
   __shared__ double xF[KS], t1[KS], t2[KS], rx[KS];
-  __shared__ double Sm[PG_MB * PG_MB], lamv[PG_MB], wl[PG_MB], rl[PG_MB], dAv[PG_MB];
-  __shared__ int s_al[PG_MB];   // bordered row a: general row s_al[a] (a < ma) or F-position (a >= ma)
+  __shared__ double Sm[WMA * WMA], lamv[WMA], wl[WMA], rl[WMA], dAv[WMA];
+  __shared__ int s_al[WMA];
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING) return;
@@ -562,19 +497,13 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
     if (threadIdx.x == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
-  const bool upd = R[R_MODE] != 0.0;
-  const int nd = upd ? (int)R[R_ND] : 0;
-  const int mb = ma + nd;                     // bordered rows: active general rows, then unit rows
   const int n = pb.n, ld = pb.ld;
   const int l = lane_id();
   const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
   PGWork wk(st, b, ld);
   const double sc = R[R_SC];
   const double delta = s.delta * sc;
-  double* K = st.K + (int64_t)b * st.K_stride;   // P_FF (both triangles), kept for the residuals
-  double* Ls = upd_ok ? K + (int64_t)PG_KMAX * ldk : nullptr;     // saved packed factor
-  double* Ub = upd_ok ? Ls + PG_NPMAX : wk.U;                      // U = L^-1 C_b' rows
-  const int64_t ustr = upd_ok ? PG_KMAX : ld;
+  const double* K = st.K + (int64_t)b * st.K_stride;   // P_FF (both triangles), kept for the residuals
 #ifdef PQ_PROFILE
   long long t_last_ = wall_clock64();
 #define WSTAMP(k_)                                                         \
@@ -585,10 +514,8 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
 #else
 #define WSTAMP(k_) do { } while (0)
 #endif
-  const int np_ = k * (k + 1) / 2;
-  if (upd) {   // the factor of the round that formed this free list
-    for (int e = l; e < np_; e += 64) Lp[e] = Ls[e];
-  } else {   // packed triangle, flat index (independent loads, 64 per trip)
+  {   // packed triangle, flat index (independent loads, 64 per trip)
+    const int np_ = k * (k + 1) / 2;
     int r = 0, e0 = 0;   // row of the lane's element: advance incrementally
     for (int eb = 0; eb < np_; eb += 64 * 8) {   // 8 loads in flight per lane
       double v[8];
@@ -616,62 +543,45 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
     s_al[l] = (int)R[R_AL + l];
     lamv[l] = R[R_SOL + l];
     dAv[l] = R[R_DA + l];
-  } else if (l < mb) {
-    s_al[l] = (int)R[R_DP + l - ma];
-    lamv[l] = 0.0;
-    dAv[l] = R[R_DV + l - ma];
   }
   WSTAMP(0);
-  if (!upd) {
-    if (w_potrf(Lp, k, R + 16)) {
-      if (l == 0) R[R_STATE] = PQ_PG_FALLBACK;
-      return;
-    }
-    if (upd_ok) {   // saved for the Schur-update rounds that may follow
-      WSYNC();
-      for (int e = l; e < np_; e += 64) Ls[e] = Lp[e];
-      if (l == 0) R[R_LSV] = 1.0;
-    }
+  if (w_potrf(Lp, k, R + 16)) {
+    if (l == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
   }
   WSTAMP(1);
-  // U = L^-1 C_b' (row a: general row s_al[a], or the unit vector of position s_al[a]),
-  // S = U'U + delta I (the bordered unit rows carry no delta: they are exact)
-  WSYNC();
-  for (int a = 0; a < mb; ++a) {
-    if (a < ma) {
-      const double* cr = Cg + (int64_t)s_al[a] * ld;
-      for (int p = l; p < k; p += 64) t1[p] = cr[wk.Fl[p]];
-    } else {
-      for (int p = l; p < k; p += 64) t1[p] = (p == s_al[a]) ? 1.0 : 0.0;
-    }
+  // U = L^-1 C_aF' (row a of the global U scratch), S = U'U + delta I
+  for (int a = 0; a < ma; ++a) {
+    const double* cr = Cg + (int64_t)s_al[a] * ld;
+    for (int p = l; p < k; p += 64) t1[p] = cr[wk.Fl[p]];
     WSYNC();
     w_fwd(Lp, k, t1, t2);
-    for (int p = l; p < k; p += 64) Ub[(int64_t)a * ustr + p] = t2[p];
+    for (int p = l; p < k; p += 64) wk.U[(int64_t)a * ld + p] = t2[p];
   }
   WSYNC();
-  for (int e = 0; e < mb * mb; ++e) {
-    const int ii = e / mb, jj = e % mb;
+  for (int e = 0; e < ma * ma; ++e) {
+    const int ii = e / ma, jj = e % ma;
     if (jj > ii) continue;
-    const double* ui = Ub + (int64_t)ii * ustr;
-    const double* uj = Ub + (int64_t)jj * ustr;
+    const double* ui = wk.U + (int64_t)ii * ld;
+    const double* uj = wk.U + (int64_t)jj * ld;
     double sum = 0.0;
     for (int p = l; p < k; p += 64) sum += ui[p] * uj[p];
     sum = wave_sum(sum);
-    if (l == 0) Sm[ii * PG_MB + jj] = sum + (ii == jj && ii < ma ? delta : 0.0);
+    if (l == 0) Sm[ii * WMA + jj] = sum + (ii == jj ? delta : 0.0);
   }
   WSYNC();
   int sbad = 0;
-  if (l == 0) {   // tiny Cholesky of S (mb <= PG_MB), one lane
-    for (int c = 0; c < mb && !sbad; ++c) {
-      double d = Sm[c * PG_MB + c];
-      for (int m = 0; m < c; ++m) d -= Sm[c * PG_MB + m] * Sm[c * PG_MB + m];
+  if (l == 0) {   // tiny Cholesky of S (ma <= 8), one lane
+    for (int c = 0; c < ma && !sbad; ++c) {
+      double d = Sm[c * WMA + c];
+      for (int m = 0; m < c; ++m) d -= Sm[c * WMA + m] * Sm[c * WMA + m];
       if (!(d > 0.0) || !isfinite(d)) { sbad = 1; break; }
       d = sqrt(d);
-      Sm[c * PG_MB + c] = d;
-      for (int r = c + 1; r < mb; ++r) {
-        double v = Sm[r * PG_MB + c];
-        for (int m = 0; m < c; ++m) v -= Sm[r * PG_MB + m] * Sm[c * PG_MB + m];
-        Sm[r * PG_MB + c] = v / d;
+      Sm[c * WMA + c] = d;
+      for (int r = c + 1; r < ma; ++r) {
+        double v = Sm[r * WMA + c];
+        for (int m = 0; m < c; ++m) v -= Sm[r * WMA + m] * Sm[c * WMA + m];
+        Sm[r * WMA + c] = v / d;
       }
     }
   }
@@ -682,11 +592,8 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   }
   WSTAMP(2);
   // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------
-  // an update round refines at least twice: its start (the previous round's x_F) is further
-  // from the new point than the ADMM point of a first round
-  const int nref = upd ? max(s.refine_iters, 2) : s.refine_iters;
-  for (int itr = 0; itr < nref; ++itr) {
-    // rx = rF - P_FF x - C_aF' lam - sum_unit e_p lam  (lane per row, P_FF from the K scratch)
+  for (int itr = 0; itr < s.refine_iters; ++itr) {
+    // rx = rF - P_FF x - C_aF' lam  (lane per row, P_FF from the K scratch)
     for (int p = l; p < k; p += 64) {   // P_FF is symmetric in K: column p, coalesced over lanes
       double sum = 0.0;
 #pragma unroll 8
@@ -694,19 +601,13 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
       double v = wk.rF[p] - sum;
       const int fp = wk.Fl[p];
       for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + fp] * lamv[a];
-      for (int a = ma; a < mb; ++a)
-        if (s_al[a] == p) v -= lamv[a];
       rx[p] = v;
     }
-    for (int a = 0; a < mb; ++a) {
+    for (int a = 0; a < ma; ++a) {
+      const double* cr = Cg + (int64_t)s_al[a] * ld;
       double sum = 0.0;
-      if (a < ma) {
-        const double* cr = Cg + (int64_t)s_al[a] * ld;
-        for (int p = l; p < k; p += 64) sum += cr[wk.Fl[p]] * xF[p];
-        sum = wave_sum(sum);
-      } else {
-        sum = xF[s_al[a]];
-      }
+      for (int p = l; p < k; p += 64) sum += cr[wk.Fl[p]] * xF[p];
+      sum = wave_sum(sum);
       if (l == 0) {
         const double v = dAv[a] - sum;
         rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dAv[a]) + fabs(sum)) ? 0.0 : v;
@@ -716,13 +617,13 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
     WSTAMP(3);
     double rm = 0.0;
     for (int p = l; p < k; p += 64) rm = fmax(rm, fabs(rx[p]));
-    if (l < mb) rm = fmax(rm, fabs(rl[l]));
+    if (l < ma) rm = fmax(rm, fabs(rl[l]));
     if (wave_max(rm) <= 1e-13 * sc) break;
     for (int p = l; p < k; p += 64) t1[p] = rx[p];
     WSYNC();
     w_fwd(Lp, k, t1, t2);   // t2 = L^-1 rx
-    for (int a = 0; a < mb; ++a) {   // wl = U' t2 - rl
-      const double* ua = Ub + (int64_t)a * ustr;
+    for (int a = 0; a < ma; ++a) {   // wl = U' t2 - rl
+      const double* ua = wk.U + (int64_t)a * ld;
       double sum = 0.0;
       for (int p = l; p < k; p += 64) sum += ua[p] * t2[p];
       sum = wave_sum(sum);
@@ -730,32 +631,30 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
     }
     WSYNC();
     if (l == 0) {   // dlam = S^-1 wl
-      for (int ii = 0; ii < mb; ++ii) {
+      for (int ii = 0; ii < ma; ++ii) {
         double v = wl[ii];
-        for (int jj = 0; jj < ii; ++jj) v -= Sm[ii * PG_MB + jj] * wl[jj];
-        wl[ii] = v / Sm[ii * PG_MB + ii];
+        for (int jj = 0; jj < ii; ++jj) v -= Sm[ii * WMA + jj] * wl[jj];
+        wl[ii] = v / Sm[ii * WMA + ii];
       }
-      for (int ii = mb - 1; ii >= 0; --ii) {
+      for (int ii = ma - 1; ii >= 0; --ii) {
         double v = wl[ii];
-        for (int jj = ii + 1; jj < mb; ++jj) v -= Sm[jj * PG_MB + ii] * wl[jj];
-        wl[ii] = v / Sm[ii * PG_MB + ii];
+        for (int jj = ii + 1; jj < ma; ++jj) v -= Sm[jj * WMA + ii] * wl[jj];
+        wl[ii] = v / Sm[ii * WMA + ii];
       }
     }
     WSYNC();
     for (int p = l; p < k; p += 64) {
       double v = t2[p];
-      for (int a = 0; a < mb; ++a) v -= Ub[(int64_t)a * ustr + p] * wl[a];
+      for (int a = 0; a < ma; ++a) v -= wk.U[(int64_t)a * ld + p] * wl[a];
       t1[p] = v;
     }
     WSYNC();
     w_bwd(Lp, k, t1, t2);   // t2 = L^-T (t2 - U dlam)
     for (int p = l; p < k; p += 64) xF[p] += t2[p];
-    if (l < mb) lamv[l] += wl[l];
+    if (l < ma) lamv[l] += wl[l];
     WSYNC();
     WSTAMP(4);
   }
-  if (l >= ma && l < mb) xF[s_al[l]] = dAv[l];   // fixed again: exactly at the bound
-  WSYNC();
   // ---- expand: xs = x_B off F, x_F on F; general multipliers by row ------------------------
   for (int ii = l; ii < n; ii += 64) wk.xs[ii] = wk.xb[ii];
   WSYNC();
@@ -814,8 +713,7 @@ __device__ __forceinline__ bool pass_setup(const PassGroup& pg, const pq_lowrank
     int on = 0;
     if (t < pg.G) {
       const double* R = rec + (int64_t)(pg.d0 + t) * PGR;
-      // pass 0 (P x_B) only in a full round: an update round keeps x_B off the factored list
-      on = R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || (R[R_NZB] != 0.0 && R[R_MODE] == 0.0));
+      on = R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || R[R_NZB] != 0.0);
       g_T[t] = lr.tlen[pg.d0 + t];
       g_off[t] = uoff[pg.d0 + t];
     }
@@ -1007,7 +905,7 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
                                                 const double* scr) {
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
-  if (!(R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || (R[R_NZB] != 0.0 && R[R_MODE] == 0.0)))) return;
+  if (!(R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || R[R_NZB] != 0.0))) return;
   int lo = 0, hi = ngroups;   // group of date b: gdates[grp] <= b < gdates[grp + 1]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
@@ -1151,7 +1049,7 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
     o[PQ_OUT_DUAL] = dres;
     o[PQ_OUT_GAP] = fabs(xpx + qx + gapb);
     o[PQ_OUT_RHO] = st.rho[b];
-    o[PQ_OUT_NFREE] = R[R_K] - R[R_ND];
+    o[PQ_OUT_NFREE] = R[R_K];
     o[PQ_OUT_ROUNDS] = R[R_ROUNDS];
     st.status[b] = PQ_SOLVED;
     R[R_STATE] = PQ_PG_DONE;
@@ -1190,8 +1088,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   hipStream_t str = (hipStream_t)stream;
   const int B = pb->batch;
   const int kmax = ldk < pq::PG_KMAX ? ldk : pq::PG_KMAX;
-  const int upd = pq::pg_update_ok(ldk) ? 1 : 0;   // room for the saved factor in the K scratch
-  hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax, upd);
+  hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax);
   const dim3 gsplit(ngroups * pq::QS);
   hipLaunchKernelGGL(pq::k_pg_passA<0>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
@@ -1201,11 +1098,11 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
                      pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
   // one wave per date, the LDS triangle sized to the free set (more dates per CU when small)
-  hipLaunchKernelGGL(pq::k_pg_solve<48>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 0, upd);
-  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 48, upd);
-  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 64, upd);
-  if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 80, upd);
-  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 96, upd);
+  hipLaunchKernelGGL(pq::k_pg_solve<48>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 0);
+  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 48);
+  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 64);
+  if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 80);
+  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 96);
   hipLaunchKernelGGL(pq::k_pg_passA<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_passB<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
