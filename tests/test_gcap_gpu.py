@@ -44,9 +44,9 @@ def _problem(device, n, T, D, ub, stride=1, centred=True):
     return qb, lr, gp
 
 
-def _run(qb, lr, gp, gcap, settings):
+def _run(qb, lr, gp, gcap, settings, polish=True):
     ws = engine.Workspace(qb, dense=False)
-    res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, gcap=gcap)
+    res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, gcap=gcap, polish=polish)
     torch.cuda.synchronize()
     return (res.x.cpu().numpy().copy(), res.status.cpu().numpy().copy(), res.iters.cpu().numpy().copy(),
             res.capacitance, res.refactors)
@@ -87,14 +87,28 @@ def test_gcap_group_rho_adaptation(device):
 
 @pytest.mark.parametrize("n,T,D,ub,stride", [(1000, 252, 48, 1.0, 1), (494, 252, 40, 1.0, 1), (300, 60, 30, 0.2, 3)])
 def test_gcap_uncentred_same_iterates_with_one_rho(device, n, T, D, ub, stride):
+    """The ADMM iterates themselves (no polish): the tracking P = 2 X'X has rank T < n, so
+    the optimum can be a face and polished points of two exact solvers need not coincide."""
     qb, lr, gp = _problem(device, n, T, D, ub, stride, centred=False)
     st = engine.Settings(rho0_rel=0.0, rho0=0.05, rho0_qrel=0.0, adapt_interval=0)
-    xa, sa, ia, cap_a, _ = _run(qb, lr, gp, False, st)
-    xb, sb, ib, cap_b, _ = _run(qb, lr, gp, True, st)
+    xa, sa, ia, cap_a, _ = _run(qb, lr, gp, False, st, polish=False)
+    xb, sb, ib, cap_b, _ = _run(qb, lr, gp, True, st, polish=False)
     assert cap_a == "band" and cap_b == "group"
     assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED), (sa, sb)
-    assert np.abs(ia - ib).max() <= 1, (ia, ib)
-    assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()
+    assert np.array_equal(ia, ib), (ia, ib)
+    # uncentred windows leave the market mode in X_U X_U' (the centred case removes it), so
+    # the Woodbury correction H_b is worse conditioned and rounding differences between the
+    # per-date and the group form grow to ~2e-9 over ~20 iterations (measured; x ~ 1e-3)
+    assert np.abs(xa - xb).max() <= 1e-8, np.abs(xa - xb).max()
+
+
+def _objective(qb, lr, x):
+    """1/2 x'P x + q'x with P = 2 X'X of each date's window (torch, independent of the engine)."""
+    R = lr.panel.R
+    X = R[lr.rows.long()] * (torch.arange(lr.tmax, device=R.device)[None, :] < lr.tlen[:, None]).to(R.dtype)[:, :, None]
+    xt = torch.from_numpy(x).to(R.device)
+    v = torch.bmm(X, xt[:, :, None])[:, :, 0]
+    return ((v * v).sum(1) + (qb.q[:, :x.shape[1]] * xt).sum(1)).cpu().numpy()
 
 
 def test_gcap_uncentred_tracking_default_settings(device):
@@ -104,4 +118,6 @@ def test_gcap_uncentred_tracking_default_settings(device):
     xb, sb, _, cap, _ = _run(qb, lr, gp, True, st)
     assert cap == "group"
     assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED)
-    assert np.abs(xa - xb).max() <= 1e-8, np.abs(xa - xb).max()
+    fa, fb = _objective(qb, lr, xa), _objective(qb, lr, xb)
+    assert np.abs(fa - fb).max() <= 1e-9 * np.abs(fa).max(), np.abs(fa - fb).max()
+    assert np.abs(xb.sum(1) - 1).max() < 1e-10 and xb.min() > -1e-10
