@@ -369,18 +369,39 @@ int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st
  * window passes of a group run split over 4 workgroups (column slices), with
  * pass_scratch = ngroups * PQ_PG_PASS_SCRATCH doubles for their partial products.
  * Replaces, with pq_polish_w_batched, the accuracy of qpsolvers (src/qp_problems.py:211-214). */
-#define PQ_PG_RECORD 320
+#define PQ_PG_RECORD 384
 #define PQ_PG_PASS_SCRATCH 20816   /* doubles per group: 4 x 324 x 16 + 4 x 16 + 16 */
 #define PQ_PG_PENDING 0
 #define PQ_PG_DONE 1
 #define PQ_PG_FALLBACK 2
 #define PQ_PG_SKIP 3
+/* Wide rounds (polish_gw.hip, wide != NULL): a pending problem whose free set exceeds
+ * min(128, ldk) with at most PQ_PG_WMB bordered rows (active general rows + variables at a
+ * bound) solves its round's KKT system in n-space by a group capacitance of the polish
+ * matrix K = P + d I, d = p_diag + gc->grho[g] (one value per group: built by
+ * pq_gcap_assemble / pq_factor_batched / pq_gcap_prepare with mg = 0 and a unit box, so
+ * that the box rho is grho), the bordered rows eliminated by a per-date Schur complement,
+ * and refine_steps proximal refinement steps (early exit at convergence) whose window products are MFMA
+ * passes over the union rows of the group (16 dates per pass).  pc / ldpc / r0 / cc: the
+ * band setup's panel-row products with the general rows and C C'; nzr / nzv / nzmax: their
+ * column-sparse form (needed when mg > 4; mg <= 24); wscr: PQ_PG_WSCR(k_ld) doubles per
+ * problem, wscr_stride apart.  Replaces, with the rest of the round, the accuracy of
+ * qpsolvers' answer for free sets of any size (src/qp_problems.py:211-214). */
+#define PQ_PG_WMB 8
+#define PQ_PG_WSCR(k_ld) (2 * PQ_PG_WMB * (int64_t)(k_ld))
+typedef struct pq_pg_wide {
+  const pq_gcap* gc;
+  const double* pc; int64_t ldpc; int32_t r0; const double* cc;
+  const int32_t* nzr; const double* nzv; int32_t nzmax;
+  double* wscr; int64_t wscr_stride;
+  int32_t refine_steps;         /* proximal refinement steps per wide round (>= 1)          */
+} pq_pg_wide;
 int pq_polish_grouped_init(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
                            const pq_settings* s, void* stream);
 int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec, int32_t ldk,
                             const int32_t* gdates, int32_t ngroups, const int32_t* urows, const int32_t* ucnt,
                             const int32_t* uoff, int32_t umax, const pq_settings* s, double* pass_scratch,
-                            void* stream);
+                            const pq_pg_wide* wide, void* stream);
 
 /* Strategy simulation: one holding period per rebalance date.
  * Replaces Strategy.simulate (src/portfolio.py:209-248) with floating_weights

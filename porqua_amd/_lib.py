@@ -25,10 +25,11 @@ PQ_PRIMAL_INFEASIBLE = -3
 PQ_DUAL_INFEASIBLE = -4
 PQ_NON_CONVEX = -5
 
-PQ_PG_RECORD = 320                   # doubles per problem of the grouped polish record
+PQ_PG_RECORD = 384                   # doubles per problem of the grouped polish record
 PQ_PG_PASS_SCRATCH = 20816           # doubles per slide group of the split polish window passes
 PQ_PG_PENDING, PQ_PG_DONE, PQ_PG_FALLBACK, PQ_PG_SKIP = range(4)
 PQ_PG_STATE = 3                      # record field holding the state
+PQ_PG_K, PQ_PG_SC, PQ_PG_W = 0, 5, 320   # record fields: free count, problem scale, wide round
 
 PQ_OUT_OBJ, PQ_OUT_PRIM, PQ_OUT_DUAL, PQ_OUT_GAP, PQ_OUT_RHO, PQ_OUT_NFREE, PQ_OUT_ROUNDS = range(7)
 PQ_OUT_FIELDS = 8
@@ -103,6 +104,25 @@ class PQGcap(ctypes.Structure):
     ]
 
 
+class PQPgWide(ctypes.Structure):
+    """pq_pg_wide: the wide rounds of the grouped polish (include/porqua_hip.h)."""
+    _fields_ = [
+        ("gc", ctypes.POINTER(PQGcap)),
+        ("pc", c_dp), ("ldpc", c_int64), ("r0", c_int32), ("cc", c_dp),
+        ("nzr", c_dp), ("nzv", c_dp), ("nzmax", c_int32),
+        ("wscr", c_dp), ("wscr_stride", c_int64),
+        ("refine_steps", c_int32),
+    ]
+
+
+PQ_PG_WMB = 8                        # bordered rows per date of a wide round
+
+
+def pg_wscr(k_ld: int) -> int:
+    """PQ_PG_WSCR(k_ld): doubles per problem of the wide rounds' scratch."""
+    return 2 * PQ_PG_WMB * int(k_ld)
+
+
 _EXPORTS = {
     "pq_version": ([], c_int32),
     "pq_last_error": ([], ctypes.c_char_p),
@@ -163,7 +183,7 @@ _EXPORTS = {
                                 c_dp, ctypes.POINTER(PQSettings), c_dp], c_int32),
     "pq_polish_grouped_round": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                                  c_dp, c_int32, c_dp, c_int32, c_dp, c_dp, c_dp, c_int32,
-                                 ctypes.POINTER(PQSettings), c_dp, c_dp], c_int32),
+                                 ctypes.POINTER(PQSettings), c_dp, ctypes.POINTER(PQPgWide), c_dp], c_int32),
     "pq_gcap_assemble": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQGcap),
                           ctypes.POINTER(PQSettings), c_dp, c_int64, c_int32, c_dp, c_int64, c_dp, c_dp], c_int32),
     "pq_gcap_prepare": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),

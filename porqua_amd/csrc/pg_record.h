@@ -1,0 +1,51 @@
+// The per-date record and work layout of the grouped polish pipeline (polish_g.hip) and its
+// wide-free-set solve (polish_gw.hip).
+#pragma once
+#include "common.h"
+#include "../../include/porqua_hip.h"
+
+namespace pq {
+
+// per-date polish record (doubles), PQ_PG_RECORD in include/porqua_hip.h
+constexpr int PGR = PQ_PG_RECORD;
+enum : int {
+  R_K = 0, R_MA = 1, R_NZB = 2, R_STATE = 3, R_ROUNDS = 4, R_SC = 5,
+  R_ACT = 64, R_LAM = 128, R_DA = 192, R_SOL = 256, R_AL = 288,
+  // wide mode: R_W = 1 this round, R_NFX fixed variables at R_FIX (indices), R_FIXV (bound
+  // values), R_FXL (their multipliers = box duals)
+  R_W = 320, R_NFX = 321, R_FIX = 324, R_FIXV = 332, R_FXL = 340
+};
+constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
+constexpr int PG_MGMAX = 32;   // general rows
+// wide mode (polish_gw.hip): the free set exceeds the LDS solve, so the round solves the full
+// n-space reduced KKT by the group capacitance with the active general rows and the fixed
+// variables as bordered rows (at most PG_WMB of them)
+constexpr int PG_WMB = 8;
+constexpr int PG_WG_MAX = 24;   // general rows of the wide mode
+static_assert(R_FXL + PG_WMB <= PQ_PG_RECORD, "PQ_PG_RECORD too small");
+
+struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
+  double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;
+  int *Fl, *fl;
+  __device__ __forceinline__ PGWork(const pq_state& st, int b, int ld) {
+    double* W = st.work + (int64_t)b * st.work_stride;
+    xs = W;
+    xb = W + ld;
+    g = W + 2 * (int64_t)ld;
+    Px = W + 3 * (int64_t)ld;
+    Fl = reinterpret_cast<int*>(W + 4 * (int64_t)ld);
+    rF = W + 5 * (int64_t)ld;
+    solx = W + 6 * (int64_t)ld;
+    pxb = W + 7 * (int64_t)ld;
+    U = W + 8 * (int64_t)ld;
+    fl = reinterpret_cast<int*>(U + (int64_t)st.mg_pad * ld);
+  }
+};
+
+__device__ __forceinline__ int pk(int r, int c) { return ((r * (r + 1)) >> 1) + c; }
+
+}  // namespace pq
+
+// wide rounds (polish_gw.hip), launched by pq_polish_grouped_round
+int pq_pg_wide_launch(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec, const pq_settings* s,
+                      const pq_pg_wide* wd, hipStream_t stream);

@@ -30,37 +30,10 @@
 // example/compare_solver.ipynb:212-216.
 #include "polish_dev.h"
 #include "capi_util.h"
+#include "pg_record.h"
 
 namespace pq {
 
-// per-date polish record (doubles), PQ_PG_RECORD in include/porqua_hip.h
-constexpr int PGR = PQ_PG_RECORD;
-enum : int {
-  R_K = 0, R_MA = 1, R_NZB = 2, R_STATE = 3, R_ROUNDS = 4, R_SC = 5,
-  R_ACT = 64, R_LAM = 128, R_DA = 192, R_SOL = 256, R_AL = 288
-};
-constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
-constexpr int PG_MGMAX = 32;   // general rows
-
-struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
-  double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;
-  int *Fl, *fl;
-  __device__ __forceinline__ PGWork(const pq_state& st, int b, int ld) {
-    double* W = st.work + (int64_t)b * st.work_stride;
-    xs = W;
-    xb = W + ld;
-    g = W + 2 * (int64_t)ld;
-    Px = W + 3 * (int64_t)ld;
-    Fl = reinterpret_cast<int*>(W + 4 * (int64_t)ld);
-    rF = W + 5 * (int64_t)ld;
-    solx = W + 6 * (int64_t)ld;
-    pxb = W + 7 * (int64_t)ld;
-    U = W + 8 * (int64_t)ld;
-    fl = reinterpret_cast<int*>(U + (int64_t)st.mg_pad * ld);
-  }
-};
-
-__device__ __forceinline__ int pk(int r, int c) { return ((r * (r + 1)) >> 1) + c; }
 
 // ---------------------------------------------------------------------------------------
 // init: classification from the ADMM point (polish_w.hip's, verbatim) + problem scale
@@ -95,6 +68,7 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
   for (int i = t; i < n; i += PT) sc = fmax(sc, fmax(fabs(q[i]), fabs(psw * dgb[i] + pd)));
   sc = block_max(sc, red);
   sc = fmax(sc, 1e-300);
+  double nfree = 0.0;
   for (int i = t; i < ld; i += PT) {
     int f = 0;
     if (i < n && has_box) {
@@ -105,7 +79,9 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
     }
     wk.fl[i] = (i < n) ? f : 1;
     wk.xs[i] = (i < n) ? sx[i] : 0.0;
+    nfree += (i < n && f == 0) ? 1.0 : 0.0;
   }
+  nfree = block_sum(nfree, red);   // the caller reads it to decide whether wide rounds can occur
   if (t < 64) {
     int a = 0;
     double lam = 0.0;
@@ -123,8 +99,9 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
     R[R_STATE] = PQ_PG_PENDING;
     R[R_ROUNDS] = 0;
     R[R_SC] = sc;
-    R[R_K] = 0;
+    R[R_K] = nfree;
     R[R_NZB] = 0;
+    R[R_W] = 0;
   }
 #ifdef PQ_PROFILE
   if (t >= 8 && t < 20) R[t] = 0.0;
@@ -134,7 +111,7 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
 // ---------------------------------------------------------------------------------------
 // setup: free list, active rows, x_B, dA, the starting point of the refinement
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, double* rec, int kmax) {
+__global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, double* rec, int kmax, int wide_ok) {
   __shared__ int wcnt[PW];
   __shared__ int s_al[PG_MGMAX + 1];
   __shared__ double red[16];
@@ -173,6 +150,42 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     k += wcnt[ww];
   }
   const int ma = s_al[PG_MGMAX];
+  // ---- wide mode (polish_gw.hip): a free set beyond the LDS solve with at most PG_WMB
+  // bordered rows (active general rows + fixed variables); the group solve works in n-space
+  // from x = xs, so neither the free list nor x_B is built -------------------------------
+  const int nfx = n - k;
+  if (wide_ok && k > kmax && mg <= PG_WG_MAX && ma + nfx <= PG_WMB) {   // uniform
+    if (w == 0) {   // fixed variables, ascending
+      int nb = 0;
+      for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + l;
+        const int f = i < n ? wk.fl[i] : 0;
+        const unsigned long long m = __ballot(f != 0);
+        if (f != 0) {
+          const int j = nb + __popcll(m & ((1ull << l) - 1ull));
+          R[R_FIX + j] = i;
+          R[R_FIXV + j] = f == 1 ? lb[i] : ub[i];
+          R[R_FXL + j] = st.y[(int64_t)b * st.m_ld + st.mg_pad + i];   // the ADMM box dual
+        }
+        nb += __popcll(m);
+      }
+    }
+    if (t < ma) {
+      const int r = s_al[t];
+      R[R_AL + t] = r;
+      R[R_SOL + t] = R[R_LAM + r];
+      R[R_DA + t] = R[R_ACT + r] == 1.0 ? lg[r] : ug[r];
+    }
+    if (t == 0) {
+      R[R_K] = k;
+      R[R_MA] = ma;
+      R[R_NZB] = 0;
+      R[R_W] = 1;
+      R[R_NFX] = nfx;
+      R[R_ROUNDS] += 1.0;
+    }
+    return;
+  }
   // every variable at a bound (a vertex, e.g. nearly linear objectives): x = x_B, and the
   // multiplier of at most one active equality row is chosen in the post from the dual
   // feasibility interval of the bound variables (k_pg_post); otherwise the per-date kernel
@@ -221,6 +234,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     R[R_K] = k;
     R[R_MA] = ma;
     R[R_NZB] = nzb;
+    R[R_W] = 0;
     R[R_ROUNDS] += 1.0;
   }
 }
@@ -242,7 +256,7 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPIT];
   const int b = blockIdx.x;
   const double* R = rec + (int64_t)b * PGR;
-  if (R[R_STATE] != PQ_PG_PENDING) return;
+  if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;   // wide dates: polish_gw.hip
   const int k = (int)R[R_K];
   if (k > PG_KMAX || k == 0) return;
   const int ld = pb.ld;
@@ -489,7 +503,7 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   __shared__ int s_al[WMA];
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
-  if (R[R_STATE] != PQ_PG_PENDING) return;
+  if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;
   const int k = (int)R[R_K];
   if (k <= klo || k > KS) return;
   const int ma = (int)R[R_MA];
@@ -1075,7 +1089,7 @@ extern "C" int pq_polish_grouped_init(const pq_lowrank* lr, const pq_problem* pb
 extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
                                        int32_t ldk, const int32_t* gdates, int32_t ngroups, const int32_t* urows,
                                        const int32_t* ucnt, const int32_t* uoff, int32_t umax, const pq_settings* s,
-                                       double* pass_scratch, void* stream) {
+                                       double* pass_scratch, const pq_pg_wide* wide, void* stream) {
   PQ_CHECK_ARG(lr && pb && st && s && rec && pass_scratch, "pq_polish_grouped_round: null argument");
   static_assert(pq::QSCR == PQ_PG_PASS_SCRATCH, "PQ_PG_PASS_SCRATCH out of date");
   PQ_CHECK_ARG(gdates && urows && ucnt && uoff && umax > 0 && umax <= pq::QU,
@@ -1088,7 +1102,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   hipStream_t str = (hipStream_t)stream;
   const int B = pb->batch;
   const int kmax = ldk < pq::PG_KMAX ? ldk : pq::PG_KMAX;
-  hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax);
+  hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax, wide ? 1 : 0);
   const dim3 gsplit(ngroups * pq::QS);
   hipLaunchKernelGGL(pq::k_pg_passA<0>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
@@ -1103,6 +1117,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 64);
   if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 80);
   if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 96);
+  if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, str)) return -1;   // free sets beyond kmax
   hipLaunchKernelGGL(pq::k_pg_passA<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_passB<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,

@@ -79,6 +79,14 @@ class Settings:
     # window path: initial rho >= rho0_qrel * max|q| (host-side, not in pq_settings): for
     # nearly linear objectives (small risk aversion) 4 mean(diag P) is far too small a rho
     rho0_qrel: float = 10.0
+    # wide rounds of the grouped polish (polish_gw.hip, host-side): refinement steps per round
+    # (early exit at the 1e-13 residual) and the group capacitance's diagonal relative to the
+    # problem scale (the reduced KKT system keeps delta).  Measured on config 4
+    # (profiles/r03c_config4_grid.log, steps 2/4/6/10 x 1e-9/1e-7): at 1e-9 the explicit M_U^-1
+    # (condition ~1e11) limits each step to ~1e-5, so 2 steps leave 2e-7 stationarity and 1.8
+    # rounds; 1e-7 converges in <= 4 steps to 5e-13 (87k QPs/s, polish 40 ms, 1.0 rounds)
+    refine_wide: int = 6
+    delta_wide: float = 1e-7
 
     def to_c(self) -> _lib.PQSettings:
         names = {f[0] for f in _lib.PQSettings._fields_}
@@ -602,7 +610,7 @@ def _band_setup(qb: QPBatch, lr: LowRank, strm, w_min: int = 0):
                "pq_lr_band_gram")
     C = qb.Cg[0, :mg, :n]
     cc = (C @ C.T).contiguous() if mg else torch.zeros((1, 1), dtype=F64, device=dev)
-    return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc}
+    return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc, "W": W}
 
 
 def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan", settings: Settings):
@@ -658,11 +666,96 @@ def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan"
     return buf
 
 
+def _pg_wide_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan", bd: dict, rec: torch.Tensor,
+                   settings: Settings, sparse_cols, strm):
+    """Group capacitance of the polish matrix K = P + d I for the wide rounds of the grouped
+    polish (polish_gw.hip), d = p_diag + delta_g with delta_g the geometric mean of the
+    group's dates' delta (settings.delta x problem scale, record field PQ_PG_SC): the same
+    assemble / factor / prepare as the ADMM's group capacitance, with no general rows in the
+    capacitance and a unit box whose rho is delta_g.  Returns the pq_pg_wide argument
+    (its buffers kept alive on ws), or None when the wide form does not apply."""
+    lib = _lib.load()
+    B, dev, mg, G = qb.batch, qb.device, qb.mg, groups.ngroups
+    nzr, nzv, nzmax = sparse_cols if mg > 4 else (None, None, 0)
+    # uncentred windows only (LeastSquares tracking): with a mean column the correction H_b has
+    # the entry 1 - (cT/d)(mu'mu - a'q/d), which cancels catastrophically at the polish's small d
+    if (lr.mu is not None or bd is None or bd["W"] < groups.span_max or not qb.shared or mg > 24
+            or (mg > 4 and nzmax == 0) or groups.ucnt_max + mg > 320 or groups.corr_max > 64):
+        return None
+    ps = qb.p_scale if qb.p_scale is not None else torch.ones(B, dtype=F64, device=dev)
+    c = ps * (lr.w_scale if lr.w_scale is not None else torch.ones(B, dtype=F64, device=dev))
+    pd = qb.p_diag if qb.p_diag is not None else torch.zeros(B, dtype=F64, device=dev)
+    first = groups.gdates[:-1].long()[groups.gidx.long()]
+    if not bool(((c == c[first]) & (pd == pd[first])).all().item()):
+        return None
+    k_ld = round_up(groups.ucnt_max, 64)
+    ldh = min(64, round_up(groups.corr_max, 8))
+    key = (B, G, k_ld, ldh)
+    buf = getattr(ws, "_pgw", None)
+    if buf is None or buf["key"] != key:
+        buf = {"key": key,
+               "M": torch.empty((G, k_ld, k_ld), dtype=F64, device=dev),
+               "Minv": torch.empty((G, k_ld, k_ld), dtype=F64, device=dev),
+               "Dt": torch.empty((G, k_ld // 64, 64, 64), dtype=F64, device=dev),
+               "grho": torch.empty(G, dtype=F64, device=dev),
+               "iters": torch.zeros(G, dtype=torch.int32, device=dev),
+               "status": torch.zeros(max(G, B), dtype=torch.int32, device=dev),
+               "info": torch.zeros(G, dtype=torch.int32, device=dev),
+               "aq": torch.empty((B, 2 * k_ld), dtype=F64, device=dev),
+               "hinv": torch.empty((B, ldh, ldh), dtype=F64, device=dev),
+               "wscr": torch.empty((B, _lib.pg_wscr(k_ld)), dtype=F64, device=dev),
+               "lb": torch.zeros(2, dtype=F64, device=dev), "ub": torch.ones(2, dtype=F64, device=dev)}
+        ws._pgw = buf
+    gi = groups.gidx.long()
+    ld = torch.log(torch.clamp(settings.delta_wide * rec[:, _lib.PQ_PG_SC], min=1e-300))
+    gl = torch.zeros(G, dtype=F64, device=dev).index_add_(0, gi, ld)
+    buf["grho"].copy_(torch.exp(gl / torch.from_numpy(groups.sizes.astype(np.float64)).to(dev)))
+    gc = _lib.PQGcap(gdates=groups.gdates.data_ptr(), ngroups=G, urows=groups.urows.data_ptr(),
+                     ucnt=groups.ucnt.data_ptr(), uoff=groups.uoff.data_ptr(), umax=groups.umax,
+                     gidx=groups.gidx.data_ptr(), grho=buf["grho"].data_ptr(), M=buf["M"].data_ptr(),
+                     Minv=buf["Minv"].data_ptr(), k_ld=k_ld, M_stride=k_ld * k_ld, aq=buf["aq"].data_ptr(),
+                     aq_stride=2 * k_ld, hinv=buf["hinv"].data_ptr(), ldh=ldh)
+    # the polish matrix: no general rows in the capacitance, a unit box (rho = delta_g), sigma 0
+    pbw = qb.c_struct()
+    pbw.mg = 0
+    pbw.lb, pbw.ub, pbw.box_stride = buf["lb"].data_ptr(), buf["ub"].data_ptr(), 0
+    sw = Settings(sigma=0.0).to_c()
+    stw = _lib.PQState(status=buf["status"].data_ptr())
+    L_ = ctypes.byref(lr.c_struct())
+    band, ldo, r0 = bd["band"].data_ptr(), bd["ldo"], bd["r0"]
+    pcp, ldpc = bd["pc"].data_ptr(), bd["pc"].stride(0)
+    _lib.check(lib.pq_gcap_assemble(L_, ctypes.byref(pbw), ctypes.byref(gc), ctypes.byref(sw), band, ldo, r0, pcp,
+                                    ldpc, bd["cc"].data_ptr(), strm), "pq_gcap_assemble (polish)")
+    pbf = _lib.PQProblem(n=groups.ucnt_max, ld=k_ld, batch=G, mg=0, P=buf["M"].data_ptr(), P_stride=k_ld * k_ld,
+                         q=qb.q.data_ptr(), q_stride=qb.q.stride(0), Cg=qb.Cg.data_ptr(), lg=qb.lg.data_ptr(),
+                         ug=qb.ug.data_ptr())
+    stf = _lib.PQState(K=buf["Minv"].data_ptr(), K_stride=k_ld * k_ld, Dt=buf["Dt"].data_ptr(),
+                       Dt_stride=(k_ld // 64) * 4096, x=ws.x.data_ptr(), Px=ws.Px.data_ptr(), z=ws.z.data_ptr(),
+                       y=ws.y.data_ptr(), m_ld=ws.m_ld, mg_pad=ws.mg_pad, rho=buf["grho"].data_ptr(),
+                       iters=buf["iters"].data_ptr(), status=buf["status"].data_ptr(), info=buf["info"].data_ptr(),
+                       out=ws.out.data_ptr(), work=ws.work.data_ptr(), work_stride=ws.work_stride)
+    _lib.check(lib.pq_factor_batched(ctypes.byref(pbf), ctypes.byref(stf), None, 0, ctypes.byref(sw), 2, strm),
+               "pq_factor_batched (polish M_U)")
+    buf["status"].zero_()
+    _lib.check(lib.pq_gcap_prepare(L_, ctypes.byref(pbw), ctypes.byref(stw), ctypes.byref(gc), ctypes.byref(sw),
+                                   None, 0, band, ldo, r0, pcp, ldpc, strm), "pq_gcap_prepare (polish)")
+    # a date whose correction H_b is not SPD to rounding, or whose group's M_U failed, keeps the
+    # per-date kernel (state FALLBACK before the first round)
+    bad = (buf["status"][:B] == _lib.PQ_NON_CONVEX) | (buf["info"][gi] != 0)
+    rec[:, _lib.PQ_PG_STATE] = torch.where(bad & (rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_PENDING),
+                                           float(_lib.PQ_PG_FALLBACK), rec[:, _lib.PQ_PG_STATE])
+    buf["gc"] = gc
+    buf["wide"] = _lib.PQPgWide(gc=ctypes.pointer(gc), pc=pcp, ldpc=ldpc, r0=r0, cc=bd["cc"].data_ptr(),
+                                nzr=_ptr(nzr), nzv=_ptr(nzv), nzmax=nzmax, wscr=buf["wscr"].data_ptr(),
+                                wscr_stride=buf["wscr"].stride(0), refine_steps=int(settings.refine_wide))
+    return buf["wide"]
+
+
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
                   fuse: bool = True, grouped_polish: bool = True, gcap: bool = True,
-                  eig: "EigCap | None" = None) -> BatchResult:
+                  eig: "EigCap | None" = None, wide_polish: bool = True) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -815,10 +908,17 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         if scr is None or scr.numel() < g.ngroups * _lib.PQ_PG_PASS_SCRATCH:
             scr = torch.empty(g.ngroups * _lib.PQ_PG_PASS_SCRATCH, dtype=F64, device=dev)
             ws._pg_pass = scr
+        # free sets beyond the LDS solve (k_pg_init left each date's free count in PQ_PG_K): the
+        # wide rounds' group capacitance, built once for the whole polish
+        wide = None
+        if wide_polish and bool((rec[:, _lib.PQ_PG_K] > min(ldk, 128)).any()):   # host sync: one flag
+            wide = _pg_wide_setup(qb, lr, ws, g, bd, rec, settings or Settings(), sparse_cols, strm)
+        wide_p = ctypes.byref(wide) if wide is not None else None
+        cnt["pg_wide"] = wide is not None
         for r in range(int(s.polish_rounds)):
             _lib.check(lib.pq_polish_grouped_round(L_, P_, S_, rp, ldk, _ptr(g.gdates), g.ngroups, _ptr(g.urows),
-                                                   _ptr(g.ucnt), _ptr(g.uoff), g.umax, SS_main, scr.data_ptr(), strm),
-                       "pq_polish_grouped_round")
+                                                   _ptr(g.ucnt), _ptr(g.uoff), g.umax, SS_main, scr.data_ptr(),
+                                                   wide_p, strm), "pq_polish_grouped_round")
             if r >= 1 and not bool((rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_PENDING).any()):   # host sync
                 break
         fb = torch.nonzero(rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_FALLBACK).flatten().to(torch.int32)

@@ -197,7 +197,7 @@ class TrackingBacktest:
 
 
 def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_row=None, b=None, lb=None, ub=None,
-                       chunk: int = 256, C=None, lg=None, ug=None, rows_of=None) -> dict:
+                       chunk: int = 256, C=None, lg=None, ug=None, rows_of=None, p_diag=None) -> dict:
     """KKT residuals of every solution of a window-path batch, P_p = scale_p * Xc_p' Xc_p
     (Xc = window rows minus ``mu``; ``mu`` None = uncentred).  P x is recomputed here with
     torch from the panel rows, not by the engine's kernels.
@@ -207,7 +207,8 @@ def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_r
     ``A_row' x = b`` is one equality row.  Box ``lb <= x <= ub`` with multipliers
     ``res.z_box``.  ``rows_of`` (optional int64 device tensor, one entry per problem) maps
     problem p to its window / moments row in ``rows``, ``tlen``, ``mu`` (e.g. the date of a
-    risk-aversion sweep problem).
+    risk-aversion sweep problem).  ``p_diag`` (optional, one value per problem): a ridge,
+    P_p = scale_p Xc_p'Xc_p + p_diag_p I.
 
     Returns the maxima over the batch of
       * ``max_violation``: max(|C x - b| on equality rows, [C x - ug]+, [lg - C x]+,
@@ -245,6 +246,8 @@ def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_r
         X = X * valid[:, :, None]
         v = torch.bmm(X, x[:, :, None])                                 # (b, tmax, 1)
         Px = scale[s:e, None] * torch.bmm(X.transpose(1, 2), v)[:, :, 0]
+        if p_diag is not None:
+            Px = Px + p_diag[s:e, None] * x
         y = res.y[s:e, :mg]
         zb = res.z_box[s:e]
         Cty = y @ C

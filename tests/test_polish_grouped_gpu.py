@@ -43,9 +43,12 @@ def _problem(device, n, T, D, ub, ngroups_rows=0, cap=0.3, centred=True, stride=
 
 
 def _solve(qb, lr, gp, grouped_polish, settings=None):
+    """(wide rounds off: this file pins the LDS-solve pipeline against the per-date kernel;
+    tests/test_polish_wide_gpu.py covers the wide rounds)"""
     ws = engine.Workspace(qb, dense=False)
     assert engine.grouped_applicable(qb, lr, gp, ws)
-    res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, grouped_polish=grouped_polish)
+    res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, grouped_polish=grouped_polish,
+                               wide_polish=False)
     torch.cuda.synchronize()
     rec = ws.pg_record()[:, _lib.PQ_PG_STATE].cpu().numpy().copy() if grouped_polish else None
     return (res.x.cpu().numpy().copy(), res.status.cpu().numpy().copy(), res.obj.cpu().numpy().copy(),
