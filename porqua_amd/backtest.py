@@ -24,6 +24,7 @@ to force the serial loop, which still solves each date on the device).
 """
 from __future__ import annotations
 
+import gc
 import os
 import pickle
 from typing import Optional
@@ -442,15 +443,24 @@ class Backtest:
         none = [None] * n
         append_fun = bs.settings.get("append_fun")
         portfolios = self.strategy.portfolios
-        for i, d in enumerate(rebdates):
-            if append_fun is None and solved[i]:
-                # the weights stay a row of W until read (Portfolio._from_row); the dict is
-                # == pd.Series(w, index=universe).to_dict() (Python floats)
-                portfolios.append(Portfolio._from_row(d, keys, W[i]))
-                continue
-            w = W[i].tolist() if solved[i] else none
-            opt.results = {"weights": dict(zip(keys, w)), "status": bool(solved[i])}
-            self._after_solve(bs, d)
+        # thousands of small objects: a cyclic-GC pass over the process's ~2e5 torch / pandas
+        # objects can land in this loop (measured 5 -> 110 ms for 4544 dates); nothing here
+        # creates reference cycles, so the collector is paused for it
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            for i, d in enumerate(rebdates):
+                if append_fun is None and solved[i]:
+                    # the weights stay a row of W until read (Portfolio._from_row); the dict is
+                    # == pd.Series(w, index=universe).to_dict() (Python floats)
+                    portfolios.append(Portfolio._from_row(d, keys, W[i]))
+                    continue
+                w = W[i].tolist() if solved[i] else none
+                opt.results = {"weights": dict(zip(keys, w)), "status": bool(solved[i])}
+                self._after_solve(bs, d)
+        finally:
+            if gc_was:
+                gc.enable()
         if rebdates:   # the optimisation's results hold the last date's, as after the serial loop
             last = len(rebdates) - 1
             w = W[last].tolist() if solved[last] else none

@@ -581,14 +581,35 @@ def _sparse_columns(qb: QPBatch, nz_limit: int = 4):
     return rows.T.contiguous(), vals.T.contiguous(), nzmax
 
 
+def _tkey(*ts):
+    """Cache key of tensors (None allowed): storage, shape and in-place version counter, so
+    it changes when a tensor is replaced or modified in place."""
+    return tuple(None if t is None else (t.data_ptr(), tuple(t.shape), t._version) for t in ts)
+
+
+def _cached(owner, name: str, key, fn):
+    """fn() cached on ``owner`` under ``name`` while ``key`` is unchanged (host-side checks
+    with device syncs and constant tables are then paid once per batch, not per solve)."""
+    hit = getattr(owner, name, None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    val = fn()
+    setattr(owner, name, (key, val))
+    return val
+
+
 def _uniform_box(qb: QPBatch) -> bool:
     """Every box row of every problem gets the same ADMM rho (pq_lr_capacitance_band)."""
     if qb.lb is None:
         return True
     n = qb.n
-    lo, up = qb.lb[:, :n], qb.ub[:, :n]
-    cls = torch.where(torch.isinf(lo) & torch.isinf(up), 1, torch.where(lo == up, 2, 0))
-    return bool((cls == cls[:, :1]).all().item()) and (qb.lb.shape[0] == 1 or bool((cls[:, 0] == cls[0, 0]).all().item()))
+
+    def check():
+        lo, up = qb.lb[:, :n], qb.ub[:, :n]
+        cls = torch.where(torch.isinf(lo) & torch.isinf(up), 1, torch.where(lo == up, 2, 0))
+        return bool((cls == cls[:, :1]).all().item()) and (qb.lb.shape[0] == 1 or
+                                                          bool((cls[:, 0] == cls[0, 0]).all().item()))
+    return _cached(qb, "_c_ubox", _tkey(qb.lb, qb.ub), check)
 
 
 def _band_setup(qb: QPBatch, lr: LowRank, strm, w_min: int = 0):
@@ -602,14 +623,17 @@ def _band_setup(qb: QPBatch, lr: LowRank, strm, w_min: int = 0):
     W = min(max(W, int(w_min)), nrows)
     dev, n, mg = qb.device, qb.n, qb.mg
     ldo = round_up(W, 2)
-    band = torch.empty((nrows, ldo), dtype=F64, device=dev)
-    pc = torch.empty((nrows, max(mg, 1)), dtype=F64, device=dev)
+    band, pc = _cached(lr, "_c_bandbuf", (nrows, ldo, mg),
+                       lambda: (torch.empty((nrows, ldo), dtype=F64, device=dev),
+                                torch.empty((nrows, max(mg, 1)), dtype=F64, device=dev)))
     R = lr.panel.R
     _lib.check(lib.pq_lr_band_gram(R.data_ptr(), R.stride(0), n, r0, nrows, W, band.data_ptr(), ldo,
                                    qb.Cg.data_ptr(), mg, qb.ld, pc.data_ptr(), pc.stride(0), strm),
                "pq_lr_band_gram")
-    C = qb.Cg[0, :mg, :n]
-    cc = (C @ C.T).contiguous() if mg else torch.zeros((1, 1), dtype=F64, device=dev)
+    def cgram():
+        C = qb.Cg[0, :mg, :n]
+        return (C @ C.T).contiguous() if mg else torch.zeros((1, 1), dtype=F64, device=dev)
+    cc = _cached(qb, "_c_cc", _tkey(qb.Cg), cgram)
     return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc, "W": W}
 
 
@@ -618,12 +642,15 @@ def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan"
     of some group do not share c = p_scale w_scale and p_diag.  Also sets one rho per group
     (the mean of its dates' initial rho) in ws.rho."""
     B, dev, mg = qb.batch, qb.device, qb.mg
-    ps = qb.p_scale if qb.p_scale is not None else torch.ones(B, dtype=F64, device=dev)
-    wsc = lr.w_scale if lr.w_scale is not None else torch.ones(B, dtype=F64, device=dev)
-    c = ps * wsc
-    pd = qb.p_diag if qb.p_diag is not None else torch.zeros(B, dtype=F64, device=dev)
-    first = groups.gdates[:-1].long()[groups.gidx.long()]
-    if not bool(((c == c[first]) & (pd == pd[first])).all().item()):
+
+    def uniform():
+        ps = qb.p_scale if qb.p_scale is not None else torch.ones(B, dtype=F64, device=dev)
+        wsc = lr.w_scale if lr.w_scale is not None else torch.ones(B, dtype=F64, device=dev)
+        c = ps * wsc
+        pd = qb.p_diag if qb.p_diag is not None else torch.zeros(B, dtype=F64, device=dev)
+        first = groups.gdates[:-1].long()[groups.gidx.long()]
+        return bool(((c == c[first]) & (pd == pd[first])).all().item())
+    if not _cached(ws, "_c_gcap_uniform", (id(groups),) + _tkey(qb.p_scale, lr.w_scale, qb.p_diag), uniform):
         return None
     G = groups.ngroups
     k_ld = round_up(groups.ucnt_max + mg, 64)
@@ -643,10 +670,11 @@ def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan"
                "hinv": torch.empty((B, ldh, ldh), dtype=F64, device=dev)}
         ws._gcap = buf
     # one rho per group: the mean of the dates' initial rho (scale-aware, _rho_floor_q included)
-    gr = torch.zeros(G, dtype=F64, device=dev).index_add_(0, groups.gidx.long(), ws.rho)
-    gr /= torch.from_numpy(groups.sizes.astype(np.float64)).to(dev)
-    buf["grho"].copy_(gr)
-    ws.rho.copy_(gr[groups.gidx.long()])
+    gidx, sizes = groups.device_index()
+    gr = buf["grho"]
+    gr.zero_().index_add_(0, gidx, ws.rho)
+    gr /= sizes
+    torch.index_select(gr, 0, gidx, out=ws.rho)
     kmax = groups.ucnt_max + mg
     buf["c"] = _lib.PQGcap(gdates=groups.gdates.data_ptr(), ngroups=G, urows=groups.urows.data_ptr(),
                            ucnt=groups.ucnt.data_ptr(), uoff=groups.uoff.data_ptr(), umax=groups.umax,
@@ -706,10 +734,10 @@ def _pg_wide_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPl
                "wscr": torch.empty((B, _lib.pg_wscr(k_ld)), dtype=F64, device=dev),
                "lb": torch.zeros(2, dtype=F64, device=dev), "ub": torch.ones(2, dtype=F64, device=dev)}
         ws._pgw = buf
-    gi = groups.gidx.long()
+    gi, sizes = groups.device_index()
     ld = torch.log(torch.clamp(settings.delta_wide * rec[:, _lib.PQ_PG_SC], min=1e-300))
     gl = torch.zeros(G, dtype=F64, device=dev).index_add_(0, gi, ld)
-    buf["grho"].copy_(torch.exp(gl / torch.from_numpy(groups.sizes.astype(np.float64)).to(dev)))
+    buf["grho"].copy_(torch.exp(gl / sizes))
     gc = _lib.PQGcap(gdates=groups.gdates.data_ptr(), ngroups=G, urows=groups.urows.data_ptr(),
                      ucnt=groups.ucnt.data_ptr(), uoff=groups.uoff.data_ptr(), umax=groups.umax,
                      gidx=groups.gidx.data_ptr(), grho=buf["grho"].data_ptr(), M=buf["M"].data_ptr(),
@@ -940,11 +968,13 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             tl("polish", polish_grouped)
         else:
             polish_w(None, 0)
-        rp = _repolish_set(ws, settings or Settings())
+        # one host sync: nothing rejected (the usual case) skips both repairs
+        rejected = bool((ws.status == _lib.PQ_SOLVED_INACCURATE).any().item())
+        rp = _repolish_set(ws, settings or Settings()) if rejected else None
         if rp is not None:      # polish rejected: polish again with more refinement steps
             pidx, pn, s3 = rp
             polish_w(pidx, pn, ctypes.byref(s3))
-        retry = _retry_set(ws, settings or Settings())
+        retry = _retry_set(ws, settings or Settings()) if rejected else None
         if retry is not None:   # polish rejected: resume ADMM to eps_retry, polish again
             ridx, rn, s2 = retry
             admm_rounds(ridx, rn, ctypes.byref(s2))
@@ -1144,6 +1174,13 @@ class GroupPlan:
         self.ucnt = torch.from_numpy(ucnt).to(device)
         self.uoff = torch.from_numpy(uoff).to(device)
         self.gidx = torch.from_numpy(gidx).to(device)
+        self._dev_index = None
+
+    def device_index(self):
+        """(group of each date as int64, dates per group as FP64) on the device, built once."""
+        if self._dev_index is None:
+            self._dev_index = (self.gidx.long(), torch.from_numpy(self.sizes.astype(np.float64)).to(self.gidx.device))
+        return self._dev_index
 
 
 class Panel:
