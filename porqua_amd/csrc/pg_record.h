@@ -10,6 +10,10 @@ namespace pq {
 constexpr int PGR = PQ_PG_RECORD;
 enum : int {
   R_K = 0, R_MA = 1, R_NZB = 2, R_STATE = 3, R_ROUNDS = 4, R_SC = 5,
+  // R_FORMED = 1: the K scratch holds P_FF of the free list of the last form (its positions
+  // in PGWork::posF); R_REUSE = 1: this round's free list is a subset of it, so the round
+  // gathers its P_FF from K instead of forming it again
+  R_FORMED = 6, R_REUSE = 7,
   R_ACT = 64, R_LAM = 128, R_DA = 192, R_SOL = 256, R_AL = 288,
   // wide mode: R_W = 1 this round, R_NFX fixed variables at R_FIX (indices), R_FIXV (bound
   // values), R_FXL (their multipliers = box duals)
@@ -26,7 +30,8 @@ static_assert(R_FXL + PG_WMB <= PQ_PG_RECORD, "PQ_PG_RECORD too small");
 
 struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
   double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;
-  int *Fl, *fl;
+  int *Fl, *fl, *posF;   // posF (n ints, the upper half of Fl's slot): position of a variable
+                         // in the free list of the last form, -1 when not in it
   __device__ __forceinline__ PGWork(const pq_state& st, int b, int ld) {
     double* W = st.work + (int64_t)b * st.work_stride;
     xs = W;
@@ -34,6 +39,7 @@ struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | p
     g = W + 2 * (int64_t)ld;
     Px = W + 3 * (int64_t)ld;
     Fl = reinterpret_cast<int*>(W + 4 * (int64_t)ld);
+    posF = Fl + ld;
     rF = W + 5 * (int64_t)ld;
     solx = W + 6 * (int64_t)ld;
     pxb = W + 7 * (int64_t)ld;

@@ -102,6 +102,8 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
     R[R_K] = nfree;
     R[R_NZB] = 0;
     R[R_W] = 0;
+    R[R_FORMED] = 0;
+    R[R_REUSE] = 0;
   }
 #ifdef PQ_PROFILE
   if (t >= 8 && t < 20) R[t] = 0.0;
@@ -201,6 +203,15 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     if (f) wk.Fl[base + __popcll(m & ((1ull << l) - 1ull))] = i;
     base += __popcll(m);
   }
+  // ---- P_FF reuse: every free variable in the free list of the last form (the usual later
+  //      round only fixes variables) -> the solve gathers P_FF from K ---------------------------
+  int reuse = 0;
+  if (R[R_FORMED] == 1.0) {
+    __syncthreads();   // Fl complete
+    int miss = 0;
+    for (int p = t; p < k; p += PT) miss |= wk.posF[wk.Fl[p]] < 0;
+    reuse = !block_or(miss, red);
+  }
   // ---- fixed values, nzb -------------------------------------------------------------------
   int nzb = 0;
   for (int i = t; i < ld; i += PT) {
@@ -235,6 +246,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     R[R_MA] = ma;
     R[R_NZB] = nzb;
     R[R_W] = 0;
+    R[R_REUSE] = reuse;
     R[R_ROUNDS] += 1.0;
   }
 }
@@ -251,14 +263,22 @@ constexpr int FT = 512;             // threads (8 waves)
 constexpr int FNW = FT / 64;
 constexpr int FTW = 5;              // 16x16 tiles per wave (36 lower tiles for k <= 128)
 
-__global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, const double* rec,
+__global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
                                                 int ldk) {
   __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPIT];
   const int b = blockIdx.x;
-  const double* R = rec + (int64_t)b * PGR;
+  double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;   // wide dates: polish_gw.hip
   const int k = (int)R[R_K];
   if (k > PG_KMAX || k == 0) return;
+  if (R[R_REUSE] != 0.0) {   // P_FF is a principal submatrix of the formed one: nothing to form
+    if (R[R_NZB] != 0.0) {   // (the reduced rhs still takes P_FB x_B from pass 0)
+      PGWork wk0(st, b, pb.ld);
+      const double ps0 = pb.p_scale ? pb.p_scale[b] : 1.0;
+      for (int p = threadIdx.x; p < k; p += FT) wk0.rF[p] -= ps0 * wk0.pxb[wk0.Fl[p]];
+    }
+    return;
+  }
   const int ld = pb.ld;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   PGWork wk(st, b, ld);
@@ -333,6 +353,10 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
     buf ^= 1;
   }
   double* K = st.K + (int64_t)b * st.K_stride;
+  for (int i = t; i < pb.n; i += FT) wk.posF[i] = -1;   // positions of the formed free list
+  __syncthreads();
+  for (int p = t; p < k; p += FT) wk.posF[wk.Fl[p]] = p;
+  if (t == 0) R[R_FORMED] = 1.0;
 #pragma unroll
   for (int j = 0; j < FTW; ++j) {
     if (w + FNW * j < ntile) {
@@ -501,6 +525,7 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   __shared__ double xF[KS], t1[KS], t2[KS], rx[KS];
   __shared__ double Sm[WMA * WMA], lamv[WMA], wl[WMA], rl[WMA], dAv[WMA];
   __shared__ int s_al[WMA];
+  __shared__ int s_map[KS];
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;
@@ -528,6 +553,11 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
 #else
 #define WSTAMP(k_) do { } while (0)
 #endif
+  // the K scratch rows / columns of this round's free positions: identity, or (P_FF reused
+  // from an earlier round's form) the positions in that free list
+  const bool reuse = R[R_REUSE] != 0.0;
+  for (int p = l; p < k; p += 64) s_map[p] = reuse ? wk.posF[wk.Fl[p]] : p;
+  WSYNC();
   {   // packed triangle, flat index (independent loads, 64 per trip)
     const int np_ = k * (k + 1) / 2;
     int r = 0, e0 = 0;   // row of the lane's element: advance incrementally
@@ -541,7 +571,7 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
         if (e < np_) {
           while (e >= e0 + r + 1) { e0 += r + 1; ++r; }
           const int c = e - e0;
-          v[j] = K[(int64_t)r * ldk + c];
+          v[j] = K[(int64_t)s_map[r] * ldk + s_map[c]];
           dg |= (r == c) << j;
         }
       }
@@ -611,7 +641,7 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
     for (int p = l; p < k; p += 64) {   // P_FF is symmetric in K: column p, coalesced over lanes
       double sum = 0.0;
 #pragma unroll 8
-      for (int qq = 0; qq < k; ++qq) sum = fma(K[(int64_t)qq * ldk + p], xF[qq], sum);
+      for (int qq = 0; qq < k; ++qq) sum = fma(K[(int64_t)s_map[qq] * ldk + s_map[p]], xF[qq], sum);
       double v = wk.rF[p] - sum;
       const int fp = wk.Fl[p];
       for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + fp] * lamv[a];

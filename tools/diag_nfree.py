@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Free-set sizes of the polished answers (out[PQ_OUT_NFREE]) at the config-4 and config-5
-shapes -- which polish path (grouped LDS buckets <= 128, or the per-date fallback) they need.
-Experiment tool: python tools/diag_nfree.py"""
+"""Free-set sizes of the polished answers (out[PQ_OUT_NFREE]) at the config-2, config-4 and
+config-5 shapes -- which polish path (grouped LDS buckets <= 128, wide rounds, or the per-date
+fallback) they need.  Experiment tool: python tools/diag_nfree.py [2]"""
 import json
 import os
 import sys
@@ -40,8 +40,35 @@ def hist(res, tag, ws=None):
           flush=True)
 
 
+def config2(dev):
+    """The config-2 engine problem: SPTR replication on the usa-shaped panel, every date,
+    least-squares tracking with budget + long-only box (tests/test_configs12_gpu.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_configs12_gpu import usa_data
+    X, yb = usa_data()
+    d = X.index.values.astype("datetime64[D]")
+    rows, tlen = engine.window_rows(d, d[251:], 252)
+    n, D = X.shape[1], len(rows)
+    pan = engine.Panel(X.to_numpy(), yb.to_numpy()[:, 0], device=dev)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    qb = engine.QPBatch.from_dense(None, None, n=n, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n),
+                                   device=dev)
+    qb.batch = D
+    qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)
+    xty, _ = pan.gram_xy(r_d, t_d)
+    qb.q = (-2.0 * xty).contiguous()
+    lr = engine.LowRank(pan, r_d, t_d, mu=None)
+    gp = engine.GroupPlan(rows, tlen, dev)
+    st = engine.Settings.from_params({"rho0_rel": 0.2, "rho0_qrel": 0.0})   # LeastSquares' defaults
+    ws = engine.Workspace(qb, dense=False)
+    hist(engine.solve_lowrank(qb, lr, st, groups=gp, ws=ws), f"config2 ({D} daily dates)", ws)
+
+
 def main():
     dev = torch.device("cuda", 0)
+    if len(sys.argv) > 1 and sys.argv[1] == "2":
+        config2(dev)
+        return
     n, T, ns, cap, D = 3000, 252, 20, 0.15, 600
     dates, R, y, sec = factor_panel(T - 1 + D, n, n_sectors=ns)
     rows, tlen = engine.window_rows(dates, dates[T - 1:], T)
