@@ -844,7 +844,10 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                 and (qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
                 and groups.ucnt_max + qb.mg <= 320 and groups.corr_max <= 64)
     if band:
-        bd = tl("gram", lambda: _band_setup(qb, lr, strm, w_min=groups.span_max if gcap_try else 0))
+        # the band must cover every union the capacitances read: the ADMM's groups and the
+        # polish's (wide rounds)
+        wmin = max(groups.span_max, groups.polish_plan().span_max) if (gcap_try or (grouped and wide_polish)) else 0
+        bd = tl("gram", lambda: _band_setup(qb, lr, strm, w_min=wmin))
     gc = _gcap_setup(qb, lr, ws, groups, settings or Settings()) if (gcap_try and bd is not None) else None
 
     def refactor_groups():
@@ -930,7 +933,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         (FALLBACK) go through pq_polish_w_batched from their ADMM point."""
         rec = ws.pg_record()
         rp = rec.data_ptr()
-        g = groups
+        g = groups.polish_plan()
         _lib.check(lib.pq_polish_grouped_init(L_, P_, S_, rp, SS_main, strm), "pq_polish_grouped_init")
         scr = getattr(ws, "_pg_pass", None)
         if scr is None or scr.numel() < g.ngroups * _lib.PQ_PG_PASS_SCRATCH:
@@ -1100,6 +1103,8 @@ class GroupPlan:
         rows = np.asarray(rows)
         tlen = np.asarray(tlen)
         B = len(tlen)
+        self._host = (rows, tlen, device, umax, smax)
+        self._polish_plan = None
         # balance: one group per CU per round (one 512-thread workgroup fits a CU), as few
         # rounds as gmax allows, groups as even as possible within them
         rounds = max(1, -(-B // (gmax * cus)))
@@ -1175,6 +1180,18 @@ class GroupPlan:
         self.uoff = torch.from_numpy(uoff).to(device)
         self.gidx = torch.from_numpy(gidx).to(device)
         self._dev_index = None
+
+    def polish_plan(self) -> "GroupPlan":
+        """The plan of the grouped polish: full 16-date groups (its window passes run split
+        over 4 workgroups per group, so fewer, fuller groups read fewer union rows; measured at
+        the config-3 shape, profiles/r03i_bench_gmin*.log: polish 5.26 -> 4.92 ms at 16 dates per
+        group, while the ADMM wants the CU-balanced size: 8.06 -> 8.51 ms)."""
+        if self._polish_plan is None:
+            rows, tlen, device, umax, smax = self._host
+            full = self.ngroups == 0 or int(self.sizes.max()) >= GROUP_MAX_DATES
+            self._polish_plan = self if full else GroupPlan(rows, tlen, device, umax=umax, smax=smax,
+                                                            gmin=GROUP_MAX_DATES)
+        return self._polish_plan
 
     def device_index(self):
         """(group of each date as int64, dates per group as FP64) on the device, built once."""

@@ -21,10 +21,11 @@ PHASES = ["setup+classify", "free list", "rF/dA", "cholesky", "U+S", "refine", "
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     cfg4 = "--config4" in sys.argv   # n = 3000 tracking LS with 20 sector caps (tools/bench_configs.py)
-    n, T, D = (3000 if cfg4 else 1000), 252, int(args[0]) if args else (2000 if cfg4 else 4749)
+    lsq = "--lsq494" in sys.argv     # config 2's shape: n = 494 tracking LS, budget + long-only box
+    n, T, D = (3000 if cfg4 else (494 if lsq else 1000)), 252, int(args[0]) if args else (2000 if cfg4 else 4749)
     dates, R, y, sec = factor_panel(T - 1 + D, n, n_sectors=20 if cfg4 else 10)
     rows, tlen = engine.window_rows(dates, dates[T - 1:T - 1 + D], T)
-    pan = engine.Panel(R, y if cfg4 else None)
+    pan = engine.Panel(R, y if (cfg4 or lsq) else None)
     r_d, t_d = pan.rows_to_device(rows, tlen)
     G = np.stack([(sec == g).astype(float) for g in range(20)]) if cfg4 else None
     qb = engine.QPBatch.from_dense(None, None, n=n, A=np.ones((1, n)), b=np.ones(1), G=G,
@@ -35,7 +36,7 @@ def main():
     qb.P = None   # window path: P stays in window form
     qb.q = torch.zeros((D, qb.ld), dtype=torch.float64, device=dev)
     qb.p_scale = torch.full((D,), 2.0, dtype=torch.float64, device=dev)
-    if cfg4:
+    if cfg4 or lsq:
         xty, _ = pan.gram_xy(r_d, t_d)
         qb.q = (-2.0 * xty).contiguous()
         lr = engine.LowRank(pan, r_d, t_d, mu=None)
@@ -47,7 +48,8 @@ def main():
     for _ in range(2):
         ev = []
         ws.work[:, off + 16:off + 24].zero_()
-        st = engine.Settings.from_params({"rho0_rel": 0.1, "rho0_qrel": 0.0}) if cfg4 else engine.Settings()
+        st = (engine.Settings.from_params({"rho0_rel": 0.1 if cfg4 else 0.2, "rho0_qrel": 0.0}) if (cfg4 or lsq)
+              else engine.Settings())
         for a in sys.argv:   # --refine=N: proximal refinement steps per polish round
             if a.startswith("--refine="):
                 st.refine_iters = int(a.split("=")[1])
