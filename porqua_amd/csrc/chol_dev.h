@@ -113,6 +113,117 @@ __device__ void tile_trinv(const double* T, double* X, int nvalid) {
 }
 
 
+// Cholesky AND inverse of the 64x64 tile T (pitch DP, lower used, rows / columns >= nvalid
+// the identity) by the whole 256-thread workgroup in 16-column blocks: wave 0 factors and
+// inverts each 16x16 diagonal block in registers (wave_chol_inv16: cross-lane shuffles, no
+// LDS round trip per pivot), the panel L_ip = A_ip L_pp^-T and the trailing update
+// A_ij -= L_ip L_jp' are 16x16x4 MFMA tiles spread over the four waves, and the off-diagonal
+// blocks of L^-1 follow by blocked forward substitution (one wave per block column).  On
+// exit T's lower triangle holds L and X (pitch DP) holds X[c][r] = (L^-1)[r][c] (the layout
+// of tile_trinv).  Returns 0, or 1 + the first column of the 16-block whose pivot failed
+// (uniform).  Replaces tile_potrf + tile_trinv, whose 64-step single-wave pivot chains
+// through LDS dominated the blocked factorisations (k_factor, pq_polish_w_batched).
+__device__ int tile_chol_inv64(double* T, double* X, int nvalid) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int cc = l & 15, gg = l >> 4;
+  const int nv = nvalid < 0 ? 0 : (nvalid > TB ? TB : nvalid);
+  for (int e = t; e < TB * DP; e += blockDim.x) X[e] = 0.0;
+  __syncthreads();   // T written by every wave; X cleared
+  for (int p = 0; p < 4; ++p) {
+    const int p0 = 16 * p;
+    if (w == 0) {   // diagonal block: L_pp (lower, into T) and L_pp^-1 (into X, transposed)
+      double A[4], Bv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = gg + 4 * q;
+        const bool in = p0 + r < nv && p0 + cc < nv;
+        A[q] = in ? (cc <= r ? T[(p0 + r) * DP + p0 + cc] : T[(p0 + cc) * DP + p0 + r]) : (r == cc ? 1.0 : 0.0);
+        Bv[q] = (r == cc) ? 1.0 : 0.0;
+      }
+      const int bad = wave_chol_inv16(A, Bv);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = gg + 4 * q;
+        if (cc <= r) {
+          T[(p0 + r) * DP + p0 + cc] = A[q];
+          X[(p0 + cc) * DP + p0 + r] = Bv[q];
+        }
+      }
+      if (l == 0) T[TB] = bad ? (double)(p0 + 1) : 0.0;   // row 0's padding slot carries the result
+    }
+    __syncthreads();
+    if (T[TB] != 0.0) {
+      const int bad = (int)T[TB];
+      __syncthreads();
+      return bad;
+    }
+    // panel: L_ip = A_ip L_pp^-T, i = p + 1 + w (MFMA: A[m][k] = A_ip[m][k], B[k][n] = Linv_pp[n][k])
+    const int i_p = p + 1 + w;
+    if (i_p < 4) {
+      const int i0 = 16 * i_p;
+      f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int k = 4 * s4 + gg;
+        const double av = T[(i0 + cc) * DP + p0 + k];
+        const double bv = X[(p0 + k) * DP + p0 + cc];   // Linv_pp[cc][k] (0 for k > cc)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();   // every lane's reads of A_ip precede the writes
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) T[(i0 + gg + 4 * rr) * DP + p0 + cc] = acc[rr];
+    }
+    __syncthreads();
+    // trailing update A_ij -= L_ip L_jp' for p < j <= i (lower 16x16 tiles, round-robin over waves)
+    const int m = 3 - p, ntr = m * (m + 1) / 2;
+    for (int tt = w; tt < ntr; tt += 4) {
+      int ii = 0;
+      while ((ii + 1) * (ii + 2) / 2 <= tt) ++ii;
+      const int jj = tt - ii * (ii + 1) / 2;
+      const int i0 = 16 * (p + 1 + ii), j0 = 16 * (p + 1 + jj);
+      f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int k = 4 * s4 + gg;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(T[(i0 + cc) * DP + p0 + k], T[(j0 + cc) * DP + p0 + k], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) T[(i0 + gg + 4 * rr) * DP + j0 + cc] -= acc[rr];
+    }
+    __syncthreads();
+  }
+  // L^-1 below the diagonal blocks, block column p = w:  Linv_ip = -Linv_ii sum_{k=p}^{i-1} L_ik Linv_kp
+  if (w < 3) {
+    const int p = w, p0 = 16 * p;
+    for (int i = p + 1; i < 4; ++i) {
+      const int i0 = 16 * i;
+      f64x4 S = f64x4{0.0, 0.0, 0.0, 0.0};
+      for (int k = p; k < i; ++k) {
+        const int k0 = 16 * k;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int tk = 4 * s4 + gg;
+          S = __builtin_amdgcn_mfma_f64_16x16x4f64(T[(i0 + cc) * DP + k0 + tk], X[(p0 + cc) * DP + k0 + tk], S, 0, 0, 0);
+        }
+      }
+      // S in the C layout is the B operand of the next product: lane l holds S[gg + 4 s4][cc]
+      f64x4 o = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int tk = 4 * s4 + gg;
+        o = __builtin_amdgcn_mfma_f64_16x16x4f64(X[(i0 + tk) * DP + i0 + cc], S[s4], o, 0, 0, 0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) X[(p0 + cc) * DP + i0 + gg + 4 * rr] = -o[rr];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  __syncthreads();
+  return 0;
+}
+
 // KKT matrix K = ps P + pd I + sigma I + Cg' R Cg + R_box, element by element (K2 / K2L)
 struct FormCtx {
   const double* P;
@@ -179,10 +290,9 @@ __device__ int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, int nv,
           const int i = acc_row(m, r), j = acc_col(nn);
           stg[i * DP + j] = f(J * TB + i, J * TB + j) - acc.c[m][nn][r];
         }
-    const int bad = tile_potrf(stg, nv - J * TB);
-    if (bad) return J * TB + bad;
     double* X = sD;  // inverse computed with pitch DP inside the sD region
-    tile_trinv(stg, X, nv - J * TB);
+    const int bad = tile_chol_inv64(stg, X, nv - J * TB);
+    if (bad) return J * TB + bad;
     double xr[TB * TB / 256];
 #pragma unroll
     for (int q = 0; q < TB * TB / 256; ++q) {

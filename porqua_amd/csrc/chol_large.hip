@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void k_l_diag(LargeCtx c, int J) {
     T[i * DP + j] = K[(int64_t)(J * TB + i) * ld + J * TB + j];
   }
   const int nv = c.pb.n - J * TB;
-  const int bad = tile_potrf(T, nv);
+  const int bad = tile_chol_inv64(T, X, nv);
   if (bad) {
     if (threadIdx.x == 0) {
       c.st.info[b] = J * TB + bad;
@@ -99,7 +99,6 @@ __global__ __launch_bounds__(256) void k_l_diag(LargeCtx c, int J) {
     }
     return;
   }
-  tile_trinv(T, X, nv);
   for (int e = threadIdx.x; e < TB * TB; e += blockDim.x) {
     const int i = e >> 6, j = e & 63;
     K[(int64_t)(J * TB + i) * ld + J * TB + j] = (j <= i) ? T[i * DP + j] : 0.0;

@@ -28,6 +28,8 @@
 // Replaces, with polish_w.hip, the accuracy of qpsolvers' interior-point answer
 // (src/qp_problems.py:211-214); scoring as src/qp_problems.py:219-221 and
 // example/compare_solver.ipynb:212-216.
+#include <mutex>
+
 #include "polish_dev.h"
 #include "capi_util.h"
 #include "pg_record.h"
@@ -1116,6 +1118,40 @@ extern "C" int pq_polish_grouped_init(const pq_lowrank* lr, const pq_problem* pb
   return 0;
 }
 
+namespace pq {
+// Side streams of a round's per-date solves: the free-set buckets and the wide rounds touch
+// disjoint dates, so they run concurrently (fork / join events on the caller's stream)
+// instead of one launch after another, each with its own tail.  Created once per device on
+// first use; NULL when that fails (everything then runs on the caller's stream).  One host
+// thread per device drives a round at a time (the engine's use).
+struct PgSide {
+  static constexpr int NS = 6;
+  bool ok = false;
+  hipStream_t s[NS];
+  hipEvent_t fork, join[NS];
+};
+static PgSide* pg_side() {
+  static PgSide sides[64];
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  PgSide& p = sides[dev];
+  if (!p.ok) {
+    bool good = hipEventCreateWithFlags(&p.fork, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < PgSide::NS && good; ++i)
+      good = hipStreamCreateWithFlags(&p.s[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&p.join[i], hipEventDisableTiming) == hipSuccess;
+    if (!good) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    p.ok = true;
+  }
+  return &p;
+}
+}  // namespace pq
+
 extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
                                        int32_t ldk, const int32_t* gdates, int32_t ngroups, const int32_t* urows,
                                        const int32_t* ucnt, const int32_t* uoff, int32_t umax, const pq_settings* s,
@@ -1141,13 +1177,28 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   hipLaunchKernelGGL(pq::k_pg_post<0>, dim3(B), dim3(64), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
                      pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
-  // one wave per date, the LDS triangle sized to the free set (more dates per CU when small)
-  hipLaunchKernelGGL(pq::k_pg_solve<48>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 0);
-  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 48);
-  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 64);
-  if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 80);
-  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, 96);
-  if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, str)) return -1;   // free sets beyond kmax
+  // one wave per date, the LDS triangle sized to the free set (more dates per CU when small);
+  // the buckets (and the wide rounds) on side streams, joined before the exact-P x passes
+  pq::PgSide* side = pq::pg_side();
+  int used = 0;
+  if (side && hipEventRecord(side->fork, str) != hipSuccess) side = nullptr;
+  auto on = [&](int i) -> hipStream_t {
+    if (!side || hipStreamWaitEvent(side->s[i], side->fork, 0) != hipSuccess) return str;
+    used |= 1 << i;
+    return side->s[i];
+  };
+  hipLaunchKernelGGL(pq::k_pg_solve<48>, dim3(B), dim3(64), 0, on(0), *pb, *st, rec, *s, ldk, 0);
+  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(64), 0, on(1), *pb, *st, rec, *s, ldk, 48);
+  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, on(2), *pb, *st, rec, *s, ldk, 64);
+  if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, on(3), *pb, *st, rec, *s, ldk, 80);
+  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, on(4), *pb, *st, rec, *s, ldk, 96);
+  if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, on(5))) return -1;   // free sets beyond kmax
+  for (int i = 0; side && i < pq::PgSide::NS; ++i)
+    if ((used & (1 << i)) && (hipEventRecord(side->join[i], side->s[i]) != hipSuccess ||
+                              hipStreamWaitEvent(str, side->join[i], 0) != hipSuccess)) {
+      pq::set_error("pq_polish_grouped_round: joining the solve streams failed");
+      return -2;
+    }
   hipLaunchKernelGGL(pq::k_pg_passA<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_passB<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,

@@ -485,14 +485,18 @@ class EigCap:
     problem's own scale and rho -- no per-problem factorisation, and an adaptive-rho change
     is a re-form.  The Gram and the border W = Xc Cg' come from the hand-written window Gram
     kernel (pq_lr_capacitance with D = I, unit row weights); the eigendecomposition itself
-    is rocSOLVER's (torch.linalg.eigh), once per date.
+    is rocSOLVER's (torch.linalg.eigh, ``backend`` 'rocsolver', the default) or the hand-written
+    block-Jacobi solver (jacobi.hip, helper_functions.sym_eig, 'jacobi'), once per date.
+    Measured for the 64 window Grams of config 5 (profiles/r03k_exp_eigh.log): syevd 10.4 ms,
+    the block-Jacobi kernels 64.5 ms (eigenvalues to 1.2e-12) -- the Jacobi form serves the
+    nearestPD repair, whose matrices need no ordering and few sweeps.
 
     rows / tlen / mu: per-date device tensors (every tlen == tmax); pdate: date of each
     problem (int32, device); Cg: the shared general rows (qb.Cg, mg <= 4)."""
 
     MG = 4
 
-    def __init__(self, panel, rows, tlen, mu, qb: "QPBatch", pdate, k_ld: int):
+    def __init__(self, panel, rows, tlen, mu, qb: "QPBatch", pdate, k_ld: int, backend: str = "rocsolver"):
         lib = _lib.load()
         nd, tmax = int(rows.shape[0]), int(rows.shape[1])
         mg, n, dev = qb.mg, qb.n, qb.device
@@ -520,7 +524,17 @@ class EigCap:
         T = tmax
         Mt = M[:, :T, :T]
         G = torch.tril(Mt) + torch.tril(Mt, -1).mT - torch.eye(T, dtype=F64, device=dev)
-        ev, V = torch.linalg.eigh(G)
+        if backend == "jacobi":   # zero padding to a multiple of 64: its pairs never rotate
+            from .helper_functions import sym_eig
+            ldj = round_up(T, 64)
+            Gp = torch.zeros((nd, ldj, ldj), dtype=F64, device=dev)
+            Gp[:, :T, :T] = G
+            evj, Vj = sym_eig(Gp, T)
+            ev, V = evj[:, :T], Vj[:, :T, :T]
+        elif backend == "rocsolver":
+            ev, V = torch.linalg.eigh(G)
+        else:
+            raise ValueError("EigCap: backend must be 'jacobi' or 'rocsolver'")
         self.V = torch.zeros((nd, k_ld, k_ld), dtype=F64, device=dev)
         self.V[:, :T, :T] = V
         self.evals = torch.zeros((nd, k_ld), dtype=F64, device=dev)

@@ -44,7 +44,8 @@ SWEEP_RHO0_QREL = 30.0
 def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0, budget=1.0,
                         geometric=True, settings: engine.Settings | None = None, group=True,
                         factor: str = "auto", gmax: int = engine.GROUP_MAX_DATES,
-                        events: list | None = None, ws: "engine.Workspace | None" = None):
+                        events: list | None = None, ws: "engine.Workspace | None" = None,
+                        eig_backend: str = "rocsolver"):
     """Solve min lam x'Sigma_d x - mu_d'x  s.t. 1'x = budget, lb <= x <= ub for every
     rebalance window (rows, tlen: host arrays of engine.window_rows) and every lam.
 
@@ -83,7 +84,7 @@ def mean_variance_sweep(panel: engine.Panel, rows, tlen, lambdas, lb=0.0, ub=1.0
     if factor == "eig" and full and engine.lowrank_shape_ok(n, rows.shape[1], qb.mg):
         k_ld = engine.round_up(rows.shape[1] + qb.mg, 64)
         pdate = torch.arange(nd, dtype=torch.int32, device=dev).repeat_interleave(L)
-        eig = tl("eig", lambda: engine.EigCap(panel, r_d, t_d, mu_c, qb, pdate, k_ld))
+        eig = tl("eig", lambda: engine.EigCap(panel, r_d, t_d, mu_c, qb, pdate, k_ld, backend=eig_backend))
     gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax) if group else None
     if settings is None:
         settings = engine.Settings(rho0_qrel=SWEEP_RHO0_QREL)

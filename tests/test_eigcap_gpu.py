@@ -42,7 +42,8 @@ def _sweep_batch(pan, rows, tlen, lambdas, dev):
     return qb, lr, r_d, t_d, mu
 
 
-def test_eigcap_form_matches_capacitance_inverse(device):
+@pytest.mark.parametrize("backend", ["jacobi", "rocsolver"])
+def test_eigcap_form_matches_capacitance_inverse(device, backend):
     n, T, nd = 400, 120, 3
     lambdas = np.array([0.1, 1.0, 7.5, 100.0])
     L = len(lambdas)
@@ -66,7 +67,7 @@ def test_eigcap_form_matches_capacitance_inverse(device):
     Mf = torch.tril(M) + torch.tril(M, -1).mT
     ref = torch.linalg.inv(Mf)
     pdate = torch.arange(nd, dtype=torch.int32, device=device).repeat_interleave(L)
-    eig = engine.EigCap(pan, r_d, t_d, mu, qb, pdate, k_ld)
+    eig = engine.EigCap(pan, r_d, t_d, mu, qb, pdate, k_ld, backend=backend)
     Minv = torch.full((B, k_ld, k_ld), np.nan, dtype=torch.float64, device=device)
     eig.form(ctypes.byref(lrs), ctypes.byref(pb), ctypes.byref(st), ctypes.byref(s), Minv, None, 0, engine._stream())
     torch.cuda.synchronize()

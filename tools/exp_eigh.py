@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
 """Batched symmetric eigendecomposition of 64 window Grams (T = 252, the config-5 EigCap
 input): torch.linalg.eigh against rocSOLVER's strided-batched syevd / syevj called directly
-(torch's own bundled librocsolver).  Experiment tool: python tools/exp_eigh.py"""
+(torch's own bundled librocsolver) and the hand-written block-Jacobi kernels
+(helper_functions.sym_eig, jacobi.hip).  Experiment tool: python tools/exp_eigh.py"""
 import ctypes
 import json
 import os
 import time
 
+import sys
+
 import torch
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 TL = os.path.join(os.path.dirname(torch.__file__), "lib")
 
 
@@ -76,6 +80,18 @@ def main():
     out["rocsolver_syevj_batched_ms"] = ms
     out["syevj_max_eig_err"] = float((W - ref).abs().max())
     out["syevj_sweeps_max"] = int(nsw.max())
+    from porqua_amd.helper_functions import sym_eig
+    Gp = torch.zeros((nb, 256, 256), dtype=torch.float64, device=dev)
+
+    def jac():
+        Gp.zero_()
+        Gp[:, :T, :T] = G
+        return sym_eig(Gp, T)
+    (evj, Vj), ms = timed(jac)
+    out["jacobi_sym_eig_ms"] = ms
+    out["jacobi_max_eig_err"] = float((torch.sort(evj[:, :T], 1)[0] - ref).abs().max())
+    Vt = Vj[:, :T, :T]
+    out["jacobi_max_recon_err"] = float((Vt @ torch.diag_embed(evj[:, :T]) @ Vt.mT - G).abs().max())
     print(json.dumps(out), flush=True)
 
 
