@@ -803,7 +803,10 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const int z0 = loop_zero();
       const int kq = l >> 4, ia = (l & 15) + z0;
       const int Uk = (U + 3) & ~3;
-      constexpr int PS = 4;
+#ifndef PQ_GCAP_PS
+#define PQ_GCAP_PS 4
+#endif
+      constexpr int PS = PQ_GCAP_PS;   // union rows per pass-2 load step (x 4 lanes)
       bool mact[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
