@@ -1110,14 +1110,17 @@ class GroupPlan:
     when some window cannot be grouped (the per-date kernel is used then)."""
 
     def __init__(self, rows, tlen, device, gmax: int = GROUP_MAX_DATES, umax: int = GROUP_MAX_UNION,
-                 smax: int = 64, cus: int = 256, gmin: int = 4, breaks=None):
+                 smax: int = 64, cus: int = 256, gmin: int = 4, breaks=None, polish_full: bool = False):
         """``breaks`` (bool per problem, optional): True starts a new group at that problem
         (e.g. the risk-aversion buckets of porqua_amd.sweep, whose problems may share a
-        capacitance only within a rho bucket)."""
+        capacitance only within a rho bucket).  ``polish_full``: polish_plan() builds a second plan
+        of full 16-date groups for the grouped polish (a second host pass over the windows: worth
+        it for a batch solved repeatedly, e.g. the bench workloads)."""
         rows = np.asarray(rows)
         tlen = np.asarray(tlen)
         B = len(tlen)
         self._host = (rows, tlen, device, umax, smax)
+        self._polish_full = polish_full
         self._polish_plan = None
         # balance: one group per CU per round (one 512-thread workgroup fits a CU), as few
         # rounds as gmax allows, groups as even as possible within them
@@ -1200,12 +1203,16 @@ class GroupPlan:
         over 4 workgroups per group, so fewer, fuller groups read fewer union rows; measured at
         the config-3 shape, profiles/r03i_bench_gmin*.log: polish 5.26 -> 4.92 ms at 16 dates per
         group, while the ADMM wants the CU-balanced size: 8.06 -> 8.51 ms)."""
+        if not self._polish_full:
+            return self
         if self._polish_plan is None:
             rows, tlen, device, umax, smax = self._host
             full = self.ngroups == 0 or int(self.sizes.max()) >= GROUP_MAX_DATES
-            self._polish_plan = self if full else GroupPlan(rows, tlen, device, umax=umax, smax=smax,
+            self._polish_plan = None if full else GroupPlan(rows, tlen, device, umax=umax, smax=smax,
                                                             gmin=GROUP_MAX_DATES)
-        return self._polish_plan
+            if full:
+                self._polish_full = False
+        return self._polish_plan if self._polish_plan is not None else self
 
     def device_index(self):
         """(group of each date as int64, dates per group as FP64) on the device, built once."""

@@ -61,7 +61,7 @@ class MinVarianceBacktest:
         self.rows_d, self.tlen_d = self.pan.rows_to_device(self.rows, self.tlen)
         self.plan = engine.SlidePlan(self.rows, self.tlen, dev) if slide else None
         gmin = int(os.environ.get("PQ_GROUP_MIN", "4"))     # experiments: smallest slide group size
-        self.gplan = engine.GroupPlan(self.rows, self.tlen, dev, gmin=gmin) if group else None
+        self.gplan = engine.GroupPlan(self.rows, self.tlen, dev, gmin=gmin, polish_full=True) if group else None
         qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)),
                                        b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), device=dev)
         qb.batch = D                                             # D problems sharing constraints
@@ -164,7 +164,7 @@ class TrackingBacktest:
         self.qb = qb
         self.plan = None
         self.mu = None
-        self.gplan = engine.GroupPlan(self.rows, self.tlen, dev)
+        self.gplan = engine.GroupPlan(self.rows, self.tlen, dev, polish_full=True)
         self.lr = engine.LowRank(self.pan, self.rows_d, self.tlen_d, mu=None)
         self.use_lr, self.with_cov = True, False
         # tracking objectives start at a small rho (engine.Settings docs; tools/bench_configs.py)
