@@ -124,7 +124,7 @@ __device__ __forceinline__ void tree_reduce(double2 (&acc)[NQ], double* tree) {
 // beyond n); tree: 4 * NQ*128 doubles.  RU rows per wave are in flight at a time (their
 // loads are issued together; the accumulation order is fixed).  All threads must call.
 template <int NQ, int RU>
-__device__ void symv_lower(const double* A, int64_t ld, int n, const double* v, double* y,
+PQ_DEVFN void symv_lower(const double* A, int64_t ld, int n, const double* v, double* y,
                            double* dotv, double* tree) {
   const int w = wave_id(), l = lane_id();
   double2 acc[NQ];

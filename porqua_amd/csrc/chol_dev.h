@@ -55,7 +55,7 @@ __device__ int tile_potrf(double* T, int nvalid) {
 
 // The same factorisation with the whole workgroup and LDS only (few registers): for the
 // small Schur-complement tile of the polish, whose valid size is the number of active rows.
-__device__ int tile_potrf_lds(double* T, int nvalid) {
+PQ_DEVFN int tile_potrf_lds(double* T, int nvalid) {
   const int t = threadIdx.x;
   const int kend = nvalid < TB ? (nvalid > 0 ? nvalid : 0) : TB;
   for (int k = 0; k < kend; ++k) {
@@ -123,7 +123,7 @@ __device__ void tile_trinv(const double* T, double* X, int nvalid) {
 // of tile_trinv).  Returns 0, or 1 + the first column of the 16-block whose pivot failed
 // (uniform).  Replaces tile_potrf + tile_trinv, whose 64-step single-wave pivot chains
 // through LDS dominated the blocked factorisations (k_factor, pq_polish_w_batched).
-__device__ int tile_chol_inv64(double* T, double* X, int nvalid) {
+PQ_DEVFN int tile_chol_inv64(double* T, double* X, int nvalid) {
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const int cc = l & 15, gg = l >> 4;
   const int nv = nvalid < 0 ? 0 : (nvalid > TB ? TB : nvalid);
@@ -273,7 +273,7 @@ constexpr int CHOL_LDS = 4 * STAGE + TB * LDW;
 // kStoreDiag = false leaves K's diagonal 64x64 blocks untouched (nothing downstream of the
 // polish reads them: the solves use Dt), so they can keep the matrix being factored.
 template <bool kStoreDiag = true, typename Form>
-__device__ int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, int nv, double* Dt, double* smem) {
+PQ_DEVFN int wg_cholesky(const Form& f, double* K, int64_t ld, int nb, int nv, double* Dt, double* smem) {
   double* stg = smem;
   double* sD = smem + 4 * STAGE;
   for (int J = 0; J < nb; ++J) {

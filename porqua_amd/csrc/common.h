@@ -15,6 +15,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// The device helpers a kernel calls from several places (window passes, tile Cholesky,
+// P_FF forms): forced inline -- a real call makes the callee keep the calling convention's
+// register split and save / restore through scratch (k_admm: 92-308 bytes of scratch per
+// lane before).  -DPQ_DEVFN=__device__ leaves the choice to the compiler (A/B builds).
+#ifndef PQ_DEVFN
+#define PQ_DEVFN __device__ __forceinline__
+#endif
+
 namespace pq {
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));

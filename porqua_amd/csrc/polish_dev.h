@@ -132,7 +132,7 @@ __device__ __forceinline__ void rows_dot_vec(const double* P, int64_t ld, int n,
 // lr_pass1: u_t = Xc_t . x = X_t . x - mu . x for t < T (u in LDS, >= T doubles).  Row t
 // is always owned by the same wave, so its partial dot products accumulate across column
 // chunks in u[t] without barriers.  Ends with a barrier.
-__device__ void lr_pass1(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* red) {
+PQ_DEVFN void lr_pass1(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* red) {
   constexpr int NQ = 8, RU = 4, LM = NQ * 128;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const int T = lr.tlen[b];
@@ -255,7 +255,7 @@ __device__ void lr_pass2(const pq_lowrank& lr, int b, int n, const double* u, do
 // lr_pass1 for an x supported on k listed columns (x_F compact in LDS, index list Fl in
 // LDS): u_t = sum_p X_t,F[p] x_F[p] - mu . x, gathered from the window rows -- k
 // instead of n loads per row.  4 rows per wave in flight.  Ends with a barrier.
-__device__ void lr_pass1_sparse(const pq_lowrank& lr, int b, const int* Fl, int k, const double* xF,
+PQ_DEVFN void lr_pass1_sparse(const pq_lowrank& lr, int b, const int* Fl, int k, const double* xF,
                                 double* u, double* red) {
   constexpr int RU = 4;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
@@ -293,7 +293,7 @@ __device__ void lr_pass1_sparse(const pq_lowrank& lr, int b, const int* Fl, int 
 
 // emit(i, w_scale * (Xc' Xc x)_i) for i < n: both passes (u: LDS >= tmax doubles).
 template <typename EmitF>
-__device__ void lr_px(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* tree,
+PQ_DEVFN void lr_px(const pq_lowrank& lr, int b, int n, const double* x, double* u, double* tree,
                       double* red, EmitF emit) {
   const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
   lr_pass1(lr, b, n, x, u, red);

@@ -28,6 +28,7 @@
 // Replaces, with polish_w.hip, the accuracy of qpsolvers' interior-point answer
 // (src/qp_problems.py:211-214); scoring as src/qp_problems.py:219-221 and
 // example/compare_solver.ipynb:212-216.
+#include <cstdlib>
 #include <mutex>
 
 #include "polish_dev.h"
@@ -374,64 +375,108 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
 }
 
 // ---------------------------------------------------------------------------------------
-// solve, one WAVE per date: factor P_FF + delta I in LDS, Schur complement of the active
-// rows, proximal iterative refinement -- wave-synchronous (no block barriers, no idle waves
-// waiting on the serial pivot chain); the concurrency comes from several dates per CU
-// (LDS: one packed triangle per date).  Same arithmetic as polish_w.hip's compact mode.
+// solve, one workgroup of NW waves per date: factor P_FF + delta I in LDS, Schur complement
+// of the active rows, proximal iterative refinement.  One packed triangle per date in LDS
+// bounds the dates per CU, so the waves of a date share its work: wave 0 runs the serial
+// 16x16 pivot chain of each diagonal block in registers while the others wait; the panel
+// tiles, the trailing MFMA tiles, the triangular-solve updates (four lanes per row), the
+// residual's P_FF product (one column slice per wave) and the dot products of the active
+// rows are spread over all waves.  Same arithmetic as polish_w.hip's compact mode.
 // ---------------------------------------------------------------------------------------
-#define WSYNC()                                                   \
-  do {                                                            \
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");        \
-    __builtin_amdgcn_wave_barrier();                              \
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");        \
-  } while (0)
+constexpr int WMA = 8;   // active general rows handled by the solve (more: fallback)
 
-constexpr int WMA = 8;   // active general rows handled by the wave solve (more: fallback)
+__device__ __forceinline__ double sum16(double v) {   // over the 16 lanes of a DPP row
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double sum4(double v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  return v;
+}
 
-// Packed lower Cholesky by one wave.  16-column panels: the 16x16 diagonal block lives in
-// registers in the MFMA C layout (lane l: rows l>>4 + 4q of column l&15, both triangles);
-// each pivot step reads the pivot, row kk and column kk by cross-lane shuffles (uniform, no
-// LDS round trip) and updates the trailing block in registers; the block's inverse follows
-// by forward substitution on the identity in the same layout and REPLACES L11 in Lp (the
-// solves and the panel below use only the inverse).  The panel below is L21 = A21 L11^-T
-// and the trailing update A22 -= L21 L21', both 16x16x4 MFMA tiles by the same wave.
-__device__ int w_potrf(double* Lp, int k, double* prof = nullptr) {
-  const int l = lane_id();
+// Packed lower Cholesky of Lp (k x k) by the NW waves of the workgroup.  16-column panels:
+// the 16x16 diagonal block lives in wave 0's registers in the MFMA C layout (lane l: rows
+// l>>4 + 4q of column l&15, both triangles); each pivot step reads the pivot, row kk and
+// column kk by cross-lane shuffles and updates the trailing block in registers; the block's
+// inverse follows in the same chain and REPLACES L11 in Lp (the solves and the panel below
+// use only the inverse).  The panel below is L21 = A21 L11^-T (16x16x4 MFMA tiles dealt
+// round-robin over the waves).  The trailing update A22 -= L21 L21' is deferred into the
+// next block's step: wave 0 updates only the next diagonal tile and goes straight on to its
+// pivot chain while the other waves update the remaining tiles, so the serial chain and the
+// trailing MFMA work overlap (two barriers per block).  Returns 0, or (first bad column + 1)
+// -- uniform over the workgroup.
+template <int NW>
+__device__ __forceinline__ int b_potrf(double* Lp, int k, int* s_bad, double* prof) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
 #ifdef PQ_PROFILE
   long long tp_ = wall_clock64();
-#define WP_STAMP(k_)                                                                  \
+#define BP_STAMP(k_)                                                                  \
   do {                                                                                \
-    WSYNC();                                                                          \
-    if (l == 0 && prof) { const long long n_ = wall_clock64(); prof[k_] += (double)(n_ - tp_); tp_ = n_; } \
+    if (t == 0 && prof) { const long long n_ = wall_clock64(); prof[k_] += (double)(n_ - tp_); tp_ = n_; } \
   } while (0)
 #else
-#define WP_STAMP(k_) do { } while (0)
+#define BP_STAMP(k_) do { } while (0)
 #endif
   const int cc = l & 15, gg = l >> 4;
+  const int j16 = l & 15, kq = l >> 4;
+  // tile (I, J) of the trailing block at p0 (rows p0 + 16 I.., columns p0 + 16 J..) minus the
+  // product of its rows and columns in panel column block pc
+  auto trail_tile = [&](int p0, int I, int J, int pc) {
+    const int ri = p0 + 16 * I + j16, cj = p0 + 16 * J + j16;
+    f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int kc = pc + 4 * s4 + kq;
+      const double av = ri < k ? Lp[pk(ri, kc)] : 0.0;
+      const double bv = cj < k ? Lp[pk(cj, kc)] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int gr = p0 + 16 * I + kq + 4 * rr, gc = p0 + 16 * J + j16;
+      if (gr < k && gc <= gr) Lp[pk(gr, gc)] -= acc[rr];
+    }
+  };
   for (int p0 = 0; p0 < k; p0 += 16) {
     const int nb = min(16, k - p0);
-    // the 16x16 diagonal block in the MFMA C layout: lane l holds A[gg + 4q][cc], q = 0..3,
-    // both triangles (padding rows/cols beyond nb are the identity)
-    double A[4], Bv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = gg + 4 * q;
-      A[q] = (r < nb && cc < nb) ? (cc <= r ? Lp[pk(p0 + r, p0 + cc)] : Lp[pk(p0 + cc, p0 + r)])
-                                 : (r == cc ? 1.0 : 0.0);
-      Bv[q] = (r == cc) ? 1.0 : 0.0;
+    if (p0 > 0) {   // the previous column block's trailing update A22 -= L21 L21'
+      const int nt = (k - p0 + 15) >> 4;
+      int cnt = 0;
+      for (int I = 0; I < nt; ++I)
+        for (int J = 0; J <= I; ++J) {
+          int owner = 0;   // the diagonal tile (0, 0) feeds wave 0's chain: wave 0's
+          if (I > 0 && NW > 1) owner = 1 + (cnt++ % (NW - 1));
+          if (owner == w) trail_tile(p0, I, J, p0 - 16);
+        }
     }
-    const int bad = wave_chol_inv16(A, Bv);
-    if (bad) return p0 + 1;
+    if (w == 0) {
+      double A[4], Bv[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {   // the diagonal block now holds L11^-1
-      const int r = gg + 4 * q;
-      if (r < nb && cc <= r) Lp[pk(p0 + r, p0 + cc)] = Bv[q];
+      for (int q = 0; q < 4; ++q) {
+        const int r = gg + 4 * q;
+        A[q] = (r < nb && cc < nb) ? (cc <= r ? Lp[pk(p0 + r, p0 + cc)] : Lp[pk(p0 + cc, p0 + r)])
+                                   : (r == cc ? 1.0 : 0.0);
+        Bv[q] = (r == cc) ? 1.0 : 0.0;
+      }
+      const int bad = wave_chol_inv16(A, Bv);
+      if (!bad) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {   // the diagonal block now holds L11^-1
+          const int r = gg + 4 * q;
+          if (r < nb && cc <= r) Lp[pk(p0 + r, p0 + cc)] = Bv[q];
+        }
+      }
+      if (l == 0) *s_bad = bad;
     }
-    WSYNC();
-    WP_STAMP(0);
-    const int j16 = l & 15, kq = l >> 4;
-    for (int r1 = p0 + 16; r1 < k; r1 += 16) {   // L21 = A21 L11^-T
-      const int ri = r1 + j16;
+    __syncthreads();
+    if (*s_bad) return p0 + 1;
+    BP_STAMP(0);
+    const int q0 = p0 + 16;
+    const int nt = q0 < k ? (k - q0 + 15) >> 4 : 0;
+    for (int i = w; i < nt; i += NW) {   // L21 = A21 L11^-T
+      const int r1 = q0 + 16 * i, ri = r1 + j16;
       f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
@@ -445,101 +490,109 @@ __device__ int w_potrf(double* Lp, int k, double* prof = nullptr) {
         const int gr = r1 + kq + 4 * rr;
         if (gr < k && j16 < nb) Lp[pk(gr, p0 + j16)] = acc[rr];
       }
-      WSYNC();
     }
-    WP_STAMP(1);
-    const int q0 = p0 + 16;
-    if (q0 < k) {   // A22 -= L21 L21' (lower 16x16 tiles)
-      const int nt = (k - q0 + 15) >> 4;
-      for (int I = 0; I < nt; ++I)
-        for (int J = 0; J <= I; ++J) {
-          const int ri = q0 + 16 * I + j16, cj = q0 + 16 * J + j16;
-          f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            const int kc = p0 + 4 * s4 + kq;
-            const double av = ri < k ? Lp[pk(ri, kc)] : 0.0;
-            const double bv = cj < k ? Lp[pk(cj, kc)] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-          }
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const int gr = q0 + 16 * I + kq + 4 * rr, gc = q0 + 16 * J + j16;
-            if (gr < k && gc <= gr) Lp[pk(gr, gc)] -= acc[rr];
-          }
-        }
-      WSYNC();
-    }
-    WP_STAMP(2);
+    __syncthreads();
+    BP_STAMP(1);
   }
-#undef WP_STAMP
+#undef BP_STAMP
   return 0;
 }
 
-// yo <- L^-1 y (y consumed), one wave; diagonal blocks of Lp hold their inverses
-__device__ void w_fwd(const double* Lp, int k, double* y, double* yo) {
-  const int l = lane_id();
+// yo <- L^-1 y (y consumed); diagonal blocks of Lp hold their inverses.  Per 16-row block:
+// the 16x16 inverse times the block of y (one product per thread of a 256-thread slice, a
+// 16-lane sum), then the rows below subtract their 16-column panel product, four lanes per
+// row.  Entered and left with the workgroup synchronised.
+template <int NW>
+__device__ __forceinline__ void b_fwd(const double* Lp, int k, double* y, double* yo) {
+  constexpr int T = 64 * NW;
+  const int t = threadIdx.x;
   for (int p0 = 0; p0 < k; p0 += 16) {
     const int nb = min(16, k - p0);
-    if (l < nb) {
-      double v = 0.0;
-      for (int m = 0; m <= l; ++m) v = fma(Lp[pk(p0 + l, p0 + m)], y[p0 + m], v);
-      yo[p0 + l] = v;
+    for (int e = t; e < 256; e += T) {
+      const int i = e >> 4, m = e & 15;
+      double v = (i < nb && m <= i) ? Lp[pk(p0 + i, p0 + m)] * y[p0 + m] : 0.0;
+      v = sum16(v);
+      if (m == 0 && i < nb) yo[p0 + i] = v;
     }
-    WSYNC();
-    for (int r = p0 + nb + l; r < k; r += 64) {
-      double v = y[r];
-      const double* lr_ = Lp + pk(r, p0);
-#pragma unroll 4
-      for (int j = 0; j < nb; ++j) v = fma(-lr_[j], yo[p0 + j], v);
-      y[r] = v;
+    __syncthreads();
+    if (p0 + nb < k) {
+      const int jq = t & 3;
+      for (int r0 = p0 + nb; r0 < k; r0 += T / 4) {
+        const int r = r0 + (t >> 2);
+        double v = 0.0;
+        if (r < k) {
+          const double* lr_ = Lp + pk(r, p0) + 4 * jq;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) v = fma(lr_[jj], yo[p0 + 4 * jq + jj], v);
+        }
+        v = sum4(v);
+        if (r < k && jq == 0) y[r] -= v;
+      }
+      __syncthreads();
     }
-    WSYNC();
   }
 }
 
-// xo <- L^-T y (y consumed)
-__device__ void w_bwd(const double* Lp, int k, double* y, double* xo) {
-  const int l = lane_id();
+// xo <- L^-T y (y consumed), blocks from the last: the transposed 16x16 inverse times the
+// block of y, then the columns left of the block subtract the block rows' product.
+template <int NW>
+__device__ __forceinline__ void b_bwd(const double* Lp, int k, double* y, double* xo) {
+  constexpr int T = 64 * NW;
+  const int t = threadIdx.x;
   for (int B = ((k + 15) >> 4) - 1; B >= 0; --B) {
     const int p0 = 16 * B, nb = min(16, k - p0);
-    if (l < nb) {
-      double v = 0.0;
-      for (int m = l; m < nb; ++m) v = fma(Lp[pk(p0 + m, p0 + l)], y[p0 + m], v);
-      xo[p0 + l] = v;
+    for (int e = t; e < 256; e += T) {
+      const int i = e >> 4, m = e & 15;
+      double v = (i < nb && m >= i && m < nb) ? Lp[pk(p0 + m, p0 + i)] * y[p0 + m] : 0.0;
+      v = sum16(v);
+      if (m == 0 && i < nb) xo[p0 + i] = v;
     }
-    WSYNC();
-    for (int c = l; c < p0; c += 64) {
-      double v = y[c];
-#pragma unroll 4
-      for (int j = 0; j < nb; ++j) v = fma(-Lp[pk(p0 + j, c)], xo[p0 + j], v);
-      y[c] = v;
+    __syncthreads();
+    if (p0 > 0) {
+      const int jq = t & 3;
+      for (int c0 = 0; c0 < p0; c0 += T / 4) {
+        const int c = c0 + (t >> 2);
+        double v = 0.0;
+        if (c < p0) {
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * jq + jj;
+            if (j < nb) v = fma(Lp[pk(p0 + j, c)], xo[p0 + j], v);
+          }
+        }
+        v = sum4(v);
+        if (c < p0 && jq == 0) y[c] -= v;
+      }
+      __syncthreads();
     }
-    WSYNC();
   }
 }
 
-template <int KS>
-__global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s, int ldk,
-                                                 int klo) {
+template <int KS, int NW>
+__global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s,
+                                                      int ldk, int klo) {
+  constexpr int T = 64 * NW;
   constexpr int NP = KS * (KS + 1) / 2;
   __shared__ double Lp[NP];
-  __shared__ double xF[KS], t1[KS], t2[KS], rx[KS];
-  __shared__ double Sm[WMA * WMA], lamv[WMA], wl[WMA], rl[WMA], dAv[WMA];
+  __shared__ double xF[KS], rx[KS], sc4[4 * KS];   // sc4: t1 | t2, or the residual's column-slice partials
+  __shared__ double Sm[WMA * WMA], lamv[WMA], wl[WMA], rl[WMA], dAv[WMA], red[16];
   __shared__ int s_al[WMA];
   __shared__ int s_map[KS];
+  __shared__ int s_flag;
+  double* t1 = sc4;
+  double* t2 = sc4 + KS;
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;
   const int k = (int)R[R_K];
   if (k <= klo || k > KS) return;
   const int ma = (int)R[R_MA];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
   if (ma > WMA) {
-    if (threadIdx.x == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
   const int n = pb.n, ld = pb.ld;
-  const int l = lane_id();
   const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
   PGWork wk(st, b, ld);
   const double sc = R[R_SC];
@@ -549,8 +602,8 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   long long t_last_ = wall_clock64();
 #define WSTAMP(k_)                                                         \
   do {                                                                     \
-    WSYNC();                                                               \
-    if (l == 0) { const long long n_ = wall_clock64(); R[8 + (k_)] += (double)(n_ - t_last_); t_last_ = n_; } \
+    __syncthreads();                                                       \
+    if (t == 0) { const long long n_ = wall_clock64(); R[8 + (k_)] += (double)(n_ - t_last_); t_last_ = n_; } \
   } while (0)
 #else
 #define WSTAMP(k_) do { } while (0)
@@ -558,17 +611,17 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
   // the K scratch rows / columns of this round's free positions: identity, or (P_FF reused
   // from an earlier round's form) the positions in that free list
   const bool reuse = R[R_REUSE] != 0.0;
-  for (int p = l; p < k; p += 64) s_map[p] = reuse ? wk.posF[wk.Fl[p]] : p;
-  WSYNC();
-  {   // packed triangle, flat index (independent loads, 64 per trip)
+  for (int p = t; p < k; p += T) s_map[p] = reuse ? wk.posF[wk.Fl[p]] : p;
+  __syncthreads();
+  {   // packed triangle, flat index (independent loads, 8 per thread in flight)
     const int np_ = k * (k + 1) / 2;
-    int r = 0, e0 = 0;   // row of the lane's element: advance incrementally
-    for (int eb = 0; eb < np_; eb += 64 * 8) {   // 8 loads in flight per lane
+    int r = 0, e0 = 0;   // row of the thread's element: advance incrementally
+    for (int eb = 0; eb < np_; eb += T * 8) {
       double v[8];
       int dg = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int e = eb + 64 * j + l;
+        const int e = eb + T * j + t;
         v[j] = 0.0;
         if (e < np_) {
           while (e >= e0 + r + 1) { e0 += r + 1; ++r; }
@@ -579,33 +632,34 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int e = eb + 64 * j + l;
+        const int e = eb + T * j + t;
         if (e < np_) Lp[e] = v[j] + ((dg >> j) & 1 ? delta : 0.0);
       }
     }
   }
-  for (int p = l; p < k; p += 64) xF[p] = wk.solx[p];
-  if (l < ma) {
-    s_al[l] = (int)R[R_AL + l];
-    lamv[l] = R[R_SOL + l];
-    dAv[l] = R[R_DA + l];
+  for (int p = t; p < k; p += T) xF[p] = wk.solx[p];
+  if (t < ma) {
+    s_al[t] = (int)R[R_AL + t];
+    lamv[t] = R[R_SOL + t];
+    dAv[t] = R[R_DA + t];
   }
   WSTAMP(0);
-  if (w_potrf(Lp, k, R + 16)) {
-    if (l == 0) R[R_STATE] = PQ_PG_FALLBACK;
+  __syncthreads();
+  if (b_potrf<NW>(Lp, k, &s_flag, R + 16)) {
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
   WSTAMP(1);
   // U = L^-1 C_aF' (row a of the global U scratch), S = U'U + delta I
   for (int a = 0; a < ma; ++a) {
     const double* cr = Cg + (int64_t)s_al[a] * ld;
-    for (int p = l; p < k; p += 64) t1[p] = cr[wk.Fl[p]];
-    WSYNC();
-    w_fwd(Lp, k, t1, t2);
-    for (int p = l; p < k; p += 64) wk.U[(int64_t)a * ld + p] = t2[p];
+    for (int p = t; p < k; p += T) t1[p] = cr[wk.Fl[p]];
+    __syncthreads();
+    b_fwd<NW>(Lp, k, t1, t2);
+    for (int p = t; p < k; p += T) wk.U[(int64_t)a * ld + p] = t2[p];
   }
-  WSYNC();
-  for (int e = 0; e < ma * ma; ++e) {
+  __syncthreads();
+  for (int e = w; e < ma * ma; e += NW) {
     const int ii = e / ma, jj = e % ma;
     if (jj > ii) continue;
     const double* ui = wk.U + (int64_t)ii * ld;
@@ -615,9 +669,9 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
     sum = wave_sum(sum);
     if (l == 0) Sm[ii * WMA + jj] = sum + (ii == jj ? delta : 0.0);
   }
-  WSYNC();
-  int sbad = 0;
-  if (l == 0) {   // tiny Cholesky of S (ma <= 8), one lane
+  __syncthreads();
+  if (t == 0) {   // tiny Cholesky of S (ma <= 8), one lane
+    int sbad = 0;
     for (int c = 0; c < ma && !sbad; ++c) {
       double d = Sm[c * WMA + c];
       for (int m = 0; m < c; ++m) d -= Sm[c * WMA + m] * Sm[c * WMA + m];
@@ -630,26 +684,27 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
         Sm[r * WMA + c] = v / d;
       }
     }
+    s_flag = sbad;
   }
-  sbad = __shfl(sbad, 0, 64);
-  if (sbad) {
-    if (l == 0) R[R_STATE] = PQ_PG_FALLBACK;
+  __syncthreads();
+  if (s_flag) {
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
   WSTAMP(2);
   // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------
+  const int qs = (k + NW - 1) / NW, qa = w * qs, qb = min(k, qa + qs);
   for (int itr = 0; itr < s.refine_iters; ++itr) {
-    // rx = rF - P_FF x - C_aF' lam  (lane per row, P_FF from the K scratch)
-    for (int p = l; p < k; p += 64) {   // P_FF is symmetric in K: column p, coalesced over lanes
+    // rx = rF - P_FF x - C_aF' lam: wave w sums the column slice [qa, qb) of P_FF x (P_FF
+    // symmetric in K: row p of the slice is column p, coalesced over lanes); the slices add
+    // in a fixed order
+    for (int p = l; p < k; p += 64) {
       double sum = 0.0;
 #pragma unroll 8
-      for (int qq = 0; qq < k; ++qq) sum = fma(K[(int64_t)s_map[qq] * ldk + s_map[p]], xF[qq], sum);
-      double v = wk.rF[p] - sum;
-      const int fp = wk.Fl[p];
-      for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + fp] * lamv[a];
-      rx[p] = v;
+      for (int qq = qa; qq < qb; ++qq) sum = fma(K[(int64_t)s_map[qq] * ldk + s_map[p]], xF[qq], sum);
+      sc4[w * KS + p] = sum;
     }
-    for (int a = 0; a < ma; ++a) {
+    for (int a = w; a < ma; a += NW) {
       const double* cr = Cg + (int64_t)s_al[a] * ld;
       double sum = 0.0;
       for (int p = l; p < k; p += 64) sum += cr[wk.Fl[p]] * xF[p];
@@ -659,24 +714,31 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
         rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dAv[a]) + fabs(sum)) ? 0.0 : v;
       }
     }
-    WSYNC();
-    WSTAMP(3);
+    __syncthreads();
     double rm = 0.0;
-    for (int p = l; p < k; p += 64) rm = fmax(rm, fabs(rx[p]));
-    if (l < ma) rm = fmax(rm, fabs(rl[l]));
-    if (wave_max(rm) <= 1e-13 * sc) break;
-    for (int p = l; p < k; p += 64) t1[p] = rx[p];
-    WSYNC();
-    w_fwd(Lp, k, t1, t2);   // t2 = L^-1 rx
-    for (int a = 0; a < ma; ++a) {   // wl = U' t2 - rl
+    for (int p = t; p < k; p += T) {
+      double sum = sc4[p];
+#pragma unroll
+      for (int j = 1; j < NW; ++j) sum += sc4[j * KS + p];
+      double v = wk.rF[p] - sum;
+      const int fp = wk.Fl[p];
+      for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + fp] * lamv[a];
+      rx[p] = v;
+      rm = fmax(rm, fabs(v));
+    }
+    if (t < ma) rm = fmax(rm, fabs(rl[t]));
+    WSTAMP(3);
+    if (block_max(rm, red) <= 1e-13 * sc) break;   // (its barriers also order rx / sc4)
+    b_fwd<NW>(Lp, k, rx, t2);   // t2 = L^-1 rx (rx consumed)
+    for (int a = w; a < ma; a += NW) {   // wl = U' t2 - rl
       const double* ua = wk.U + (int64_t)a * ld;
       double sum = 0.0;
       for (int p = l; p < k; p += 64) sum += ua[p] * t2[p];
       sum = wave_sum(sum);
       if (l == 0) wl[a] = sum - rl[a];
     }
-    WSYNC();
-    if (l == 0) {   // dlam = S^-1 wl
+    __syncthreads();
+    if (t == 0) {   // dlam = S^-1 wl
       for (int ii = 0; ii < ma; ++ii) {
         double v = wl[ii];
         for (int jj = 0; jj < ii; ++jj) v -= Sm[ii * WMA + jj] * wl[jj];
@@ -688,31 +750,31 @@ __global__ __launch_bounds__(64) void k_pg_solve(pq_problem pb, pq_state st, dou
         wl[ii] = v / Sm[ii * WMA + ii];
       }
     }
-    WSYNC();
-    for (int p = l; p < k; p += 64) {
+    __syncthreads();
+    for (int p = t; p < k; p += T) {
       double v = t2[p];
       for (int a = 0; a < ma; ++a) v -= wk.U[(int64_t)a * ld + p] * wl[a];
       t1[p] = v;
     }
-    WSYNC();
-    w_bwd(Lp, k, t1, t2);   // t2 = L^-T (t2 - U dlam)
-    for (int p = l; p < k; p += 64) xF[p] += t2[p];
-    if (l < ma) lamv[l] += wl[l];
-    WSYNC();
+    __syncthreads();
+    b_bwd<NW>(Lp, k, t1, t2);   // t2 = L^-T (t2 - U dlam)
+    for (int p = t; p < k; p += T) xF[p] += t2[p];
+    if (t < ma) lamv[t] += wl[t];
+    __syncthreads();
     WSTAMP(4);
   }
   // ---- expand: xs = x_B off F, x_F on F; general multipliers by row ------------------------
-  for (int ii = l; ii < n; ii += 64) wk.xs[ii] = wk.xb[ii];
-  WSYNC();
-  for (int p = l; p < k; p += 64) {
+  for (int ii = t; ii < n; ii += T) wk.xs[ii] = wk.xb[ii];
+  __syncthreads();
+  for (int p = t; p < k; p += T) {
     wk.xs[wk.Fl[p]] = xF[p];
     wk.solx[p] = xF[p];
   }
-  R[R_LAM + l] = 0.0;   // 64 lanes clear the 64 row slots
-  WSYNC();
-  if (l < ma) {
-    R[R_LAM + s_al[l]] = lamv[l];
-    R[R_SOL + l] = lamv[l];
+  if (t < 64) R[R_LAM + t] = 0.0;   // the 64 row slots
+  __syncthreads();
+  if (t < ma) {
+    R[R_LAM + s_al[t]] = lamv[t];
+    R[R_SOL + t] = lamv[t];
   }
   WSTAMP(5);
 #undef WSTAMP
@@ -1150,6 +1212,39 @@ static PgSide* pg_side() {
   }
   return &p;
 }
+
+// waves per date of the solve, per free-set bucket (48, 64, 80, 96, 128): PQ_PG_SOLVE_NW
+// (1, 2 or 4) overrides all buckets
+static int solve_waves(int bucket) {
+  static const int forced = [] {
+    const char* e = getenv("PQ_PG_SOLVE_NW");
+    const int v = e ? atoi(e) : 0;
+    return v == 1 || v == 2 || v == 4 ? v : 0;
+  }();
+  static const int def[5] = {2, 2, 4, 4, 4};
+  return forced ? forced : def[bucket];
+}
+
+template <int KS>
+static void launch_solve_ks(int nw, int B, hipStream_t str, const pq_problem* pb, pq_state* st, double* rec,
+                            const pq_settings* s, int ldk, int klo) {
+  if (nw == 1)
+    hipLaunchKernelGGL((k_pg_solve<KS, 1>), dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, klo);
+  else if (nw == 2)
+    hipLaunchKernelGGL((k_pg_solve<KS, 2>), dim3(B), dim3(128), 0, str, *pb, *st, rec, *s, ldk, klo);
+  else
+    hipLaunchKernelGGL((k_pg_solve<KS, 4>), dim3(B), dim3(256), 0, str, *pb, *st, rec, *s, ldk, klo);
+}
+static void launch_solve(int bucket, int nw, int B, hipStream_t str, const pq_problem* pb, pq_state* st,
+                         double* rec, const pq_settings* s, int ldk, int klo) {
+  switch (bucket) {
+    case 0: launch_solve_ks<48>(nw, B, str, pb, st, rec, s, ldk, klo); break;
+    case 1: launch_solve_ks<64>(nw, B, str, pb, st, rec, s, ldk, klo); break;
+    case 2: launch_solve_ks<80>(nw, B, str, pb, st, rec, s, ldk, klo); break;
+    case 3: launch_solve_ks<96>(nw, B, str, pb, st, rec, s, ldk, klo); break;
+    default: launch_solve_ks<128>(nw, B, str, pb, st, rec, s, ldk, klo); break;
+  }
+}
 }  // namespace pq
 
 extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec,
@@ -1177,7 +1272,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   hipLaunchKernelGGL(pq::k_pg_post<0>, dim3(B), dim3(64), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
                      pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
-  // one wave per date, the LDS triangle sized to the free set (more dates per CU when small);
+  // one workgroup per date, the LDS triangle sized to the free set (more dates per CU when small);
   // the buckets (and the wide rounds) on side streams, joined before the exact-P x passes
   pq::PgSide* side = pq::pg_side();
   int used = 0;
@@ -1187,11 +1282,11 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
     used |= 1 << i;
     return side->s[i];
   };
-  hipLaunchKernelGGL(pq::k_pg_solve<48>, dim3(B), dim3(64), 0, on(0), *pb, *st, rec, *s, ldk, 0);
-  hipLaunchKernelGGL(pq::k_pg_solve<64>, dim3(B), dim3(64), 0, on(1), *pb, *st, rec, *s, ldk, 48);
-  if (kmax > 64) hipLaunchKernelGGL(pq::k_pg_solve<80>, dim3(B), dim3(64), 0, on(2), *pb, *st, rec, *s, ldk, 64);
-  if (kmax > 80) hipLaunchKernelGGL(pq::k_pg_solve<96>, dim3(B), dim3(64), 0, on(3), *pb, *st, rec, *s, ldk, 80);
-  if (kmax > 96) hipLaunchKernelGGL(pq::k_pg_solve<128>, dim3(B), dim3(64), 0, on(4), *pb, *st, rec, *s, ldk, 96);
+  for (int i = 0; i < 5; ++i) {
+    static const int KSB[5] = {48, 64, 80, 96, 128};
+    if (i >= 2 && kmax <= KSB[i - 1]) break;
+    pq::launch_solve(i, pq::solve_waves(i), B, on(i), pb, st, rec, s, ldk, i ? KSB[i - 1] : 0);
+  }
   if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, on(5))) return -1;   // free sets beyond kmax
   for (int i = 0; side && i < pq::PgSide::NS; ++i)
     if ((used & (1 << i)) && (hipEventRecord(side->join[i], side->s[i]) != hipSuccess ||

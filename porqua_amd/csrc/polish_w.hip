@@ -49,7 +49,7 @@ __device__ __forceinline__ double pc_at(const double* K, int64_t ld, int p, int 
 // P_FF = psw Xc_F' Xc_F + pd I into the compact storage (lower tiles computed; diagonal
 // tiles stored in full, off-diagonal tiles transposed into the upper half).  One MFMA
 // tile product per lower tile, contracted over the window in 16-row chunks staged into LDS.
-__device__ void form_pff(const pq_lowrank& lr, int b, const int* Fl, int k, int nbk, double psw,
+PQ_DEVFN void form_pff(const pq_lowrank& lr, int b, const int* Fl, int k, int nbk, double psw,
                          double pd, double* Ks, int64_t ldk, double* smem) {
   const int T = lr.tlen[b];
   const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
@@ -259,7 +259,7 @@ struct FormRead {   // the lower tiles (diagonal tiles in full) as written
 // double-buffered so the next chunk's gathers (2 rows x 4 NB columns per thread, all in
 // flight together) overlap the MFMAs: 8 dependent gather round trips for T = 252.
 template <int NB>
-__device__ void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k, double psw, double pd,
+PQ_DEVFN void form_pff_small(const pq_lowrank& lr, int b, const int* Fl, int k, double psw, double pd,
                                double* Ks, int64_t ldk, double* smem) {
   constexpr int PIT = NB * TB + 16;
   constexpr int NT = NB * (NB + 1) / 2;

@@ -81,7 +81,7 @@ def main():
             print("  %-12s %8.1f us" % (nm, rec[:, i].mean()))
         print("  rounds mean %.2f" % done.mean())
         pp = ws.pg_record()[:, 16:19].cpu().numpy() * 10e-3
-        for i, nm in enumerate(["potrf: diag 16x16", "potrf: panel trsm", "potrf: MFMA update"]):
+        for i, nm in enumerate(["potrf: diag chain (+ deferred MFMA update)", "potrf: panel trsm", "potrf: (unused)"]):
             print("  %-20s %8.1f us" % (nm, pp[:, i].mean()))
     for name, a, b in ev:
         print("stage", name, "%.1f ms" % a.elapsed_time(b))
