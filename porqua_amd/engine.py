@@ -87,6 +87,16 @@ class Settings:
     # rounds; 1e-7 converges in <= 4 steps to 5e-13 (87k QPs/s, polish 40 ms, 1.0 rounds)
     refine_wide: int = 6
     delta_wide: float = 1e-7
+    # centred windows (mean-variance family) on the group capacitance with the grouped polish
+    # (host-side): the ADMM stops at this looser eps -- it only has to predict the active
+    # set, the pipeline's rounds are cheap and every answer is certified -- and the dates the
+    # pipeline hands to the per-date polish resume ADMM to eps_abs / eps_rel first (their
+    # rounds are not cheap).  Measured (profiles/r03s_*, r03t_*, r03u_*): config 3 2e-3 /
+    # 1e-2 / 2e-2 / 1e-1 -> 311k / 335k / 343k / 353k QPs/s (20 / 16 / 15 / 11 iterations,
+    # 2.7 / 3.1 / 3.2 / 3.8 rounds).  Tracking (uncentred) windows keep eps_abs: their free
+    # sets mostly exceed the LDS solve -- config 2 53.0k at 2e-3, 45.0k at 1e-2 from the loose
+    # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
+    eps_grouped: float = 2e-2
 
     def to_c(self) -> _lib.PQSettings:
         names = {f[0] for f in _lib.PQSettings._fields_}
@@ -903,11 +913,11 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
 
     cnt = {"refactors": 0, "launches": 0, "pg_fallback": 0}
 
-    def admm_rounds(idx, nidx, SSx):
+    def admm_rounds(idx, nidx, SSx, name="admm"):
         nonlocal SS
         SS0, SS = SS, SSx   # admm() reads SS
         for _ in range(max_rounds):
-            _lib.check(tl("admm", lambda: admm(idx, nidx)), "pq_admm_lr")
+            _lib.check(tl(name, lambda: admm(idx, nidx)), "pq_admm_lr")
             cnt["launches"] += 1
             need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
             kk = int(need.numel())
@@ -971,6 +981,9 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         cnt["pg_fallback"] = m
         if m:
             ws.pg_fallback = fb   # the dates handed to the per-date kernel (diagnostics)
+            if SS_admm is not SS_main:   # stopped at eps_grouped: resume those to eps first
+                ws.status[fb.long()] = _lib.PQ_UNSOLVED
+                admm_rounds(fb.contiguous(), m, SS_main, name="admm (resume, inside polish)")
             # two refinement steps per round for the hand-offs (vertex cycling, failed
             # factorisations): config 5's fallback polish 31.3 -> 7.5 ms
             # (profiles/r02k_bench_config5_qrel30.log -> r02l_bench_config5_fallback_refine2.log)
@@ -978,8 +991,15 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             sfb.refine_iters = max(sfb.refine_iters, 2)
             polish_w(fb.contiguous(), m, ctypes.byref(sfb), name="polish (fallback, inside polish)")
 
-    admm_rounds(None, 0, SS)
     SS_main = SS
+    SS_admm = SS
+    st_ = settings or Settings()
+    if (gc is not None and lr.mu is not None and polish and s.polish and grouped_polish and ldk >= 64
+            and st_.eps_grouped > max(st_.eps_abs, st_.eps_rel)):
+        sl = st_.to_c()
+        sl.eps_abs = sl.eps_rel = st_.eps_grouped
+        SS_admm = ctypes.byref(sl)
+    admm_rounds(None, 0, SS_admm)
     if s.polish and polish:
         if grouped and grouped_polish and ldk >= 64:
             tl("polish", polish_grouped)

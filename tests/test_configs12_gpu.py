@@ -31,7 +31,7 @@ def usa_data():
     return X, pd.DataFrame({"SPTR": y}, index=idx)
 
 
-def service(X, y, rebdates, width=252):
+def service(X, y, rebdates, width=252, params=None):
     return BacktestService(
         data={"return_series": X, "bm_series": y},
         selection_item_builders={"data": SelectionItemBuilder(bibfn=bibfn_selection_data)},
@@ -40,7 +40,7 @@ def service(X, y, rebdates, width=252):
             "bm_series": OptimizationItemBuilder(bibfn=bibfn_bm_series, width=width, align=True),
             "budget_constraint": OptimizationItemBuilder(bibfn=bibfn_budget_constraint, budget=1),
             "box_constraints": OptimizationItemBuilder(bibfn=bibfn_box_constraints, box_type="LongOnly")},
-        optimization=LeastSquares(solver_name="mi355x"), rebdates=rebdates, quiet=True)
+        optimization=LeastSquares(solver_name="mi355x", **(params or {})), rebdates=rebdates, quiet=True)
 
 
 def test_config2_sptr_replication_matches_config1_oracle(device):

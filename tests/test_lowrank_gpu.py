@@ -119,9 +119,10 @@ def test_grouped_admm_matches_per_date_lowrank(device, n, T, D, stride, groups_r
     assert gp.ok and gp.ngroups < B
     ws_g = engine.Workspace(qb)
     assert engine.grouped_applicable(qb, lr, gp, ws_g)
-    res_g = engine.solve_lowrank(qb, lr, ws=ws_g, groups=gp)
+    st0 = engine.Settings(eps_grouped=0.0)   # both paths stop ADMM at eps_abs: same iteration counts
+    res_g = engine.solve_lowrank(qb, lr, st0, ws=ws_g, groups=gp)
     xg, itg, stg = res_g.x.cpu().numpy().copy(), res_g.iters.cpu().numpy().copy(), res_g.status.cpu().numpy().copy()
-    res_d = engine.solve_lowrank(qb, lr)
+    res_d = engine.solve_lowrank(qb, lr, st0)
     xd, itd = res_d.x.cpu().numpy(), res_d.iters.cpu().numpy()
     assert np.all(stg == 1) and np.all(res_d.status.cpu().numpy() == 1)
     assert np.abs(itg - itd).max() <= 2, (itg, itd)
@@ -207,10 +208,11 @@ def test_grouped_fused_matches_unfused(device, n, T, D, stride, groups_rows, cen
     w = 1.0 / (t_d.to(torch.float64) - 1.0) if centred else None
     lr = engine.LowRank(pan, r_d, t_d, mu=mu, w_scale=w)
     gp = engine.GroupPlan(rows, tlen, device)
-    r1 = engine.solve_lowrank(qb, lr, groups=gp, fuse=False)
+    st0 = engine.Settings(eps_grouped=0.0)   # both forms stop ADMM at eps_abs: same iteration counts
+    r1 = engine.solve_lowrank(qb, lr, st0, groups=gp, fuse=False)
     x1, i1 = r1.x.cpu().numpy().copy(), r1.iters.cpu().numpy().copy()
     assert r1.capacitance == "band"
-    r2 = engine.solve_lowrank(qb, lr, groups=gp, fuse=True)
+    r2 = engine.solve_lowrank(qb, lr, st0, groups=gp, fuse=True)
     assert np.all(r1.status.cpu().numpy() == 1) and np.all(r2.status.cpu().numpy() == 1)
     assert np.abs(r2.iters.cpu().numpy() - i1).max() <= 2
     assert np.abs(r2.x.cpu().numpy() - x1).max() < 1e-8

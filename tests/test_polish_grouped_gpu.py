@@ -42,9 +42,13 @@ def _problem(device, n, T, D, ub, ngroups_rows=0, cap=0.3, centred=True, stride=
     return qb, lr, gp
 
 
-def _solve(qb, lr, gp, grouped_polish, settings=None):
+def _solve(qb, lr, gp, grouped_polish, settings=None, eps_grouped=0.0):
     """(wide rounds off: this file pins the LDS-solve pipeline against the per-date kernel;
-    tests/test_polish_wide_gpu.py covers the wide rounds)"""
+    tests/test_polish_wide_gpu.py covers the wide rounds.  The looser ADMM stop before the
+    pipeline (Settings.eps_grouped) is off unless asked for: both sides start from the same
+    ADMM point.)"""
+    import dataclasses
+    settings = dataclasses.replace(settings or engine.Settings(), eps_grouped=eps_grouped)
     ws = engine.Workspace(qb, dense=False)
     assert engine.grouped_applicable(qb, lr, gp, ws)
     res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, grouped_polish=grouped_polish,
@@ -103,3 +107,37 @@ def test_grouped_polish_hands_large_free_sets_to_the_per_date_kernel(device):
     big = outb[:, _lib.PQ_OUT_NFREE] > 128
     assert big.any()
     assert np.all(rec[big] == _lib.PQ_PG_FALLBACK)
+
+
+def test_loose_admm_stop_before_the_pipeline(device):
+    """Settings.eps_grouped (centred windows, default 2e-2): the ADMM stops early and the
+    pipeline's rounds finish the job -- the same optimum as from the eps_abs point, fewer
+    ADMM iterations, every date SOLVED."""
+    qb, lr, gp = _problem(device, 1000, 252, 48, 1.0)
+    xa, sa, oa, *_ = _solve(qb, lr, gp, True)
+    d = engine.Settings()
+    assert d.eps_grouped > d.eps_abs
+    ws = engine.Workspace(qb, dense=False)
+    res = engine.solve_lowrank(qb, lr, None, ws=ws, groups=gp)
+    torch.cuda.synchronize()
+    assert np.all(res.status.cpu().numpy() == _lib.PQ_SOLVED)
+    ob = res.obj.cpu().numpy()
+    assert np.max(np.abs(ob - oa) / np.maximum(np.abs(oa), 1e-30)) <= 1e-9
+    ws0 = engine.Workspace(qb, dense=False)
+    import dataclasses
+    engine.solve_lowrank(qb, lr, dataclasses.replace(d, eps_grouped=0.0), ws=ws0, groups=gp)
+    torch.cuda.synchronize()
+    assert ws.iters.float().mean().item() < ws0.iters.float().mean().item()
+
+
+def test_loose_admm_stop_resumes_the_hand_offs(device):
+    """Dates the pipeline hands to the per-date kernel (a ridge keeps every asset strictly
+    inside the box: free sets of ~n > 128) resume ADMM to eps_abs before that polish, so the
+    answer is the one from the eps_abs point."""
+    qb, lr, gp = _problem(device, 400, 100, 24, 1.0)
+    qb.p_diag = torch.full((qb.batch,), 5e-3, dtype=torch.float64, device=device)
+    xa, sa, *_ = _solve(qb, lr, gp, True)
+    xb, sb, _, _, _, outb, rec = _solve(qb, lr, gp, True, eps_grouped=2e-2)
+    assert np.all(sa == _lib.PQ_SOLVED) and np.array_equal(sa, sb)
+    assert (rec == _lib.PQ_PG_FALLBACK).mean() >= 0.5, np.unique(rec, return_counts=True)
+    assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()

@@ -103,7 +103,7 @@ def config5(steps, dev, settings=None, factor="auto"):
                  "factor": meta.get("factor"), "stage_ms": stage_ms(ev)}, **summary(res))
 
 
-def config12(steps, dev):
+def config12(steps, dev, params=None):
     import pandas as pd
     from oracle.qp_ipm import solve_qp
     from oracle.ref_pipeline import objective_least_squares, window_rows
@@ -117,12 +117,13 @@ def config12(steps, dev):
     for tag, reb in (("monthly", monthly), ("daily", daily)):
         def run():
             bt = Backtest()
-            bt.run(service(X, y, reb))
+            bt.run(service(X, y, reb, params=params))
             return bt
         bt, dt = timed(run, steps)
         out.append({"config": f"config2: SPTR replication, n=494 LS tracking, {tag} ({len(reb)} dates), "
                               "Backtest.run(solver_name='mi355x')", "qps": len(reb) / dt, "ms_per_run": dt * 1e3,
-                    "dates": len(reb), "solved": bt.stats["solved"], "path": bt.stats["path"]})
+                    "dates": len(reb), "solved": bt.stats["solved"], "path": bt.stats["path"],
+                    "params": params or {}})
     Xv, yv = X.to_numpy(), y.to_numpy()[:, 0]
     n = Xv.shape[1]
     t0 = time.perf_counter()
@@ -144,12 +145,13 @@ def main():
     ap.add_argument("--only", choices=["12", "4", "5"], default=None)
     ap.add_argument("--factor", default="auto", help="config 5 capacitance factor(s): auto, eig, chol or eig,chol")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
-                    help="engine.Settings override for config 5 (experiments)")
+                    help="engine.Settings override (experiments): configs 1/2 through the optimization's "
+                         "params, configs 4/5 directly")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     if args.only in (None, "12"):
-        for line in config12(args.steps, dev):
+        for line in config12(args.steps, dev, dict(kv.split("=", 1) for kv in args.set) or None):
             print(json.dumps(line), flush=True)
     if args.only in (None, "4"):
         ov = dict(kv.split("=", 1) for kv in args.set)

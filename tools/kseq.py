@@ -14,19 +14,22 @@ def main():
     seq = []
     for r in rows:
         k = r["Kernel_Name"]
-        for pre in ("void pq::", "pq::(anonymous namespace)::", "pq::"):
+        for pre in ("void pq::", "pq::(anonymous namespace)::", "pq::", "k_"):   # (-T: truncated names)
             if k.startswith(pre):
-                k = k[len(pre):].split("(")[0]
-                seq.append((k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+                k = (k if pre == "k_" else k[len(pre):]).split("(")[0]
+                seq.append((k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3,
+                            int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
                 break
-    starts = [i for i, (k, _) in enumerate(seq) if k.startswith("k_window_moments_grp")]
+    starts = [i for i, (k, *_) in enumerate(seq) if k.startswith("k_window_moments_grp")]
     i0 = starts[step]
     i1 = starts[step + 1] if len(starts) > step + 1 else len(seq)
     tot = collections.defaultdict(float)
-    for k, d in seq[i0:i1]:
+    t00 = seq[i0][2]
+    for k, d, t0, t1 in seq[i0:i1]:   # start offset from the step's first kernel, duration
         if k.startswith(pref):
-            print(f"{k:40s} {d:9.1f} us")
+            print(f"{k:40s} @{(t0 - t00) / 1e3:9.1f} {d:9.1f} us")
         tot[k.split("<")[0]] += d
+    print(f"step span {(seq[i1 - 1][3] - t00) / 1e3:.1f} us")
     print("--- totals per kernel (us)")
     for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
         print(f"{k:40s} {v:9.1f}")
