@@ -808,6 +808,7 @@ __device__ __forceinline__ double hmax32(double v) {
 //                                      Ut = window-masked W - mu.V, X~[slice] = X_union[:, slice]' Ut
 //   k_pg_post   (group)                the per-date post-processing on the complete X~
 constexpr int QS = 4;      // workgroups per group and pass
+constexpr int QCOL = 2048; // pass A: column slices up to this long take the sparse (compacted) form
 
 struct PassGroup {
   int grp, part, d0, G, U;
@@ -859,11 +860,13 @@ __global__ __launch_bounds__(QT) void k_pg_passA(pq_lowrank lr, pq_problem pb, p
   __shared__ int s_urow[QU];
   __shared__ int g_on[QG], g_T[QG], g_off[QG];
   __shared__ int s_any;
+  __shared__ int s_col[QCOL], s_wcnt[QNW], s_ncol;
   const PassGroup pg = pass_group(gdates, ucnt_all);
   const int U = pg.U, G = pg.G, d0 = pg.d0;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   const int n = pb.n, ld = pb.ld;
   for (int u = t; u < QU; u += QT) s_urow[u] = u < U ? urows_all[(int64_t)pg.grp * umax + u] : 0;
+  if (t == 0) s_ncol = 0;
   if (!pass_setup<MODE>(pg, lr, rec, uoff, g_on, g_T, g_off, &s_any)) return;
   const int per = ((n + QS - 1) / QS + 7) & ~7;
   const int k_lo = pg.part * per, k_hi = min(n, k_lo + per);
@@ -902,16 +905,59 @@ __global__ __launch_bounds__(QT) void k_pg_passA(pq_lowrank lr, pq_problem pb, p
     aval[j] = u < U;
     arow[j] = lr.panel + (int64_t)s_urow[u < QU ? u : 0] * lr.ldp;
   }
-  for (int k0 = k_lo; k0 < k_hi; k0 += 8) {
-    const int kk = k0 + 2 * kq;
-    const bool kin = kk + 1 < k_hi;   // slice ends and n are even
-    const double2 bv = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+  if (k_hi - k_lo <= QCOL) {
+    // V is sparse (the new point is zero on the variables fixed at a zero bound: ~n - |F| of
+    // them for long-only problems): only the slice's columns where some participating date
+    // of the group is nonzero enter the product, compacted in column order (ballot + wave
+    // prefix: deterministic) -- the union rows are then read at those columns only
+    for (int cb = k_lo; cb < k_hi; cb += QT) {
+      const int i = cb + t;
+      bool nz = false;
+      if (i < k_hi)
+        for (int g = 0; g < G; ++g)
+          if (g_on[g]) {
+            PGWork wg(st, d0 + g, ld);
+            nz |= (MODE == 0 ? wg.xb : wg.xs)[i] != 0.0;
+          }
+      const unsigned long long bal = __ballot(nz);
+      if (l == 0) s_wcnt[w] = __popcll(bal);
+      __syncthreads();
+      int off = s_ncol;
+      for (int ww = 0; ww < w; ++ww) off += s_wcnt[ww];
+      if (nz) s_col[off + __popcll(bal & ((1ull << l) - 1ull))] = i;
+      __syncthreads();
+      if (t == 0) {
+        int tot = 0;
+        for (int ww = 0; ww < QNW; ++ww) tot += s_wcnt[ww];
+        s_ncol += tot;
+      }
+      __syncthreads();
+    }
+    const int ncol = s_ncol;
+    for (int k0 = 0; k0 < ncol; k0 += 4) {
+      const int kk = k0 + kq;
+      const int col = kk < ncol ? s_col[kk] : -1;
+      const double bv = (Vp && col >= 0) ? Vp[col] : 0.0;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      if (tv[j]) {
-        const double2 av = (aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
-        c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c[j], 0, 0, 0);
-        c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c[j], 0, 0, 0);
+      for (int j = 0; j < 3; ++j) {
+        if (tv[j]) {
+          const double av = (aval[j] && col >= 0) ? arow[j][col] : 0.0;
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c[j], 0, 0, 0);
+        }
+      }
+    }
+  } else {
+    for (int k0 = k_lo; k0 < k_hi; k0 += 8) {
+      const int kk = k0 + 2 * kq;
+      const bool kin = kk + 1 < k_hi;   // slice ends and n are even
+      const double2 bv = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (tv[j]) {
+          const double2 av = (aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c[j], 0, 0, 0);
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c[j], 0, 0, 0);
+        }
       }
     }
   }
@@ -1005,10 +1051,12 @@ __global__ __launch_bounds__(QT) void k_pg_passB(pq_lowrank lr, pq_problem pb, p
   }
 }
 
-// one wave per pending date (the rows of a date's vectors spread over 64 lanes; thousands of
-// waves in flight instead of one 512-thread workgroup per group)
+// one 256-thread workgroup per pending date (a date's n-vectors spread over its threads: the
+// per-date passes are load-latency bound, 4 loads per thread and vector at n = 1000 instead
+// of 16 with one wave)
+constexpr int PPT = 256;
 template <int MODE>
-__global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+__global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
                                                 pq_settings s, const int32_t* gdates, int ngroups,
                                                 const double* scr) {
   const int b = blockIdx.x;
@@ -1020,14 +1068,15 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
     if (gdates[mid] <= b) lo = mid; else hi = mid;
   }
   const int grp = lo, hg = b - gdates[grp];
-  const int hl = lane_id();
+  __shared__ double red[16];
+  const int hl = threadIdx.x;
   const int n = pb.n, ld = pb.ld, mg = pb.mg;
   PGWork wk(st, b, ld);
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
   const double su = scr[(int64_t)grp * QSCR + (int64_t)QS * (QU + 4) * QG + QS * QG + hg];
   const double wsc = lr.w_scale ? lr.w_scale[b] : 1.0;
   if (MODE == 0) {
-    for (int i = hl; i < n; i += 64) wk.pxb[i] = wsc * (wk.pxb[i] - (mu ? mu[i] * su : 0.0));
+    for (int i = hl; i < n; i += PPT) wk.pxb[i] = wsc * (wk.pxb[i] - (mu ? mu[i] * su : 0.0));
     return;
   }
   const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
@@ -1052,7 +1101,7 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
   if (vtx) {
     const double* c0 = Cg + (int64_t)r0 * ld;
     double lo = -INFINITY, hi = INFINITY;
-    for (int i = hl; i < n; i += 64) {
+    for (int i = hl; i < n; i += PPT) {
       const int f = wk.fl[i];
       const double c = c0[i];
       if (f == 0 || c == 0.0 || (has_box && lb[i] == ub[i])) continue;
@@ -1061,14 +1110,14 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
       if ((f == 1) == (c > 0.0)) lo = fmax(lo, bnd);
       else hi = fmin(hi, bnd);
     }
-    lo = wave_max(lo);
-    hi = -wave_max(-hi);
+    lo = block_max(lo, red);
+    hi = -block_max(-hi, red);
     lam0 = (isfinite(lo) && isfinite(hi)) ? 0.5 * (lo + hi) : (isfinite(lo) ? lo : (isfinite(hi) ? hi : 0.0));
   }
   auto lamof = [&](int r) -> double { return r == r0 ? lam0 : R[R_LAM + r]; };
   // exact P x and gradient g = P x + q + Cg' lam; box checks
   int bad = 0;
-  for (int i = hl; i < n; i += 64) {
+  for (int i = hl; i < n; i += PPT) {
     const double xi = wk.xs[i];
     const double pxi = ps * (wsc * (wk.g[i] - (mu ? mu[i] * su : 0.0))) + pd * xi;
     double gi = pxi + q[i];
@@ -1086,8 +1135,8 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
   for (int r = 0; r < mg; ++r) {
     const double* cr = Cg + (int64_t)r * ld;
     double sum = 0.0;
-    for (int j = hl; j < n; j += 64) sum += cr[j] * wk.xs[j];
-    sum = wave_sum(sum);
+    for (int j = hl; j < n; j += PPT) sum += cr[j] * wk.xs[j];
+    sum = block_sum(sum, red);
     if (hl == 0) {
       if (lg[r] != ug[r]) {
         const int a = (int)R[R_ACT + r];
@@ -1101,7 +1150,7 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
       }
     }
   }
-  bad = wave_max((double)bad) > 0.5;
+  bad = block_max((double)bad, red) > 0.5;
   if (vtx && hl == 0) {   // the next round starts from it (setup's R_SOL), or the scoring uses it
     R[R_LAM + r0] = lam0;
     R[R_SOL] = lam0;
@@ -1115,7 +1164,7 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
   double* sz = st.z + (int64_t)b * st.m_ld;
   double* sy = st.y + (int64_t)b * st.m_ld;
   double xpx = 0.0, qx = 0.0, pres = 0.0, dres = 0.0, gapb = 0.0;
-  for (int i = hl; i < n; i += 64) {
+  for (int i = hl; i < n; i += PPT) {
     const double xi = wk.xs[i];
     double zb = 0.0;
     if (has_box) zb = wk.fl[i] ? -wk.g[i] : 0.0;
@@ -1132,8 +1181,8 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
   for (int r = 0; r < mg; ++r) {
     const double* cr = Cg + (int64_t)r * ld;
     double sum = 0.0;
-    for (int j = hl; j < n; j += 64) sum += cr[j] * wk.xs[j];
-    sum = wave_sum(sum);
+    for (int j = hl; j < n; j += PPT) sum += cr[j] * wk.xs[j];
+    sum = block_sum(sum, red);
     const double lam = lamof(r);
     double v;
     if (lg[r] == ug[r]) v = fabs(sum - ug[r]);
@@ -1145,11 +1194,11 @@ __global__ __launch_bounds__(64) void k_pg_post(pq_lowrank lr, pq_problem pb, pq
       sz[r] = sum;
     }
   }
-  xpx = wave_sum(xpx);
-  qx = wave_sum(qx);
-  gapb = wave_sum(gapb);
-  pres = wave_max(pres);
-  dres = wave_max(dres);
+  xpx = block_sum(xpx, red);
+  qx = block_sum(qx, red);
+  gapb = block_sum(gapb, red);
+  pres = block_max(pres, red);
+  dres = block_max(dres, red);
   if (hl == 0) {
     double* o = st.out + (int64_t)b * PQ_OUT_FIELDS;
     o[PQ_OUT_OBJ] = 0.5 * xpx + qx;
@@ -1269,7 +1318,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
                      umax, pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_passB<0>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
-  hipLaunchKernelGGL(pq::k_pg_post<0>, dim3(B), dim3(64), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
+  hipLaunchKernelGGL(pq::k_pg_post<0>, dim3(B), dim3(pq::PPT), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
                      pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
   // one workgroup per date, the LDS triangle sized to the free set (more dates per CU when small);
@@ -1298,7 +1347,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
                      umax, pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_passB<1>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
-  hipLaunchKernelGGL(pq::k_pg_post<1>, dim3(B), dim3(64), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
+  hipLaunchKernelGGL(pq::k_pg_post<1>, dim3(B), dim3(pq::PPT), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
                      pass_scratch);
   PQ_CHECK_LAUNCH("pq_polish_grouped_round");
   return 0;
