@@ -17,7 +17,10 @@ enum : int {
   R_ACT = 64, R_LAM = 128, R_DA = 192, R_SOL = 256, R_AL = 288,
   // wide mode: R_W = 1 this round, R_NFX fixed variables at R_FIX (indices), R_FIXV (bound
   // values), R_FXL (their multipliers = box duals)
-  R_W = 320, R_NFX = 321, R_FIX = 324, R_FIXV = 332, R_FXL = 340
+  R_W = 320, R_NFX = 321, R_FIX = 324, R_FIXV = 332, R_FXL = 340,
+  // R_GFORM = g + 1: this round's P_FF comes from the group Gram (k_pg_form_grp) in the
+  // pass scratch of the date's polish group g (0: the date forms alone)
+  R_GFORM = 348
 };
 constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
 constexpr int PG_MGMAX = 32;   // general rows
@@ -26,7 +29,7 @@ constexpr int PG_MGMAX = 32;   // general rows
 // variables as bordered rows (at most PG_WMB of them)
 constexpr int PG_WMB = 8;
 constexpr int PG_WG_MAX = 24;   // general rows of the wide mode
-static_assert(R_FXL + PG_WMB <= PQ_PG_RECORD, "PQ_PG_RECORD too small");
+static_assert(R_FXL + PG_WMB <= R_GFORM && R_GFORM < PQ_PG_RECORD, "PQ_PG_RECORD too small");
 
 struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
   double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;

@@ -250,6 +250,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     R[R_NZB] = nzb;
     R[R_W] = 0;
     R[R_REUSE] = reuse;
+    R[R_GFORM] = 0;
     R[R_ROUNDS] += 1.0;
   }
 }
@@ -266,8 +267,90 @@ constexpr int FT = 512;             // threads (8 waves)
 constexpr int FNW = FT / 64;
 constexpr int FTW = 5;              // 16x16 tiles per wave (36 lower tiles for k <= 128)
 
+// group form (k_pg_form_grp): the Gram of a polish group's union rows over the union of its
+// forming dates' free lists, centred by one of their means, in the group's pass scratch
+// (pitch GLD), with the union free list, that mean and the union column sums beside it
+constexpr int GLD = PG_KMAX;
+constexpr int64_t GS_COL = (int64_t)GLD * GLD, GS_MU = GS_COL + GLD, GS_CS = GS_MU + GLD, GS_N = GS_CS + GLD;
+static_assert(GS_N + 1 <= PQ_PG_PASS_SCRATCH, "group form scratch exceeds the pass scratch");
+constexpr int GMO = 32;   // union rows outside a date's window (the per-date correction)
+
+// P_FF of date b from its group's Gram G (centred by mu_g over the union rows U):
+//   sum_{t in W} (x_t - mu)(x_t - mu)' = G_FF - sum_{o in U \ W} x~_o x~_o'
+//                                         - d s' - s d' + T d d'
+// with x~ = x - mu_g, d = mu - mu_g and s = sum_{t in W} x~_t (union column sums minus the
+// outside rows) -- exact for any centring vector mu.  The outside rows (U - T <= GMO) are
+// staged in LDS; one thread per lower entry.
+__device__ __forceinline__ void form_from_group(const pq_lowrank& lr, const pq_problem& pb, const pq_state& st,
+                                                double* R, int b, int k, int ldk, const int32_t* gdates,
+                                                int ngroups, const int32_t* urows_all, const int32_t* ucnt_all,
+                                                const int32_t* uoff, int umax, const double* scr, double* S) {
+  __shared__ int s_cu[GLD], s_pi[PG_KMAX];
+  __shared__ double s_gmu[GLD], s_d[PG_KMAX], s_s[PG_KMAX];
+  const int ld = pb.ld;
+  const int t = threadIdx.x;
+  const int grp = (int)R[R_GFORM] - 1;   // set by k_pg_form_grp
+  const double* Gs = scr + (int64_t)grp * PQ_PG_PASS_SCRATCH;
+  const int nc = (int)Gs[GS_N];
+  const int U = ucnt_all[grp], off = uoff[b], T = lr.tlen[b], mo = U - T;
+  PGWork wk(st, b, ld);
+  const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  for (int c = t; c < nc; c += FT) {
+    s_cu[c] = (int)Gs[GS_COL + c];
+    s_gmu[c] = Gs[GS_MU + c];
+  }
+  __syncthreads();
+  for (int p = t; p < k; p += FT) {   // union position of each free variable (s_cu ascending)
+    const int i = wk.Fl[p];
+    int a = 0, z = nc;
+    while (z - a > 1) {
+      const int mid = (a + z) >> 1;
+      if (s_cu[mid] <= i) a = mid; else z = mid;
+    }
+    s_pi[p] = a;
+    s_d[p] = (mu ? mu[i] : 0.0) - s_gmu[a];
+  }
+  __syncthreads();
+  // outside rows x~_o (F columns) into S, pitch k; s = union column sums - outside rows
+  const int32_t* ur = urows_all + (int64_t)grp * umax;
+  for (int e = t; e < mo * k; e += FT) {
+    const int o = e / k, p = e - o * k;
+    const int u = o < off ? o : o + T;
+    S[e] = lr.panel[(int64_t)ur[u] * lr.ldp + wk.Fl[p]] - s_gmu[s_pi[p]];
+  }
+  __syncthreads();
+  for (int p = t; p < k; p += FT) {
+    double v = Gs[GS_CS + s_pi[p]];
+    for (int o = 0; o < mo; ++o) v -= S[o * k + p];
+    s_s[p] = v;
+  }
+  __syncthreads();
+  double* K = st.K + (int64_t)b * st.K_stride;
+  const double Td = (double)T;
+  for (int e = t; e < k * k; e += FT) {
+    const int p = e / k, q = e - p * k;
+    if (q > p) continue;
+    double v = Gs[(int64_t)s_pi[p] * GLD + s_pi[q]];
+    for (int o = 0; o < mo; ++o) v = fma(-S[o * k + p], S[o * k + q], v);
+    v -= s_d[p] * s_s[q] + s_s[p] * s_d[q];
+    v = fma(Td * s_d[p], s_d[q], v);
+    const double val = psw * v + (p == q ? pd : 0.0);
+    K[(int64_t)p * ldk + q] = val;
+    K[(int64_t)q * ldk + p] = val;
+  }
+  for (int i = t; i < pb.n; i += FT) wk.posF[i] = -1;   // positions of the formed free list
+  __syncthreads();
+  for (int p = t; p < k; p += FT) wk.posF[wk.Fl[p]] = p;
+  if (t == 0) R[R_FORMED] = 1.0;
+}
+
 __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
-                                                int ldk) {
+                                                int ldk, const int32_t* gdates, int ngroups,
+                                                const int32_t* urows_all, const int32_t* ucnt_all,
+                                                const int32_t* uoff, int umax, const double* scr) {
   __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPIT];
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
@@ -290,6 +373,10 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
   if (R[R_NZB] != 0.0)   // rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F  (pass 0 left it in pxb)
     for (int p = t; p < k; p += FT) wk.rF[p] -= ps * wk.pxb[wk.Fl[p]];
+  if (R[R_GFORM] != 0.0) {   // from the group Gram (k_pg_form_grp)
+    form_from_group(lr, pb, st, R, b, k, ldk, gdates, ngroups, urows_all, ucnt_all, uoff, umax, scr, S);
+    return;
+  }
   const int T = lr.tlen[b];
   const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
@@ -372,6 +459,161 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// group form: one workgroup per polish group with dates that form P_FF this round (pending,
+// not reusing K, 0 < |F| <= 128, at most GMO union rows outside the window).  Their free
+// lists are merged in column order; when the union stays within PG_KMAX columns, the Gram of
+// the group's union rows over it (centred by the first forming date's mean) is one MFMA tile
+// product as in k_pg_form -- the union is gathered once for up to 16 dates instead of each
+// window once per date -- and k_pg_form derives each date's P_FF from it (form_from_group).
+// Otherwise the dates keep R_GFORM = 0 and k_pg_form forms them alone.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(FT) void k_pg_form_grp(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                    const int32_t* gdates, const int32_t* urows_all,
+                                                    const int32_t* ucnt_all, int umax, double* scr,
+                                                    int min_dates) {
+  __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPIT];
+  __shared__ int s_col[PG_KMAX], s_on[16], s_wcnt[FNW], s_ncol;
+  __shared__ double s_gm[PG_KMAX];
+  const int grp = xcd_slot(blockIdx.x, gridDim.x);
+  const int d0 = gdates[grp], G = gdates[grp + 1] - d0, U = ucnt_all[grp];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int n = pb.n, ld = pb.ld;
+  if (t < 16) {
+    int on = 0;
+    if (t < G) {
+      const double* R = rec + (int64_t)(d0 + t) * PGR;
+      const int k = (int)R[R_K];
+      on = R[R_STATE] == PQ_PG_PENDING && R[R_W] == 0.0 && R[R_REUSE] == 0.0 && k > 0 && k <= PG_KMAX &&
+           U - lr.tlen[d0 + t] <= GMO;
+    }
+    s_on[t] = on;
+  }
+  if (t == 0) s_ncol = 0;
+  __syncthreads();
+  int first = -1, non = 0;
+  for (int g = G - 1; g >= 0; --g)
+    if (s_on[g]) {
+      first = g;
+      ++non;
+    }
+  if (non < min_dates) return;   // uniform: too few to pay for the union pass, they form alone
+  // ---- union of the forming dates' free lists, in column order (ballot + wave prefix) ----
+  for (int cb = 0; cb < n; cb += FT) {
+    const int i = cb + t;
+    bool f = false;
+    if (i < n)
+      for (int g = 0; g < G; ++g)
+        if (s_on[g]) {
+          PGWork wg(st, d0 + g, ld);
+          f |= wg.fl[i] == 0;
+        }
+    const unsigned long long bal = __ballot(f);
+    if (l == 0) s_wcnt[w] = __popcll(bal);
+    __syncthreads();
+    int pos = s_ncol;
+    for (int ww = 0; ww < w; ++ww) pos += s_wcnt[ww];
+    pos += __popcll(bal & ((1ull << l) - 1ull));
+    if (f && pos < PG_KMAX) s_col[pos] = i;
+    __syncthreads();
+    if (t == 0)
+      for (int ww = 0; ww < FNW; ++ww) s_ncol += s_wcnt[ww];
+    __syncthreads();
+  }
+  const int nc = s_ncol;
+  if (nc > PG_KMAX) return;   // uniform: the dates form alone
+  const double* mug = lr.mu ? lr.mu + (int64_t)(d0 + first) * lr.mu_stride : nullptr;
+  for (int c = t; c < PG_KMAX; c += FT) s_gm[c] = (c < nc && mug) ? mug[s_col[c]] : 0.0;
+  __syncthreads();
+  // ---- Gram of the union rows over the union free list (k_pg_form's tiling) ---------------
+  const int32_t* ur = urows_all + (int64_t)grp * umax;
+  const int nt = (nc + 15) >> 4, ntile = nt * (nt + 1) / 2;
+  const int kp = nt * 16;
+  const int gr = t >> 5, gc = t & 31;
+  int col[4];
+  double mc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int p = gc + 32 * c;
+    col[c] = p < nc ? s_col[p] : -1;
+    mc[c] = p < nc ? s_gm[p] : 0.0;
+  }
+  double v[4];
+  auto gather = [&](int t0) {
+    const int tt = t0 + gr;
+    const double* row = tt < U ? lr.panel + (int64_t)ur[tt] * lr.ldp : nullptr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = (row && col[c] >= 0) ? row[col[c]] - mc[c] : 0.0;
+  };
+  auto put = [&](double* Sb) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (gc + 32 * c < kp) Sb[gr * FPIT + gc + 32 * c] = v[c];
+  };
+  int tI[FTW], tJ[FTW];
+#pragma unroll
+  for (int j = 0; j < FTW; ++j) {
+    const int q = w + FNW * j;
+    int I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= q) ++I;
+    while (I * (I + 1) / 2 > q) --I;
+    tI[j] = I;
+    tJ[j] = q - I * (I + 1) / 2;
+  }
+  f64x4 acc[FTW];
+#pragma unroll
+  for (int j = 0; j < FTW; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+  auto mma = [&](const double* Sb) {
+#pragma unroll
+    for (int kk = 0; kk < FKCH; kk += 4) {
+      const double* r = Sb + (kk + (l >> 4)) * FPIT + (l & 15);
+#pragma unroll
+      for (int j = 0; j < FTW; ++j)
+        if (w + FNW * j < ntile)
+          acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 * tI[j]], r[16 * tJ[j]], acc[j], 0, 0, 0);
+    }
+  };
+  double csum = 0.0;   // thread t < nc: column sum of the centred union rows
+  auto colsum = [&](const double* Sb, int t0) {
+    if (t < nc)
+      for (int rr = 0; rr < FKCH && t0 + rr < U; ++rr) csum += Sb[rr * FPIT + t];
+  };
+  double* S0 = S;
+  double* S1 = S + FKCH * FPIT;
+  gather(0);
+  put(S0);
+  __syncthreads();
+  int buf = 0;
+  for (int t0 = 0; t0 < U; t0 += FKCH) {
+    const bool more = t0 + FKCH < U;
+    if (more) gather(t0 + FKCH);
+    mma(buf ? S1 : S0);
+    colsum(buf ? S1 : S0, t0);
+    if (more) put(buf ? S0 : S1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  double* Gs = scr + (int64_t)grp * PQ_PG_PASS_SCRATCH;
+#pragma unroll
+  for (int j = 0; j < FTW; ++j) {
+    if (w + FNW * j < ntile) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
+        Gs[(int64_t)gi * GLD + gj] = acc[j][r];
+        if (tI[j] != tJ[j]) Gs[(int64_t)gj * GLD + gi] = acc[j][r];
+      }
+    }
+  }
+  for (int c = t; c < nc; c += FT) {
+    Gs[GS_COL + c] = s_col[c];
+    Gs[GS_MU + c] = s_gm[c];
+  }
+  if (t < nc) Gs[GS_CS + t] = csum;
+  if (t == 0) Gs[GS_N] = nc;
+  if (t < G && s_on[t]) rec[(int64_t)(d0 + t) * PGR + R_GFORM] = grp + 1;   // the date's group, + 1
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1262,6 +1504,18 @@ static PgSide* pg_side() {
   return &p;
 }
 
+// the group form for groups with at least this many forming dates (fewer: a single window
+// pass per date is cheaper than the union pass); PQ_PG_GFORM overrides, 0 = off.  Config 3
+// (profiles/r03J_bench_gform*.log): 1 / 2 / 3 / 5 -> polish 4.83 / 4.86 / 4.87 / 4.91 ms
+// (5.03 ms without, r03G_bench_nogform.log) -- within the run-to-run spread of each other
+static int group_form_min() {
+  static const int v = [] {
+    const char* e = getenv("PQ_PG_GFORM");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 // waves per date of the solve, per free-set bucket (48, 64, 80, 96, 128): PQ_PG_SOLVE_NW
 // (1, 2 or 4) overrides all buckets
 static int solve_waves(int bucket) {
@@ -1320,7 +1574,11 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
                      umax, pass_scratch);
   hipLaunchKernelGGL(pq::k_pg_post<0>, dim3(B), dim3(pq::PPT), 0, str, *lr, *pb, *st, rec, *s, gdates, ngroups,
                      pass_scratch);
-  hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk);
+  if (pq::group_form_min() > 0)   // P_FF from one union Gram per polish group (k_pg_form_grp)
+    hipLaunchKernelGGL(pq::k_pg_form_grp, dim3(ngroups), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, gdates, urows,
+                       ucnt, umax, pass_scratch, pq::group_form_min());
+  hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk, gdates, ngroups, urows,
+                     ucnt, uoff, umax, pass_scratch);
   // one workgroup per date, the LDS triangle sized to the free set (more dates per CU when small);
   // the buckets (and the wide rounds) on side streams, joined before the exact-P x passes
   pq::PgSide* side = pq::pg_side();

@@ -4,7 +4,10 @@ it restructures (polish_w.hip, pq_polish_w_batched): same ADMM point in, the sam
 weights, statuses, objective and multipliers out (to rounding), on the shapes the
 backtests use -- long-only min-variance at n = 1000 (bench), capped boxes (fixed weights at
 an upper bound: the P x_B pass), sector caps (active general rows), uncentred least
-squares, and a free set beyond the LDS solve (handed to the per-date kernel)."""
+squares, and a free set beyond the LDS solve (handed to the per-date kernel).  The grouped
+side forms P_FF from one union Gram per polish group where at least three of its dates form
+in a round (k_pg_form_grp), so these cases also pin that derivation against the per-date
+window products."""
 import numpy as np
 import pytest
 import torch
@@ -59,7 +62,7 @@ def _solve(qb, lr, gp, grouped_polish, settings=None, eps_grouped=0.0):
             res.y.cpu().numpy().copy(), res.z_box.cpu().numpy().copy(), res.out.cpu().numpy().copy(), rec)
 
 
-@pytest.mark.parametrize("case", ["bench", "capped", "sectors", "lsq", "small_T"])
+@pytest.mark.parametrize("case", ["bench", "capped", "sectors", "lsq", "uncentred_q0", "small_T"])
 def test_grouped_polish_matches_per_date_polish(device, case):
     if case == "bench":
         qb, lr, gp = _problem(device, 1000, 252, 48, 1.0)
@@ -73,6 +76,10 @@ def test_grouped_polish_matches_per_date_polish(device, case):
     elif case == "lsq":
         qb, lr, gp = _problem(device, 500, 120, 30, 0.1, centred=False)
         settings = engine.Settings(rho0_rel=0.5)
+    elif case == "uncentred_q0":   # uncentred Gram, q = 0 (minimum second moment): sparse free sets
+        qb, lr, gp = _problem(device, 600, 150, 40, 1.0, centred=False)   # inside the LDS solve, no mean
+        qb.q.zero_()
+        settings = None
     else:
         qb, lr, gp = _problem(device, 300, 60, 40, 1.0)
         settings = None
