@@ -83,6 +83,10 @@ typedef struct pq_settings {
   double rho0, rho0_rel, sigma, alpha, eps_abs, eps_rel, rho_min, rho_max, adapt_tol, eq_scale,
       delta, dual_tol;
   int32_t max_iter, adapt_interval, polish, polish_rounds, refine_iters;
+  /* grouped polish (pq_polish_grouped_init), centred windows: a variable also starts fixed at
+   * its lower bound when x - lb < polish_fix_rel * max_j (x_j - lb_j) at the ADMM point
+   * (0: OSQP's rule alone) */
+  double polish_fix_rel;
 } pq_settings;
 
 /* Low-rank description of P for T < n (the backtest path): P_eff = p_scale[b] *

@@ -71,12 +71,23 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
   for (int i = t; i < n; i += PT) sc = fmax(sc, fmax(fabs(q[i]), fabs(psw * dgb[i] + pd)));
   sc = block_max(sc, red);
   sc = fmax(sc, 1e-300);
+  // centred windows (the mean-variance family, sparse long-only optima): a variable far
+  // below the largest distance to its lower bound starts fixed there too (s.polish_fix_rel;
+  // the ADMM point of a loose eps leaves small positive weights).  Tracking windows keep
+  // OSQP's rule: their free sets are large and the wide rounds border few fixed variables
+  double fix_thr = -INFINITY;
+  if (s.polish_fix_rel > 0.0 && has_box && lr.mu) {
+    double dm = 0.0;
+    for (int i = t; i < n; i += PT)
+      if (!isinf(lb[i])) dm = fmax(dm, sx[i] - lb[i]);
+    fix_thr = s.polish_fix_rel * block_max(dm, red);
+  }
   double nfree = 0.0;
   for (int i = t; i < ld; i += PT) {
     int f = 0;
     if (i < n && has_box) {
       const double zi = sz[st.mg_pad + i], yi = sy[st.mg_pad + i];
-      if (!isinf(lb[i]) && zi - lb[i] < -yi) f = 1;
+      if (!isinf(lb[i]) && (zi - lb[i] < -yi || sx[i] - lb[i] < fix_thr)) f = 1;
       else if (!isinf(ub[i]) && ub[i] - zi < yi) f = 2;
       if (lb[i] == ub[i]) f = 1;
     }

@@ -99,6 +99,14 @@ class Settings:
     # sets mostly exceed the LDS solve -- config 2 53.0k at 2e-3, 45.0k at 1e-2 from the loose
     # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
     eps_grouped: float = 3e-2
+    # grouped polish: variables with x - lb < polish_fix_rel * max(x - lb) at the ADMM point
+    # also start fixed at lb (besides OSQP's z - lb < -y): the loose ADMM point leaves small
+    # positive weights that the first rounds would only fix later.  Numpy model of config 3
+    # (tests/engine_model.py, eps 3e-2, 10 dates): 0 / 0.05 / 0.1 / 0.2 -> 3.0 / 2.6 / 2.3 /
+    # 3.3 rounds, first free sets 79 / 71 / 62 / 47 (wrong fixes cost the rounds back); on
+    # the GPU (profiles/r03N_*): 0 / 0.05 / 0.1 -> 363k / 378k / 372k QPs/s, 3.31 / 2.86 / 3.0
+    # rounds on average, at most 5 / 5 / 6.  Centred windows only (k_pg_init)
+    polish_fix_rel: float = 0.05
 
     def to_c(self) -> _lib.PQSettings:
         names = {f[0] for f in _lib.PQSettings._fields_}

@@ -45,13 +45,15 @@ def _problem(device, n, T, D, ub, ngroups_rows=0, cap=0.3, centred=True, stride=
     return qb, lr, gp
 
 
-def _solve(qb, lr, gp, grouped_polish, settings=None, eps_grouped=0.0):
+def _solve(qb, lr, gp, grouped_polish, settings=None, eps_grouped=0.0, polish_fix_rel=0.0):
     """(wide rounds off: this file pins the LDS-solve pipeline against the per-date kernel;
     tests/test_polish_wide_gpu.py covers the wide rounds.  The looser ADMM stop before the
-    pipeline (Settings.eps_grouped) is off unless asked for: both sides start from the same
-    ADMM point.)"""
+    pipeline (Settings.eps_grouped) and the pipeline's extra lower-bound classification
+    (Settings.polish_fix_rel) are off unless asked for: both sides start from the same ADMM
+    point and the same active set.)"""
     import dataclasses
-    settings = dataclasses.replace(settings or engine.Settings(), eps_grouped=eps_grouped)
+    settings = dataclasses.replace(settings or engine.Settings(), eps_grouped=eps_grouped,
+                                   polish_fix_rel=polish_fix_rel)
     ws = engine.Workspace(qb, dense=False)
     assert engine.grouped_applicable(qb, lr, gp, ws)
     res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, grouped_polish=grouped_polish,
@@ -148,3 +150,22 @@ def test_loose_admm_stop_resumes_the_hand_offs(device):
     assert np.all(sa == _lib.PQ_SOLVED) and np.array_equal(sa, sb)
     assert (rec == _lib.PQ_PG_FALLBACK).mean() >= 0.5, np.unique(rec, return_counts=True)
     assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()
+
+
+@pytest.mark.parametrize("case", ["bench", "capped", "sectors", "small_T"])
+def test_fix_rel_classification_same_optimum(device, case):
+    """Settings.polish_fix_rel (the default 0.05): small ADMM weights start fixed at the
+    lower bound -- a different first active set, the same certified optimum (to the proximal
+    refinement's accuracy)."""
+    args = {"bench": (1000, 252, 48, 1.0), "capped": (400, 120, 40, 0.05),
+            "sectors": (600, 150, 36, 0.2), "small_T": (300, 60, 40, 1.0)}[case]
+    kw = dict(ngroups_rows=5, cap=0.25, stride=2) if case == "sectors" else {}
+    qb, lr, gp = _problem(device, *args, **kw)
+    d = engine.Settings()
+    assert d.polish_fix_rel > 0
+    xa, sa, oa, *_ = _solve(qb, lr, gp, True)
+    xb, sb, ob, _, _, outb, rec = _solve(qb, lr, gp, True, polish_fix_rel=d.polish_fix_rel)
+    assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED)
+    assert (rec == _lib.PQ_PG_DONE).mean() >= 0.8, np.unique(rec, return_counts=True)
+    assert np.abs(xa - xb).max() <= 1e-8, np.abs(xa - xb).max()
+    assert np.max(np.abs(ob - oa) / np.maximum(np.abs(oa), 1e-30)) <= 1e-12
