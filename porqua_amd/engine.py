@@ -95,10 +95,11 @@ class Settings:
     # 1e-2 / 2e-2 / 1e-1 -> 311k / 335k / 343k / 353k QPs/s (20 / 16 / 15 / 11 iterations,
     # 2.7 / 3.1 / 3.2 / 3.8 rounds); with the sparse exact-P x pass (r03y_*) 2e-2 / 3e-2 /
     # 5e-2 / 1e-1 -> 347k / 357k / 358k / 360k at 5 / 5 / 6 / 6 rounds at most (of the 8
-    # allowed): 3e-2 keeps the round count of 2e-2.  Tracking (uncentred) windows keep eps_abs: their free
+    # allowed): 3e-2 keeps the round count of 2e-2; with polish_fix_rel = 0.05 (r03Q_grid*):
+    # 3e-2 / 5e-2 -> 374k / 389k at 2.86 / 2.99 rounds, at most 5 / 5.  Tracking (uncentred) windows keep eps_abs: their free
     # sets mostly exceed the LDS solve -- config 2 53.0k at 2e-3, 45.0k at 1e-2 from the loose
     # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
-    eps_grouped: float = 3e-2
+    eps_grouped: float = 5e-2
     # grouped polish: variables with x - lb < polish_fix_rel * max(x - lb) at the ADMM point
     # also start fixed at lb (besides OSQP's z - lb < -y): the loose ADMM point leaves small
     # positive weights that the first rounds would only fix later.  Numpy model of config 3
