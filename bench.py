@@ -14,10 +14,13 @@ its own contiguous block of 4749 dates of a longer panel (weak scaling); the onl
 collective is the all-gather of the weight panels.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with a `roofline` object
-for the dominant kernel (K3 ADMM, HBM-bound: algorithmic bytes = 8 n(n+1)/2 per iteration
-for the lower-triangle K^-1 stream, timed with HIP events on the launch stream) and a `cpu_baseline` object
-(the reference per-date path restated in numpy, oracle/cpu_baseline.py, on a bounded
-sample of dates).
+for the dominant kernel (K3 ADMM, `k_admm_gcap` on the group-capacitance window path; HBM
+roofline; algorithmic bytes per date-iteration = (2 x 8 U n union-row passes + 8 k(k+1)/2
+for the group's M_U^-1) / dates per group + 12 x 8 n of per-date ADMM state, timed with HIP
+events on the launch stream), the measured HBM fraction from the committed
+rocprofv3 PMC summary of the same code (``frac_hbm_measured``: PMC bytes per date-iteration
+x date-iterations / kernel time / peak), and a `cpu_baseline` object (the reference
+per-date path restated in numpy, oracle/cpu_baseline.py, on a bounded sample of dates).
 """
 from __future__ import annotations
 
@@ -34,10 +37,61 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from porqua_amd import engine  # noqa: E402
-from porqua_amd.workloads import MinVarianceBacktest, TrackingBacktest  # noqa: E402
+from porqua_amd.workloads import (MinVarianceBacktest, ReplicationBacktest, SweepBacktest,  # noqa: E402
+                                  TrackingBacktest)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 matrix spec
+
+
+WORKLOAD_TEXT = {
+    "config2": "config2: SPTR index replication, LS tracking (P=2 X'X, q=-2 X'y), budget + box [0,1], n=494 "
+               "usa-shaped panel on the real SPTR calendar, every daily rebalance date (4544)",
+    "config3": "config3: long-only min-variance (P=2*Pearson cov, budget + box [0,1]), daily rebalance",
+    "config4": "config4: tracking-error LS (P=2 X'X, q=-2 X'y), budget + box [0,1] + 20 sector caps <= 0.15, "
+               "daily rebalance",
+    "config5": "config5: mean-variance sweep (P=2 lam Sigma, q=-mu geometric), budget + box [0,1], n=5000, "
+               "64 monthly dates x 64 risk aversions log-spaced in [0.1, 100]",
+}
+
+
+def dropin_config2(wl, T):
+    """Config 2 through the reference API (rank 0, N = 1, outside the timed region):
+    Backtest.run(bs) with LeastSquares(solver_name='mi355x') on the same panel and dates, from
+    the host DataFrames to the Portfolio objects (upload, staging, download included)."""
+    import pandas as pd
+    from porqua_amd.backtest import Backtest, BacktestService
+    from porqua_amd.builders import (OptimizationItemBuilder, SelectionItemBuilder, bibfn_bm_series,
+                                     bibfn_box_constraints, bibfn_budget_constraint, bibfn_return_series,
+                                     bibfn_selection_data)
+    from porqua_amd.optimization import LeastSquares
+    idx = pd.DatetimeIndex(wl.dates_rank)
+    X = pd.DataFrame(wl.R_rank, index=idx, columns=[f"u{i:03d}" for i in range(wl.n)])
+    y = pd.DataFrame({"SPTR": wl.y_rank}, index=idx)
+    reb = [str(d.date()) for d in idx[wl.ends_local]]
+
+    def run():
+        svc = BacktestService(
+            data={"return_series": X, "bm_series": y},
+            selection_item_builders={"data": SelectionItemBuilder(bibfn=bibfn_selection_data)},
+            optimization_item_builders={
+                "return_series": OptimizationItemBuilder(bibfn=bibfn_return_series, width=T),
+                "bm_series": OptimizationItemBuilder(bibfn=bibfn_bm_series, width=T, align=True),
+                "budget_constraint": OptimizationItemBuilder(bibfn=bibfn_budget_constraint, budget=1),
+                "box_constraints": OptimizationItemBuilder(bibfn=bibfn_box_constraints, box_type="LongOnly")},
+            optimization=LeastSquares(solver_name="mi355x"), rebdates=reb, quiet=True)
+        bt = Backtest()
+        bt.run(svc)
+        torch.cuda.synchronize()
+        return bt
+    run()
+    t = time.perf_counter()
+    bt = run()
+    t = time.perf_counter() - t
+    return {"api": "porqua_amd.backtest.Backtest.run(bs), LeastSquares(solver_name='mi355x')",
+            "qps": len(reb) / t, "s": t, "dates": len(reb), "solved": bt.stats["solved"], "path": bt.stats["path"],
+            "note": "host DataFrames in, Portfolio objects out: panel upload, window staging, device solve and "
+                    "weight download included"}
 
 
 def parse():
@@ -47,13 +101,18 @@ def parse():
                          "them itself, one child process per GPU, before anything touches the GPU")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["config3", "config4"], default="config3",
-                    help="config3: n=1000 long-only min-variance (the metric's configuration); config4: "
-                         "n=3000 tracking LS with 20 sector caps (BASELINE configs[3], 'dates sharded')")
-    ap.add_argument("--n", type=int, default=None, help="assets (config3: 1000, config4: 3000)")
+    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5"], default="config3",
+                    help="config3: n=1000 long-only min-variance (the metric's configuration); config2: SPTR "
+                         "replication, n=494 LS tracking on the usa-shaped panel, all 4544 daily dates (BASELINE "
+                         "configs[1]; strong scaling: the fixed date set split over the ranks); config4: n=3000 "
+                         "tracking LS with 20 sector caps (configs[3], 'dates sharded'); config5: n=5000 "
+                         "mean-variance, 64 dates x 64 risk aversions (configs[4]; strong scaling, sharded by "
+                         "date with every lambda of a date on one rank)")
+    ap.add_argument("--n", type=int, default=None, help="assets (config3: 1000, config4: 3000, config5: 5000)")
     ap.add_argument("--window", type=int, default=252)
     ap.add_argument("--dates", type=int, default=None,
-                    help="rebalance dates per rank (--strong: in total); config3: 4749, config4: 9749")
+                    help="rebalance dates per rank (--strong: in total); config3: 4749, config4: 9749; "
+                         "config5: 64 dates in total")
     ap.add_argument("--path", choices=["auto", "dense", "lowrank"], default="auto",
                     help="dense K^-1 (K2 n^3 + K3 n^2 stream) or Woodbury low-rank (T + mg < n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -72,6 +131,50 @@ def parse():
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="override an engine.Settings field (experiments)")
     return ap.parse_args()
+
+
+def profile_order(tag: str):
+    """Sort key of a profile tag ``rNNx``: round NN, then the run letter in the order the
+    rounds used them (a..z first, then A..Z)."""
+    import re
+    m = re.match(r"r(\d+)([a-zA-Z]*)", tag)
+    if not m:
+        return (-1, 0, "")
+    rnd, let = int(m.group(1)), m.group(2)
+    return (rnd, 1 if let[:1].isupper() else 0, let)
+
+
+def select_pmc_summary(kern: str, it_bytes: float, iters_per_step: int, root: str = ROOT):
+    """The PMC summary (tools/pmc_summary.py output under profiles/) that describes this
+    run's code: the one ``profiles/EVIDENCE.json`` names if it matches, otherwise the newest
+    by profile order, among those whose kernel ``kern`` has the same algorithmic bytes per
+    date-iteration AND the same date-iterations per step.  Returns (path, summary) or None."""
+    import glob
+
+    def matches(pm):
+        k = pm.get("kernels", {}).get(kern)
+        return (k is not None and "hbm_bytes_per_admm_iteration" in k
+                and int(round(k["algorithmic_bytes_per_admm_iteration"])) == int(it_bytes)
+                and int(pm.get("admm_iterations_per_step", -1)) == int(iters_per_step))
+
+    pdir = os.path.join(root, "profiles")
+    cands = []
+    man = os.path.join(pdir, "EVIDENCE.json")
+    if os.path.exists(man):
+        try:
+            cands.append(os.path.join(pdir, json.load(open(man))["pmc_summary"]))
+        except (OSError, ValueError, KeyError):
+            pass
+    cands += sorted(glob.glob(os.path.join(pdir, "*_pmc_summary.json")),
+                    key=lambda f: profile_order(os.path.basename(f)), reverse=True)
+    for f in cands:
+        try:
+            pm = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if matches(pm):
+            return f, pm
+    return None
 
 
 def launch_plan(gpus: int, env: dict):
@@ -124,11 +227,14 @@ def main():
     plan = launch_plan(args.gpus, os.environ)
     if plan is not None:
         sys.exit(run_ranks(plan, sys.argv[1:]))
-    cfg4 = args.workload == "config4"
+    wname = args.workload
+    cfg4 = wname == "config4"
+    if wname in ("config2", "config5"):
+        args.strong = True                 # a fixed problem set split over the ranks
     if args.n is None:
-        args.n = 3000 if cfg4 else 1000
+        args.n = {"config2": 494, "config4": 3000, "config5": 5000}.get(wname, 1000)
     if args.dates is None:
-        args.dates = 9749 if cfg4 else 4749
+        args.dates = {"config4": 9749, "config5": 64}.get(wname, 4749)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -137,7 +243,7 @@ def main():
     # CPU baseline first, in a child process, before this process touches the GPU (its
     # process pool forks; bench.py itself never forks after HIP initialisation)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not cfg4:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wname == "config3":
         import subprocess
         cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--n", str(args.n), "--window", str(args.window),
                "--dates", str(args.dates), "--budget", str(args.cpu_budget)]
@@ -155,11 +261,20 @@ def main():
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     n, T = args.n, args.window
+    ov = dict(kv.split("=", 1) for kv in args.set)
     if cfg4:
-        settings = engine.Settings.from_params(dict({"rho0_rel": 0.1, "rho0_qrel": 0.0},
-                                                    **dict(kv.split("=", 1) for kv in args.set)))
+        settings = engine.Settings.from_params(dict({"rho0_rel": 0.1, "rho0_qrel": 0.0}, **ov))
         wl = TrackingBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
                               strong=args.strong)
+    elif wname == "config2":
+        g = np.load(os.path.join(ROOT, "tests", "golden", "sptr.npz"), allow_pickle=False)
+        settings = engine.Settings.from_params(dict({"rho0_rel": 0.2, "rho0_qrel": 0.0}, **ov))
+        wl = ReplicationBacktest(g["days"], g["returns"], T=T, rank=rank, world=world, device=dev,
+                                 settings=settings, n=n)
+    elif wname == "config5":
+        from porqua_amd.sweep import SWEEP_RHO0_QREL
+        settings = engine.Settings.from_params(dict({"rho0_qrel": SWEEP_RHO0_QREL}, **ov))
+        wl = SweepBacktest(n=n, T=T, dates=args.dates, rank=rank, world=world, device=dev, settings=settings)
     else:
         settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))
         wl = MinVarianceBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
@@ -318,22 +433,21 @@ def main():
     # two exact P x window passes (2 x 2 T n)
     polish_flops = float(((prounds * (nfree ** 2 * T + nfree ** 3 / 3.0)).sum() + 4.0 * T * n * D) * args.steps)
 
-    traffic, traffic_src = None, None
-    mfma_busy, mfma_src = None, None
-    import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
-        try:
-            pm = json.load(open(f))
-            k = pm["kernels"][kern]
-            if int(round(k["algorithmic_bytes_per_admm_iteration"])) == int(it_bytes):
-                traffic, traffic_src = k["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
-                if "mfma_busy_fraction" in pm:
-                    mfma_busy = {kk: pm["mfma_busy_fraction"][kk] for kk in
-                                 ("k_band_gram", "k_factor", "k_admm_grp", "k_admm_gcap", "k_polish_w", "k_pg_form",
-                                  "k_pg_solve", "k_pg_pass") if kk in pm["mfma_busy_fraction"]}
-                    mfma_src = os.path.relpath(f, ROOT)
-        except Exception:
-            pass
+    traffic, traffic_src, mfma_busy, mfma_src = None, None, None, None
+    pm_sel = select_pmc_summary(kern, it_bytes, total_iters // args.steps)
+    if pm_sel is not None:
+        f, pm = pm_sel
+        traffic, traffic_src = pm["kernels"][kern]["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
+        if "mfma_busy_fraction" in pm:
+            mfma_busy = {kk: pm["mfma_busy_fraction"][kk] for kk in
+                         ("k_band_gram", "k_factor", "k_gcap_prep", "k_admm_grp", "k_admm_gcap", "k_polish_w",
+                          "k_pg_form", "k_pg_form_grp", "k_pg_solve", "k_pg_passA", "k_pg_passB")
+                         if kk in pm["mfma_busy_fraction"]}
+            mfma_src = traffic_src
+    # measured HBM fraction: the PMC bytes of the same kernel (same code: algorithmic bytes and
+    # date-iterations per step both match) over this run's HIP-event time of the stage
+    frac_hbm_measured = (traffic * (total_iters // args.steps) / (tk["admm"] / args.steps) / 1e9 / HBM_PEAK_GBS
+                         if traffic is not None else None)
 
     qps = D_all * args.steps / dt
     out = {
@@ -348,12 +462,13 @@ def main():
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (factor-model panel, seed 20240314; usa_returns absent)",
-        "config": {"workload": ("config4: tracking-error LS (P=2 X'X, q=-2 X'y), budget + box [0,1] + 20 sector "
-                                "caps <= 0.15, daily rebalance" if cfg4 else
-                                "config3: long-only min-variance (P=2*Pearson cov, budget + box [0,1]), "
-                                "daily rebalance"), "n_assets": n, "window": T,
-                   "dates_per_gpu": D, "global_batch": D_all, "parallelism": f"dates-sharded x{world}"},
+        "data": ("synthetic usa-shaped panel (494 assets loading on the real SPTR returns, seed 20240101; "
+                 "usa_returns absent) on the real SPTR calendar" if wname == "config2" else
+                 "synthetic (factor-model panel, seed 20240314; usa_returns absent)"),
+        "config": {"workload": WORKLOAD_TEXT[wname], "n_assets": n, "window": T,
+                   "dates_per_gpu": D, "global_batch": D_all,
+                   "parallelism": (f"dates-sharded x{world} (every lambda of a date on its rank)"
+                                   if wname == "config5" else f"dates-sharded x{world}")},
         "roofline": {"bound": "hbm", "kernel": kern + (" (K3, grouped low-rank)" if grouped else " (K3)"),
                      "achieved": admm_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": admm_gbs / HBM_PEAK_GBS,
@@ -361,6 +476,11 @@ def main():
                      "traffic_unit": "HBM bytes per date-iteration (PMC: 2*FETCH_SIZE + WRITE_SIZE, "
                                      "gfx950 correction; committed rocprofv3 pass)",
                      "traffic_source": traffic_src,
+                     "frac_hbm_measured": frac_hbm_measured,
+                     "frac_hbm_measured_note": "traffic x date-iterations per step / this run's kernel time / "
+                                               "peak: the HBM bytes the kernel really moves (frac counts the "
+                                               "algorithmic bytes, most union rows of which are served by "
+                                               "L2 / MALL)",
                      "algorithmic_bytes_per_iteration": int(it_bytes),
                      "algorithmic_bytes_note": ("per date-iteration: (union rows 2 x 8Un + lower-triangle M_U^-1 "
                                                 "8k(k+1)/2, k = U + mg) / dates per group + ADMM state 12 x 8n"
@@ -406,7 +526,9 @@ def main():
                                                    "from the panel rows (torch), not by the engine")},
         "cpu_baseline": None,
     }
-    if cfg4:   # the next-row and drop-in legs below are config-3 (n = 1000 min-variance) lines
+    if wname == "config2" and world == 1 and not args.no_dropin:
+        out["end_to_end"] = dropin_config2(wl, T)
+    if wname != "config3":   # the next-row and drop-in legs below are config-3 (n = 1000 min-variance) lines
         if rank == 0:
             print(json.dumps(out), flush=True)
         if dist:

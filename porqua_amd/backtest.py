@@ -279,24 +279,54 @@ class Backtest:
             self._after_solve(bs, rebalancing_date)
 
     def _run_batched(self, bs) -> bool:
+        """Two-phase batched run: host staging once (phase A), this rank's contiguous block
+        of dates solved on the device (phase B, ``_solve_shard``), the blocks all-gathered
+        when torch.distributed is initialised (one collective), then the Portfolio objects
+        (phase C).  False: not batchable (the caller runs the serial loop)."""
         import torch
+        st = self._stage_batched(bs)
+        if st is None:
+            return False
+        world, rank, dist = 1, 0, None
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            dist = torch.distributed
+            world, rank = dist.get_world_size(), dist.get_rank()
+        nreb = len(st["rebdates"])
+        lo, hi = shard_range(nreb, rank, world)
+        ok, W, ST, OBJ, path = self._solve_shard(bs, st, lo, hi)
+        # batchability of a chunk depends on its own windows (window lengths, WLS runs): a
+        # rank that cannot batch must not return while the others block in the all-gather,
+        # so every rank finishes its shard and the verdict is agreed collectively
+        if dist is not None:
+            ok = agree_all(ok, dist)
+        if not ok:
+            return False                      # some rank cannot batch: serial path everywhere
+        if dist is not None:
+            W, ST, OBJ = gather_shards(W, ST, OBJ, nreb, world, dist, None)
+        self._finish_batched(bs, st, W, ST, OBJ, path)
+        return True
+
+    def _stage_batched(self, bs):
+        """Phase A (host, once): selection and constraints of the first date (date-invariant
+        builders), window row lists of every rebalance date, benchmark alignment, G/h/A/b and
+        the box.  Returns the staging dict, or None when the run cannot batch."""
         from . import engine
         rebdates = list(bs.settings["rebdates"])
         if not rebdates:
-            return True
+            return None
         opt = bs.optimization
         # ---- phase A: static selection / constraints, window row lists ------------------
         bs.prepare_rebalancing(rebalancing_date=rebdates[0])
         cons = opt.constraints
         universe = bs.selection.selected
-        from .l1split import merge_batch, split_batch, split_settings, term_from_model
+        from .l1split import term_from_model
         l1term = term_from_model(cons, opt.params, universe)   # src/optimization.py:125-142
         l1both = None
         if l1term == "unsupported":           # turnover and leverage together: device IPM
             from .ipm_l1 import terms_from_model
             l1both = terms_from_model(cons, opt.params, universe)
             if l1both is None:
-                return False
+                return None
             l1term = None
         X = bs.data.get("return_series")
         if X is None:
@@ -306,7 +336,7 @@ class Backtest:
             if bld.arguments.get("bibfn") is _b.bibfn_return_series:
                 width = bld.arguments.get("width")
         if width is None:
-            return False
+            return None
         # the whole frame when the selection is every column in order (no 8 T n-byte copy)
         Xs = X if list(X.columns) == list(universe) else X[universe]
         idx = pd.DatetimeIndex(Xs.index)
@@ -325,23 +355,27 @@ class Backtest:
         boxed = cons.box["box_type"] != "NA"
         lb = cons.box["lower"].to_numpy(dtype=np.float64) if boxed else None
         ub = cons.box["upper"].to_numpy(dtype=np.float64) if boxed else None
+        return {"rebdates": rebdates, "universe": universe, "Xs": Xs, "bm": bm, "rows": rows, "tlen": tlen,
+                "GhAb": GhAb, "lb": lb, "ub": ub, "l1term": l1term, "l1both": l1both}
 
-        # ---- phase B: device ---------------------------------------------------------------
+    def _solve_shard(self, bs, st, lo: int, hi: int):
+        """Phase B (device): dates [lo, hi) of the staged run, chunked to bound HBM use.
+        Returns (ok, W [hi - lo, n], status, objective, path)."""
+        import torch
+        from . import engine
+        from .l1split import merge_batch, split_batch, split_settings
+        opt = bs.optimization
+        rows, tlen, GhAb, lb, ub = st["rows"], st["tlen"], st["GhAb"], st["lb"], st["ub"]
+        l1term, l1both = st["l1term"], st["l1both"]
         dev = engine.default_device()
-        world, rank = 1, 0
-        dist = None
-        if torch.distributed.is_available() and torch.distributed.is_initialized():
-            dist = torch.distributed
-            world, rank = dist.get_world_size(), dist.get_rank()
-        lo, hi = shard_range(len(rebdates), rank, world)
         settings = engine.Settings.from_params(opt.params)
-        panel = engine.Panel(Xs.to_numpy(dtype=np.float64), bm, device=dev)
+        panel = engine.Panel(st["Xs"].to_numpy(dtype=np.float64), st["bm"], device=dev)
         n = panel.n
         # windows with missing values (checked on the device copy): the objectives that
         # support them batch with the pairwise-complete covariance (MeanVariance); the others
         # keep the serial path
         if panel.has_nan and not getattr(opt, "batch_handles_nan", False):
-            return False
+            return False, None, None, None, None
         chunk = int(bs.settings.get("batch_chunk", 0) or _auto_chunk(n))
         W = np.zeros((hi - lo, n))
         ST = np.zeros(hi - lo, dtype=np.int32)
@@ -350,13 +384,13 @@ class Backtest:
         split_panel = None
         if l1term is not None:
             if lb is None or ub is None:
-                return False                  # the split needs a box (serial path raises)
+                return False, None, None, None, None   # the split needs a box (serial path raises)
             split_panel = engine.Panel(torch.cat([panel.R, -panel.R], 1).contiguous(), None, device=dev)
             mg += 1 if l1term.kind == "budget" else 0
         lad = hasattr(opt, "lad_batch")       # LAD: the LP on the device IPM (porqua_amd/lad.py)
         if lad:
             if l1term is not None or l1both is not None:
-                return False
+                return False, None, None, None, None
             tm = int(tlen.max())
             if tm < n:    # m-space normal equations: (mc + T) x n rows + k_ld^2 factor buffers
                 k_ld = (tm + mg + 63) // 64 * 64
@@ -365,9 +399,6 @@ class Backtest:
                 per = 8 * (n + 64) ** 2 + 64 * n * tm
             chunk = min(chunk, max(1, (1 << 35) // per))
         path = "lp-ipm" if lad else "dense"
-        # batchability of a chunk depends on its own windows (window lengths, WLS runs): a
-        # rank that cannot batch must not return while the others block in the all-gather,
-        # so every rank finishes its loop and the verdict is agreed collectively below
         ok = True
         for s in range(lo, hi, chunk):
             e = min(hi, s + chunk)
@@ -426,12 +457,13 @@ class Backtest:
                 W[s - lo:e - lo] = res.x[:, :n].cpu().numpy()
                 OBJ[s - lo:e - lo] = res.obj.cpu().numpy()
             ST[s - lo:e - lo] = res.status.cpu().numpy()
-        if dist is not None:
-            ok = agree_all(ok, dist, dev)
-        if not ok:
-            return False                      # some rank cannot batch: serial path everywhere
-        if dist is not None:
-            W, ST, OBJ = gather_shards(W, ST, OBJ, len(rebdates), world, dist, dev)
+        return ok, W, ST, OBJ, path
+
+    def _finish_batched(self, bs, st, W, ST, OBJ, path) -> None:
+        """Phase C (host): Portfolio objects in date order, ``append_fun`` per date."""
+        opt = bs.optimization
+        rebdates, universe = st["rebdates"], st["universe"]
+        n = W.shape[1]
         # ---- phase C: portfolios -----------------------------------------------------------
         from . import _lib
         solved = (ST == _lib.PQ_SOLVED) | (ST == _lib.PQ_SOLVED_INACCURATE)
@@ -465,7 +497,6 @@ class Backtest:
             last = len(rebdates) - 1
             w = W[last].tolist() if solved[last] else none
             opt.results = {"weights": dict(zip(keys, w)), "status": bool(solved[last])}
-        return True
 
     def save(self, filename: str, path: Optional[str] = None) -> None:
         try:
@@ -484,29 +515,38 @@ def _auto_chunk(n: int) -> int:
     return max(1, int((96 << 30) // per))
 
 
-def agree_all(ok: bool, dist, device) -> bool:
+def agree_all(ok: bool, dist, device=None) -> bool:
     """True iff ``ok`` holds on every rank (one MIN all-reduce)."""
     import torch
-    dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    dev = comm_device(dist, device)
     t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
 
 
-def gather_shards(W, ST, OBJ, total, world, dist, device):
-    """All-gather every rank's contiguous block (RCCL over xGMI on GPUs, gloo on CPU)."""
+def comm_device(dist, device=None):
+    """Device of the collective buffers: the rank's GPU under RCCL ('nccl'), the host under gloo."""
+    import torch
+    if dist.get_backend() == "nccl":
+        return device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def gather_blocks(block, total: int, world: int, dist, device=None) -> np.ndarray:
+    """All-gather every rank's contiguous block of ``total`` rows (rank r holds rows
+    shard_range(total, r, world); ``block`` is its (rows, m) numpy array or FP64 tensor) with
+    one collective: RCCL ``all_gather_into_tensor`` over xGMI, gloo ``all_gather`` on CPU.
+    Returns the whole (total, m) panel as numpy on every rank."""
     import torch
     per = -(-total // world)
-    n = W.shape[1]
-    be = dist.get_backend()
-    dev = device if be == "nccl" else torch.device("cpu")
-    buf = torch.zeros((per, n + 2), dtype=torch.float64, device=dev)
-    k = W.shape[0]
-    buf[:k, :n] = torch.from_numpy(W).to(dev)
-    buf[:k, n] = torch.from_numpy(ST.astype(np.float64)).to(dev)
-    buf[:k, n + 1] = torch.from_numpy(OBJ).to(dev)
-    if be == "nccl":
-        out = torch.zeros((world * per, n + 2), dtype=torch.float64, device=dev)
+    dev = comm_device(dist, device if device is not None else
+                      (block.device if isinstance(block, torch.Tensor) and block.is_cuda else None))
+    blk = block if isinstance(block, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(block))
+    k, m = int(blk.shape[0]), int(blk.shape[1])
+    buf = torch.zeros((per, m), dtype=torch.float64, device=dev)
+    buf[:k] = blk.to(dev, torch.float64)
+    if dist.get_backend() == "nccl":
+        out = torch.zeros((world * per, m), dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(out, buf)
     else:
         parts_t = [torch.zeros_like(buf) for _ in range(world)]
@@ -517,7 +557,15 @@ def gather_shards(W, ST, OBJ, total, world, dist, device):
     for r in range(world):
         s, e = shard_range(total, r, world)
         parts.append(out[r * per:r * per + (e - s)])
-    full = np.concatenate(parts)
+    return np.concatenate(parts)
+
+
+def gather_shards(W, ST, OBJ, total, world, dist, device):
+    """All-gather every rank's contiguous block of weights, status and objective (RCCL over
+    xGMI on GPUs, gloo on CPU)."""
+    n = W.shape[1]
+    blk = np.concatenate([W, ST.astype(np.float64)[:, None], np.asarray(OBJ, dtype=np.float64)[:, None]], 1)
+    full = gather_blocks(blk, total, world, dist, device if dist.get_backend() == "nccl" else None)
     return full[:, :n], full[:, n].astype(np.int32), full[:, n + 1]
 
 

@@ -116,48 +116,28 @@ class MinVarianceBacktest:
                                   b=1.0, lb=lb, ub=ub, chunk=chunk)
 
 
-class TrackingBacktest:
-    """Config 4 on one device (BASELINE.json configs[3]): a synthetic factor panel with 20
-    sectors, n = 3000 assets, 252-day windows, daily rebalancing, tracking-error least
-    squares P = 2 X'X (uncentred), q = -2 X'y (LeastSquares.set_objective,
-    src/optimization.py:206-226) with budget 1'x = 1, long-only box [0, 1] and 20 sector
-    caps G x <= 0.15 (Constraints.add_linear / to_GhAb, src/constraints.py:66-94, 114-167):
-    21 shared general rows.  ``strong``: ``D`` dates in total, contiguous block per rank;
-    otherwise ``D`` dates per rank of one longer panel.  q is formed inside ``step`` (the
-    X'y window products are part of the per-date objective)."""
+class _LSTrackingBatch:
+    """Least-squares tracking backtest on one device (LeastSquares.set_objective,
+    src/optimization.py:206-226): P = 2 X'X (uncentred window Gram), q = -2 X'y, budget
+    1'x = 1, long-only box [0, 1] and optional shared general rows G x <= h
+    (Constraints.add_linear / to_GhAb, src/constraints.py:66-94, 114-167).  The panel slice
+    ``R`` / ``y`` / ``dates`` holds exactly the rows this rank's windows touch; its ``D``
+    rebalance dates are the slice's rows T - 1 .. T - 2 + D.  q is formed inside ``step``
+    (the X'y window products are part of the per-date objective)."""
 
-    N_SECTORS = 20
-    CAP = 0.15
-
-    def __init__(self, n: int = 3000, T: int = 252, D: int = 9749, rank: int = 0, world: int = 1,
-                 device=None, settings: engine.Settings | None = None, strong: bool = False):
-        self.n, self.T = n, T
+    def _setup(self, dates, R, y, T, D, device, settings, G=None, h=None):
+        self.T = T
         self.device = dev = device or engine.default_device()
-        if strong:
-            per = -(-D // world)
-            lo = rank * per
-            self.D = max(0, min(D, lo + per) - lo)
-            d_total = T - 1 + D
-        else:
-            lo = rank * D
-            self.D = D
-            d_total = T - 1 + D * world
-        self.global_dates = D if strong else D * world
-        D = self.D
-        dates, R, y, sec = factor_panel(d_total, n, n_sectors=self.N_SECTORS)
-        self.R_rank = R[lo:lo + T - 1 + D]
-        self.y_rank = y[lo:lo + T - 1 + D]
+        self.D = D
+        self.n = n = R.shape[1]
+        self.R_rank, self.y_rank, self.dates_rank = R, y, dates
         self.ends_local = np.arange(T - 1, T - 1 + D)
-        self.row_offset = lo
-        sl_dates = dates[lo:lo + T - 1 + D]
-        self.dates_rank = sl_dates
-        self.rows, self.tlen = engine.window_rows(sl_dates, sl_dates[self.ends_local], T)
-        self.pan = engine.Panel(self.R_rank, self.y_rank, device=dev)
+        self.rows, self.tlen = engine.window_rows(dates, dates[self.ends_local], T)
+        self.pan = engine.Panel(R, y, device=dev)
         self.rows_d, self.tlen_d = self.pan.rows_to_device(self.rows, self.tlen)
-        self.G = np.stack([(sec == g).astype(float) for g in range(self.N_SECTORS)])
-        qb = engine.QPBatch.from_dense(None, None, A=np.ones((1, n)), b=np.ones(1), G=self.G,
-                                       h=np.full(self.N_SECTORS, self.CAP), lb=np.zeros(n), ub=np.ones(n),
-                                       device=dev, n=n)
+        self.G = G
+        qb = engine.QPBatch.from_dense(None, None, A=np.ones((1, n)), b=np.ones(1), G=G, h=h, lb=np.zeros(n),
+                                       ub=np.ones(n), device=dev, n=n)
         qb.batch = D
         qb.q = torch.zeros((D, qb.ld), dtype=F64, device=dev)
         qb.p_scale = torch.full((D,), 2.0, dtype=F64, device=dev)
@@ -167,8 +147,7 @@ class TrackingBacktest:
         self.gplan = engine.GroupPlan(self.rows, self.tlen, dev, polish_full=True)
         self.lr = engine.LowRank(self.pan, self.rows_d, self.tlen_d, mu=None)
         self.use_lr, self.with_cov = True, False
-        # tracking objectives start at a small rho (engine.Settings docs; tools/bench_configs.py)
-        self.settings = settings or engine.Settings(rho0_rel=0.1, rho0_qrel=0.0)
+        self.settings = settings
         self.ws = engine.Workspace(qb, dense=False)
 
     @property
@@ -194,6 +173,110 @@ class TrackingBacktest:
                                   lb=torch.zeros(n, dtype=F64, device=self.device),
                                   ub=torch.ones(n, dtype=F64, device=self.device), chunk=chunk,
                                   C=qb.Cg[0, :qb.mg, :n], lg=qb.lg[0, :qb.mg], ug=qb.ug[0, :qb.mg])
+
+
+class TrackingBacktest(_LSTrackingBatch):
+    """Config 4 on one device (BASELINE.json configs[3]): a synthetic factor panel with 20
+    sectors, n = 3000 assets, 252-day windows, daily rebalancing, tracking-error least
+    squares with budget, long-only box and 20 sector caps G x <= 0.15: 21 shared general
+    rows.  ``strong``: ``D`` dates in total, contiguous block per rank; otherwise ``D`` dates
+    per rank of one longer panel."""
+
+    N_SECTORS = 20
+    CAP = 0.15
+
+    def __init__(self, n: int = 3000, T: int = 252, D: int = 9749, rank: int = 0, world: int = 1,
+                 device=None, settings: engine.Settings | None = None, strong: bool = False):
+        if strong:
+            per = -(-D // world)
+            lo = rank * per
+            Dr = max(0, min(D, lo + per) - lo)
+            d_total = T - 1 + D
+        else:
+            lo = rank * D
+            Dr = D
+            d_total = T - 1 + D * world
+        self.global_dates = D if strong else D * world
+        dates, R, y, sec = factor_panel(d_total, n, n_sectors=self.N_SECTORS)
+        self.row_offset = lo
+        G = np.stack([(sec == g).astype(float) for g in range(self.N_SECTORS)])
+        # tracking objectives start at a small rho (engine.Settings docs; tools/bench_configs.py)
+        self._setup(dates[lo:lo + T - 1 + Dr], R[lo:lo + T - 1 + Dr], y[lo:lo + T - 1 + Dr], T, Dr, device,
+                    settings or engine.Settings(rho0_rel=0.1, rho0_qrel=0.0), G=G,
+                    h=np.full(self.N_SECTORS, self.CAP))
+
+
+class ReplicationBacktest(_LSTrackingBatch):
+    """Config 2 on one device (BASELINE.json configs[1]): the reference notebook's SPTR index
+    replication (example/backtest.ipynb: LeastSquares, budget + LongOnly box, width 252) on
+    the usa-shaped panel (synthetic.usa_panel: 494 assets on the last 4795 real SPTR dates;
+    usa_returns itself is absent from the reference tree), rebalanced on EVERY date from the
+    first full window on: 4795 - 251 = 4544 daily QPs.  ``sptr_days`` / ``sptr``: the real
+    SPTR series (tests/golden/sptr.npz, captured from the reference's data/SPTR.csv).
+
+    Multi-GPU: the fixed set of dates is split into contiguous blocks (strong scaling,
+    backtest.shard_range); each rank uploads only the panel rows its windows touch."""
+
+    def __init__(self, sptr_days, sptr, T: int = 252, rank: int = 0, world: int = 1, device=None,
+                 settings: engine.Settings | None = None, n: int = 494, n_rows: int = 4795):
+        from .backtest import shard_range
+        from .synthetic import usa_panel
+        days, R, y = usa_panel(sptr_days, sptr, n_assets=n, n_rows=n_rows)
+        total = len(days) - (T - 1)
+        self.global_dates = total
+        lo, hi = shard_range(total, rank, world)
+        self.row_offset = lo
+        # LeastSquares' tracking rho (porqua_amd/optimization.py: rho0_rel 0.2, no |q| floor)
+        self._setup(days[lo:hi + T - 1], R[lo:hi + T - 1], y[lo:hi + T - 1], T, hi - lo, device,
+                    settings or engine.Settings(rho0_rel=0.2, rho0_qrel=0.0))
+        if self.D and int(self.tlen.min()) != T:
+            raise ValueError("ReplicationBacktest: the SPTR calendar slice has a short window")
+
+
+class SweepBacktest:
+    """Config 5 (BASELINE.json configs[4]): synthetic 5000-asset factor panel, ``dates``
+    monthly rebalance dates (every 21st row, 252-day windows) x ``n_lambdas`` risk aversions
+    log-spaced in [0.1, 100]: 64 x 64 = 4096 mean-variance QPs P = 2 lam Sigma_d, q = -mu_d
+    (geometric), budget + long-only box (porqua_amd.sweep; src/optimization.py:157-174).
+
+    Multi-GPU: the fixed grid is sharded by DATE (strong scaling), every
+    risk aversion of a date on the rank that owns it, so the date's window Gram and
+    eigendecomposition are shared by its lambda row."""
+
+    def __init__(self, n: int = 5000, T: int = 252, dates: int = 64, n_lambdas: int = 64, stride: int = 21,
+                 rank: int = 0, world: int = 1, device=None, settings: engine.Settings | None = None,
+                 factor: str = "auto"):
+        from .sweep import MeanVarianceSweep
+        self.n, self.T = n, T
+        self.device = dev = device or engine.default_device()
+        d_all, R, y, _ = factor_panel(T - 1 + stride * dates, n)
+        ends = np.arange(T - 1, T - 1 + stride * dates, stride)
+        rows, tlen = engine.window_rows(d_all, d_all[ends], T)
+        self.R_rank, self.y_rank, self.dates_rank = R, y, d_all
+        self.pan = engine.Panel(R, device=dev)
+        self.lambdas = np.logspace(-1, 2, n_lambdas)
+        self.sweep = MeanVarianceSweep(self.pan, rows, tlen, self.lambdas, settings=settings, factor=factor,
+                                       rank=rank, world=world)
+        sw = self.sweep
+        self.D = sw.B                                   # problems of this rank
+        self.global_dates = dates * n_lambdas           # problems of the whole job
+        self.ends_local = ends[sw.lo:sw.hi]
+        self.qb, self.lr, self.gplan, self.ws = sw.qb, sw.lr, sw.gp, sw.ws
+        self.plan, self.mu = None, sw.mu_c
+        self.use_lr, self.with_cov = True, False
+        self.settings = sw.settings
+        self._meta = None
+
+    @property
+    def grouped(self) -> bool:
+        return self.gplan is not None and engine.grouped_applicable(self.qb, self.lr, self.gplan, self.ws)
+
+    def step(self, events: list | None = None) -> engine.BatchResult:
+        res, self._meta = self.sweep.solve(events)
+        return res
+
+    def certificate(self, res: engine.BatchResult, chunk: int = 128) -> dict:
+        return sweep_certificate(self.pan, res, self._meta, chunk=chunk)
 
 
 def window_certificate(R, rows, tlen, mu, scale, q, res: engine.BatchResult, A_row=None, b=None, lb=None, ub=None,
