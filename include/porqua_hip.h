@@ -477,6 +477,13 @@ int pq_sym_eig_batched(double* A, int32_t ld, int64_t a_stride, int32_t n, int32
                        int64_t v_stride, double* evals, int64_t e_stride, double* work, int64_t w_stride,
                        int32_t max_sweeps, double tol, void* stream);
 
+/* Convergence of the batch after pq_sym_eig_batched (same work buffer, same max_sweeps):
+ * conv[b] = 1 when the last sweep rotated nothing in matrix b (every off-diagonal entry met
+ * the tolerance), 0 when max_sweeps ran out first -- the caller must not use unconverged
+ * eigenpairs as if they were the reference's (np.linalg.eigvals / SVD, :42-56).          */
+int pq_sym_eig_converged(const double* work, int32_t ld, int64_t w_stride, int32_t batch, int32_t max_sweeps,
+                         int32_t* conv, void* stream);
+
 /* out = V diag(max(evals, 0)) V' (full ld x ld, columns k >= n of V ignored): the PSD
  * projection A2 of nearestPD (src/helper_functions.py:43-44) on FP64 MFMA.               */
 int pq_psd_form_batched(const double* V, int64_t v_stride, const double* evals, int64_t e_stride, int32_t ld,

@@ -157,6 +157,7 @@ _EXPORTS = {
     "pq_sym_eig_work_doubles": ([c_int32], c_int64),
     "pq_sym_eig_batched": ([c_dp, c_int32, c_int64, c_int32, c_int32, c_dp, c_int64, c_dp, c_int64, c_dp, c_int64,
                             c_int32, ctypes.c_double, c_dp], c_int32),
+    "pq_sym_eig_converged": ([c_dp, c_int32, c_int64, c_int32, c_int32, c_dp, c_dp], c_int32),
     "pq_psd_form_batched": ([c_dp, c_int64, c_dp, c_int64, c_int32, c_int32, c_int32, c_dp, c_int64, c_dp], c_int32),
     "pq_tile_gemm_batched": ([c_dp, c_int64, c_int32, c_dp, c_int64, c_int32, c_dp, c_int64, c_int32, c_int32,
                               c_dp], c_int32),

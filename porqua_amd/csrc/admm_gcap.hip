@@ -389,6 +389,14 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   long long tclk = wall_clock64();
 #endif
 
+  // a group beyond pass 1's rows (U + mg > CP1_ROWS) or the MFMA N cannot be solved here:
+  // its dates fail loudly (status NON_CONVEX, found = False) instead of dropping rows
+  // (uniform exit, before any barrier; GroupPlan never builds such a group)
+  if (kU > CP1_ROWS || U > CU_MAX || G > CG_MAX || kU > k_ld) {
+    for (int g = t; g < G; g += CT) st.status[d0 + g] = PQ_NON_CONVEX;
+    return;
+  }
+
   // ---- setup -------------------------------------------------------------------------------
   for (int u = t; u < CU_MAX; u += CT) s_urow[u] = u < U ? gc.urows[(int64_t)grp * gc.umax + u] : 0;
   for (int e = t; e < (CU_MAX + 4) * CG_MAX; e += CT) UT[e] = 0.0;
@@ -1113,7 +1121,7 @@ static int gcap_check(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap*
   PQ_CHECK_ARG(gc->umax > 0 && gc->umax <= pq::CU_MAX, "%s: umax must be in (0, %d]", who, pq::CU_MAX);
   PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::CMGW && pb->Cg_stride == 0 && pb->g_stride == 0,
                "%s: needs shared general rows, mg <= %d", who, pq::CMGW);
-  // (the caller guarantees ucnt[g] + mg <= k_ld for every group; U <= umax <= 320)
+  // (a group with ucnt[g] + mg beyond k_ld or pass 1 fails its dates in k_admm_gcap; U <= umax <= 320)
   PQ_CHECK_ARG(gc->k_ld % 64 == 0 && gc->k_ld >= 64 && gc->k_ld <= 384,
                "%s: need 64 <= k_ld <= 384, a multiple of 64 (k_ld=%d)", who, gc->k_ld);
   return 0;

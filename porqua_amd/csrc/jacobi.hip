@@ -247,6 +247,18 @@ __global__ __launch_bounds__(256) void k_jac_diag(JacCtx c, double* evals, int64
     evals[(int64_t)b * e_stride + i] = A[(int64_t)i * c.ld + i];
 }
 
+// conv[b] = 1 iff the last queued sweep (index last) rotated nothing in matrix b: every
+// off-diagonal entry of every subproblem met the tolerance, i.e. the matrix converged
+__global__ __launch_bounds__(256) void k_jac_conv(JacCtx c, int last, int32_t* conv) {
+  __shared__ double red[16];
+  const int b = blockIdx.x;
+  const double* f = jac_flags(c, b, last & 1);
+  double any = 0.0;
+  for (int i = threadIdx.x; i < c.nrounds * c.npairs; i += blockDim.x) any = fmax(any, f[i]);
+  any = block_max(any, red);
+  if (threadIdx.x == 0) conv[b] = any > 0.0 ? 0 : 1;
+}
+
 // out = V diag(max(lam, 0)) V' (tile (I, J) of the full matrix): Vs = V sqrt(max(lam, 0))
 // staged column-scaled into LDS, one MFMA tile product of depth ld
 __global__ __launch_bounds__(256) void k_psd_form(const double* V, int64_t v_stride, const double* evals,
@@ -324,6 +336,20 @@ extern "C" int pq_sym_eig_batched(double* A, int32_t ld, int64_t a_stride, int32
     }
   hipLaunchKernelGGL(pq::k_jac_diag, dim3((ld + 255) / 256, batch), blk, 0, str, c, evals, e_stride);
   PQ_CHECK_LAUNCH("pq_sym_eig_batched");
+  return 0;
+}
+
+extern "C" int pq_sym_eig_converged(const double* work, int32_t ld, int64_t w_stride, int32_t batch,
+                                    int32_t max_sweeps, int32_t* conv, void* stream) {
+  PQ_CHECK_ARG(work && conv && ld % 64 == 0 && ld > 0 && batch >= 0 && max_sweeps >= 1,
+               "pq_sym_eig_converged: bad arguments");
+  PQ_CHECK_ARG(w_stride >= pq_sym_eig_work_doubles(ld), "pq_sym_eig_converged: work stride too small");
+  if (batch == 0) return 0;
+  pq::JacCtx c{};
+  c.work = const_cast<double*>(work); c.w_stride = w_stride;
+  c.ld = ld; c.nbk = ld / pq::JB; c.npairs = c.nbk / 2; c.nrounds = c.nbk - 1;
+  hipLaunchKernelGGL(pq::k_jac_conv, dim3(batch), dim3(256), 0, (hipStream_t)stream, c, max_sweeps - 1, conv);
+  PQ_CHECK_LAUNCH("pq_sym_eig_converged");
   return 0;
 }
 

@@ -78,6 +78,17 @@ __global__ __launch_bounds__(YT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int hg = t >> 5, hl = t & 31;
   const int hbase = (hg & 1) * 32;
 
+  // a group whose union + general rows exceed pass 1's YU rows (or whose dates exceed YG)
+  // cannot be solved here: its pending dates go to the per-date kernel (uniform exit, before
+  // any barrier)
+  if (U + mg > YU || G > YG) {
+    for (int j = t; j < G; j += YT) {
+      double* R = rec + (int64_t)(d0 + j) * PGR;
+      if (R[R_STATE] == PQ_PG_PENDING) R[R_STATE] = PQ_PG_FALLBACK;
+    }
+    return;
+  }
+
   // ---- setup ---------------------------------------------------------------------------
   for (int u = t; u < YU; u += YT) s_urow[u] = u < U ? gc.urows[(int64_t)grp * gc.umax + u] : 0;
   for (int e = t; e < (YU + 4) * YG; e += YT) WU[e] = 0.0;
@@ -702,7 +713,7 @@ int pq_pg_wide_launch(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, 
   const pq_gcap* gc = wd->gc;
   PQ_CHECK_ARG(gc && gc->Minv && gc->aq && gc->hinv && gc->grho && gc->ngroups > 0,
                "pq_polish_grouped_round: wide mode needs the polish group capacitance");
-  // (the caller guarantees ucnt[g] + mg <= 320 for every group: union rows + general rows of pass 1)
+  // (a group with ucnt[g] + mg > YU rows hands its pending dates to the per-date kernel in k_pgw)
   PQ_CHECK_ARG(gc->umax > 0 && gc->umax <= pq::YU && gc->k_ld % 64 == 0 && gc->k_ld <= 384 && gc->ldh > 0 &&
                    gc->ldh <= pq::YCH,
                "pq_polish_grouped_round: wide mode needs umax <= %d, k_ld <= 384, ldh <= %d", pq::YU, pq::YCH);

@@ -622,14 +622,19 @@ def _tkey(*ts):
     return tuple(None if t is None else (t.data_ptr(), tuple(t.shape), t._version) for t in ts)
 
 
-def _cached(owner, name: str, key, fn):
+def _cached(owner, name: str, key, fn, keep=()):
     """fn() cached on ``owner`` under ``name`` while ``key`` is unchanged (host-side checks
-    with device syncs and constant tables are then paid once per batch, not per solve)."""
+    with device syncs and constant tables are then paid once per batch, not per solve).
+
+    ``keep``: the objects whose identity the key encodes (``id()``s, tensor data pointers).
+    The cache entry holds strong references to them, so while the entry lives no other
+    object can reuse those ids or the caching allocator those addresses, and a key match
+    means the same objects (in-place changes bump ``_version``, which the key includes)."""
     hit = getattr(owner, name, None)
     if hit is not None and hit[0] == key:
         return hit[1]
     val = fn()
-    setattr(owner, name, (key, val))
+    setattr(owner, name, (key, val, tuple(keep)))
     return val
 
 
@@ -644,7 +649,7 @@ def _uniform_box(qb: QPBatch) -> bool:
         cls = torch.where(torch.isinf(lo) & torch.isinf(up), 1, torch.where(lo == up, 2, 0))
         return bool((cls == cls[:, :1]).all().item()) and (qb.lb.shape[0] == 1 or
                                                           bool((cls[:, 0] == cls[0, 0]).all().item()))
-    return _cached(qb, "_c_ubox", _tkey(qb.lb, qb.ub), check)
+    return _cached(qb, "_c_ubox", _tkey(qb.lb, qb.ub), check, keep=(qb.lb, qb.ub))
 
 
 def _band_setup(qb: QPBatch, lr: LowRank, strm, w_min: int = 0):
@@ -668,7 +673,7 @@ def _band_setup(qb: QPBatch, lr: LowRank, strm, w_min: int = 0):
     def cgram():
         C = qb.Cg[0, :mg, :n]
         return (C @ C.T).contiguous() if mg else torch.zeros((1, 1), dtype=F64, device=dev)
-    cc = _cached(qb, "_c_cc", _tkey(qb.Cg), cgram)
+    cc = _cached(qb, "_c_cc", _tkey(qb.Cg), cgram, keep=(qb.Cg,))
     return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc, "W": W}
 
 
@@ -685,7 +690,8 @@ def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan"
         pd = qb.p_diag if qb.p_diag is not None else torch.zeros(B, dtype=F64, device=dev)
         first = groups.gdates[:-1].long()[groups.gidx.long()]
         return bool(((c == c[first]) & (pd == pd[first])).all().item())
-    if not _cached(ws, "_c_gcap_uniform", (id(groups),) + _tkey(qb.p_scale, lr.w_scale, qb.p_diag), uniform):
+    if not _cached(ws, "_c_gcap_uniform", (id(groups),) + _tkey(qb.p_scale, lr.w_scale, qb.p_diag), uniform,
+                   keep=(groups, qb.p_scale, lr.w_scale, qb.p_diag)):
         return None
     G = groups.ngroups
     k_ld = round_up(groups.ucnt_max + mg, 64)
@@ -1150,7 +1156,7 @@ class GroupPlan:
         rows = np.asarray(rows)
         tlen = np.asarray(tlen)
         B = len(tlen)
-        self._host = (rows, tlen, device, umax, smax)
+        self._host = (rows, tlen, device, umax, smax, breaks, cus, gmax)
         self._polish_full = polish_full
         self._polish_plan = None
         # balance: one group per CU per round (one 512-thread workgroup fits a CU), as few
@@ -1237,10 +1243,11 @@ class GroupPlan:
         if not self._polish_full:
             return self
         if self._polish_plan is None:
-            rows, tlen, device, umax, smax = self._host
-            full = self.ngroups == 0 or int(self.sizes.max()) >= GROUP_MAX_DATES
-            self._polish_plan = None if full else GroupPlan(rows, tlen, device, umax=umax, smax=smax,
-                                                            gmin=GROUP_MAX_DATES)
+            rows, tlen, device, umax, smax, breaks, cus, gmax0 = self._host
+            full = self.ngroups == 0 or int(self.sizes.max()) >= min(gmax0, GROUP_MAX_DATES)
+            # same breaks (e.g. rho buckets) and CU count: polish groups never straddle a break
+            self._polish_plan = None if full else GroupPlan(rows, tlen, device, umax=umax, smax=smax, cus=cus,
+                                                            gmax=gmax0, gmin=gmax0, breaks=breaks)
             if full:
                 self._polish_full = False
         return self._polish_plan if self._polish_plan is not None else self

@@ -85,7 +85,9 @@ def sym_eig(A: torch.Tensor, n: int, vectors: bool = True, max_sweeps: int = 30,
     """Symmetric eigendecomposition of the device batch A (B, ld, ld), ld a multiple of 64,
     by the hand-written block-Jacobi kernels (pq_sym_eig_batched).  A is overwritten
     (diagonalised).  Returns (evals (B, ld): eigenvalue j of matrix b at evals[b, j], j < n,
-    unsorted; V (B, ld, ld) with the eigenvectors as columns, or None)."""
+    unsorted; V (B, ld, ld) with the eigenvectors as columns, or None).  A matrix still
+    unconverged after ``max_sweeps`` (pq_sym_eig_converged) is finished by rocSOLVER's eigh
+    from its partially diagonalised state; ``sym_eig.last_unconverged`` counts them."""
     from . import _lib, engine
     lib = _lib.load()
     B, ld = A.shape[0], A.shape[-1]
@@ -102,6 +104,27 @@ def sym_eig(A: torch.Tensor, n: int, vectors: bool = True, max_sweeps: int = 30,
                                           None if V is None else V[s0:].data_ptr(), ld * ld, ev[s0:].data_ptr(),
                                           ld, work[s0:].data_ptr(), w, max_sweeps, tol, engine._stream()),
                    "pq_sym_eig_batched")
+    # convergence (one host sync): a matrix whose last sweep still rotated is finished by
+    # rocSOLVER from where the Jacobi sweeps left it -- A is now Q' A0 Q with Q = V, so
+    # eigh(A) = (lam, W) gives A0's eigenpairs (lam, Q W) -- never used unconverged
+    conv = torch.empty(B, dtype=torch.int32, device=dev)
+    for s0 in range(0, B, 65535):
+        e0 = min(B, s0 + 65535)
+        _lib.check(lib.pq_sym_eig_converged(work[s0:].data_ptr(), ld, w, e0 - s0, max_sweeps, conv[s0:].data_ptr(),
+                                            engine._stream()), "pq_sym_eig_converged")
+    bad = torch.nonzero(conv == 0).flatten()
+    if bad.numel():
+        As = A[bad]
+        As = 0.5 * (As + As.mT)
+        lam, Wr = torch.linalg.eigh(As[:, :n, :n])
+        ev[bad] = 0.0
+        ev[bad, :n] = lam
+        if V is not None:
+            V[bad, :, :n] = V[bad][:, :, :n] @ Wr
+        Ad = torch.zeros((len(bad), ld, ld), dtype=F64, device=dev)
+        Ad[:, :n, :n] = torch.diag_embed(lam)
+        A[bad] = Ad                                                    # diagonalised, as on convergence
+    sym_eig.last_unconverged = int(bad.numel())
     return ev, V
 
 

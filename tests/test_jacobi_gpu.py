@@ -59,3 +59,24 @@ def test_psd_projection_of_rank_deficient_covariance(device):
     L, Q = np.linalg.eigh(S)
     ref = (Q * np.maximum(L, 0)) @ Q.T
     assert np.abs(out[0, :n, :n].cpu().numpy() - ref).max() <= 5e-13 * (ld // 32) * np.abs(S).max()
+
+
+def test_unconverged_sweeps_are_flagged_and_finished(device):
+    """pq_sym_eig_converged: after too few sweeps the matrices are reported unconverged and
+    sym_eig finishes them (never hands out unconverged eigenpairs); with enough sweeps every
+    matrix converges and nothing is finished elsewhere."""
+    rng = np.random.default_rng(11)
+    n = 200
+    M = rng.normal(size=(2, n, n))
+    A = 0.5 * (M + M.transpose(0, 2, 1))
+    ld = engine.round_up(n, 64)
+    ev, V = sym_eig(_dev_batch(A, ld), n, max_sweeps=1)
+    assert sym_eig.last_unconverged == 2
+    ev, V = ev.cpu().numpy()[:, :n], V.cpu().numpy()[:, :n, :n]
+    for b in range(2):
+        ref = np.linalg.eigvalsh(A[b])
+        nrm = np.abs(ref).max()
+        assert np.abs(np.sort(ev[b]) - ref).max() <= 1e-12 * nrm
+        assert np.abs((V[b] * ev[b]) @ V[b].T - A[b]).max() <= 1e-12 * nrm
+    sym_eig(_dev_batch(A, ld), n)
+    assert sym_eig.last_unconverged == 0
