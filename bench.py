@@ -124,6 +124,9 @@ def parse():
     ap.add_argument("--with-cov", action="store_true",
                     help="low-rank path: also materialise every date's n x n covariance with K1 "
                          "(nothing on that path reads it)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="config3: host-driven solve (a host check after the ADMM and after every polish "
+                         "round) instead of the sync-free solve whose stages replay as HIP graphs")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --dates rebalance dates in total, split over the ranks "
                          "(default: weak scaling, --dates per rank)")
@@ -279,7 +282,9 @@ def main():
         settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))
         wl = MinVarianceBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
                                  path=args.path, group=not args.no_group, slide=not args.no_slide,
-                                 with_cov=args.with_cov, strong=args.strong)
+                                 with_cov=args.with_cov, strong=args.strong, graph=not args.no_graph)
+    if hasattr(wl, "prepare"):   # graph mode: the cache-filling step and the capture, untimed
+        wl.prepare()
     gloo = dist is not None and dist.get_backend() != "nccl"
     D = wl.D                                            # dates of this rank
     D_all = wl.global_dates                             # dates of the whole job

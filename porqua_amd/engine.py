@@ -349,19 +349,69 @@ class BatchResult:
         return (self.status == _lib.PQ_SOLVED) | (self.status == _lib.PQ_SOLVED_INACCURATE)
 
 
-class _Timeline:
-    """Optional per-launch HIP event pairs on the launch stream (no host syncs)."""
+class StageGraphs:
+    """HIP graphs of the stages of a solve that is repeated on the same buffers (a backtest
+    re-solved every step, the bench workloads): the first time a stage runs its launches are
+    captured into a graph (torch.cuda.CUDAGraph over the caller's stream: the library's
+    kernels, the side-stream forks / joins of the polish and the torch glue), every later
+    time the graph is replayed -- one launch per stage instead of dozens, no host work
+    between them.  Stages are keyed by name and occurrence within one solve (``begin``).
 
-    def __init__(self, sink):
+    Only sync-free stages may be captured (solve_lowrank(sync_free=True) is); kernel
+    arguments -- device pointers and settings -- are frozen at capture, so the owner must
+    keep the same problem, window and workspace objects alive and in place."""
+
+    def __init__(self):
+        self.graphs = {}
+        self.pool = None
+        self._seen = {}
+        self._warm = set()
+
+    def begin(self):
+        self._seen = {}
+
+    def run(self, name, fn):
+        """First call of a stage: eager (it fills the host-side caches -- plans, uniformity
+        checks -- whose first evaluation synchronises); second: capture + replay; then replay."""
+        k = self._seen.get(name, 0)
+        self._seen[name] = k + 1
+        key = (name, k)
+        hit = self.graphs.get(key)
+        if hit is None:
+            if key not in self._warm:
+                self._warm.add(key)
+                return fn()
+            # captured on the caller's (non-default) stream itself: the solve passes that
+            # stream to the library explicitly, so it must be the capturing one
+            cur = torch.cuda.current_stream()
+            if cur == torch.cuda.default_stream(cur.device):
+                raise RuntimeError("StageGraphs: run the solve on a non-default stream (torch.cuda.stream(...))")
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.pool, stream=cur):
+                r = fn()
+            self.pool = g.pool()
+            hit = self.graphs[key] = (g, r)
+        hit[0].replay()
+        return hit[1]
+
+
+class _Timeline:
+    """Optional per-launch HIP event pairs on the launch stream (no host syncs); with
+    ``graphs`` (StageGraphs) each stage is captured once and replayed afterwards (the events
+    then bracket the graph launch)."""
+
+    def __init__(self, sink, graphs: "StageGraphs | None" = None):
         self.sink = sink
+        self.graphs = graphs
 
     def __call__(self, name, fn):
+        run = (lambda: self.graphs.run(name, fn)) if self.graphs is not None else fn
         if self.sink is None:
-            return fn()
+            return run()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        r = fn()
+        r = run()
         e1.record()
         self.sink.append((name, e0, e1))
         return r
@@ -824,12 +874,25 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
                   fuse: bool = True, grouped_polish: bool = True, gcap: bool = True,
-                  eig: "EigCap | None" = None, wide_polish: bool = True) -> BatchResult:
+                  eig: "EigCap | None" = None, wide_polish: bool = True, sync_free: bool = False,
+                  graphs: "StageGraphs | None" = None, sf_rounds: int | None = None) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
-    may be None): P is the window (lr) throughout."""
-    tl = _Timeline(events)
+    may be None): P is the window (lr) throughout.
+
+    ``sync_free`` (group capacitance with the grouped polish, no wide rounds): the stages
+    run without any host synchronisation -- one ADMM launch, ``sf_rounds`` polish rounds
+    (default settings.polish_rounds) -- and one flag read at the end decides whether the
+    usual host-driven repairs must run (an adaptive-rho refactorisation: the whole solve is
+    redone the host-driven way; dates still pending, handed back, or rejected: the remaining
+    rounds, the per-date polish and the ADMM retry, exactly as without it).  With ``graphs``
+    (StageGraphs) the sync-free stages are captured once and replayed."""
+    if sync_free and not (gcap and eig is None and groups is not None and grouped_polish and polish):
+        sync_free = False
+    tl = _Timeline(events, graphs if sync_free else None)
+    if tl.graphs is not None:
+        tl.graphs.begin()
     lib = _lib.load()
     s = (settings or Settings()).to_c()
     ws = ws or Workspace(qb, dense=False)
@@ -929,6 +992,9 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                                       nidx, SS, int(s.max_iter), strm)
 
     cnt = {"refactors": 0, "launches": 0, "pg_fallback": 0}
+    if sync_free and gc is None:   # the group capacitance did not apply: host-driven solve
+        sync_free = False
+        tl.graphs = None
 
     def admm_rounds(idx, nidx, SSx, name="admm"):
         nonlocal SS
@@ -936,6 +1002,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         for _ in range(max_rounds):
             _lib.check(tl(name, lambda: admm(idx, nidx)), "pq_admm_lr")
             cnt["launches"] += 1
+            if sync_free:   # NEED_REFACTOR is caught by the flag at the end
+                break
             need = torch.nonzero(ws.status == _lib.PQ_NEED_REFACTOR).flatten().to(torch.int32)
             kk = int(need.numel())
             if kk == 0:
@@ -969,13 +1037,13 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                                                                         SS, kmax, 1, *bk, strm)),
                            "pq_polish_w_batched (relaunch)")
 
-    def polish_grouped():
-        """Grouped polish pipeline (polish_g.hip) for every date; the dates it hands back
-        (FALLBACK) go through pq_polish_w_batched from their ADMM point."""
+    pg = {}
+
+    def pg_start(allow_wide: bool):
+        """k_pg_init (classification from the ADMM point) + the wide rounds' capacitance."""
         rec = ws.pg_record()
-        rp = rec.data_ptr()
         g = groups.polish_plan()
-        _lib.check(lib.pq_polish_grouped_init(L_, P_, S_, rp, SS_main, strm), "pq_polish_grouped_init")
+        _lib.check(lib.pq_polish_grouped_init(L_, P_, S_, rec.data_ptr(), SS_main, strm), "pq_polish_grouped_init")
         scr = getattr(ws, "_pg_pass", None)
         if scr is None or scr.numel() < g.ngroups * _lib.PQ_PG_PASS_SCRATCH:
             scr = torch.empty(g.ngroups * _lib.PQ_PG_PASS_SCRATCH, dtype=F64, device=dev)
@@ -983,16 +1051,53 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         # free sets beyond the LDS solve (k_pg_init left each date's free count in PQ_PG_K): the
         # wide rounds' group capacitance, built once for the whole polish
         wide = None
-        if wide_polish and bool((rec[:, _lib.PQ_PG_K] > min(ldk, 128)).any()):   # host sync: one flag
+        if allow_wide and wide_polish and bool((rec[:, _lib.PQ_PG_K] > min(ldk, 128)).any()):   # host sync
             wide = _pg_wide_setup(qb, lr, ws, g, bd, rec, settings or Settings(), sparse_cols, strm)
-        wide_p = ctypes.byref(wide) if wide is not None else None
         cnt["pg_wide"] = wide is not None
-        for r in range(int(s.polish_rounds)):
-            _lib.check(lib.pq_polish_grouped_round(L_, P_, S_, rp, ldk, _ptr(g.gdates), g.ngroups, _ptr(g.urows),
-                                                   _ptr(g.ucnt), _ptr(g.uoff), g.umax, SS_main, scr.data_ptr(),
-                                                   wide_p, strm), "pq_polish_grouped_round")
-            if r >= 1 and not bool((rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_PENDING).any()):   # host sync
+        pg.update(rec=rec, g=g, scr=scr, wide=wide, wide_p=ctypes.byref(wide) if wide is not None else None,
+                  rounds=0)
+
+    def pg_round():
+        g, rec = pg["g"], pg["rec"]
+        _lib.check(lib.pq_polish_grouped_round(L_, P_, S_, rec.data_ptr(), ldk, _ptr(g.gdates), g.ngroups,
+                                               _ptr(g.urows), _ptr(g.ucnt), _ptr(g.uoff), g.umax, SS_main,
+                                               pg["scr"].data_ptr(), pg["wide_p"], strm), "pq_polish_grouped_round")
+        pg["rounds"] += 1
+
+    def pg_rounds_host():
+        """The remaining rounds, each followed by a host check for dates still pending."""
+        rec = pg["rec"]
+        while pg["rounds"] < int(s.polish_rounds):
+            if pg["rounds"] >= 2 and not bool((rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_PENDING).any()):   # sync
                 break
+            pg_round()
+
+    def polish_grouped():
+        """Grouped polish pipeline (polish_g.hip) for every date; the dates it hands back
+        (FALLBACK) go through pq_polish_w_batched from their ADMM point."""
+        pg_start(True)
+        pg_round()
+        pg_rounds_host()
+        pg_finish()
+
+    def polish_sync_free():
+        """The grouped polish with a fixed number of rounds and no host check (dates done
+        early skip the later rounds' kernels), then one device flag: anything left for the
+        host-driven repairs (dates pending, handed back or rejected, or an ADMM refactor)."""
+        pg_start(False)
+        for _ in range(min(int(sf_rounds or s.polish_rounds), int(s.polish_rounds))):
+            pg_round()
+        st_pg = pg["rec"][:, _lib.PQ_PG_STATE]
+        flag = ((st_pg == _lib.PQ_PG_PENDING) | (st_pg == _lib.PQ_PG_FALLBACK) |
+                (ws.status == _lib.PQ_NEED_REFACTOR) | (ws.status == _lib.PQ_SOLVED_INACCURATE) |
+                (ws.status == _lib.PQ_UNSOLVED)).any()
+        if getattr(ws, "_sf_flag", None) is None:
+            ws._sf_flag = torch.zeros((), dtype=torch.bool, device=dev)
+        ws._sf_flag.copy_(flag)
+        return dict(pg)   # the pipeline state (a replayed graph does not run this function)
+
+    def pg_finish():
+        rec = pg["rec"]
         fb = torch.nonzero(rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_FALLBACK).flatten().to(torch.int32)
         m = int(fb.numel())
         cnt["pg_fallback"] = m
@@ -1016,12 +1121,31 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         sl = st_.to_c()
         sl.eps_abs = sl.eps_rel = st_.eps_grouped
         SS_admm = ctypes.byref(sl)
+    if sync_free and not (grouped and ldk >= 64 and s.polish):
+        sync_free = False
+        tl.graphs = None
     admm_rounds(None, 0, SS_admm)
+    if sync_free:
+        pg.update(tl("polish", polish_sync_free))
+        if not bool(ws._sf_flag.item()):   # the one host sync of the step: nothing left to repair
+            return _lowrank_result(qb, ws, cnt, "group")
+        if bool((ws.status == _lib.PQ_NEED_REFACTOR).any() | (ws.status == _lib.PQ_UNSOLVED).any()):
+            # an adaptive-rho refactorisation was requested: redo the whole solve host-driven
+            return solve_lowrank(qb, lr, settings, ws, max_rounds, events, polish, groups, band, fuse,
+                                 grouped_polish, gcap, eig, wide_polish)
+        tl.graphs = None   # the repairs below are host-driven
+        sync_free = False  # (admm_rounds checks for refactorisations again)
+        pg_rounds_host()   # dates still pending: the remaining rounds
+        pg_finish()        # dates handed back: the per-date polish
+        polished = True
+    else:
+        polished = False
     if s.polish and polish:
-        if grouped and grouped_polish and ldk >= 64:
-            tl("polish", polish_grouped)
-        else:
-            polish_w(None, 0)
+        if not polished:
+            if grouped and grouped_polish and ldk >= 64:
+                tl("polish", polish_grouped)
+            else:
+                polish_w(None, 0)
         # one host sync: nothing rejected (the usual case) skips both repairs
         rejected = bool((ws.status == _lib.PQ_SOLVED_INACCURATE).any().item())
         rp = _repolish_set(ws, settings or Settings()) if rejected else None
@@ -1035,13 +1159,15 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             s4 = (settings or Settings()).to_c()
             s4.refine_iters = max(s4.refine_iters, (settings or Settings()).refine_retry)
             polish_w(ridx, rn, ctypes.byref(s4))
-    refactors, launches = cnt["refactors"], cnt["launches"]
+    return _lowrank_result(qb, ws, cnt, "group" if gc is not None else ("eig" if eig is not None else
+                                                                       ("band" if bd is not None else "direct")))
+
+
+def _lowrank_result(qb: QPBatch, ws: Workspace, cnt: dict, capacitance: str) -> BatchResult:
     n, mg = qb.n, qb.mg
     return BatchResult(x=ws.x[:, :n], y=ws.y[:, :mg], z_box=ws.y[:, ws.mg_pad:ws.mg_pad + n],
-                       status=ws.status, iters=ws.iters, out=ws.out, refactors=refactors,
-                       admm_launches=launches, polish_fallbacks=cnt["pg_fallback"],
-                       capacitance="group" if gc is not None else ("eig" if eig is not None else
-                                                                    ("band" if bd is not None else "direct")))
+                       status=ws.status, iters=ws.iters, out=ws.out, refactors=cnt["refactors"],
+                       admm_launches=cnt["launches"], polish_fallbacks=cnt["pg_fallback"], capacitance=capacitance)
 
 
 def factor_only(qb: QPBatch, invert: bool = False, sigma: float = 0.0):
@@ -1083,10 +1209,14 @@ def window_rows(dates: np.ndarray, rebdates, width: int):
     tmax = max(1, int(tlen.max())) if B else 1
     if not len(wpos):
         return np.zeros((B, tmax), dtype=np.int32), tlen
-    j = np.arange(tmax, dtype=np.int64)[None, :]
-    rows = np.take(wpos, first[:, None] + j, mode="clip")
-    rows[j >= tlen[:, None]] = 0
-    return rows, tlen
+    # int32 index arithmetic; a calendar without weekend rows (the usual return panel) needs
+    # no position lookup at all (wpos is the identity)
+    j = np.arange(tmax, dtype=np.int32)[None, :]
+    idx = first.astype(np.int32)[:, None] + j
+    if len(wpos) != len(dates):
+        idx = wpos[np.minimum(idx, len(wpos) - 1)]
+    rows = idx * (j < tlen[:, None])
+    return rows.astype(np.int32, copy=False), tlen
 
 
 def slide_plan(rows, tlen, group: int = 32, smax: int = 64, smin: int = 1):

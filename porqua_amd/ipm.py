@@ -242,14 +242,23 @@ def active_set_polish(P, q, A, b, G, h, lb, ub, x, y, z, zb, rounds: int = 8):
         if bool(fac.factor(PFF[None], 0.0, retries=0).any()):
             return x, y, z, zb, False
         HiC = fac.solve_mat(CF.T[None].contiguous())[0] if m else None
+        if m:
+            # Schur complement of the active rows, S = C_F P_FF^-1 C_F' (m x m, SPD; rows that
+            # are dependent make it singular), factored and inverted on K2 with a shift of
+            # 1e-14 of its diagonal (grown by K2's retries when a row is dependent) -- on the
+            # device, no host copy; the refinement step below absorbs the shift
+            S = 0.5 * (CF @ HiC + (CF @ HiC).T)
+            sfac = _NormalFactor(1, m, dev)
+            sfac.factor(S[None], 1e-14 * S.diagonal().abs().amax().clamp(min=1e-300) *
+                        torch.ones((1, m), dtype=F64, device=dev))
 
         def solve(f, g):
             hf = fac.solve_mat(f[None, :, None].contiguous())[0, :, 0]
             if not m:
                 return hf, torch.zeros(0, dtype=F64, device=dev)
-            S = (CF @ HiC).cpu().numpy()
-            lam = np.linalg.lstsq(S, (CF @ hf - g).cpu().numpy(), rcond=1e-13)[0]
-            lam = torch.from_numpy(lam).to(dev)
+            r = (CF @ hf - g)[None, :, None].contiguous()
+            lam = sfac.solve_mat(r)
+            lam = (lam + sfac.solve_mat(r - S[None] @ lam))[0, :, 0]   # one refinement step
             return hf - HiC @ lam, lam
 
         xF, lam = solve(rF, dF)

@@ -34,8 +34,13 @@ class MinVarianceBacktest:
     def __init__(self, n: int = 1000, T: int = 252, D: int = 4749, rank: int = 0, world: int = 1,
                  device=None, settings: engine.Settings | None = None, path: str = "auto",
                  group: bool = True, slide: bool = True, with_cov: bool = False, strong: bool = False,
-                 seed: int | None = None):
+                 seed: int | None = None, graph: bool = False):
         self.n, self.T = n, T
+        # graph mode: the step's stages are sync-free and captured as HIP graphs after a first
+        # eager step (engine.StageGraphs), on a stream of its own
+        self.graph = graph
+        self.graphs = None
+        self.sf_rounds = None
         self.device = dev = device or engine.default_device()
         if strong:   # D dates in total, contiguous blocks (the last rank takes the remainder)
             per = -(-D // world)
@@ -85,27 +90,56 @@ class MinVarianceBacktest:
 
     def step(self, events: list | None = None) -> engine.BatchResult:
         """One pass of the hot path over every date of this rank (inputs resident in HBM):
-        window moments [-> K1 covariance] -> K2 -> K3 -> K4.  Weights stay on the device."""
-        if events is not None:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-        if self.use_lr and self.gplan is not None and self.gplan.ok:
-            # mu and diag(Xc'Xc) (the only O(n) per-date moments) in one sliding pass per group
-            mu, _ = self.pan.window_moments_grouped(self.gplan, self.tlen_d, self.mu, self.lr.dg)
-        else:
-            mu = self.pan.window_means(self.rows_d, self.tlen_d, out=self.mu)
-            if self.use_lr:
-                self.lr.refresh()
-        if self.with_cov:
-            self.pan.cov(self.rows_d, self.tlen_d, mode=0, out=self.qb.P, mu=mu, plan=self.plan,
-                         lower_only=self.use_lr)
-        if events is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            events.append(("moments+cov" if self.with_cov else "moments", e0, e1))
+        window moments [-> K1 covariance] -> K2 -> K3 -> K4.  Weights stay on the device.
+
+        Graph mode (``graph=True``, the group-capacitance path): the solve is sync-free
+        (engine.solve_lowrank(sync_free=True): one ADMM launch, a fixed number of polish
+        rounds -- the most the previous step needed -- and one flag read that runs the
+        host-driven repairs only when something is left), every stage after the first step a
+        replayed HIP graph on the workload's own stream (joined to the caller's stream on
+        both sides, no host sync)."""
+        if not (self.graph and self.use_lr and self.grouped):
+            return self._step(events)
+        if self.graphs is None:
+            self.graphs = engine.StageGraphs()
+            self._stream = torch.cuda.Stream(device=self.device)
+        cur = torch.cuda.current_stream()
+        self._stream.wait_stream(cur)
+        with torch.cuda.stream(self._stream):
+            self.graphs.begin()
+            res = self._step(events)
+        cur.wait_stream(self._stream)
+        if self.sf_rounds is None:   # rounds the polish needed (one host read, first step only)
+            self.sf_rounds = max(2, int(res.out[:, engine._lib.PQ_OUT_ROUNDS].max().item()))
+        return res
+
+    def prepare(self):
+        """Graph mode: the first (eager, cache-filling) step and the capturing step, outside
+        any timed region -- afterwards every step replays the captured stages."""
+        if self.graph:
+            for _ in range(2):
+                self.step()
+            torch.cuda.synchronize()
+
+    def _step(self, events):
+        tl = engine._Timeline(events, self.graphs)
+
+        def moments():
+            if self.use_lr and self.gplan is not None and self.gplan.ok:
+                # mu and diag(Xc'Xc) (the only O(n) per-date moments) in one sliding pass per group
+                mu, _ = self.pan.window_moments_grouped(self.gplan, self.tlen_d, self.mu, self.lr.dg)
+            else:
+                mu = self.pan.window_means(self.rows_d, self.tlen_d, out=self.mu)
+                if self.use_lr:
+                    self.lr.refresh()
+            if self.with_cov:
+                self.pan.cov(self.rows_d, self.tlen_d, mode=0, out=self.qb.P, mu=mu, plan=self.plan,
+                             lower_only=self.use_lr)
+        tl("moments+cov" if self.with_cov else "moments", moments)
         if self.use_lr:
             return engine.solve_lowrank(self.qb, self.lr, self.settings, self.ws, events=events,
-                                        groups=self.gplan)
+                                        groups=self.gplan, sync_free=self.graphs is not None,
+                                        graphs=self.graphs, sf_rounds=self.sf_rounds)
         return engine.solve(self.qb, self.settings, self.ws, events=events)
 
     def certificate(self, res: engine.BatchResult, chunk: int = 256) -> dict:

@@ -149,3 +149,20 @@ def test_pairwise_cov_oracle_matches_reference_nan_windows():
         assert np.array_equal(np.isnan(S), np.isnan(ref)), case
         ok = ~np.isnan(ref)
         assert np.abs(S[ok] - ref[ok]).max() <= 1e-14 * np.abs(ref[ok]).max(), case
+
+
+def test_vectorised_pairwise_oracle_matches_reference_and_loop():
+    """oracle cov_pairwise_rows (the pair loop vectorised over one row at a time, used at the
+    config sizes) == the reference's DataFrame.cov() fixtures and == cov_pairwise."""
+    g = load_golden("nan_cov")
+    for case in ("msci_holes", "wide", "sparse"):
+        S = rp.cov_pairwise_rows(g[f"{case}__X"])
+        ref = g[f"{case}__raw"]
+        assert np.array_equal(np.isnan(S), np.isnan(ref)), case
+        ok = ~np.isnan(ref)
+        assert np.abs(S[ok] - ref[ok]).max() <= 1e-14 * np.abs(ref[ok]).max(), case
+    rng = np.random.default_rng(3)
+    X = rng.normal(3e-4, 0.02, size=(60, 40))
+    X[rng.random(X.shape) < 0.1] = np.nan
+    A, B = rp.cov_pairwise_rows(X), rp.cov_pairwise(X)
+    assert np.array_equal(np.isnan(A), np.isnan(B)) and np.nanmax(np.abs(A - B)) <= 1e-15 * np.nanmax(np.abs(B))
