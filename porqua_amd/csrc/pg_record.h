@@ -23,6 +23,7 @@ enum : int {
   R_GFORM = 348
 };
 constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
+constexpr int PG_KBIG = 256;   // largest free set of the grouped large-free-set solve (k_pg_big)
 constexpr int PG_MGMAX = 32;   // general rows
 // wide mode (polish_gw.hip): the free set exceeds the LDS solve, so the round solves the full
 // n-space reduced KKT by the group capacitance with the active general rows and the fixed

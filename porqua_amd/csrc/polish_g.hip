@@ -127,7 +127,8 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
 // ---------------------------------------------------------------------------------------
 // setup: free list, active rows, x_B, dA, the starting point of the refinement
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, double* rec, int kmax, int wide_ok) {
+__global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, double* rec, int kmax, int wide_ok,
+                                                 int kbig) {
   __shared__ int wcnt[PW];
   __shared__ int s_al[PG_MGMAX + 1];
   __shared__ double red[16];
@@ -206,7 +207,8 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
   // multiplier of at most one active equality row is chosen in the post from the dual
   // feasibility interval of the bound variables (k_pg_post); otherwise the per-date kernel
   const bool vertex_ok = ma == 0 || (ma == 1 && lg[s_al[0]] == ug[s_al[0]]);
-  if ((k == 0 && !vertex_ok) || k > kmax || ma > PG_MGMAX) {   // uniform
+  // (kmax < k <= kbig: the large-free-set solve k_pg_big)
+  if ((k == 0 && !vertex_ok) || k > kbig || ma > PG_MGMAX) {   // uniform
     if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
@@ -1034,6 +1036,195 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
 }
 
 // ---------------------------------------------------------------------------------------
+// solve for the free sets beyond the LDS solve, PG_KMAX < k <= ldk (the tracking windows of
+// configs 1/2: 160..220 free assets at n = 494), one 256-thread workgroup per date inside the
+// grouped pipeline instead of handing the date to the per-date kernel (pq_polish_w_batched,
+// which runs every round's window passes per date as well): P_FF from the window in the
+// compact storage (form_pff: MFMA tiles, diagonal tiles in full, off-diagonal tiles
+// transposed), its factor in place (wg_cholesky: 64 x 64 MFMA tiles, diagonal-block inverses
+// in Dt), the Schur complement of the active rows and the proximal refinement with the
+// blocked solves -- polish_w.hip's compact-mode arithmetic.  The round's grouped passes
+// (exact P x, checks, scoring) then treat the date like every other.  The factor overwrites
+// the lower tiles of K, so the date's next round forms again (R_FORMED = 0).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                 pq_settings s, int ldk, int kmin) {
+  __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS];   // exactly 80 KiB: 2 per CU
+  const int b = blockIdx.x;
+  double* R = rec + (int64_t)b * PGR;
+  if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;
+  const int k = (int)R[R_K];
+  if (k <= kmin || k > ldk) return;
+  const int ma = (int)R[R_MA];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  if (ma > WMA) {
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  const int n = pb.n, ld = pb.ld;
+  const double* Cg = pb.Cg ? pb.Cg + (int64_t)b * pb.Cg_stride : nullptr;
+  PGWork wk(st, b, ld);
+  const double sc = R[R_SC];
+  const double delta = s.delta * sc;
+  const double ps = pb.p_scale ? pb.p_scale[b] : 1.0;
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  double* K = st.K + (int64_t)b * st.K_stride;
+  double* Dt = st.Dt + (int64_t)b * st.Dt_stride;
+  const int nbk = (k + TB - 1) / TB;
+  const int kp = nbk * TB;
+  // reduced rhs: rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F (pass 0 left the window part in pxb)
+  if (R[R_NZB] != 0.0)
+    for (int p = t; p < k; p += PT) wk.rF[p] -= ps * wk.pxb[wk.Fl[p]];
+  __syncthreads();
+  form_pff(lr, b, wk.Fl, k, nbk, psw, pd, K, ldk, smem);
+  const int info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
+  if (t == 0) R[R_FORMED] = 0.0;   // the lower tiles now hold L: no reuse of this P_FF
+  if (info) {
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  // vectors in the (now free) factor workspace
+  double* rx = smem;
+  double* t1 = smem + PG_KBIG;
+  double* dx = smem + 2 * PG_KBIG;
+  double* sx = smem + 3 * PG_KBIG;
+  double* t64 = smem + 4 * PG_KBIG;
+  double* y64p = t64 + TB;
+  double* part = y64p + 4 * TB;
+  double* U = wk.U;   // rows a of L^-1 C_aF' (pitch ld >= kp)
+  double* red = part + 4 * TB;
+  double* Sm = red + 16;
+  double* lamv = Sm + WMA * WMA;
+  double* dAv = lamv + WMA;
+  double* rl = dAv + WMA;
+  double* wl = rl + WMA;
+  int* s_al = reinterpret_cast<int*>(wl + WMA);
+  static_assert(5 * PG_KBIG + 6 * TB + 16 + WMA * WMA + 5 * WMA + WMA <= CHOL_LDS, "k_pg_big LDS layout");
+  __syncthreads();   // the factor is done with smem
+  if (t < ma) {
+    s_al[t] = (int)R[R_AL + t];
+    lamv[t] = R[R_SOL + t];
+    dAv[t] = R[R_DA + t];
+  }
+  __syncthreads();
+  // ---- U = L^-1 C_aF', S = U'U + delta I (tiny Cholesky, one thread) -------------------------
+  for (int a = 0; a < ma; ++a) {
+    const double* cr = Cg + (int64_t)s_al[a] * ld;
+    for (int p = t; p < kp; p += PT) rx[p] = p < k ? cr[wk.Fl[p]] : 0.0;
+    __syncthreads();
+    fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+    for (int p = t; p < kp; p += PT) U[(int64_t)a * ld + p] = t1[p];
+    __syncthreads();
+  }
+  for (int e = w; e < ma * ma; e += PW) {
+    const int ii = e / ma, jj = e % ma;
+    if (jj > ii) continue;
+    double sum = 0.0;
+    for (int p = l; p < k; p += 64) sum += U[(int64_t)ii * ld + p] * U[(int64_t)jj * ld + p];
+    sum = wave_sum(sum);
+    if (l == 0) Sm[ii * WMA + jj] = sum + (ii == jj ? delta : 0.0);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int sbad = 0;
+    for (int c = 0; c < ma && !sbad; ++c) {
+      double d = Sm[c * WMA + c];
+      for (int m = 0; m < c; ++m) d -= Sm[c * WMA + m] * Sm[c * WMA + m];
+      if (!(d > 0.0) || !isfinite(d)) { sbad = 1; break; }
+      d = sqrt(d);
+      Sm[c * WMA + c] = d;
+      for (int r = c + 1; r < ma; ++r) {
+        double v = Sm[r * WMA + c];
+        for (int m = 0; m < c; ++m) v -= Sm[r * WMA + m] * Sm[c * WMA + m];
+        Sm[r * WMA + c] = v / d;
+      }
+    }
+    red[0] = sbad;
+  }
+  __syncthreads();
+  if (red[0] != 0.0) {
+    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+    return;
+  }
+  for (int p = t; p < kp; p += PT) sx[p] = p < k ? wk.solx[p] : 0.0;
+  __syncthreads();
+  // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------------
+  for (int itr = 0; itr < s.refine_iters; ++itr) {
+    for (int p = w; p < k; p += PW) {   // rx = rF - P_FF x - C_aF' lam
+      double sum = 0.0;
+      for (int qq = l; qq < k; qq += 64) sum += pc_at(K, ldk, p, qq) * sx[qq];
+      sum = wave_sum(sum);
+      if (l == 0) {
+        double v = wk.rF[p] - sum;
+        for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + wk.Fl[p]] * lamv[a];
+        rx[p] = v;
+      }
+    }
+    for (int p = k + t; p < kp; p += PT) rx[p] = 0.0;
+    for (int a = w; a < ma; a += PW) {   // rl = dA - C_aF x
+      const double* c = Cg + (int64_t)s_al[a] * ld;
+      double sum = 0.0;
+      for (int p = l; p < k; p += 64) sum += c[wk.Fl[p]] * sx[p];
+      sum = wave_sum(sum);
+      if (l == 0) {
+        const double v = dAv[a] - sum;
+        rl[a] = fabs(v) <= 1e-14 * (1.0 + fabs(dAv[a]) + fabs(sum)) ? 0.0 : v;
+      }
+    }
+    __syncthreads();
+    double rm = 0.0;
+    for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
+    if (t < ma) rm = fmax(rm, fabs(rl[t]));
+    if (block_max(rm, red) <= 1e-13 * sc) break;
+    fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+    for (int a = w; a < ma; a += PW) {   // wl = U' t1 - rl
+      double sum = 0.0;
+      for (int p = l; p < k; p += 64) sum += U[(int64_t)a * ld + p] * t1[p];
+      sum = wave_sum(sum);
+      if (l == 0) wl[a] = sum - rl[a];
+    }
+    __syncthreads();
+    if (t == 0) {   // dlam = S^-1 wl
+      for (int ii = 0; ii < ma; ++ii) {
+        double v = wl[ii];
+        for (int jj = 0; jj < ii; ++jj) v -= Sm[ii * WMA + jj] * wl[jj];
+        wl[ii] = v / Sm[ii * WMA + ii];
+      }
+      for (int ii = ma - 1; ii >= 0; --ii) {
+        double v = wl[ii];
+        for (int jj = ii + 1; jj < ma; ++jj) v -= Sm[jj * WMA + ii] * wl[jj];
+        wl[ii] = v / Sm[ii * WMA + ii];
+      }
+    }
+    __syncthreads();
+    for (int p = t; p < kp; p += PT) {   // t1 <- t1 - U dlam ; dx = L^-T t1
+      double v = t1[p];
+      for (int a = 0; a < ma; ++a) v -= U[(int64_t)a * ld + p] * wl[a];
+      t1[p] = v;
+    }
+    __syncthreads();
+    bwd_solve(K, ldk, Dt, nbk, t1, dx, t64, part, y64p);
+    for (int p = t; p < k; p += PT) sx[p] += dx[p];
+    if (t < ma) lamv[t] += wl[t];
+    __syncthreads();
+  }
+  // ---- expand: xs = x_B off F, x_F on F; general multipliers by row ------------------------
+  for (int ii = t; ii < n; ii += PT) wk.xs[ii] = wk.xb[ii];
+  __syncthreads();
+  for (int p = t; p < k; p += PT) {
+    wk.xs[wk.Fl[p]] = sx[p];
+    wk.solx[p] = sx[p];
+  }
+  if (t < 64) R[R_LAM + t] = 0.0;
+  __syncthreads();
+  if (t < ma) {
+    R[R_LAM + s_al[t]] = lamv[t];
+    R[R_SOL + t] = lamv[t];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // grouped window passes: MODE 0 -> pxb = w_scale Xc'Xc x_B (dates with x_B != 0);
 // MODE 1 -> exact P x, gradient, active-set checks, final scoring of accepted dates
 // ---------------------------------------------------------------------------------------
@@ -1489,7 +1680,7 @@ namespace pq {
 // first use; NULL when that fails (everything then runs on the caller's stream).  One host
 // thread per device drives a round at a time (the engine's use).
 struct PgSide {
-  static constexpr int NS = 6;
+  static constexpr int NS = 7;
   bool ok = false;
   hipStream_t s[NS];
   hipEvent_t fork, join[NS];
@@ -1523,6 +1714,16 @@ static int group_form_min() {
   static const int v = [] {
     const char* e = getenv("PQ_PG_GFORM");
     return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
+// free sets beyond the LDS solve inside the pipeline (k_pg_big); PQ_PG_BIG=0 hands them to the
+// per-date kernel as before (A/B)
+static int pg_big() {
+  static const int v = [] {
+    const char* e = getenv("PQ_PG_BIG");
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
@@ -1577,7 +1778,9 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   hipStream_t str = (hipStream_t)stream;
   const int B = pb->batch;
   const int kmax = ldk < pq::PG_KMAX ? ldk : pq::PG_KMAX;
-  hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax, wide ? 1 : 0);
+  // free sets between the LDS solve and the K scratch: the grouped large-free-set solve
+  const int kbig = (pq::pg_big() && ldk > kmax) ? (ldk < pq::PG_KBIG ? ldk : pq::PG_KBIG) : kmax;
+  hipLaunchKernelGGL(pq::k_pg_setup, dim3(B), dim3(pq::PT), 0, str, *pb, *st, rec, kmax, wide ? 1 : 0, kbig);
   const dim3 gsplit(ngroups * pq::QS);
   hipLaunchKernelGGL(pq::k_pg_passA<0>, gsplit, dim3(pq::QT), 0, str, *lr, *pb, *st, rec, gdates, urows, ucnt, uoff,
                      umax, pass_scratch);
@@ -1606,6 +1809,8 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
     pq::launch_solve(i, pq::solve_waves(i), B, on(i), pb, st, rec, s, ldk, i ? KSB[i - 1] : 0);
   }
   if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, on(5))) return -1;   // free sets beyond kmax
+  if (kbig > kmax)
+    hipLaunchKernelGGL(pq::k_pg_big, dim3(B), dim3(pq::PT), 0, on(6), *lr, *pb, *st, rec, *s, ldk, kmax);
   for (int i = 0; side && i < pq::PgSide::NS; ++i)
     if ((used & (1 << i)) && (hipEventRecord(side->join[i], side->s[i]) != hipSuccess ||
                               hipStreamWaitEvent(str, side->join[i], 0) != hipSuccess)) {

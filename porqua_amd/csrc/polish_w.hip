@@ -28,87 +28,6 @@ namespace pq {
 
 constexpr int KMAX = 1024;   // free variables held in LDS
 
-// P_FF (+ dadd on the diagonal) in the compact polish storage described above
-struct FormW {
-  const double* K;
-  int64_t ld;
-  int k;
-  double dadd;
-  __device__ __forceinline__ double operator()(int gi, int gj) const {
-    if (gi >= k || gj >= k) return gi == gj ? 1.0 : 0.0;
-    double v = ((gi >> 6) == (gj >> 6)) ? K[(int64_t)gi * ld + gj] : K[(int64_t)min(gi, gj) * ld + max(gi, gj)];
-    if (gi == gj) v += dadd;
-    return v;
-  }
-};
-
-__device__ __forceinline__ double pc_at(const double* K, int64_t ld, int p, int q) {
-  return ((p >> 6) == (q >> 6)) ? K[(int64_t)p * ld + q] : K[(int64_t)min(p, q) * ld + max(p, q)];
-}
-
-// P_FF = psw Xc_F' Xc_F + pd I into the compact storage (lower tiles computed; diagonal
-// tiles stored in full, off-diagonal tiles transposed into the upper half).  One MFMA
-// tile product per lower tile, contracted over the window in 16-row chunks staged into LDS.
-PQ_DEVFN void form_pff(const pq_lowrank& lr, int b, const int* Fl, int k, int nbk, double psw,
-                         double pd, double* Ks, int64_t ldk, double* smem) {
-  const int T = lr.tlen[b];
-  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
-  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
-  const int t = threadIdx.x;
-  const int kr = t >> 4, i4 = (t & 15) * 4;
-  double* SA = smem;
-  double* SB = smem + STAGE;
-  const int ntile = nbk * (nbk + 1) / 2;
-  for (int tile = 0; tile < ntile; ++tile) {
-    int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-    while ((I + 1) * (I + 2) / 2 <= tile) ++I;
-    while (I * (I + 1) / 2 > tile) --I;
-    const int J = tile - I * (I + 1) / 2;
-    int ca[4], cb[4];
-    double ma[4], mb[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int pa = I * TB + i4 + e, pb_ = J * TB + i4 + e;
-      ca[e] = pa < k ? Fl[pa] : -1;
-      cb[e] = pb_ < k ? Fl[pb_] : -1;
-      ma[e] = (ca[e] >= 0 && mu) ? mu[ca[e]] : 0.0;
-      mb[e] = (cb[e] >= 0 && mu) ? mu[cb[e]] : 0.0;
-    }
-    Acc acc;
-    acc.zero();
-    for (int t0 = 0; t0 < T; t0 += KC) {
-      const int tt = t0 + kr;
-      const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
-      double va[4], vb[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        va[e] = (row && ca[e] >= 0) ? row[ca[e]] - ma[e] : 0.0;
-        vb[e] = (row && cb[e] >= 0) ? row[cb[e]] - mb[e] : 0.0;
-      }
-      __syncthreads();   // the previous chunk's MFMAs are done with SA / SB
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        SA[kr * LDW + i4 + e] = va[e];
-        SB[kr * LDW + i4 + e] = vb[e];
-      }
-      __syncthreads();
-      mma_lds(acc, SA, SB, KC);
-    }
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int nn = 0; nn < 2; ++nn)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gi = I * TB + acc_row(m, r), gj = J * TB + acc_col(nn);
-          const double v = psw * acc.c[m][nn][r] + (gi == gj ? pd : 0.0);
-          if (I == J) Ks[(int64_t)gi * ldk + gj] = v;
-          else Ks[(int64_t)gj * ldk + gi] = v;
-        }
-  }
-  __syncthreads();
-}
-
 // Woodbury mode: C = cdiag I + Xc diag(free) Xc' (T x T) into the lower tiles (diagonal
 // tiles in full) of Ks; rows / columns >= T are the identity.  Contraction over all n
 // columns (free-masked), 16 at a time through LDS, one MFMA tile product per lower tile.

@@ -1240,11 +1240,17 @@ def slide_plan(rows, tlen, group: int = 32, smax: int = 64, smin: int = 1):
         h = min(tmax, int(smax) + 1)
         s = ((prev[:, :h] < cur[:, :1]) & (col[None, :h] < tp[:, None])).sum(1)
         cand = (tp == tc) & (tc > 1) & (s >= smin) & (s <= smax)
-        match = np.zeros(B - 1, dtype=bool)
-        for sv in np.unique(s[cand]).tolist():   # rows[d][:T-s] == rows[d-1][s:T], per shift value
+        # windows that are one contiguous run of panel rows (no gap: last - first = T - 1)
+        # overlap exactly when they have the same length -- no element compare needed
+        last = rows[np.arange(B), np.maximum(tlen - 1, 0)]
+        contig = (last - rows[:, 0]) == (tlen - 1)
+        match = cand & contig[:-1] & contig[1:]
+        need = cand & ~match
+        for sv in np.unique(s[need]).tolist():   # rows[d][:T-s] == rows[d-1][s:T], per shift value
+            sel = np.flatnonzero(need & (s == sv))
             w = tmax - sv
-            ok = ((prev[:, sv:] == cur[:, :w]) | (col[None, :w] >= (tc - sv)[:, None])).all(1)
-            match |= cand & (s == sv) & ok
+            ok = ((prev[sel, sv:] == cur[sel, :w]) | (col[None, :w] >= (tc[sel] - sv)[:, None])).all(1)
+            match[sel[ok]] = True
         good = cand & match
         shift[1:] = np.where(good, s, 0)
     else:
@@ -1296,8 +1302,15 @@ class GroupPlan:
         self.ok = B > 0 and int(tlen.min()) >= 2 and int(tlen.max()) <= umax
         gs, sh = slide_plan(rows, tlen, group=gmax, smax=smax, smin=0)
         groups = []
+        # a slide group whose whole union fits (first window + every later shift <= umax) is
+        # one date group; only the others are cut greedily, date by date
+        cs = np.concatenate([[0], np.cumsum(sh[1:], dtype=np.int64)]) if B else np.zeros(1, np.int64)
+        fits = (tlen[gs[:-1]] + cs[gs[1:] - 1] - cs[gs[:-1]]) <= umax if B else np.zeros(0, bool)
         tl_l, sh_l = tlen.tolist(), sh.tolist()
-        for a, b in zip(gs[:-1].tolist(), gs[1:].tolist()):
+        for a, b, f in zip(gs[:-1].tolist(), gs[1:].tolist(), fits.tolist()):
+            if f:
+                groups.append((a, b))
+                continue
             start, U = a, tl_l[a]
             for d in range(a + 1, b):
                 if U + sh_l[d] > umax:

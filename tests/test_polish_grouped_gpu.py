@@ -4,7 +4,8 @@ it restructures (polish_w.hip, pq_polish_w_batched): same ADMM point in, the sam
 weights, statuses, objective and multipliers out (to rounding), on the shapes the
 backtests use -- long-only min-variance at n = 1000 (bench), capped boxes (fixed weights at
 an upper bound: the P x_B pass), sector caps (active general rows), uncentred least
-squares, and a free set beyond the LDS solve (handed to the per-date kernel).  The grouped
+squares, free sets beyond the LDS solve (the pipeline's large-free-set solve up to the K
+scratch's 256, the per-date kernel beyond).  The grouped
 side forms P_FF from one union Gram per polish group where at least three of its dates form
 in a round (k_pg_form_grp), so these cases also pin that derivation against the per-date
 window products."""
@@ -104,18 +105,39 @@ def test_grouped_polish_matches_per_date_polish(device, case):
 
 
 def test_grouped_polish_hands_large_free_sets_to_the_per_date_kernel(device):
-    """Free sets beyond the LDS solve (k > 128: the tracking problem holds most assets
-    strictly inside the box) are FALLBACK problems and still end SOLVED with the per-date
-    kernel's answer."""
+    """Free sets beyond the K scratch of the pipeline (k > ldk = 256: the tracking problem holds
+    most of its 500 assets strictly inside the box) are FALLBACK problems and still end SOLVED
+    with the per-date kernel's answer."""
     qb, lr, gp = _problem(device, 500, 120, 30, 0.1, centred=False)
     st_ = engine.Settings(rho0_rel=0.5)
     xa, sa, oa, *_ = _solve(qb, lr, gp, False, st_)
     xb, sb, ob, _, _, outb, rec = _solve(qb, lr, gp, True, st_)
     assert np.array_equal(sa, sb)
     assert np.abs(xa - xb).max() <= 1e-10
-    big = outb[:, _lib.PQ_OUT_NFREE] > 128
+    big = outb[:, _lib.PQ_OUT_NFREE] > 256
     assert big.any()
     assert np.all(rec[big] == _lib.PQ_PG_FALLBACK)
+
+
+def test_large_free_sets_are_solved_inside_the_pipeline(device):
+    """Free sets between the LDS solve and the K scratch (128 < k <= 256: a ridge keeps most of
+    400 assets strictly inside the box, as the tracking windows of configs 1/2 do with 160..220
+    free assets) go through the grouped large-free-set solve (k_pg_big: P_FF formed from the
+    window, MFMA tile Cholesky, Schur complement, proximal refinement) instead of the per-date
+    kernel, and give its answers to rounding."""
+    qb, lr, gp = _problem(device, 400, 100, 24, 1.0)
+    qb.p_diag = torch.full((qb.batch,), 5e-3, dtype=torch.float64, device=device)
+    xa, sa, oa, ya, za, outa, _ = _solve(qb, lr, gp, False)
+    xb, sb, ob, yb, zb, outb, rec = _solve(qb, lr, gp, True)
+    assert np.all(sa == _lib.PQ_SOLVED) and np.array_equal(sa, sb)
+    k = outb[:, _lib.PQ_OUT_NFREE]
+    assert ((k > 128) & (k <= 256)).mean() >= 0.5, k
+    assert np.all(rec == _lib.PQ_PG_DONE), np.unique(rec, return_counts=True)
+    assert np.abs(xa - xb).max() <= 1e-10, np.abs(xa - xb).max()
+    assert np.abs(oa - ob).max() <= 1e-12 * max(1.0, np.abs(oa).max()) + 1e-15
+    sc = max(np.abs(ya).max(), np.abs(za).max(), 1e-30)
+    assert np.abs(ya - yb).max() <= 1e-8 * sc and np.abs(za - zb).max() <= 1e-8 * sc
+    assert np.array_equal(outa[:, _lib.PQ_OUT_NFREE], k)
 
 
 def test_loose_admm_stop_before_the_pipeline(device):
@@ -140,11 +162,11 @@ def test_loose_admm_stop_before_the_pipeline(device):
 
 
 def test_loose_admm_stop_resumes_the_hand_offs(device):
-    """Dates the pipeline hands to the per-date kernel (a ridge keeps every asset strictly
-    inside the box: free sets of ~n > 128) resume ADMM to eps_abs before that polish, so the
-    answer is the one from the eps_abs point."""
-    qb, lr, gp = _problem(device, 400, 100, 24, 1.0)
-    qb.p_diag = torch.full((qb.batch,), 5e-3, dtype=torch.float64, device=device)
+    """Dates the pipeline hands to the per-date kernel (a strong ridge keeps every asset
+    strictly inside the box: free sets beyond the K scratch, k = n = 800 > 256) resume ADMM to
+    eps_abs before that polish, so the answer is the one from the eps_abs point."""
+    qb, lr, gp = _problem(device, 800, 100, 24, 1.0)
+    qb.p_diag = torch.full((qb.batch,), 5e-2, dtype=torch.float64, device=device)
     xa, sa, *_ = _solve(qb, lr, gp, True)
     xb, sb, _, _, _, outb, rec = _solve(qb, lr, gp, True, eps_grouped=2e-2)
     assert np.all(sa == _lib.PQ_SOLVED) and np.array_equal(sa, sb)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """cProfile of the drop-in path: Backtest.run(solver_name='mi355x') after one warm-up run --
 default: the usa-shaped panel, every date (configs 1/2 shape); ``mv3``: bench.py's end-to-end
-line (MeanVariance, config-3 synthetic panel, 4749 daily dates).  Experiment tooling."""
+line (MeanVariance, config-3 synthetic panel, 4749 daily dates); ``monthly``: config 2 as the
+reference notebook runs it (13 monthly dates).  Experiment tooling."""
 import cProfile
 import os
 import pstats
@@ -43,6 +44,11 @@ def mv3_service():
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "mv3":
         make = mv3_service()
+    elif len(sys.argv) > 1 and sys.argv[1] == "monthly":   # config 2 as the notebook runs it: 13 dates
+        X, y = usa_data()
+        d = X.index.values.astype("datetime64[D]")
+        reb = [str(r) for r in d[d > np.datetime64("2022-06-01")][::21]]
+        make = lambda: service(X, y, reb)  # noqa: E731
     else:
         X, y = usa_data()
         d = X.index.values.astype("datetime64[D]")
