@@ -87,6 +87,10 @@ typedef struct pq_settings {
    * its lower bound when x - lb < polish_fix_rel * max_j (x_j - lb_j) at the ADMM point
    * (0: OSQP's rule alone) */
   double polish_fix_rel;
+  /* grouped polish, LDS solve: free variables the solve leaves outside their box are fixed at
+   * that bound and the reduced system solved again inside the same round, at most this many
+   * times (0: one solve per round, the checks of the round's end fix them) */
+  int32_t polish_inner;
 } pq_settings;
 
 /* Low-rank description of P for T < n (the backtest path): P_eff = p_scale[b] *

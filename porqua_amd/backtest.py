@@ -208,6 +208,35 @@ class BatchStage:
         return self._log_panel
 
 
+class _PanelUpload:
+    """The return panel's host -> device copy on a worker thread (torch releases the GIL for
+    the copy, so the caller's host work -- window rows, constraints, the group plan -- runs
+    meanwhile).  ``result()`` joins and returns the device tensor (or re-raises)."""
+
+    def __init__(self, frame):
+        import threading
+        self._out = None
+        self._err = None
+        self._frame = frame
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _run(self):
+        import torch
+        from . import engine
+        try:   # (no device: the error surfaces in result(), where the serial path would raise it too)
+            R = np.ascontiguousarray(self._frame.to_numpy(dtype=np.float64))
+            self._out = torch.from_numpy(R).to(engine.default_device())
+        except BaseException as ex:   # re-raised in the caller's thread
+            self._err = ex
+
+    def result(self):
+        self._t.join()
+        if self._err is not None:
+            raise self._err
+        return self._out
+
+
 def _batchable(bs) -> bool:
     """Batched mode needs builders whose output does not depend on the date beyond the
     return / benchmark windows: the standard ones, or any set the caller declares
@@ -339,6 +368,9 @@ class Backtest:
             return None
         # the whole frame when the selection is every column in order (no 8 T n-byte copy)
         Xs = X if list(X.columns) == list(universe) else X[universe]
+        # the panel upload (D x n FP64 over PCIe) runs on a worker thread while this thread
+        # builds the window and group plans (the copy releases the GIL); _solve_shard joins it
+        upload = _PanelUpload(Xs)
         idx = pd.DatetimeIndex(Xs.index)
         dates = idx.values.astype("datetime64[D]")
         rows, tlen = engine.window_rows(dates, np.array(rebdates, dtype="datetime64[D]"), width)
@@ -356,7 +388,7 @@ class Backtest:
         lb = cons.box["lower"].to_numpy(dtype=np.float64) if boxed else None
         ub = cons.box["upper"].to_numpy(dtype=np.float64) if boxed else None
         return {"rebdates": rebdates, "universe": universe, "Xs": Xs, "bm": bm, "rows": rows, "tlen": tlen,
-                "GhAb": GhAb, "lb": lb, "ub": ub, "l1term": l1term, "l1both": l1both}
+                "GhAb": GhAb, "lb": lb, "ub": ub, "l1term": l1term, "l1both": l1both, "upload": upload}
 
     def _solve_shard(self, bs, st, lo: int, hi: int):
         """Phase B (device): dates [lo, hi) of the staged run, chunked to bound HBM use.
@@ -369,25 +401,37 @@ class Backtest:
         l1term, l1both = st["l1term"], st["l1both"]
         dev = engine.default_device()
         settings = engine.Settings.from_params(opt.params)
-        panel = engine.Panel(st["Xs"].to_numpy(dtype=np.float64), st["bm"], device=dev)
-        n = panel.n
+        mg = sum(0 if GhAb[k] is None else np.atleast_2d(GhAb[k]).shape[0] for k in ("A", "G"))
+        if l1term is not None:
+            mg += 1 if l1term.kind == "budget" else 0
+        n = len(st["universe"])
+        lad = hasattr(opt, "lad_batch")       # LAD: the LP on the device IPM (porqua_amd/lad.py)
+        chunk = int(bs.settings.get("batch_chunk", 0) or _auto_chunk(n))
+        # the first chunk's group plan (host numpy) while the panel upload is still in flight
+        plan0 = None
+        if (not lad and l1both is None and bs.settings.get("lowrank", True)
+                and engine.lowrank_shape_ok(n, int(rows.shape[1]), mg)):
+            e0 = min(hi, lo + chunk)
+            plan0 = (lo, e0, engine.GroupPlan(rows[lo:e0], tlen[lo:e0], dev))
+        upload = st.get("upload")
+        R = upload.result() if upload is not None else st["Xs"].to_numpy(dtype=np.float64)
+        panel = engine.Panel(R, st["bm"], device=dev)
         # windows with missing values (checked on the device copy): the objectives that
         # support them batch with the pairwise-complete covariance (MeanVariance); the others
         # keep the serial path
         if panel.has_nan and not getattr(opt, "batch_handles_nan", False):
             return False, None, None, None, None
-        chunk = int(bs.settings.get("batch_chunk", 0) or _auto_chunk(n))
-        W = np.zeros((hi - lo, n))
+        # the weight panel lands in page-locked host memory (one DMA, no pageable bounce; the
+        # Portfolio objects keep views of its rows)
+        Wt = torch.empty((hi - lo, n), dtype=torch.float64, pin_memory=True) if dev.type == "cuda" else None
+        W = Wt.numpy() if Wt is not None else np.zeros((hi - lo, n))
         ST = np.zeros(hi - lo, dtype=np.int32)
         OBJ = np.zeros(hi - lo)
-        mg = sum(0 if GhAb[k] is None else np.atleast_2d(GhAb[k]).shape[0] for k in ("A", "G"))
         split_panel = None
         if l1term is not None:
             if lb is None or ub is None:
                 return False, None, None, None, None   # the split needs a box (serial path raises)
             split_panel = engine.Panel(torch.cat([panel.R, -panel.R], 1).contiguous(), None, device=dev)
-            mg += 1 if l1term.kind == "budget" else 0
-        lad = hasattr(opt, "lad_batch")       # LAD: the LP on the device IPM (porqua_amd/lad.py)
         if lad:
             if l1term is not None or l1both is not None:
                 return False, None, None, None, None
@@ -410,6 +454,8 @@ class Backtest:
                 W[s - lo:e - lo], ST[s - lo:e - lo], OBJ[s - lo:e - lo] = r
                 continue
             stage = BatchStage(panel, rows[s:e], tlen[s:e], dev)
+            if plan0 is not None and plan0[:2] == (s, e):
+                stage._groups = plan0[2]
             # T + mg < n: the Woodbury (window-form) solver; its consumers read P's lower
             # triangle only (engine.lowrank_shape_ok: same test as solve_lowrank's)
             stage.prefer_lowrank = (bs.settings.get("lowrank", True)
@@ -451,10 +497,18 @@ class Backtest:
                 OBJ[s - lo:e - lo] = (res.obj + const).cpu().numpy()
             else:
                 if stage.lowrank is not None:
-                    res = engine.solve_lowrank(qb, stage.lowrank, settings, groups=stage.group_plan())
+                    # centred windows (the mean-variance family: no wide polish rounds): the
+                    # sync-free stages -- one ADMM launch, four polish rounds, one flag read
+                    # (dates still pending after them take the host-driven rounds)
+                    sf = stage.lowrank.mu is not None
+                    res = engine.solve_lowrank(qb, stage.lowrank, settings, groups=stage.group_plan(),
+                                               sync_free=sf, sf_rounds=4 if sf else None)
                 else:
                     res = engine.solve(qb, settings)
-                W[s - lo:e - lo] = res.x[:, :n].cpu().numpy()
+                if Wt is not None:
+                    Wt[s - lo:e - lo].copy_(res.x[:, :n], non_blocking=True)   # ordered before the reads below
+                else:
+                    W[s - lo:e - lo] = res.x[:, :n].cpu().numpy()
                 OBJ[s - lo:e - lo] = res.obj.cpu().numpy()
             ST[s - lo:e - lo] = res.status.cpu().numpy()
         return ok, W, ST, OBJ, path

@@ -20,7 +20,10 @@ enum : int {
   R_W = 320, R_NFX = 321, R_FIX = 324, R_FIXV = 332, R_FXL = 340,
   // R_GFORM = g + 1: this round's P_FF comes from the group Gram (k_pg_form_grp) in the
   // pass scratch of the date's polish group g (0: the date forms alone)
-  R_GFORM = 348
+  R_GFORM = 348,
+  // R_KB: the free-set size setup found this round -- the LDS solve's buckets select on it
+  // (the solve's inner primal loop lowers R_K while the other buckets may still be reading)
+  R_KB = 349
 };
 constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
 constexpr int PG_KBIG = 256;   // largest free set of the grouped large-free-set solve (k_pg_big)
@@ -30,7 +33,7 @@ constexpr int PG_MGMAX = 32;   // general rows
 // variables as bordered rows (at most PG_WMB of them)
 constexpr int PG_WMB = 8;
 constexpr int PG_WG_MAX = 24;   // general rows of the wide mode
-static_assert(R_FXL + PG_WMB <= R_GFORM && R_GFORM < PQ_PG_RECORD, "PQ_PG_RECORD too small");
+static_assert(R_FXL + PG_WMB <= R_GFORM && R_KB < PQ_PG_RECORD, "PQ_PG_RECORD too small");
 
 struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
   double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;

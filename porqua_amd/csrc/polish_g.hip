@@ -259,6 +259,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
   }
   if (t == 0) {
     R[R_K] = k;
+    R[R_KB] = k;
     R[R_MA] = ma;
     R[R_NZB] = nzb;
     R[R_W] = 0;
@@ -825,7 +826,7 @@ __device__ __forceinline__ void b_bwd(const double* Lp, int k, double* y, double
 
 template <int KS, int NW>
 __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s,
-                                                      int ldk, int klo) {
+                                                      int ldk, int klo, int inner) {
   constexpr int T = 64 * NW;
   constexpr int NP = KS * (KS + 1) / 2;
   __shared__ double Lp[NP];
@@ -839,8 +840,9 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;
-  const int k = (int)R[R_K];
-  if (k <= klo || k > KS) return;
+  const int kb = (int)R[R_KB];   // (the bucket key: R_K may already be lowered by this kernel)
+  if (kb <= klo || kb > KS) return;
+  int k = kb;
   const int ma = (int)R[R_MA];
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   if (ma > WMA) {
@@ -867,7 +869,21 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
   // from an earlier round's form) the positions in that free list
   const bool reuse = R[R_REUSE] != 0.0;
   for (int p = t; p < k; p += T) s_map[p] = reuse ? wk.posF[wk.Fl[p]] : p;
+  for (int p = t; p < k; p += T) xF[p] = wk.solx[p];
+  if (t < ma) {
+    s_al[t] = (int)R[R_AL + t];
+    lamv[t] = R[R_SOL + t];
+    dAv[t] = R[R_DA + t];
+  }
+  const bool has_box = pb.lb != nullptr;
+  const double* lb = has_box ? pb.lb + (int64_t)b * pb.box_stride : nullptr;
+  const double* ub = has_box ? pb.ub + (int64_t)b * pb.box_stride : nullptr;
   __syncthreads();
+  // inner primal loop: a free variable the solve leaves outside its box is fixed at that bound
+  // and the reduced system (a principal submatrix of the same P_FF in K) solved again here,
+  // up to `inner` times, instead of one whole round (window passes, checks, setup) per such
+  // step; the round's checks then release wrongly fixed variables by their dual sign as before
+  for (int it_in = 0;; ++it_in) {
   {   // packed triangle, flat index (independent loads, 8 per thread in flight)
     const int np_ = k * (k + 1) / 2;
     int r = 0, e0 = 0;   // row of the thread's element: advance incrementally
@@ -891,12 +907,6 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
         if (e < np_) Lp[e] = v[j] + ((dg >> j) & 1 ? delta : 0.0);
       }
     }
-  }
-  for (int p = t; p < k; p += T) xF[p] = wk.solx[p];
-  if (t < ma) {
-    s_al[t] = (int)R[R_AL + t];
-    lamv[t] = R[R_SOL + t];
-    dAv[t] = R[R_DA + t];
   }
   WSTAMP(0);
   __syncthreads();
@@ -1018,6 +1028,80 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
     __syncthreads();
     WSTAMP(4);
   }
+  // ---- inner primal step: the free variables outside their box, fixed at the bound they
+  // cross (k_pg_post's test), the others compacted in order; the reduced rhs and the active
+  // rows' rhs take the fixed values (the P_FB columns are K's columns) -------------------------
+  if (it_in >= inner || !has_box) break;   // uniform
+  {
+    int* iw = reinterpret_cast<int*>(sc4 + 2 * KS);   // 4 x KS ints in the free half of sc4
+    int* s_m2 = iw;             // kept: K position
+    int* s_f2 = iw + KS;        // kept: variable
+    int* s_vp = iw + 2 * KS;    // violator: K position
+    int* s_vi = iw + 3 * KS;    // violator: 4 variable + bound side (1 lower, 2 upper)
+    double* s_vv = rx;          // violator: bound value
+    if (w == 0) {
+      int nk = 0, nv = 0;
+      for (int p0 = 0; p0 < k; p0 += 64) {
+        const int p = p0 + l;
+        int f = 0, i = 0;
+        double v = 0.0;
+        if (p < k) {
+          i = wk.Fl[p];
+          const double xi = xF[p];
+          if (!isinf(lb[i]) && xi < lb[i] - 1e-12 * (1.0 + fabs(lb[i]))) { f = 1; v = lb[i]; }
+          else if (!isinf(ub[i]) && xi > ub[i] + 1e-12 * (1.0 + fabs(ub[i]))) { f = 2; v = ub[i]; }
+        }
+        const unsigned long long mv = __ballot(p < k && f != 0);
+        const unsigned long long mk = __ballot(p < k && f == 0);
+        const unsigned long long below = (1ull << l) - 1ull;
+        if (p < k && f != 0) {
+          const int j = nv + __popcll(mv & below);
+          s_vp[j] = s_map[p];
+          s_vi[j] = 4 * i + f;
+          s_vv[j] = v;
+        } else if (p < k) {
+          const int j = nk + __popcll(mk & below);
+          s_m2[j] = s_map[p];
+          s_f2[j] = i;
+          t1[j] = xF[p];
+          t2[j] = wk.rF[p];
+        }
+        nv += __popcll(mv);
+        nk += __popcll(mk);
+      }
+      if (l == 0) s_flag = nv;
+    }
+    __syncthreads();
+    const int nv = s_flag;
+    if (nv == 0 || nv == k) break;   // uniform: feasible, or nothing left free (the rounds decide)
+    const int k2 = k - nv;
+    for (int p = t; p < k2; p += T) {
+      const int mp = s_m2[p];
+      double r = t2[p];
+      for (int j = 0; j < nv; ++j)
+        if (s_vv[j] != 0.0) r = fma(-K[(int64_t)mp * ldk + s_vp[j]], s_vv[j], r);
+      wk.rF[p] = r;
+      wk.Fl[p] = s_f2[p];
+      s_map[p] = mp;
+      xF[p] = t1[p];
+    }
+    for (int j = t; j < nv; j += T) {
+      const int i = s_vi[j] >> 2;
+      wk.fl[i] = s_vi[j] & 3;
+      wk.xb[i] = s_vv[j];
+    }
+    for (int a = w; a < ma; a += NW) {
+      const double* cr = Cg + (int64_t)s_al[a] * ld;
+      double sum = 0.0;
+      for (int j = l; j < nv; j += 64) sum += cr[s_vi[j] >> 2] * s_vv[j];
+      sum = wave_sum(sum);
+      if (l == 0) dAv[a] -= sum;
+    }
+    if (t == 0) R[R_K] = k2;
+    k = k2;
+    __syncthreads();
+  }
+  }   // inner primal loop
   // ---- expand: xs = x_B off F, x_F on F; general multipliers by row ------------------------
   for (int ii = t; ii < n; ii += T) wk.xs[ii] = wk.xb[ii];
   __syncthreads();
@@ -1743,12 +1827,13 @@ static int solve_waves(int bucket) {
 template <int KS>
 static void launch_solve_ks(int nw, int B, hipStream_t str, const pq_problem* pb, pq_state* st, double* rec,
                             const pq_settings* s, int ldk, int klo) {
+  const int inner = s->polish_inner > 0 ? s->polish_inner : 0;
   if (nw == 1)
-    hipLaunchKernelGGL((k_pg_solve<KS, 1>), dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, klo);
+    hipLaunchKernelGGL((k_pg_solve<KS, 1>), dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, klo, inner);
   else if (nw == 2)
-    hipLaunchKernelGGL((k_pg_solve<KS, 2>), dim3(B), dim3(128), 0, str, *pb, *st, rec, *s, ldk, klo);
+    hipLaunchKernelGGL((k_pg_solve<KS, 2>), dim3(B), dim3(128), 0, str, *pb, *st, rec, *s, ldk, klo, inner);
   else
-    hipLaunchKernelGGL((k_pg_solve<KS, 4>), dim3(B), dim3(256), 0, str, *pb, *st, rec, *s, ldk, klo);
+    hipLaunchKernelGGL((k_pg_solve<KS, 4>), dim3(B), dim3(256), 0, str, *pb, *st, rec, *s, ldk, klo, inner);
 }
 static void launch_solve(int bucket, int nw, int B, hipStream_t str, const pq_problem* pb, pq_state* st,
                          double* rec, const pq_settings* s, int ldk, int klo) {

@@ -108,6 +108,10 @@ class Settings:
     # the GPU (profiles/r03N_*): 0 / 0.05 / 0.1 -> 363k / 378k / 372k QPs/s, 3.31 / 2.86 / 3.0
     # rounds on average, at most 5 / 5 / 6.  Centred windows only (k_pg_init)
     polish_fix_rel: float = 0.05
+    # grouped polish, LDS solve (k_pg_solve): free variables outside their box are fixed at
+    # it and the reduced system re-solved inside the round, up to this many times per round,
+    # instead of one whole round (window passes, checks, setup) per such step
+    polish_inner: int = 2
 
     def to_c(self) -> _lib.PQSettings:
         names = {f[0] for f in _lib.PQSettings._fields_}

@@ -23,13 +23,15 @@ from porqua_amd.synthetic import factor_panel
 pytestmark = pytest.mark.gpu
 
 
-def _problem(device, n, T, D, ub, stride=1, centred=True):
+def _problem(device, n, T, D, ub, stride=1, centred=True, budget=True, caps=0):
     ends = list(range(T + 5, T + 5 + D * stride, stride))
     dates, R, y, sec = factor_panel(max(ends) + 1, n)
     rows, tlen = engine.window_rows(dates, dates[ends], T)
     pan = engine.Panel(R, y, device=device)
     r_d, t_d = pan.rows_to_device(rows, tlen)
-    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)), b=np.ones(1),
+    G = np.stack([(sec == g).astype(float) for g in range(caps)]) if caps else None
+    qb = engine.QPBatch.from_dense(np.zeros((1, n, n)), np.zeros((1, n)), A=np.ones((1, n)) if budget else None,
+                                   b=np.ones(1) if budget else None, G=G, h=np.full(caps, 0.3) if caps else None,
                                    lb=np.zeros(n), ub=np.full(n, ub), device=device)
     qb.batch = D
     qb.P = None
@@ -126,3 +128,21 @@ def test_gcap_uncentred_tracking_default_settings(device):
     fa, fb = _objective(qb, lr, xa), _objective(qb, lr, xb)
     assert np.abs(fa - fb).max() <= 1e-9 * np.abs(fa).max(), np.abs(fa - fb).max()
     assert np.abs(xb.sum(1) - 1).max() < 1e-10 and xb.min() > -1e-10
+
+
+@pytest.mark.parametrize("budget,caps", [(False, 0), (True, 2)])
+def test_gcap_general_row_variants_same_iterates(device, budget, caps):
+    """The kernel's general-row variants beyond the budget alone: none (box only; q = -mu so
+    the optimum is not the origin) and the budget with two sector caps (three register-resident
+    rows): the same ADMM iterates as the per-date form with one fixed rho."""
+    qb, lr, gp = _problem(device, 600, 150, 40, 0.2, budget=budget, caps=caps)
+    if not budget:
+        qb.q = (-lr.mu * 50.0).contiguous()
+    assert qb.mg == int(budget) + caps
+    st = engine.Settings(rho0_rel=0.0, rho0=0.01, rho0_qrel=0.0, adapt_interval=0)
+    xa, sa, ia, cap_a, _ = _run(qb, lr, gp, False, st, polish=False)
+    xb, sb, ib, cap_b, _ = _run(qb, lr, gp, True, st, polish=False)
+    assert cap_a == "band" and cap_b == "group"
+    assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED), (sa, sb)
+    assert np.abs(ia - ib).max() <= 1, (ia, ib)
+    assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()

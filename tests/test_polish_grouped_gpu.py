@@ -46,15 +46,15 @@ def _problem(device, n, T, D, ub, ngroups_rows=0, cap=0.3, centred=True, stride=
     return qb, lr, gp
 
 
-def _solve(qb, lr, gp, grouped_polish, settings=None, eps_grouped=0.0, polish_fix_rel=0.0):
+def _solve(qb, lr, gp, grouped_polish, settings=None, eps_grouped=0.0, polish_fix_rel=0.0, polish_inner=0):
     """(wide rounds off: this file pins the LDS-solve pipeline against the per-date kernel;
     tests/test_polish_wide_gpu.py covers the wide rounds.  The looser ADMM stop before the
-    pipeline (Settings.eps_grouped) and the pipeline's extra lower-bound classification
-    (Settings.polish_fix_rel) are off unless asked for: both sides start from the same ADMM
-    point and the same active set.)"""
+    pipeline (Settings.eps_grouped), the pipeline's extra lower-bound classification
+    (Settings.polish_fix_rel) and its inner primal steps (Settings.polish_inner) are off unless
+    asked for: both sides start from the same ADMM point and take the same active sets.)"""
     import dataclasses
     settings = dataclasses.replace(settings or engine.Settings(), eps_grouped=eps_grouped,
-                                   polish_fix_rel=polish_fix_rel)
+                                   polish_fix_rel=polish_fix_rel, polish_inner=polish_inner)
     ws = engine.Workspace(qb, dense=False)
     assert engine.grouped_applicable(qb, lr, gp, ws)
     res = engine.solve_lowrank(qb, lr, settings, ws=ws, groups=gp, grouped_polish=grouped_polish,
@@ -191,3 +191,26 @@ def test_fix_rel_classification_same_optimum(device, case):
     assert (rec == _lib.PQ_PG_DONE).mean() >= 0.8, np.unique(rec, return_counts=True)
     assert np.abs(xa - xb).max() <= 1e-8, np.abs(xa - xb).max()
     assert np.max(np.abs(ob - oa) / np.maximum(np.abs(oa), 1e-30)) <= 1e-12
+
+
+def test_inner_primal_steps_same_optimum_fewer_rounds(device):
+    """Settings.polish_inner (k_pg_solve fixes the free variables its solve leaves outside the
+    box and re-solves the reduced system inside the round): the bench shape with the bench's
+    settings (loose ADMM stop, first-active-set rule) reaches the same certified optimum as one
+    solve per round, in no more rounds on average."""
+    qb, lr, gp = _problem(device, 1000, 252, 48, 1.0)
+    d = engine.Settings()
+    assert d.polish_inner > 0
+    runs = {}
+    for inner in (0, d.polish_inner):
+        runs[inner] = _solve(qb, lr, gp, True, d, eps_grouped=d.eps_grouped, polish_fix_rel=d.polish_fix_rel,
+                             polish_inner=inner)
+    xa, sa, oa, _, _, outa, reca = runs[0]
+    xb, sb, ob, _, _, outb, recb = runs[d.polish_inner]
+    assert np.all(sa == _lib.PQ_SOLVED) and np.array_equal(sa, sb)
+    assert np.all(recb == _lib.PQ_PG_DONE), np.unique(recb, return_counts=True)
+    assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()
+    assert np.abs(oa - ob).max() <= 1e-10 * max(1.0, np.abs(oa).max())
+    assert np.array_equal(outa[:, _lib.PQ_OUT_NFREE], outb[:, _lib.PQ_OUT_NFREE])
+    ra, rb = outa[:, _lib.PQ_OUT_ROUNDS], outb[:, _lib.PQ_OUT_ROUNDS]
+    assert rb.mean() <= ra.mean(), (ra.mean(), rb.mean())

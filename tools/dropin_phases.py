@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Phase split of the drop-in Backtest.run at the config-3 shape (bench.py's end_to_end line:
+MeanVariance, 4749 daily dates, n = 1000): each phase bracketed by device synchronisations so
+host and device time land on the phase that causes them.  Experiment tooling.
+
+    python tools/dropin_phases.py [runs]"""
+import os
+import sys
+import time
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from porqua_amd import backtest as bt_mod, engine  # noqa: E402
+from porqua_amd.backtest import Backtest  # noqa: E402
+from tools.prof_dropin import mv3_service  # noqa: E402
+
+ACC = defaultdict(float)
+CNT = defaultdict(int)
+
+
+def timed(owner, name, label):
+    fn = getattr(owner, name)
+
+    def wrap(*a, **k):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = fn(*a, **k)
+        torch.cuda.synchronize()
+        ACC[label] += time.perf_counter() - t0
+        CNT[label] += 1
+        return r
+    setattr(owner, name, wrap)
+
+
+def main():
+    runs = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    make = mv3_service()
+    Backtest().run(make())          # warm-up (library load, allocator, plans' first use)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(runs):
+        Backtest().run(make())
+    torch.cuda.synchronize()
+    plain = (time.perf_counter() - t0) / runs
+    print(f"plain run: {plain * 1e3:.2f} ms  ({4749 / plain:.0f} QPs/s)", flush=True)
+    timed(bt_mod.BacktestService, "prepare_rebalancing", "prepare_rebalancing (builders, first date)")
+    timed(engine, "window_rows", "window_rows")
+    timed(engine.Panel, "__init__", "Panel upload")
+    timed(bt_mod.BatchStage, "__init__", "BatchStage (rows upload)")
+    timed(engine.QPBatch, "from_dense", "QPBatch.from_dense")
+    timed(bt_mod.BatchStage, "group_plan", "GroupPlan")
+    timed(engine, "solve_lowrank", "solve_lowrank")
+    timed(Backtest, "_finish_batched", "finish (Portfolio objects)")
+    opt_cls = type(make().optimization)
+    timed(opt_cls, "objective_batch", "objective_batch")
+    ACC.clear()
+    CNT.clear()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(runs):
+        Backtest().run(make())
+    torch.cuda.synchronize()
+    tot = (time.perf_counter() - t0) / runs
+    print(f"bracketed run: {tot * 1e3:.2f} ms", flush=True)
+    named = 0.0
+    for k, v in sorted(ACC.items(), key=lambda kv: -kv[1]):
+        print(f"  {k:48s} {v / runs * 1e3:8.2f} ms  ({CNT[k] // runs} calls)")
+        named += v / runs
+    print(f"  {'(rest: service build, result copies, glue)':48s} {(tot - named) * 1e3:8.2f} ms")
+
+
+if __name__ == "__main__":
+    main()
