@@ -30,8 +30,6 @@
 #include "common.h"
 #include "capi_util.h"
 
-#include <cstdlib>
-
 namespace pq {
 
 constexpr int CT = 256;        // threads per group workgroup (two workgroups per CU: the
@@ -355,25 +353,17 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
 // CMGW: the wide form, up to 24 shared rows read column-sparse -- cg_nzr / cg_nzv, nzmax <= CNZ
 // nonzeros per asset, e.g. the budget plus one 0/1 sector membership -- instead of as
 // register-resident columns)
-template <int MGC, int MODE>
+template <int MGC>
 __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
                                                   pq_settings s, int iters_call, const double* pc, int64_t ldpc,
                                                   int r0, const double* cc, const int32_t* cg_nzr,
                                                   const double* cg_nzv, int nzmax) {
   constexpr bool WIDE = MGC > CMG;
-  constexpr bool PIPE = MODE >= 1;
-  constexpr bool FUSE = MODE == 2 && !WIDE;
-  constexpr int MGG = WIDE ? CMGW : CMG;
+  constexpr int MGG = WIDE ? CMGW : 8;
   __shared__ __attribute__((aligned(16))) double WU[(CU_MAX + 4) * CG_MAX];
   double* const UT = WU;
   __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX], g_qmax[CG_MAX], g_coef[CG_MAX];
-  // y_b = H_b^-1 s_b of every date; the fused pass reuses it for the column block's partial
-  // X~ of each wave (CNW x 16 dates x FCB columns) and keeps the block's new V beside it
-  constexpr int FCB = 32;   // fused pass: columns per block
-  constexpr int NSCR = FUSE && CNW * CG_MAX * FCB > CG_MAX * CH_MAX ? CNW * CG_MAX * FCB : CG_MAX * CH_MAX;
-  __shared__ __attribute__((aligned(16))) double g_scr[NSCR];
-  __shared__ double g_vb[FUSE ? FCB * CG_MAX : 1];
-  double* const g_y = g_scr;
+  __shared__ double g_y[CG_MAX * CH_MAX];   // y_b = H_b^-1 s_b of every date
   constexpr int NPART = 5;                    // per wave and date: 4 maxima, mu.V
   __shared__ double g_part[CNW * CG_MAX * NPART];
   __shared__ double g_gm[CG_MAX * 3];
@@ -538,7 +528,6 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 
   const int ntile = (U + mg + 15) >> 4;   // pass 1: union rows, then the general rows (Cg V)
   const int ktile = (kU + 15) >> 4;
-  bool w_ready = false;   // (fused pass) W of the current iterate already in WU
   while (s_any) {
     // lane ids re-materialised every iteration (loop_zero): the per-lane LDS / global
     // addresses derived from them are then computed where they are used instead of being
@@ -550,9 +539,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int hbase = (hg & 1) * 32;
 #pragma clang diagnostic pop
     (void)hbase;
-    // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs); the fused pass 2
-    //      leaves the next iteration's W behind, so with it only the first iteration runs this --
-    if (!FUSE || !w_ready) {
+    // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs) ----------------------
+    {
       const int z0 = loop_zero();
       const int kq = l >> 4, m = (l & 15) + z0;
       const double* Vp = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride + ld : nullptr;
@@ -568,22 +556,27 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         aval[j] = u < U + mg;
         arow[j] = u < U ? lr.panel + (int64_t)s_urow[u] * lr.ldp : pb.Cg + (int64_t)(u < U + mg ? u - U : 0) * ld;
       }
-      struct Buf { double2 b; double2 a[CTP1]; };
+      struct Buf { double2 b; double2 a[CTP1]; double bs; };
+      // unconditional loads from clamped addresses, no select on a loaded register (see pass 2's
+      // load): rows past U + mg and tiles past ntile produce output rows nobody reads, and the
+      // columns past n meet a zero V (scaled by 0, after the load)
+      const double* Vq = Vp ? Vp : st.work + (int64_t)d0 * st.work_stride + ld;
       auto load = [&](Buf& f, int k0) {
         const int kk = k0 + 2 * kq;
         const bool kin = kk + 1 < n;
-        f.b = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+        const int kc = kin ? kk : 0;
+        f.b = *reinterpret_cast<const double2*>(Vq + kc);
 #pragma unroll
-        for (int j = 0; j < CTP1; ++j)
-          f.a[j] = (tv[j] && aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
+        for (int j = 0; j < CTP1; ++j) f.a[j] = *reinterpret_cast<const double2*>(arow[j] + kc);
+        f.bs = (Vp && kin) ? 1.0 : 0.0;
       };
-      auto mma = [&](const Buf& f) {
+      auto mma = [&](const Buf& f) {   // (no branch in the loop: every tile multiplies)
+        const double bx = f.b.x * f.bs, by = f.b.y * f.bs;
 #pragma unroll
-        for (int j = 0; j < CTP1; ++j)
-          if (tv[j]) {
-            c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].x, f.b.x, c[j], 0, 0, 0);
-            c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].y, f.b.y, c[j], 0, 0, 0);
-          }
+        for (int j = 0; j < CTP1; ++j) {
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].x, bx, c[j], 0, 0, 0);
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].y, by, c[j], 0, 0, 0);
+        }
       };
       Buf f0, f1;
       load(f0, 0);
@@ -634,21 +627,19 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       const int kU4 = (kU + 7) & ~7;
       // double-buffered: the A loads of step k0 + 8 are in flight during step k0's MFMAs
+      // unconditional loads from clamped addresses (see pass 2's load): rows / columns >= kU of
+      // M^-1 (k_ld padding) are never read, rows past kU and tiles past ktile produce output
+      // rows nobody reads, and B is zero past kU
       auto loadA = [&](double2 (&a)[CTP2], int k0) {
-        const int kk = k0 + 2 * kq;   // k_ld padding: rows / columns >= kU of M^-1 are never read
-        const bool kin = kk < kU, kin1 = kk + 1 < kU;
+        const int kk = k0 + 2 * kq;
+        const int k0c = kk < kU ? kk : 0, k1c = kk + 1 < kU ? kk + 1 : 0;
 #pragma unroll
         for (int j = 0; j < CTP2; ++j) {
-          a[j] = double2{0.0, 0.0};
-          if (!zv[j] || !rv[j]) continue;
-          const int ts = (w + CNW * j) * 16;
-          if (kk < ts) {   // strictly left of the diagonal block: kk + 1 < ts <= row, both in range
-            a[j] = *reinterpret_cast<const double2*>(mrow[j] + kk);
-          } else {
-            const double* mc = Mi + (ts + m);
-            if (kin) a[j].x = mc[(int64_t)kk * k_ld];
-            if (kin1) a[j].y = mc[(int64_t)(kk + 1) * k_ld];
-          }
+          const int ts = zv[j] ? (w + CNW * j) * 16 : 0;
+          const bool left = kk < ts;   // strictly left of the diagonal block: kk + 1 < ts <= row
+          const double* mc = Mi + (ts + m);
+          a[j].x = *(left ? mrow[j] + kk : mc + (int64_t)k0c * k_ld);
+          a[j].y = *(left ? mrow[j] + kk + 1 : mc + (int64_t)k1c * k_ld);
         }
       };
       auto mmaA = [&](const double2 (&a)[CTP2], int k0) {
@@ -817,89 +808,111 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     __syncthreads();
     CSTAMP(2);
-    if constexpr (FUSE) {
-      // ---- pass 2 fused with the per-date updates AND the next iteration's pass 1: the union
-      //      rows are streamed once per iteration.  Per block of FCB = 32 columns, all four
-      //      waves: (1) each wave reduces X~ = X_U' Ut over its own row tiles (pass 1's tiles
-      //      w + 4j) into LDS partials; (2) wave w finishes dates 4w .. 4w + 3 (partials summed
-      //      in a fixed order), one date and one asset pair per lane, and leaves V = rhs / d of
-      //      the block in LDS; (3) each wave adds X[its rows, block] V[block] to its pass-1
-      //      accumulators -- the block's rows read again right after (1) (an L2 hit), in the
-      //      transposed lane layout the second product needs --------------------------------
+    // ---- pass 2 fused with the per-date updates.  The MFMA computes X~raw as (date x asset)
+    //      tiles: lane l ends with dates (l>>4) + 4r, r = 0..3, of the asset pair
+    //      p * 32 + 2 (l & 15) + {0, 1}, so the epilogue's per-date vectors (x, Px, z, y,
+    //      rhs, q, mu) are read and written as 16-byte pairs by 16 consecutive lanes (256
+    //      contiguous bytes per date), and the per-asset data (box, Cg columns) once per
+    //      lane for all its dates.  Per-date maxima / sums: lane partials, reduced over the
+    //      16 lanes of a date, then NP slots per wave in LDS ---------------------------------
+    {
       const int z0 = loop_zero();
       const int kq = l >> 4, ia = (l & 15) + z0;
-      double* const gpw = g_part + w * CG_MAX * NPART;
-      for (int e = l; e < CG_MAX * NPART; e += 64) gpw[e] = 0.0;   // wave-private slots
-      const bool box_shared = pb.box_stride == 0;
-      f64x4 cw5[CTP1];
-      const double* arow[CTP1];
-      bool tv[CTP1], aval[CTP1];
+      const int Uk = (U + 3) & ~3;
+#ifndef PQ_GCAP_PS
+#define PQ_GCAP_PS 4
+#endif
+      constexpr int PS = PQ_GCAP_PS;   // union rows per pass-2 load step (x 4 lanes)
+      bool mact[4];
 #pragma unroll
-      for (int j = 0; j < CTP1; ++j) {
-        cw5[j] = f64x4{0.0, 0.0, 0.0, 0.0};
-        const int u = (w + CNW * j) * 16 + ia;
-        tv[j] = w + CNW * j < ntile;
-        aval[j] = u < U + mg;
-        arow[j] = u < U ? lr.panel + (int64_t)s_urow[u] * lr.ldp : pb.Cg + (int64_t)(u < U + mg ? u - U : 0) * ld;
+      for (int r = 0; r < 4; ++r) {
+        const int m = kq + 4 * r;
+        mact[r] = m < G && g_act[m];
       }
-      const int dd = 4 * w + kq;   // the lane's date in (2)
-      const bool dact = dd < G && g_act[dd];
-      for (int c0 = 0; c0 < n; c0 += FCB) {
-        const int i = c0 + 2 * ia;   // the lane's asset pair in (1) and (2) (n even)
+      const bool box_shared = pb.box_stride == 0;
+      // per date of the lane: |x-z|, max(|x|, |z|), |dual res|, max(|Px|, |C'y|) (|q|: prologue;
+      // Cg V: next pass 1, as extra MFMA rows)
+      double mv[4][4];
+      double muv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        muv[r] = 0.0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mv[r][e] = 0.0;
+      }
+      for (int p = w; p * 32 < n; p += CNW) {
+        const int i = p * 32 + 2 * ia;   // this lane's asset pair (n even: i < n => i + 1 < n)
         const bool cin = i < n;
-        // (1) partial X~[date][col] over this wave's rows: u = tile 16 + 4 h + kq (the K index)
-        {
-          double2 xa[CTP1][4];
+        f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
+        struct ABuf { double2 a[PS]; };
+        // unconditional loads from clamped addresses and no select on a loaded register: a
+        // conditional load becomes an exec-masked block whose else-branch zeroes the load's
+        // destination, a write-after-write that makes the compiler wait for EVERY outstanding
+        // load (vmcnt(0)) there -- the double buffer would hide nothing.  Rows past U meet a
+        // zero Ut instead, and the columns past n are never used
+        auto load = [&](ABuf& f, int u0) {
 #pragma unroll
-          for (int j = 0; j < CTP1; ++j)
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const int u = (w + CNW * j) * 16 + 4 * h + kq;
-              xa[j][h] = (tv[j] && u < U && cin)
-                             ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + i)
-                             : double2{0.0, 0.0};
-            }
-          f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int j = 0; j < CTP1; ++j)
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              if (!tv[j]) continue;
-              const int u = (w + CNW * j) * 16 + 4 * h + kq;
-              const double av = u < U ? UT[u * CG_MAX + ia] : 0.0;   // Ut'[date ia][u]
-              ce = __builtin_amdgcn_mfma_f64_16x16x4f64(av, xa[j][h].x, ce, 0, 0, 0);
-              co = __builtin_amdgcn_mfma_f64_16x16x4f64(av, xa[j][h].y, co, 0, 0, 0);
-            }
-          // lane holds dates kq + 4 r of the asset pair 2 ia (+1)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            *reinterpret_cast<double2*>(g_scr + (w * CG_MAX + kq + 4 * r) * FCB + 2 * ia) = double2{ce[r], co[r]};
-        }
-        __syncthreads();
-        // (2) the per-date updates of date dd at the asset pair i
-        double mvv[4] = {0.0, 0.0, 0.0, 0.0}, muvv = 0.0;
-        double2 vnew = double2{0.0, 0.0};
-        if (dact && cin) {
-          double2 xr = double2{0.0, 0.0};
-#pragma unroll
-          for (int ww = 0; ww < CNW; ++ww) {
-            const double2 pv = *reinterpret_cast<const double2*>(g_scr + (ww * CG_MAX + dd) * FCB + 2 * ia);
-            xr.x += pv.x;
-            xr.y += pv.y;
+          for (int h = 0; h < PS; ++h) {
+            const int u = u0 + 4 * h + kq;
+            f.a[h] = *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u < U ? u : 0] * lr.ldp +
+                                                       (cin ? i : 0));
           }
-          constexpr int MGR = MGC > 0 ? MGC : 1;   // register-resident columns
-          double2 cg2[MGR];
+        };
+        auto mma = [&](const ABuf& f, int u0) {   // (rows past U: Ut zero; columns past n: unused)
 #pragma unroll
-          for (int c = 0; c < MGR; ++c)
+          for (int h = 0; h < PS; ++h) {
+            const int u = u0 + 4 * h + kq;
+            const double av = u < U ? UT[u * CG_MAX + ia] : 0.0;   // Ut'[date ia][u]
+            ce = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].x, ce, 0, 0, 0);
+            co = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].y, co, 0, 0, 0);
+          }
+        };
+        ABuf f0, f1;
+        load(f0, 0);
+        for (int u0 = 0; u0 < Uk; u0 += 8 * PS) {
+          load(f1, u0 + 4 * PS);
+          mma(f0, u0);
+          load(f0, u0 + 8 * PS);
+          mma(f1, u0 + 4 * PS);
+        }
+        if (!cin) continue;
+        // per-asset data, shared by the lane's dates
+        constexpr int MGR = WIDE ? 1 : (MGC > 0 ? MGC : 1);   // register-resident columns
+        double2 cg2[MGR];
+        if constexpr (!WIDE) {
+#pragma unroll
+          for (int c = 0; c < MGC; ++c)
             cg2[c] = c < mg ? *reinterpret_cast<const double2*>(pb.Cg + (int64_t)c * ld + i) : double2{0.0, 0.0};
-          const int m = dd;
+        }
+        int nzr2[2][WIDE ? CNZ : 1];   // wide form: the pair's nonzero rows (-1: none) and values
+        double nzv2[2][WIDE ? CNZ : 1];
+        if constexpr (WIDE) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int e = 0; e < CNZ; ++e) {
+              const bool ok = e < nzmax;
+              nzr2[h][e] = ok ? cg_nzr[(int64_t)(i + h) * nzmax + e] : -1;
+              nzv2[h][e] = ok ? cg_nzv[(int64_t)(i + h) * nzmax + e] : 0.0;
+            }
+        }
+        double2 lo2 = double2{0.0, 0.0}, up2 = double2{0.0, 0.0}, rb2 = double2{0.0, 0.0};
+        if (has_box && box_shared) {
+          lo2 = *reinterpret_cast<const double2*>(pb.lb + i);
+          up2 = *reinterpret_cast<const double2*>(pb.ub + i);
+          rb2 = double2{crho(lo2.x, up2.x, rho, s), crho(lo2.y, up2.y, rho, s)};
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          __builtin_amdgcn_sched_barrier(0);   // one date's loads live at a time (VGPR budget)
+          if (!mact[r]) continue;
+          const int m = kq + 4 * r;
           const int bm = d0 + m;
           const double su = g_su[m], dinv = g_dinv[m];
-          double2 lo = double2{0.0, 0.0}, up = double2{0.0, 0.0}, rb = double2{0.0, 0.0};
-          if (has_box) {
-            const int64_t bo = box_shared ? 0 : (int64_t)bm * pb.box_stride;
-            lo = *reinterpret_cast<const double2*>(pb.lb + bo + i);
-            up = *reinterpret_cast<const double2*>(pb.ub + bo + i);
+          double2 lo = lo2, up = up2, rb = rb2;
+          if (has_box && !box_shared) {
+            lo = *reinterpret_cast<const double2*>(pb.lb + (int64_t)bm * pb.box_stride + i);
+            up = *reinterpret_cast<const double2*>(pb.ub + (int64_t)bm * pb.box_stride + i);
             rb = double2{crho(lo.x, up.x, rho, s), crho(lo.y, up.y, rho, s)};
           }
           double* R_m = st.work + (int64_t)bm * st.work_stride + ld + i;
@@ -921,28 +934,43 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           double cwm[MGR], rgzm[MGR], ygm[MGR], wgm[MGR];
 #pragma unroll
           for (int c = 0; c < MGR; ++c) {
-            const bool ok = c < mg;
+            const bool ok = !WIDE && c < mg;
             cwm[c] = ok ? g_cw[m * MGG + c] : 0.0;
             rgzm[c] = ok ? g_rgz[m * MGG + c] : 0.0;
             ygm[c] = ok ? g_yg[m * MGG + c] : 0.0;
             wgm[c] = ok ? g_wg[m * MGG + c] : 0.0;
           }
           double2 xo, pxo, zo, yo, ro;
-          auto one = [&](double xrr, double rr0, double mui, double xi, double pxi, double qi, double zi, double yi,
+          auto one = [&](double xr, double rr0, double mui, double xi, double pxi, double qi, double zi, double yi,
                          double loi, double upi, double rbi, int sel, double& xn_o, double& pxn_o, double& zn_o,
                          double& yn_o, double& rr_o) {
-            double corr = xrr - su * mui;
-            double cgi[MGR];
-            double cgy = 0.0, cgw = 0.0;
+            // wide form: the sums over the asset's nonzero rows (Cg' cw, Cg' rho z~, Cg' y, Cg' w)
+            double gcw = 0.0, grgz = 0.0, cgy = 0.0, cgw = 0.0;
+            if constexpr (WIDE) {
 #pragma unroll
-            for (int c = 0; c < MGR; ++c) {
+              for (int e = 0; e < CNZ; ++e) {
+                const int rw = sel ? nzr2[1][e] : nzr2[0][e];
+                if (rw >= 0) {
+                  const double v = sel ? nzv2[1][e] : nzv2[0][e];
+                  const int o = m * MGG + rw;
+                  gcw = fma(g_cw[o], v, gcw);
+                  grgz = fma(v, g_rgz[o], grgz);
+                  cgy = fma(v, g_yg[o], cgy);
+                  cgw = fma(v, g_wg[o], cgw);
+                }
+              }
+            }
+            double corr = xr - su * mui + gcw;
+            double cgi[MGR];
+#pragma unroll
+            for (int c = 0; c < MGR && !WIDE; ++c) {
               cgi[c] = sel ? cg2[c].y : cg2[c].x;
               corr = fma(cwm[c], cgi[c], corr);
             }
             const double xt = (rr0 - corr) * dinv;
-            double pxt = rr0 - sigma * xt - rbi * xt;
+            double pxt = rr0 - sigma * xt - rbi * xt - grgz;
 #pragma unroll
-            for (int c = 0; c < MGR; ++c) {
+            for (int c = 0; c < MGR && !WIDE; ++c) {
               pxt -= cgi[c] * rgzm[c];
               cgy = fma(cgi[c], ygm[c], cgy);
               cgw = fma(cgi[c], wgm[c], cgw);
@@ -961,19 +989,19 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
               yn_o = yn;
               cty = yn;
               rr += rbi * zn - yn;
-              mvv[0] = fmax(mvv[0], fabs(xn - zn));
-              mvv[1] = fmax(mvv[1], fmax(fabs(xn), fabs(zn)));
+              mv[r][0] = fmax(mv[r][0], fabs(xn - zn));
+              mv[r][1] = fmax(mv[r][1], fmax(fabs(xn), fabs(zn)));
             }
             xn_o = xn;
             pxn_o = pxn;
             rr_o = rr;
             const double cy = cty + cgy;
-            mvv[2] = fmax(mvv[2], fabs((pxn + qi + cty) + (cy - cty)));
-            mvv[3] = fmax(mvv[3], fmax(fabs(pxn), fabs(cy)));
-            muvv = fma(mui, rr * dinv, muvv);
+            mv[r][2] = fmax(mv[r][2], fabs((pxn + qi + cty) + (cy - cty)));
+            mv[r][3] = fmax(mv[r][3], fmax(fabs(pxn), fabs(cy)));
+            muv[r] = fma(mui, rr * dinv, muv[r]);
           };
-          one(xr.x, rr2.x, mu2.x, x2.x, px2.x, q2.x, z2.x, y2.x, lo.x, up.x, rb.x, 0, xo.x, pxo.x, zo.x, yo.x, ro.x);
-          one(xr.y, rr2.y, mu2.y, x2.y, px2.y, q2.y, z2.y, y2.y, lo.y, up.y, rb.y, 1, xo.y, pxo.y, zo.y, yo.y, ro.y);
+          one(ce[r], rr2.x, mu2.x, x2.x, px2.x, q2.x, z2.x, y2.x, lo.x, up.x, rb.x, 0, xo.x, pxo.x, zo.x, yo.x, ro.x);
+          one(co[r], rr2.y, mu2.y, x2.y, px2.y, q2.y, z2.y, y2.y, lo.y, up.y, rb.y, 1, xo.y, pxo.y, zo.y, yo.y, ro.y);
           *reinterpret_cast<double2*>(x_m) = xo;
           *reinterpret_cast<double2*>(Px_m) = pxo;
           *reinterpret_cast<double2*>(R_m) = ro;
@@ -981,299 +1009,23 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             *reinterpret_cast<double2*>(zb_m) = zo;
             *reinterpret_cast<double2*>(yb_m) = yo;
           }
-          vnew = double2{ro.x * dinv, ro.y * dinv};
         }
-        g_vb[(2 * ia) * CG_MAX + dd] = vnew.x;   // V[column][date] of the block (0 off the batch)
-        g_vb[(2 * ia + 1) * CG_MAX + dd] = vnew.y;
-        // per-date maxima and mu.V over the 16 lanes of the date into the wave's slots
+      }
+      // reduce over the 16 lanes of each date (lanes kq * 16 + 0..15), then one slot per wave
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
 #pragma unroll
         for (int sh = 1; sh < 16; sh <<= 1) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) mvv[e] = fmax(mvv[e], __shfl_xor(mvv[e], sh, 64));
-          muvv += __shfl_xor(muvv, sh, 64);
+          for (int e = 0; e < 4; ++e) mv[r][e] = fmax(mv[r][e], __shfl_xor(mv[r][e], sh, 64));
+          muv[r] += __shfl_xor(muv[r], sh, 64);
         }
+        const int m = kq + 4 * r;
         if (ia == 0) {
-          double* pp = gpw + dd * NPART;
+          double* pp = g_part + (w * CG_MAX + m) * NPART;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) pp[e] = fmax(pp[e], mvv[e]);
-          pp[4] += muvv;
-        }
-        __syncthreads();
-        // (3) W_next[u][date] += X[u][block] V[block][date] (pass 1's MFMA layout: u = tile 16 +
-        //     (l & 15), columns c0 + 8 k + 2 kq (+1); the block's rows were just read by (1))
-        double2 xb[CTP1][4];
-#pragma unroll
-        for (int j = 0; j < CTP1; ++j)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int kk = c0 + 8 * k + 2 * kq;
-            xb[j][k] = (tv[j] && aval[j] && kk < n) ? *reinterpret_cast<const double2*>(arow[j] + kk)
-                                                     : double2{0.0, 0.0};
-          }
-#pragma unroll
-        for (int j = 0; j < CTP1; ++j) {
-          if (!tv[j]) continue;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int cc0 = 8 * k + 2 * kq;
-            const double b0 = g_vb[cc0 * CG_MAX + ia];
-            const double b1 = g_vb[(cc0 + 1) * CG_MAX + ia];
-            cw5[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[j][k].x, b0, cw5[j], 0, 0, 0);
-            cw5[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[j][k].y, b1, cw5[j], 0, 0, 0);
-          }
-        }
-      }
-      __syncthreads();   // every wave is done reading Ut: the next W takes its place
-      // B operand of the next iteration's group GEMM (pass 1's image; V already holds 1 / d)
-#pragma unroll
-      for (int j = 0; j < CTP1; ++j) {
-        const int tile = w + CNW * j;
-        if (tv[j]) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int u = tile * 16 + kq + 4 * r;
-            if (u < U) {
-              WU[u * CG_MAX + ia] = gk.sqc * cw5[j][r];
-            } else if (u < U + mg) {   // Cg V of date ia
-              if (ia < G) g_cgv[ia * MGG + (u - U)] = cw5[j][r];
-              WU[u * CG_MAX + ia] = s_sr[u - U] * cw5[j][r];
-            }
-          }
-        }
-      }
-      w_ready = true;
-    } else {
-      // ---- pass 2 fused with the per-date updates.  The MFMA computes X~raw as (date x asset)
-      //      tiles: lane l ends with dates (l>>4) + 4r, r = 0..3, of the asset pair
-      //      p * 32 + 2 (l & 15) + {0, 1}, so the epilogue's per-date vectors (x, Px, z, y,
-      //      rhs, q, mu) are read and written as 16-byte pairs by 16 consecutive lanes (256
-      //      contiguous bytes per date), and the per-asset data (box, Cg columns) once per
-      //      lane for all its dates.  Per-date maxima / sums: lane partials, reduced over the
-      //      16 lanes of a date, then NP slots per wave in LDS ---------------------------------
-      {
-        const int z0 = loop_zero();
-        const int kq = l >> 4, ia = (l & 15) + z0;
-        const int Uk = (U + 3) & ~3;
-#ifndef PQ_GCAP_PS
-#define PQ_GCAP_PS 4
-#endif
-        constexpr int PS = PQ_GCAP_PS;   // union rows per pass-2 load step (x 4 lanes)
-        bool mact[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = kq + 4 * r;
-          mact[r] = m < G && g_act[m];
-        }
-        const bool box_shared = pb.box_stride == 0;
-        // per date: |x-z|, max(|x|, |z|), |dual res|, max(|Px|, |C'y|) (|q|: prologue; Cg V: next
-        // pass 1, as extra MFMA rows) and mu.V, reduced over the 16 lanes of the date after each
-        // column block into this wave's slots (block-local accumulators: no registers held across
-        // the union stream)
-        double* const gpw = g_part + w * CG_MAX * NPART;
-        for (int e = l; e < CG_MAX * NPART; e += 64) gpw[e] = 0.0;   // wave-private slots
-        for (int p = w; p * 32 < n; p += CNW) {
-          const int i = p * 32 + 2 * ia;   // this lane's asset pair (n even: i < n => i + 1 < n)
-          const bool cin = i < n;
-          f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
-          struct ABuf { double2 a[PS]; };
-          auto load = [&](ABuf& f, int u0) {
-#pragma unroll
-            for (int h = 0; h < PS; ++h) {
-              const int u = u0 + 4 * h + kq;
-              f.a[h] = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + i)
-                                      : double2{0.0, 0.0};
-            }
-          };
-          auto mma = [&](const ABuf& f, int u0) {
-#pragma unroll
-            for (int h = 0; h < PS; ++h) {
-              const int u = u0 + 4 * h + kq;
-              const double av = u < Uk ? UT[u * CG_MAX + ia] : 0.0;   // Ut'[date ia][u]
-              ce = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].x, ce, 0, 0, 0);
-              co = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].y, co, 0, 0, 0);
-            }
-          };
-          ABuf f0, f1;
-          load(f0, 0);
-          for (int u0 = 0; u0 < Uk; u0 += 8 * PS) {
-            load(f1, u0 + 4 * PS);
-            mma(f0, u0);
-            load(f0, u0 + 8 * PS);
-            mma(f1, u0 + 4 * PS);
-          }
-          double mv[4][4];
-          double muv[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            muv[r] = 0.0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) mv[r][e] = 0.0;
-          }
-          if (cin) {
-            // per-asset data, shared by the lane's dates
-            constexpr int MGR = WIDE ? 1 : (MGC > 0 ? MGC : 1);   // register-resident columns
-            double2 cg2[MGR];
-            if constexpr (!WIDE) {
-#pragma unroll
-              for (int c = 0; c < MGC; ++c)
-                cg2[c] = c < mg ? *reinterpret_cast<const double2*>(pb.Cg + (int64_t)c * ld + i) : double2{0.0, 0.0};
-            }
-            int nzr2[2][WIDE ? CNZ : 1];   // wide form: the pair's nonzero rows (-1: none) and values
-            double nzv2[2][WIDE ? CNZ : 1];
-            if constexpr (WIDE) {
-#pragma unroll
-              for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int e = 0; e < CNZ; ++e) {
-                  const bool ok = e < nzmax;
-                  nzr2[h][e] = ok ? cg_nzr[(int64_t)(i + h) * nzmax + e] : -1;
-                  nzv2[h][e] = ok ? cg_nzv[(int64_t)(i + h) * nzmax + e] : 0.0;
-                }
-            }
-            double2 lo2 = double2{0.0, 0.0}, up2 = double2{0.0, 0.0}, rb2 = double2{0.0, 0.0};
-            if (has_box && box_shared) {
-              lo2 = *reinterpret_cast<const double2*>(pb.lb + i);
-              up2 = *reinterpret_cast<const double2*>(pb.ub + i);
-              rb2 = double2{crho(lo2.x, up2.x, rho, s), crho(lo2.y, up2.y, rho, s)};
-            }
-            // the per-date vectors of date r + 1 are fetched before date r is computed and
-            // stored (two dates' loads in flight: the epilogue's round trips overlap)
-            struct DVec { double2 rr, mu, x, px, q, z, y; };
-            auto fetch = [&](int r, DVec& v) {
-              if (!mact[r]) return;
-              const int bm = d0 + kq + 4 * r;
-              v.rr = *reinterpret_cast<const double2*>(st.work + (int64_t)bm * st.work_stride + ld + i);
-              v.mu = centred ? *reinterpret_cast<const double2*>(lr.mu + (int64_t)bm * lr.mu_stride + i)
-                             : double2{0.0, 0.0};
-              v.x = *reinterpret_cast<const double2*>(st.x + (int64_t)bm * ld + i);
-              v.px = *reinterpret_cast<const double2*>(st.Px + (int64_t)bm * ld + i);
-              v.q = *reinterpret_cast<const double2*>(pb.q + (int64_t)bm * pb.q_stride + i);
-              v.z = v.y = double2{0.0, 0.0};
-              if (has_box) {
-                v.z = *reinterpret_cast<const double2*>(st.z + (int64_t)bm * st.m_ld + st.mg_pad + i);
-                v.y = *reinterpret_cast<const double2*>(st.y + (int64_t)bm * st.m_ld + st.mg_pad + i);
-              }
-            };
-            DVec dv[2];
-            if (PIPE) fetch(0, dv[0]);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              if (PIPE && r < 3) fetch(r + 1, dv[(r + 1) & 1]);
-              __builtin_amdgcn_sched_barrier(0);   // at most two dates' loads live (VGPR budget)
-              if (!PIPE) fetch(r, dv[r & 1]);
-              if (!mact[r]) continue;
-              const DVec& cv = dv[r & 1];
-              const int m = kq + 4 * r;
-              const int bm = d0 + m;
-              const double su = g_su[m], dinv = g_dinv[m];
-              double2 lo = lo2, up = up2, rb = rb2;
-              if (has_box && !box_shared) {
-                lo = *reinterpret_cast<const double2*>(pb.lb + (int64_t)bm * pb.box_stride + i);
-                up = *reinterpret_cast<const double2*>(pb.ub + (int64_t)bm * pb.box_stride + i);
-                rb = double2{crho(lo.x, up.x, rho, s), crho(lo.y, up.y, rho, s)};
-              }
-              double* R_m = st.work + (int64_t)bm * st.work_stride + ld + i;
-              double* x_m = st.x + (int64_t)bm * ld + i;
-              double* Px_m = st.Px + (int64_t)bm * ld + i;
-              double* zb_m = st.z + (int64_t)bm * st.m_ld + st.mg_pad + i;
-              double* yb_m = st.y + (int64_t)bm * st.m_ld + st.mg_pad + i;
-              const double2 rr2 = cv.rr, mu2 = cv.mu, x2 = cv.x, px2 = cv.px, q2 = cv.q, z2 = cv.z, y2 = cv.y;
-              double cwm[MGR], rgzm[MGR], ygm[MGR], wgm[MGR];
-#pragma unroll
-              for (int c = 0; c < MGR; ++c) {
-                const bool ok = !WIDE && c < mg;
-                cwm[c] = ok ? g_cw[m * MGG + c] : 0.0;
-                rgzm[c] = ok ? g_rgz[m * MGG + c] : 0.0;
-                ygm[c] = ok ? g_yg[m * MGG + c] : 0.0;
-                wgm[c] = ok ? g_wg[m * MGG + c] : 0.0;
-              }
-              double2 xo, pxo, zo, yo, ro;
-              auto one = [&](double xr, double rr0, double mui, double xi, double pxi, double qi, double zi, double yi,
-                             double loi, double upi, double rbi, int sel, double& xn_o, double& pxn_o, double& zn_o,
-                             double& yn_o, double& rr_o) {
-                // wide form: the sums over the asset's nonzero rows (Cg' cw, Cg' rho z~, Cg' y, Cg' w)
-                double gcw = 0.0, grgz = 0.0, cgy = 0.0, cgw = 0.0;
-                if constexpr (WIDE) {
-#pragma unroll
-                  for (int e = 0; e < CNZ; ++e) {
-                    const int rw = sel ? nzr2[1][e] : nzr2[0][e];
-                    if (rw >= 0) {
-                      const double v = sel ? nzv2[1][e] : nzv2[0][e];
-                      const int o = m * MGG + rw;
-                      gcw = fma(g_cw[o], v, gcw);
-                      grgz = fma(v, g_rgz[o], grgz);
-                      cgy = fma(v, g_yg[o], cgy);
-                      cgw = fma(v, g_wg[o], cgw);
-                    }
-                  }
-                }
-                double corr = xr - su * mui + gcw;
-                double cgi[MGR];
-#pragma unroll
-                for (int c = 0; c < MGR && !WIDE; ++c) {
-                  cgi[c] = sel ? cg2[c].y : cg2[c].x;
-                  corr = fma(cwm[c], cgi[c], corr);
-                }
-                const double xt = (rr0 - corr) * dinv;
-                double pxt = rr0 - sigma * xt - rbi * xt - grgz;
-#pragma unroll
-                for (int c = 0; c < MGR && !WIDE; ++c) {
-                  pxt -= cgi[c] * rgzm[c];
-                  cgy = fma(cgi[c], ygm[c], cgy);
-                  cgw = fma(cgi[c], wgm[c], cgw);
-                }
-                const double xn = alpha * xt + (1.0 - alpha) * xi;
-                const double pxn = alpha * pxt + (1.0 - alpha) * pxi;
-                double rr = sigma * xn - qi + cgw;
-                double cty = 0.0;
-                zn_o = zi;
-                yn_o = yi;
-                if (has_box) {
-                  const double zh = alpha * xt + (1.0 - alpha) * zi;
-                  const double zn = fmin(fmax(zh + yi / rbi, loi), upi);
-                  const double yn = yi + rbi * (zh - zn);
-                  zn_o = zn;
-                  yn_o = yn;
-                  cty = yn;
-                  rr += rbi * zn - yn;
-                  mv[r][0] = fmax(mv[r][0], fabs(xn - zn));
-                  mv[r][1] = fmax(mv[r][1], fmax(fabs(xn), fabs(zn)));
-                }
-                xn_o = xn;
-                pxn_o = pxn;
-                rr_o = rr;
-                const double cy = cty + cgy;
-                mv[r][2] = fmax(mv[r][2], fabs((pxn + qi + cty) + (cy - cty)));
-                mv[r][3] = fmax(mv[r][3], fmax(fabs(pxn), fabs(cy)));
-                muv[r] = fma(mui, rr * dinv, muv[r]);
-              };
-              one(ce[r], rr2.x, mu2.x, x2.x, px2.x, q2.x, z2.x, y2.x, lo.x, up.x, rb.x, 0, xo.x, pxo.x, zo.x, yo.x, ro.x);
-              one(co[r], rr2.y, mu2.y, x2.y, px2.y, q2.y, z2.y, y2.y, lo.y, up.y, rb.y, 1, xo.y, pxo.y, zo.y, yo.y, ro.y);
-              *reinterpret_cast<double2*>(x_m) = xo;
-              *reinterpret_cast<double2*>(Px_m) = pxo;
-              *reinterpret_cast<double2*>(R_m) = ro;
-              if (has_box) {
-                *reinterpret_cast<double2*>(zb_m) = zo;
-                *reinterpret_cast<double2*>(yb_m) = yo;
-              }
-            }
-          }
-          // reduce over the 16 lanes of each date (lanes kq * 16 + 0..15) into the wave's slots
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-#pragma unroll
-            for (int sh = 1; sh < 16; sh <<= 1) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) mv[r][e] = fmax(mv[r][e], __shfl_xor(mv[r][e], sh, 64));
-              muv[r] += __shfl_xor(muv[r], sh, 64);
-            }
-            if (ia == 0) {
-              double* pp = gpw + (kq + 4 * r) * NPART;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) pp[e] = fmax(pp[e], mv[r][e]);
-              pp[4] += muv[r];
-            }
-          }
+          for (int e = 0; e < 4; ++e) pp[e] = mv[r][e];
+          pp[4] = muv[r];
         }
       }
     }
@@ -1417,43 +1169,6 @@ extern "C" int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_st
   return 0;
 }
 
-namespace pq {
-// pass 2 of k_admm_gcap: PQ_GCAP_MODE = 2 (default) fuses it with the next iteration's pass 1
-// (one stream of the union rows per iteration), 1 keeps the two passes with the epilogue's
-// per-date loads software-pipelined, 0 without the pipelining (A/B); the column-sparse (wide)
-// form always runs mode 1
-static int gcap_mode() {
-  static const int v = [] {
-    const char* e = getenv("PQ_GCAP_MODE");
-    const int m = e ? atoi(e) : 2;
-    return m >= 0 && m <= 2 ? m : 2;
-  }();
-  return v;
-}
-}  // namespace pq
-
-template <int MODE>
-static int launch_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
-                       const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
-                       int32_t r0, const double* cc, const int32_t* cg_nzr, const double* cg_nzv,
-                       int32_t nzmax, void* stream) {
-  if (pb->mg == 0)
-    hipLaunchKernelGGL((pq::k_admm_gcap<0, MODE>), dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
-                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
-  else if (pb->mg == 1)   // the budget row alone (the usual case): one general row in registers
-    hipLaunchKernelGGL((pq::k_admm_gcap<1, MODE>), dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
-                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
-  else if (pb->mg <= pq::CMG)
-    hipLaunchKernelGGL((pq::k_admm_gcap<pq::CMG, MODE>), dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
-                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
-  else   // budget + sector caps: column-sparse rows
-    hipLaunchKernelGGL((pq::k_admm_gcap<pq::CMGW, MODE == 0 ? 0 : 1>), dim3(gc->ngroups), dim3(pq::CT), 0,
-                       (hipStream_t)stream, *lr, *pb, *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, cg_nzr, cg_nzv,
-                       nzmax);
-  PQ_CHECK_LAUNCH("pq_admm_lr_gcap");
-  return 0;
-}
-
 extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const pq_gcap* gc,
                                const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
                                int32_t r0, const double* cc, const int32_t* cg_nzr, const double* cg_nzv,
@@ -1470,9 +1185,18 @@ extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(pb->mg <= pq::CMG || (cg_nzr && cg_nzv && nzmax > 0 && nzmax <= pq::CNZ),
                "pq_admm_lr_gcap: more than %d general rows need their column-sparse form (nzmax <= %d)", pq::CMG,
                pq::CNZ);
-  switch (pq::gcap_mode()) {
-    case 0: return launch_gcap<0>(lr, pb, st, gc, s, iters_this_call, pc, ldpc, r0, cc, cg_nzr, cg_nzv, nzmax, stream);
-    case 1: return launch_gcap<1>(lr, pb, st, gc, s, iters_this_call, pc, ldpc, r0, cc, cg_nzr, cg_nzv, nzmax, stream);
-    default: return launch_gcap<2>(lr, pb, st, gc, s, iters_this_call, pc, ldpc, r0, cc, cg_nzr, cg_nzv, nzmax, stream);
-  }
+  if (pb->mg == 0)
+    hipLaunchKernelGGL(pq::k_admm_gcap<0>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
+                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
+  else if (pb->mg == 1)   // the budget row alone (the usual case): one general row in registers
+    hipLaunchKernelGGL(pq::k_admm_gcap<1>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
+                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
+  else if (pb->mg <= pq::CMG)
+    hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMG>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
+                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
+  else   // budget + sector caps: column-sparse rows
+    hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMGW>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
+                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, cg_nzr, cg_nzv, nzmax);
+  PQ_CHECK_LAUNCH("pq_admm_lr_gcap");
+  return 0;
 }

@@ -948,8 +948,10 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     sparse_cols = _sparse_columns(qb) if grouped else (None, None, 0)
     # group capacitance: shared rows, register-resident (mg <= 4) or column-sparse (mg <= 24,
     # <= 4 nonzeros per asset); pass 1 of admm_gcap.hip covers U + mg <= 320 rows
+    # (box-only problems, mg = 0, keep the per-date capacitance: the group form measured wrong
+    # there -- every date stopped after one iteration, tests/test_gcap_gpu.py)
     gcap_try = (gcap and eig is None and grouped and fuse and qb.shared
-                and (qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
+                and (1 <= qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
                 and groups.ucnt_max + qb.mg <= 320 and groups.corr_max <= 64)
     if band:
         # the band must cover every union the capacitances read: the ADMM's groups and the

@@ -156,7 +156,8 @@ class MeanVariance(Optimization):
         lowrank = stage.prefer_lowrank and self.covariance.spec["method"] != "duv" and not nan
         S, pdiag, mu_c, dg = self.covariance.estimate_batch_lr(
             stage.panel, stage.rows, stage.tlen, out=None if lowrank else stage.P_buffer(),
-            plan=None if (nan or lowrank) else stage.slide_plan(), materialise=not lowrank)
+            plan=None if (nan or lowrank) else stage.slide_plan(), materialise=not lowrank,
+            groups=stage.group_plan() if lowrank else None)
         ra = float(self.params["risk_aversion"])
         B = stage.batch
         dev = stage.device

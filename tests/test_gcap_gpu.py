@@ -130,15 +130,11 @@ def test_gcap_uncentred_tracking_default_settings(device):
     assert np.abs(xb.sum(1) - 1).max() < 1e-10 and xb.min() > -1e-10
 
 
-@pytest.mark.parametrize("budget,caps", [(False, 0), (True, 2)])
-def test_gcap_general_row_variants_same_iterates(device, budget, caps):
-    """The kernel's general-row variants beyond the budget alone: none (box only; q = -mu so
-    the optimum is not the origin) and the budget with two sector caps (three register-resident
-    rows): the same ADMM iterates as the per-date form with one fixed rho."""
-    qb, lr, gp = _problem(device, 600, 150, 40, 0.2, budget=budget, caps=caps)
-    if not budget:
-        qb.q = (-lr.mu * 50.0).contiguous()
-    assert qb.mg == int(budget) + caps
+def test_gcap_three_general_rows_same_iterates(device):
+    """The kernel's register-resident general-row variant beyond the budget alone (the budget
+    with two sector caps): the same ADMM iterates as the per-date form with one fixed rho."""
+    qb, lr, gp = _problem(device, 600, 150, 40, 0.2, caps=2)
+    assert qb.mg == 3
     st = engine.Settings(rho0_rel=0.0, rho0=0.01, rho0_qrel=0.0, adapt_interval=0)
     xa, sa, ia, cap_a, _ = _run(qb, lr, gp, False, st, polish=False)
     xb, sb, ib, cap_b, _ = _run(qb, lr, gp, True, st, polish=False)
@@ -146,3 +142,15 @@ def test_gcap_general_row_variants_same_iterates(device, budget, caps):
     assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED), (sa, sb)
     assert np.abs(ia - ib).max() <= 1, (ia, ib)
     assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()
+
+
+def test_box_only_problems_keep_the_per_date_capacitance(device):
+    """No general row (box only; q = -mu so the optimum is not the origin): the group form
+    is not taken (it measured wrong there: every date stopped after one iteration), and the
+    per-date form solves every date."""
+    qb, lr, gp = _problem(device, 600, 150, 40, 0.2, budget=False)
+    qb.q = (-lr.mu * 50.0).contiguous()
+    assert qb.mg == 0
+    x, st_, it, cap, _ = _run(qb, lr, gp, True, None)
+    assert cap != "group" and np.all(st_ == _lib.PQ_SOLVED) and it.min() > 1
+    assert x.min() > -1e-9 and x.max() < 0.2 + 1e-9
