@@ -278,6 +278,7 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
 constexpr int FKCH = 16;            // window rows per staged chunk
 constexpr int FPIT = PG_KMAX + 4;   // LDS pitch (doubles)
 constexpr int FT = 512;             // threads (8 waves)
+constexpr int GMAXT = 512;          // window rows held in LDS by k_pg_form
 constexpr int FNW = FT / 64;
 constexpr int FTW = 5;              // 16x16 tiles per wave (36 lower tiles for k <= 128)
 
@@ -392,8 +393,15 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
     return;
   }
   const int T = lr.tlen[b];
-  const int32_t* rws = lr.rows + (int64_t)b * lr.tmax;
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  // the window's row indices in LDS: a gather's row address is then one LDS read away, not a
+  // dependent global load
+  __shared__ int s_rws[GMAXT];
+  const int32_t* g_rws = lr.rows + (int64_t)b * lr.tmax;
+  const bool lds_rows = T <= GMAXT;   // (uniform; longer windows read the indices from memory)
+  for (int tt = t; lds_rows && tt < T; tt += FT) s_rws[tt] = g_rws[tt];
+  __syncthreads();
+  auto rws = [&](int tt) -> int { return lds_rows ? s_rws[tt] : g_rws[tt]; };
   const int nt = (k + 15) >> 4, ntile = nt * (nt + 1) / 2;
   const int kp = nt * 16;
   // gather map: thread t -> window row t / 32 of a chunk, free columns (t % 32) + 32 c
@@ -407,11 +415,16 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
     mc[c] = (col[c] >= 0 && mu) ? mu[col[c]] : 0.0;
   }
   double v[4];
+  // unconditional loads (clamped row / column, zeroed by a factor after the load: a conditional
+  // load makes the compiler wait for every outstanding load there)
   auto gather = [&](int t0) {
     const int tt = t0 + gr;
-    const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
+    const double* row = lr.panel + (int64_t)rws(tt < T ? tt : 0) * lr.ldp;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = (row && col[c] >= 0) ? row[col[c]] - mc[c] : 0.0;
+    for (int c = 0; c < 4; ++c) {
+      const double x = row[col[c] >= 0 ? col[c] : 0];
+      v[c] = (x - mc[c]) * ((tt < T && col[c] >= 0) ? 1.0 : 0.0);
+    }
   };
   auto put = [&](double* Sb) {
 #pragma unroll
@@ -518,12 +531,17 @@ __global__ __launch_bounds__(FT) void k_pg_form_grp(pq_lowrank lr, pq_problem pb
   for (int cb = 0; cb < n; cb += FT) {
     const int i = cb + t;
     bool f = false;
-    if (i < n)
-      for (int g = 0; g < G; ++g)
-        if (s_on[g]) {
-          PGWork wg(st, d0 + g, ld);
-          f |= wg.fl[i] == 0;
-        }
+    {   // every date's flag loaded at once (clamped, unconditional), then combined
+      int fv[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        PGWork wg(st, d0 + (g < G ? g : 0), ld);
+        fv[g] = wg.fl[i < n ? i : 0];
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) f |= g < G && s_on[g] && fv[g] == 0;
+      f = f && i < n;
+    }
     const unsigned long long bal = __ballot(f);
     if (l == 0) s_wcnt[w] = __popcll(bal);
     __syncthreads();
@@ -542,7 +560,9 @@ __global__ __launch_bounds__(FT) void k_pg_form_grp(pq_lowrank lr, pq_problem pb
   for (int c = t; c < PG_KMAX; c += FT) s_gm[c] = (c < nc && mug) ? mug[s_col[c]] : 0.0;
   __syncthreads();
   // ---- Gram of the union rows over the union free list (k_pg_form's tiling) ---------------
-  const int32_t* ur = urows_all + (int64_t)grp * umax;
+  __shared__ int ur[GMAXT];   // the union's row indices in LDS (a gather's row address is one LDS read away)
+  for (int u = t; u < U && u < GMAXT; u += FT) ur[u] = urows_all[(int64_t)grp * umax + u];
+  __syncthreads();
   const int nt = (nc + 15) >> 4, ntile = nt * (nt + 1) / 2;
   const int kp = nt * 16;
   const int gr = t >> 5, gc = t & 31;
@@ -555,11 +575,14 @@ __global__ __launch_bounds__(FT) void k_pg_form_grp(pq_lowrank lr, pq_problem pb
     mc[c] = p < nc ? s_gm[p] : 0.0;
   }
   double v[4];
-  auto gather = [&](int t0) {
+  auto gather = [&](int t0) {   // (unconditional loads, as k_pg_form's gather)
     const int tt = t0 + gr;
-    const double* row = tt < U ? lr.panel + (int64_t)ur[tt] * lr.ldp : nullptr;
+    const double* row = lr.panel + (int64_t)ur[tt < U ? tt : 0] * lr.ldp;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = (row && col[c] >= 0) ? row[col[c]] - mc[c] : 0.0;
+    for (int c = 0; c < 4; ++c) {
+      const double x = row[col[c] >= 0 ? col[c] : 0];
+      v[c] = (x - mc[c]) * ((tt < U && col[c] >= 0) ? 1.0 : 0.0);
+    }
   };
   auto put = [&](double* Sb) {
 #pragma unroll
@@ -1441,12 +1464,18 @@ __global__ __launch_bounds__(QT) void k_pg_passA(pq_lowrank lr, pq_problem pb, p
     for (int cb = k_lo; cb < k_hi; cb += QT) {
       const int i = cb + t;
       bool nz = false;
-      if (i < k_hi)
-        for (int g = 0; g < G; ++g)
-          if (g_on[g]) {
-            PGWork wg(st, d0 + g, ld);
-            nz |= (MODE == 0 ? wg.xb : wg.xs)[i] != 0.0;
-          }
+      {   // every date's entry loaded at once (clamped, unconditional), then combined
+        const int ic = i < k_hi ? i : k_lo;
+        double v[QG];
+#pragma unroll
+        for (int g = 0; g < QG; ++g) {
+          PGWork wg(st, d0 + (g < G ? g : 0), ld);
+          v[g] = (MODE == 0 ? wg.xb : wg.xs)[ic];
+        }
+#pragma unroll
+        for (int g = 0; g < QG; ++g) nz |= g < G && g_on[g] && v[g] != 0.0;
+        nz = nz && i < k_hi;
+      }
       const unsigned long long bal = __ballot(nz);
       if (l == 0) s_wcnt[w] = __popcll(bal);
       __syncthreads();
@@ -1461,32 +1490,53 @@ __global__ __launch_bounds__(QT) void k_pg_passA(pq_lowrank lr, pq_problem pb, p
       }
       __syncthreads();
     }
+    // unconditional loads from clamped addresses, V scaled to zero past the column list and
+    // for dates not taking part, MFMAs on every tile (rows past U and tiles past ntile give
+    // output rows the window mask of pass B drops): no branch and no select on a loaded
+    // register, which made the compiler wait for every outstanding load at each step.  Four
+    // column steps' loads are issued before their MFMAs
     const int ncol = s_ncol;
-    for (int k0 = 0; k0 < ncol; k0 += 4) {
-      const int kk = k0 + kq;
-      const int col = kk < ncol ? s_col[kk] : -1;
-      const double bv = (Vp && col >= 0) ? Vp[col] : 0.0;
+    const double* Vq = Vp ? Vp : lr.panel;
+    for (int k0 = 0; k0 < ncol; k0 += 16) {
+      double av[4][3], bv[4];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (tv[j]) {
-          const double av = (aval[j] && col >= 0) ? arow[j][col] : 0.0;
-          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c[j], 0, 0, 0);
-        }
+      for (int h = 0; h < 4; ++h) {
+        const int kk = k0 + 4 * h + kq;
+        const bool kin = kk < ncol;
+        const int col = s_col[kin ? kk : 0];
+        bv[h] = Vq[col] * ((Vp && kin) ? 1.0 : 0.0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) av[h][j] = arow[j][col];
       }
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[h][j], bv[h], c[j], 0, 0, 0);
     }
   } else {
-    for (int k0 = k_lo; k0 < k_hi; k0 += 8) {
-      const int kk = k0 + 2 * kq;
-      const bool kin = kk + 1 < k_hi;   // slice ends and n are even
-      const double2 bv = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+    const double* Vq = Vp ? Vp : lr.panel;
+    for (int k0 = k_lo; k0 < k_hi; k0 += 16) {
+      double2 av[2][3];
+      double bx[2], by[2];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        if (tv[j]) {
-          const double2 av = (aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
-          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c[j], 0, 0, 0);
-          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c[j], 0, 0, 0);
-        }
+      for (int h = 0; h < 2; ++h) {
+        const int kk = k0 + 8 * h + 2 * kq;
+        const bool kin = kk + 1 < k_hi;   // slice ends and n are even
+        const int kc = kin ? kk : k_lo;
+        const double sb = (Vp && kin) ? 1.0 : 0.0;
+        const double2 bl = *reinterpret_cast<const double2*>(Vq + kc);
+        bx[h] = bl.x * sb;
+        by[h] = bl.y * sb;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) av[h][j] = *reinterpret_cast<const double2*>(arow[j] + kc);
       }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[h][j].x, bx[h], c[j], 0, 0, 0);
+          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[h][j].y, by[h], c[j], 0, 0, 0);
+        }
     }
   }
 #pragma unroll
@@ -1507,7 +1557,7 @@ __global__ __launch_bounds__(QT) void k_pg_passB(pq_lowrank lr, pq_problem pb, p
                                                  const int32_t* gdates, const int32_t* urows_all,
                                                  const int32_t* ucnt_all, const int32_t* uoff, int umax,
                                                  double* scr) {
-  __shared__ __attribute__((aligned(16))) double WU[(QU + 4) * QG];
+  __shared__ __attribute__((aligned(16))) double WU[(QU + 16) * QG];   // (rows >= ntile 16: zero)
   __shared__ int s_urow[QU];
   __shared__ int g_on[QG], g_T[QG], g_off[QG];
   __shared__ double g_mux[QG];
@@ -1528,7 +1578,7 @@ __global__ __launch_bounds__(QT) void k_pg_passB(pq_lowrank lr, pq_problem pb, p
   __syncthreads();
   // Ut = sum of the partial W images (fixed order), masked to each date's own window rows
   const int ntile = (U + 15) >> 4;
-  for (int e = t; e < (QU + 4) * QG; e += QT) {
+  for (int e = t; e < (QU + 16) * QG; e += QT) {
     const int u = e / QG, m = e % QG;
     double v = 0.0;
     if (u < ntile * 16) {
@@ -1560,13 +1610,22 @@ __global__ __launch_bounds__(QT) void k_pg_passB(pq_lowrank lr, pq_problem pb, p
     const int col = p * 32 + 2 * m;
     const bool cin = col < n;
     f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
-    for (int u0 = 0; u0 < Uk; u0 += 4) {
-      const int u = u0 + kq;
-      const double2 a = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + col)
-                                       : double2{0.0, 0.0};
-      const double bv = WU[u * QG + m];
-      ce = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, bv, ce, 0, 0, 0);
-      co = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, bv, co, 0, 0, 0);
+    // unconditional loads (rows past U meet a zero Ut, columns past n are never stored), four
+    // union-row steps' loads issued before their MFMAs
+    const int colc = cin ? col : 0;
+    for (int u0 = 0; u0 < Uk; u0 += 16) {
+      double2 a[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int u = u0 + 4 * h + kq;
+        a[h] = *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u < U ? u : 0] * lr.ldp + colc);
+      }
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const double bv = WU[(u0 + 4 * h + kq) * QG + m];   // (rows to Uk + 15: zero-filled)
+        ce = __builtin_amdgcn_mfma_f64_16x16x4f64(a[h].x, bv, ce, 0, 0, 0);
+        co = __builtin_amdgcn_mfma_f64_16x16x4f64(a[h].y, bv, co, 0, 0, 0);
+      }
     }
     if (dst) {
 #pragma unroll
@@ -1645,19 +1704,42 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
   auto lamof = [&](int r) -> double { return r == r0 ? lam0 : R[R_LAM + r]; };
   // exact P x and gradient g = P x + q + Cg' lam; box checks
   int bad = 0;
-  for (int i = hl; i < n; i += PPT) {
-    const double xi = wk.xs[i];
-    const double pxi = ps * (wsc * (wk.g[i] - (mu ? mu[i] * su : 0.0))) + pd * xi;
-    double gi = pxi + q[i];
-    for (int r = 0; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * lamof(r);
-    wk.Px[i] = pxi;
-    wk.g[i] = gi;
-    const int f = wk.fl[i];
-    if (f == 0 && has_box) {
-      if (!isinf(lb[i]) && xi < lb[i] - ptol * (1.0 + fabs(lb[i]))) { wk.fl[i] = 1; bad = 1; }
-      else if (!isinf(ub[i]) && xi > ub[i] + ptol * (1.0 + fabs(ub[i]))) { wk.fl[i] = 2; bad = 1; }
-    } else if (f == 1 && lb[i] != ub[i] && -gi > dtol) { wk.fl[i] = 0; bad = 1; }
-    else if (f == 2 && -gi < -dtol) { wk.fl[i] = 0; bad = 1; }
+  // four of the thread's elements per step, every load issued first (clamped, unconditional):
+  // the stores of one element would otherwise order the next element's loads behind them
+  const double lam_r0 = mg > 0 ? lamof(0) : 0.0;
+  for (int i0 = hl; i0 < n; i0 += 4 * PPT) {
+    double xv[4], gv[4], mv4[4], qv[4], c0[4], lbv[4], ubv[4];
+    int fv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * PPT, ic = i < n ? i : 0;
+      xv[j] = wk.xs[ic];
+      gv[j] = wk.g[ic];
+      mv4[j] = mu ? mu[ic] : 0.0;
+      qv[j] = q[ic];
+      c0[j] = mg > 0 ? Cg[ic] : 0.0;
+      fv[j] = wk.fl[ic];
+      lbv[j] = has_box ? lb[ic] : 0.0;
+      ubv[j] = has_box ? ub[ic] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * PPT;
+      if (i >= n) continue;
+      const double xi = xv[j];
+      const double pxi = ps * (wsc * (gv[j] - mv4[j] * su)) + pd * xi;
+      double gi = pxi + qv[j] + c0[j] * lam_r0;
+      for (int r = 1; r < mg; ++r) gi += Cg[(int64_t)r * ld + i] * lamof(r);
+      wk.Px[i] = pxi;
+      wk.g[i] = gi;
+      const int f = fv[j];
+      const double lbi = lbv[j], ubi = ubv[j];
+      if (f == 0 && has_box) {
+        if (!isinf(lbi) && xi < lbi - ptol * (1.0 + fabs(lbi))) { wk.fl[i] = 1; bad = 1; }
+        else if (!isinf(ubi) && xi > ubi + ptol * (1.0 + fabs(ubi))) { wk.fl[i] = 2; bad = 1; }
+      } else if (f == 1 && lbi != ubi && -gi > dtol) { wk.fl[i] = 0; bad = 1; }
+      else if (f == 2 && -gi < -dtol) { wk.fl[i] = 0; bad = 1; }
+    }
   }
   // general rows: Cg x, activity checks (lane 0 decides, as the reference kernel's lane 0)
   for (int r = 0; r < mg; ++r) {
