@@ -703,15 +703,17 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
         sj[h] = v;
       }
-      // y = H^-1 s (H^-1 row i . s): lane i computes y_i for i = hl, hl + 32
+      // y = H^-1 s (H^-1 row i . s): lane i computes y_i for i = hl, hl + 32.  Unconditional
+      // loads (rows past mh are H^-1's zero padding, row index clamped to ldh): a conditional
+      // load in the loop makes the compiler wait for every outstanding load at each j
       double yi[2] = {0.0, 0.0};
+      const int ldh = gc.ldh;
+      const double* hr0 = Hi + (int64_t)(hl < ldh ? hl : ldh - 1) * ldh;
+      const double* hr1 = Hi + (int64_t)(hl + 32 < ldh ? hl + 32 : ldh - 1) * ldh;
       for (int j = 0; j < mh; ++j) {
         const double sv = __shfl(j < 32 ? sj[0] : sj[1], hbase + (j & 31), 64);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int i = hl + 32 * h;
-          if (i < mh) yi[h] = fma(Hi[(int64_t)i * gc.ldh + j], sv, yi[h]);
-        }
+        yi[0] = fma(hr0[j], sv, yi[0]);
+        yi[1] = fma(hr1[j], sv, yi[1]);
       }
       const double ymu = __shfl(m < 32 ? yi[0] : yi[1], hbase + (m & 31), 64);
 #pragma unroll
@@ -742,13 +744,12 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int e0 = 0; e0 < NE; e0 += 4) {
           const int e = e0 + kq;
           const int cu = e < NH ? e : T0 + (e - NH);   // union row of edge e
-          double av = 0.0, bv = 0.0;
-          if (e < NE) {
-            if (ua < kU) av = Mi[(int64_t)cu * k_ld + ua];
-            if (gact) {
-              if (e < NH) bv = e < offg ? g_y[gl * CH_MAX + e] : 0.0;
-              else bv = cu >= offg + T0 ? g_y[gl * CH_MAX + (cu - T0)] : 0.0;
-            }
+          // unconditional load (clamped row / column; rows past kU unused, B zero past NE)
+          const double av = Mi[(int64_t)(e < NE ? cu : 0) * k_ld + (ua < kU ? ua : 0)];
+          double bv = 0.0;
+          if (e < NE && gact) {
+            if (e < NH) bv = e < offg ? g_y[gl * CH_MAX + e] : 0.0;
+            else bv = cu >= offg + T0 ? g_y[gl * CH_MAX + (cu - T0)] : 0.0;
           }
           z = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, z, 0, 0, 0);
         }

@@ -77,15 +77,21 @@ PQ_DEVFN void form_pff(const pq_lowrank& lr, int b, const int* Fl, int k, int nb
     }
     Acc acc;
     acc.zero();
-    for (int t0 = 0; t0 < T; t0 += KC) {
+    // unconditional loads from a clamped row / column, zeroed by a factor after the load (a
+    // conditional load makes the compiler wait for every outstanding load there), two chunks
+    // ahead of the MFMAs in registers
+    auto gather = [&](int t0, double (&va)[4], double (&vb)[4]) {
       const int tt = t0 + kr;
-      const double* row = tt < T ? lr.panel + (int64_t)rws[tt] * lr.ldp : nullptr;
-      double va[4], vb[4];
+      const bool ok = tt < T;
+      const double* row = lr.panel + (int64_t)rws[ok ? tt : 0] * lr.ldp;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        va[e] = (row && ca[e] >= 0) ? row[ca[e]] - ma[e] : 0.0;
-        vb[e] = (row && cb[e] >= 0) ? row[cb[e]] - mb[e] : 0.0;
+        const double xa = row[ca[e] >= 0 ? ca[e] : 0], xb = row[cb[e] >= 0 ? cb[e] : 0];
+        va[e] = (xa - ma[e]) * ((ok && ca[e] >= 0) ? 1.0 : 0.0);
+        vb[e] = (xb - mb[e]) * ((ok && cb[e] >= 0) ? 1.0 : 0.0);
       }
+    };
+    auto stage = [&](const double (&va)[4], const double (&vb)[4]) {
       __syncthreads();   // the previous chunk's MFMAs are done with SA / SB
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -93,6 +99,17 @@ PQ_DEVFN void form_pff(const pq_lowrank& lr, int b, const int* Fl, int k, int nb
         SB[kr * LDW + i4 + e] = vb[e];
       }
       __syncthreads();
+    };
+    double va0[4], vb0[4], va1[4], vb1[4];
+    gather(0, va0, vb0);
+    if (KC < T) gather(KC, va1, vb1);
+    for (int t0 = 0; t0 < T; t0 += 2 * KC) {
+      stage(va0, vb0);
+      if (t0 + 2 * KC < T) gather(t0 + 2 * KC, va0, vb0);
+      mma_lds(acc, SA, SB, KC);
+      if (t0 + KC >= T) break;
+      stage(va1, vb1);
+      if (t0 + 3 * KC < T) gather(t0 + 3 * KC, va1, vb1);
       mma_lds(acc, SA, SB, KC);
     }
 #pragma unroll

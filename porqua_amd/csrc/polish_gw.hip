@@ -197,17 +197,24 @@ __global__ __launch_bounds__(YT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       aval[j] = uu < U + mgp;
       arow[j] = uu < U ? lr.panel + (int64_t)s_urow[uu] * lr.ldp : pb.Cg + (int64_t)(uu < U + mgp ? uu - U : 0) * ld;
     }
+    // unconditional loads from clamped addresses, V scaled to zero past n / for empty columns
+    // (a conditional load makes the compiler wait for every outstanding load at each step);
+    // rows past U + mgp give unused outputs
+    const double* Vq = Vp ? Vp : lr.panel;
     for (int k0 = 0; k0 < n; k0 += 8) {
       const int kk = k0 + 2 * kq;
       const bool kin = kk + 1 < n;
-      const double2 bv = (Vp && kin) ? *reinterpret_cast<const double2*>(Vp + kk) : double2{0.0, 0.0};
+      const int kc = kin ? kk : 0;
+      const double2 bl = *reinterpret_cast<const double2*>(Vq + kc);
+      double2 av[YP1];
+#pragma unroll
+      for (int j = 0; j < YP1; ++j) av[j] = *reinterpret_cast<const double2*>(arow[j] + kc);
+      const double sb = (Vp && kin) ? 1.0 : 0.0;
+      const double bx = bl.x * sb, by = bl.y * sb;
 #pragma unroll
       for (int j = 0; j < YP1; ++j) {
-        if (tv[j]) {
-          const double2 av = (aval[j] && kin) ? *reinterpret_cast<const double2*>(arow[j] + kk) : double2{0.0, 0.0};
-          cacc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, cacc[j], 0, 0, 0);
-          cacc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, cacc[j], 0, 0, 0);
-        }
+        cacc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[j].x, bx, cacc[j], 0, 0, 0);
+        cacc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[j].y, by, cacc[j], 0, 0, 0);
       }
     }
     __syncthreads();   // the previous contents of WU are no longer read
@@ -248,20 +255,18 @@ __global__ __launch_bounds__(YT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const bool kin = kk < U, kin1 = kk + 1 < U;
       const double b0 = kin ? WU[kk * YG + m] : 0.0;
       const double b1 = kin1 ? WU[(kk + 1) * YG + m] : 0.0;
+      // unconditional loads from clamped addresses (B is zero past U; rows past U and tiles
+      // past ktile give unused outputs), as admm_gcap.hip's GEMM
+      const int k0c = kin ? kk : 0, k1c = kin1 ? kk + 1 : 0;
 #pragma unroll
       for (int j = 0; j < YP2; ++j) {
+        const int ts = zv[j] ? (w + YNW * j) * 16 : 0;
+        const bool left = kk < ts;
+        const double* mc = Mi + (ts + m);
+        double2 a;
+        a.x = *(left ? mrow[j] + kk : mc + (int64_t)k0c * k_ld);
+        a.y = *(left ? mrow[j] + kk + 1 : mc + (int64_t)k1c * k_ld);
         if (!zv[j]) continue;
-        double2 a = double2{0.0, 0.0};
-        if (rv[j]) {
-          const int ts = (w + YNW * j) * 16;
-          if (kk < ts) {
-            a = *reinterpret_cast<const double2*>(mrow[j] + kk);
-          } else {
-            const double* mc = Mi + (ts + m);
-            if (kin) a.x = mc[(int64_t)kk * k_ld];
-            if (kin1) a.y = mc[(int64_t)(kk + 1) * k_ld];
-          }
-        }
         z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.x, b0, z[j], 0, 0, 0);
         z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a.y, b1, z[j], 0, 0, 0);
       }
@@ -342,13 +347,12 @@ __global__ __launch_bounds__(YT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int e0 = 0; e0 < NE; e0 += 4) {
           const int e = e0 + kq;
           const int cu = e < NH ? e : T0 + (e - NH);
-          double av = 0.0, bv = 0.0;
-          if (e < NE) {
-            if (ua < U) av = Mi[(int64_t)cu * k_ld + ua];
-            if (gact) {
-              if (e < NH) bv = e < offg ? g_y[gl * YCH + e] : 0.0;
-              else bv = cu >= offg + T0 ? g_y[gl * YCH + (cu - T0)] : 0.0;
-            }
+          // unconditional load (clamped row / column; rows past U unused, B zero past NE)
+          const double av = Mi[(int64_t)(e < NE ? cu : 0) * k_ld + (ua < U ? ua : 0)];
+          double bv = 0.0;
+          if (e < NE && gact) {
+            if (e < NH) bv = e < offg ? g_y[gl * YCH + e] : 0.0;
+            else bv = cu >= offg + T0 ? g_y[gl * YCH + (cu - T0)] : 0.0;
           }
           z = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, z, 0, 0, 0);
         }
@@ -380,13 +384,23 @@ __global__ __launch_bounds__(YT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const int i = p * 32 + 2 * ia;
       const bool cin = i < n;
       f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
-      for (int u0 = 0; u0 < Uk; u0 += 4) {
-        const int u = u0 + kq;
-        const double2 a = (u < U && cin) ? *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u] * lr.ldp + i)
-                                         : double2{0.0, 0.0};
-        const double av = WU[u * YG + ia];
-        ce = __builtin_amdgcn_mfma_f64_16x16x4f64(av, a.x, ce, 0, 0, 0);
-        co = __builtin_amdgcn_mfma_f64_16x16x4f64(av, a.y, co, 0, 0, 0);
+      // unconditional loads (rows past U meet zero in WU's padding rows, columns past n are
+      // unused), four union-row steps' loads issued before their MFMAs
+      const int ic = cin ? i : 0;
+      for (int u0 = 0; u0 < Uk; u0 += 16) {
+        double2 a[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int u = u0 + 4 * h + kq;
+          a[h] = *reinterpret_cast<const double2*>(lr.panel + (int64_t)s_urow[u < U ? u : 0] * lr.ldp + ic);
+        }
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int u = u0 + 4 * h + kq;
+          const double av = u < U ? WU[u * YG + ia] : 0.0;
+          ce = __builtin_amdgcn_mfma_f64_16x16x4f64(av, a[h].x, ce, 0, 0, 0);
+          co = __builtin_amdgcn_mfma_f64_16x16x4f64(av, a[h].y, co, 0, 0, 0);
+        }
       }
       if (!cin) continue;
 #pragma unroll

@@ -7,7 +7,7 @@ for i in $(seq 1 30); do
   /usr/local/graft/bin/gpurun --timeout 1200 -- "$@" > "$LOG" 2>&1
   rc=$?
   echo "attempt $i rc=$rc" >> "$LOG.attempts"
-  grep -q '"status": "transient"' gpurun_out/.last_call.json 2>/dev/null || exit $rc
+  { grep -q '"status": "transient"' gpurun_out/.last_call.json 2>/dev/null || grep -q 'status=transient' "$LOG"; } || exit $rc
   sleep 60
 done
 exit 3
