@@ -181,6 +181,15 @@ int pq_cov_slide_batched(const double* panel, int64_t ldp, int32_t n, const int3
 
 /* X'y and y'y of each window (LeastSquares q = -2 X'y, constant = y'y,
  * src/optimization.py:216-217).                                                        */
+int pq_gram_xy_grouped(const double* panel, int64_t ldp, int32_t n, const double* bm, const int32_t* gdates,
+                       int32_t ngroups, const int32_t* urows, int32_t umax, const int32_t* uoff,
+                       const int32_t* tlen, double* xty, int64_t xty_stride, double* yty, double* dg,
+                       int64_t dg_stride, void* stream);
+/* (pq_gram_xy_grouped: the same for the dates of slide groups -- the layout of
+ * pq_window_moments_grouped -- the first window summed, the later ones by the rows that
+ * enter / leave: O(n) per date after the group's first instead of O(T n).  dg (optional):
+ * diag(X'X) of every window in the same pass, the uncentred Gram diagonal of the window
+ * form (src/optimization.py:215), instead of a separate pq_window_sumsq.)               */
 int pq_gram_xy_batched(const double* panel, int64_t ldp, int32_t n, const double* bm,
                        const int32_t* rows, const int32_t* tlen, int32_t tmax, int32_t batch,
                        double* xty, int64_t xty_stride, double* yty, void* stream);

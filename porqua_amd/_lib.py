@@ -147,6 +147,8 @@ _EXPORTS = {
     "pq_polish_w_batched": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                              c_dp, c_int32, ctypes.POINTER(PQSettings), c_int32, c_int32, c_dp, c_int64,
                              c_int32, c_dp], c_int32),
+    "pq_gram_xy_grouped": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_dp, c_int32, c_dp, c_dp, c_dp,
+                            c_int64, c_dp, c_dp, c_int64, c_dp], c_int32),
     "pq_gram_xy_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64,
                             c_dp, c_dp], c_int32),
     "pq_init_state": ([ctypes.POINTER(PQProblem), ctypes.POINTER(PQState), c_dp, c_int32,

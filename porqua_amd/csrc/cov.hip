@@ -464,6 +464,59 @@ __global__ __launch_bounds__(256) void k_gram_xy(const double* panel, int64_t ld
   }
 }
 
+// X'y and y'y for the dates of slide groups (k_window_moments_grp's layout): the first window
+// summed, the later ones by the entering / leaving union rows
+__global__ __launch_bounds__(256) void k_gram_xy_grp(const double* panel, int64_t ldp, int n, const double* bm,
+                                                     const int32_t* gdates, const int32_t* urows, int umax,
+                                                     const int32_t* uoff, const int32_t* tlen, double* xty,
+                                                     int64_t xty_stride, double* yty, double* dg,
+                                                     int64_t dg_stride) {
+  const int g = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int d0 = gdates[g], d1 = gdates[g + 1];
+  const int32_t* ur = urows + (int64_t)g * umax;
+  const int T = tlen[d0];
+  if (blockIdx.x == 0 && (int)threadIdx.x < d1 - d0) {   // y'y: one thread per date, direct sum
+    const int b = d0 + threadIdx.x, lo = uoff[b];
+    double s = 0.0;
+    for (int u = lo; u < lo + T; ++u) {
+      const double v = bm[ur[u]];
+      s = fma(v, v, s);
+    }
+    yty[b] = s;
+  }
+  if (j >= n) return;
+  int lo = uoff[d0], hi = lo + T;
+  double s = 0.0, q = 0.0;
+#pragma unroll 8
+  for (int u = lo; u < hi; ++u) {
+    const int r = ur[u];
+    const double x = panel[(int64_t)r * ldp + j];
+    s = fma(x, bm[r], s);
+    q = fma(x, x, q);
+  }
+  for (int b = d0;; ) {
+    xty[(int64_t)b * xty_stride + j] = s;
+    if (dg) dg[(int64_t)b * dg_stride + j] = q;
+    if (++b >= d1) break;
+    const int nlo = uoff[b], nhi = nlo + T;
+    for (int u = hi; u < nhi; ++u) {   // entering
+      const int r = ur[u];
+      const double x = panel[(int64_t)r * ldp + j];
+      s = fma(x, bm[r], s);
+      q = fma(x, x, q);
+    }
+    for (int u = lo; u < nlo; ++u) {   // leaving
+      const int r = ur[u];
+      const double x = panel[(int64_t)r * ldp + j];
+      s = fma(-x, bm[r], s);
+      q = fma(-x, x, q);
+    }
+    lo = nlo;
+    hi = nhi;
+  }
+}
+
 }  // namespace pq
 
 static int check_win(const double* panel, int32_t n, const int32_t* rows, const int32_t* tlen,
@@ -583,6 +636,20 @@ extern "C" int pq_cov_slide_batched(const double* panel, int64_t ldp, int32_t n,
                      (hipStream_t)stream, panel, ldp, n, rows, tlen, tmax, mode, mu, mu_stride,
                      out, ld, out_stride, gstart, shift, lower_only ? 0 : 1);
   PQ_CHECK_LAUNCH("pq_cov_slide_batched");
+  return 0;
+}
+
+extern "C" int pq_gram_xy_grouped(const double* panel, int64_t ldp, int32_t n, const double* bm,
+                                  const int32_t* gdates, int32_t ngroups, const int32_t* urows, int32_t umax,
+                                  const int32_t* uoff, const int32_t* tlen, double* xty, int64_t xty_stride,
+                                  double* yty, double* dg, int64_t dg_stride, void* stream) {
+  PQ_CHECK_ARG(panel && bm && gdates && urows && uoff && tlen && xty && yty, "pq_gram_xy_grouped: null pointer");
+  PQ_CHECK_ARG(n > 0 && umax > 0 && ngroups >= 0, "pq_gram_xy_grouped: bad sizes n=%d umax=%d ngroups=%d", n,
+               umax, ngroups);
+  if (ngroups == 0) return 0;
+  hipLaunchKernelGGL(pq::k_gram_xy_grp, dim3((n + 255) / 256, ngroups), dim3(256), 0, (hipStream_t)stream, panel,
+                     ldp, n, bm, gdates, urows, umax, uoff, tlen, xty, xty_stride, yty, dg, dg_stride);
+  PQ_CHECK_LAUNCH("pq_gram_xy_grouped");
   return 0;
 }
 

@@ -96,22 +96,31 @@ class Settings:
     # 2.7 / 3.1 / 3.2 / 3.8 rounds); with the sparse exact-P x pass (r03y_*) 2e-2 / 3e-2 /
     # 5e-2 / 1e-1 -> 347k / 357k / 358k / 360k at 5 / 5 / 6 / 6 rounds at most (of the 8
     # allowed): 3e-2 keeps the round count of 2e-2; with polish_fix_rel = 0.05 (r03Q_grid*):
-    # 3e-2 / 5e-2 -> 374k / 389k at 2.86 / 2.99 rounds, at most 5 / 5.  Tracking (uncentred) windows keep eps_abs: their free
+    # 3e-2 / 5e-2 -> 374k / 389k at 2.86 / 2.99 rounds, at most 5 / 5.  Round 4, with the
+    # inner primal steps (polish_inner) the rounds stay cheap from a looser point
+    # (profiles/r04t_eg*.log, one box, polish_inner = 1): 0.2 / 0.3 -> 461k / 466k (9 / 8
+    # iterations, 2.2 / 2.3 rounds, at most 4, largest free set 88); 0.5 and 1.0 stop after 4
+    # iterations, where the free sets outgrow the LDS solve and every date takes the per-date
+    # fallback (144k).  0.2 keeps a factor 2.5 from that cliff.  Tracking (uncentred) windows keep eps_abs: their free
     # sets mostly exceed the LDS solve -- config 2 53.0k at 2e-3, 45.0k at 1e-2 from the loose
     # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
-    eps_grouped: float = 5e-2
+    eps_grouped: float = 0.2
     # grouped polish: variables with x - lb < polish_fix_rel * max(x - lb) at the ADMM point
     # also start fixed at lb (besides OSQP's z - lb < -y): the loose ADMM point leaves small
     # positive weights that the first rounds would only fix later.  Numpy model of config 3
     # (tests/engine_model.py, eps 3e-2, 10 dates): 0 / 0.05 / 0.1 / 0.2 -> 3.0 / 2.6 / 2.3 /
     # 3.3 rounds, first free sets 79 / 71 / 62 / 47 (wrong fixes cost the rounds back); on
     # the GPU (profiles/r03N_*): 0 / 0.05 / 0.1 -> 363k / 378k / 372k QPs/s, 3.31 / 2.86 / 3.0
-    # rounds on average, at most 5 / 5 / 6.  Centred windows only (k_pg_init)
-    polish_fix_rel: float = 0.05
+    # rounds on average, at most 5 / 5 / 6.  Round 4 at eps_grouped 0.2 / 0.3 with one inner
+    # step: 0.05 / 0.1 -> 461k / 467k and 466k / 479k (profiles/r04t_eg*_in1{,_fr1}.log).
+    # Centred windows only (k_pg_init)
+    polish_fix_rel: float = 0.1
     # grouped polish, LDS solve (k_pg_solve): free variables outside their box are fixed at
     # it and the reduced system re-solved inside the round, up to this many times per round,
-    # instead of one whole round (window passes, checks, setup) per such step
-    polish_inner: int = 2
+    # instead of one whole round (window passes, checks, setup) per such step.  Measured at
+    # eps_grouped 0.3 (profiles/r04t_eg3_in{1,2}.log): 1 / 2 -> 466k / 457k QPs/s (2.29 / 2.11
+    # rounds; the second step costs more in the solve buckets than the rounds it saves)
+    polish_inner: int = 1
 
     def to_c(self) -> _lib.PQSettings:
         names = {f[0] for f in _lib.PQSettings._fields_}
@@ -1523,6 +1532,24 @@ class Panel:
         _lib.check(lib.pq_gram_xy_batched(_ptr(self.R), self.n, self.n, _ptr(self.bm), _ptr(rows),
                                           _ptr(tlen), tmax, B, _ptr(xty), xty.stride(0), _ptr(yty),
                                           _stream()), "pq_gram_xy_batched")
+        return xty, yty
+
+    def gram_xy_grouped(self, groups: "GroupPlan", tlen, dg=None, xty=None):
+        """gram_xy for the dates of a GroupPlan in one sliding pass per group
+        (pq_gram_xy_grouped: O(n) per date after each group's first window); ``dg`` (optional,
+        (B, >= n)) receives diag(X'X) of every window from the same pass."""
+        lib = _lib.load()
+        if self.bm is None:
+            raise ValueError("Benchmark return series data is missing.")
+        B = int(tlen.shape[0])
+        ld = round_up(self.n, 64)
+        if xty is None:
+            xty = torch.zeros((B, ld), dtype=F64, device=self.device)
+        yty = torch.zeros(B, dtype=F64, device=self.device)
+        _lib.check(lib.pq_gram_xy_grouped(_ptr(self.R), self.R.stride(0), self.n, _ptr(self.bm), _ptr(groups.gdates),
+                                          groups.ngroups, _ptr(groups.urows), groups.umax, _ptr(groups.uoff),
+                                          _ptr(tlen), _ptr(xty), xty.stride(0), _ptr(yty), _ptr(dg),
+                                          0 if dg is None else dg.stride(0), _stream()), "pq_gram_xy_grouped")
         return xty, yty
 
 

@@ -254,12 +254,19 @@ class LeastSquares(Optimization):
             pan = stage.log1p_panel()
         else:
             pan = stage.panel
-        if stage.prefer_lowrank:   # factored form X'X (uncentred) for the Woodbury solver (no n x n G)
+        gp = stage.group_plan() if stage.prefer_lowrank else None
+        if gp is not None and gp.ok:   # the window form with slide groups: X'y, y'y, diag(X'X) in one sliding pass
+            dg = torch.zeros((stage.batch, stage.ld), dtype=torch.float64, device=stage.device)
+            xty, yty = pan.gram_xy_grouped(gp, stage.tlen, dg=dg)
             G = None
-            stage.lowrank = engine.LowRank(pan, stage.rows, stage.tlen, mu=None)
+            stage.lowrank = engine.LowRank(pan, stage.rows, stage.tlen, mu=None, dg=dg)
         else:
-            G = pan.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer(), plan=stage.slide_plan())
-        xty, yty = pan.gram_xy(stage.rows, stage.tlen)
+            if stage.prefer_lowrank:   # factored form X'X (uncentred) for the Woodbury solver (no n x n G)
+                G = None
+                stage.lowrank = engine.LowRank(pan, stage.rows, stage.tlen, mu=None)
+            else:
+                G = pan.cov(stage.rows, stage.tlen, mode=1, out=stage.P_buffer(), plan=stage.slide_plan())
+            xty, yty = pan.gram_xy(stage.rows, stage.tlen)
         B, dev = stage.batch, stage.device
         l2 = self.params.get("l2_penalty")
         scale = torch.full((B,), 2.0, dtype=torch.float64, device=dev)

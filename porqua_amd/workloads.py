@@ -192,9 +192,12 @@ class _LSTrackingBatch:
         if events is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        xty, _ = self.pan.gram_xy(self.rows_d, self.tlen_d)
+        if self.gplan.ok:   # X'y and diag(X'X) of every window in one sliding pass per group
+            xty, _ = self.pan.gram_xy_grouped(self.gplan, self.tlen_d, dg=self.lr.dg)
+        else:
+            xty, _ = self.pan.gram_xy(self.rows_d, self.tlen_d)
+            self.lr.refresh()
         torch.mul(xty, -2.0, out=self.qb.q)
-        self.lr.refresh()
         if events is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()

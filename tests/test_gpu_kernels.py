@@ -185,3 +185,26 @@ def test_gemv_batched_matches_torch(device, m, n, B, trans, offset):
     ref = torch.bmm(U.transpose(1, 2) if trans else U, x.unsqueeze(2)).squeeze(2)
     torch.cuda.synchronize()
     assert torch.allclose(got, ref, rtol=1e-13, atol=1e-12), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("stride", [1, 21])
+def test_gram_xy_grouped_matches_per_window(device, stride):
+    """pq_gram_xy_grouped (X'y, y'y and diag(X'X) of slide-group windows by entering / leaving
+    rows) against numpy per window: daily (stride 1) and monthly (stride 21) rebalancing."""
+    n, T = 300, 120
+    D = T + 40 * stride + 10
+    dates, R, y, _ = factor_panel(D, n, seed=5)
+    reb = dates[T + 3::stride][:40]
+    rows, tlen = engine.window_rows(dates, reb, T)
+    pan = engine.Panel(R, y, device=device)
+    _, t_d = pan.rows_to_device(rows, tlen)
+    gp = engine.GroupPlan(rows, tlen, device)
+    assert gp.ok and gp.ngroups < len(reb)
+    dg = torch.zeros((len(reb), 320), dtype=torch.float64, device=device)
+    xty, yty = pan.gram_xy_grouped(gp, t_d, dg=dg)
+    xty, yty, dg = xty.cpu().numpy(), yty.cpu().numpy(), dg.cpu().numpy()
+    for b in range(len(reb)):
+        Xw, yw = R[rows[b, :tlen[b]]], y[rows[b, :tlen[b]]]
+        assert _rel(xty[b, :n], Xw.T @ yw) <= 1e-12
+        assert abs(yty[b] - yw @ yw) <= 1e-13 * (yw @ yw)
+        assert _rel(dg[b, :n], (Xw * Xw).sum(0)) <= 1e-12

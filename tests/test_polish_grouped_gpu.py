@@ -141,7 +141,7 @@ def test_large_free_sets_are_solved_inside_the_pipeline(device):
 
 
 def test_loose_admm_stop_before_the_pipeline(device):
-    """Settings.eps_grouped (centred windows, default 2e-2): the ADMM stops early and the
+    """Settings.eps_grouped (centred windows, default 0.2): the ADMM stops early and the
     pipeline's rounds finish the job -- the same optimum as from the eps_abs point, fewer
     ADMM iterations, every date SOLVED."""
     qb, lr, gp = _problem(device, 1000, 252, 48, 1.0)
@@ -176,7 +176,7 @@ def test_loose_admm_stop_resumes_the_hand_offs(device):
 
 @pytest.mark.parametrize("case", ["bench", "capped", "sectors", "small_T"])
 def test_fix_rel_classification_same_optimum(device, case):
-    """Settings.polish_fix_rel (the default 0.05): small ADMM weights start fixed at the
+    """Settings.polish_fix_rel (the default 0.1): small ADMM weights start fixed at the
     lower bound -- a different first active set, the same certified optimum (to the proximal
     refinement's accuracy)."""
     args = {"bench": (1000, 252, 48, 1.0), "capped": (400, 120, 40, 0.05),
