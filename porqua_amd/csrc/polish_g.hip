@@ -688,7 +688,7 @@ __device__ __forceinline__ double sum4(double v) {
 // -- uniform over the workgroup.
 template <int NW>
 __device__ __forceinline__ int b_potrf(double* Lp, int k, int* s_bad, double* prof) {
-  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int t = threadIdx.x + loop_zero(), l = t & 63, w = t >> 6;
 #ifdef PQ_PROFILE
   long long tp_ = wall_clock64();
 #define BP_STAMP(k_)                                                                  \
@@ -784,7 +784,7 @@ __device__ __forceinline__ int b_potrf(double* Lp, int k, int* s_bad, double* pr
 template <int NW>
 __device__ __forceinline__ void b_fwd(const double* Lp, int k, double* y, double* yo) {
   constexpr int T = 64 * NW;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x + loop_zero();
   for (int p0 = 0; p0 < k; p0 += 16) {
     const int nb = min(16, k - p0);
     for (int e = t; e < 256; e += T) {
@@ -817,7 +817,7 @@ __device__ __forceinline__ void b_fwd(const double* Lp, int k, double* y, double
 template <int NW>
 __device__ __forceinline__ void b_bwd(const double* Lp, int k, double* y, double* xo) {
   constexpr int T = 64 * NW;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x + loop_zero();
   for (int B = ((k + 15) >> 4) - 1; B >= 0; --B) {
     const int p0 = 16 * B, nb = min(16, k - p0);
     for (int e = t; e < 256; e += T) {
@@ -907,6 +907,9 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
   // up to `inner` times, instead of one whole round (window passes, checks, setup) per such
   // step; the round's checks then release wrongly fixed variables by their dual sign as before
   for (int it_in = 0;; ++it_in) {
+  // lane ids rebuilt from an opaque zero each pass: per-lane addresses derived from them stay
+  // inside the pass instead of being hoisted above the loop and held live through it
+  const int t = threadIdx.x + loop_zero(), l = t & 63, w = t >> 6;
   {   // packed triangle, flat index (independent loads, 8 per thread in flight)
     const int np_ = k * (k + 1) / 2;
     int r = 0, e0 = 0;   // row of the thread's element: advance incrementally
