@@ -56,6 +56,12 @@ def main():
         pend = state == _lib.PQ_PG_PENDING
         line = f"round {r + 1}: pending {int(pend.sum())}, done {int((state == _lib.PQ_PG_DONE).sum())}, " \
                f"fallback {int((state == _lib.PQ_PG_FALLBACK).sum())}, k mean {k.mean():.1f}"
+        kb = R[:, 349]   # R_KB (pg_record.h): the free-set size this round's setup found
+        solved = pend_in if prev_k is not None else np.ones(len(kb), bool)
+        edges = [0, 48, 64, 80, 96, 128, 256, 1 << 30]
+        hist = np.histogram(kb[solved], bins=edges)[0]
+        line += "; solve buckets " + " ".join(f"<={e}:{c}" for e, c in zip(edges[1:], hist))
+        line += f", reused P_FF {int((R[solved, 7] != 0).sum())}"
         if prev_k is not None:
             was = prev_pend
             dk = k[was] - prev_k[was]
@@ -63,6 +69,7 @@ def main():
                     f"shrank {int((dk < 0).sum())}, same {int((dk == 0).sum())}"
         print(line, flush=True)
         prev_k, prev_pend = k.copy(), pend.copy()
+        pend_in = pend.copy()
         if not pend.any():
             break
 

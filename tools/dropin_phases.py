@@ -12,6 +12,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from porqua_amd import backtest as bt_mod, engine  # noqa: E402
@@ -71,6 +72,37 @@ def main():
         print(f"  {k:48s} {v / runs * 1e3:8.2f} ms  ({CNT[k] // runs} calls)")
         named += v / runs
     print(f"  {'(rest: service build, result copies, glue)':48s} {(tot - named) * 1e3:8.2f} ms")
+    # the device solve of one more run, stage by stage (HIP events) with its iteration and
+    # round counts: where the drop-in's solve differs from the bench step's
+    from porqua_amd import _lib
+    inner = engine.solve_lowrank.__wrapped__ if hasattr(engine.solve_lowrank, "__wrapped__") else None
+    seen = {}
+
+    def probe(*a, **k):
+        ev = []
+        k["events"] = ev
+        ws = k["ws"] = engine.Workspace(a[0], dense=False)
+        r = (inner or orig)(*a, **k)
+        torch.cuda.synchronize()
+        rall = ws.pg_record().cpu().numpy()
+        print("polish rounds per date:", np.unique(rall[:, _lib.PQ_PG_STATE + 1], return_counts=True))
+        fb = getattr(ws, "pg_fallback", None)
+        if fb is not None:   # the dates the grouped polish handed back, and their records
+            R = ws.pg_record()[fb.long()].cpu().numpy()
+            o = r.out[fb.long()].cpu().numpy()
+            print("handed back:", len(R), "k", np.unique(R[:, 0], return_counts=True),
+                  "ma", np.unique(R[:, 1], return_counts=True), "rounds", np.unique(R[:, 4], return_counts=True),
+                  "final nfree", np.unique(o[:, _lib.PQ_OUT_NFREE], return_counts=True))
+        seen["ev"] = [(nm, x.elapsed_time(y)) for nm, x, y in ev]
+        out = r.out.cpu().numpy()
+        seen["stats"] = dict(iters=float(r.iters.float().mean()), rounds=float(out[:, _lib.PQ_OUT_ROUNDS].mean()),
+                             nfree=float(out[:, _lib.PQ_OUT_NFREE].mean()), kw=sorted(k))
+        return r
+    orig = engine.solve_lowrank
+    engine.solve_lowrank = probe
+    Backtest().run(make())
+    print("drop-in solve stages:", ", ".join(f"{nm} {t:.2f} ms" for nm, t in seen.get("ev", [])))
+    print("drop-in solve stats:", seen.get("stats"))
 
 
 if __name__ == "__main__":
