@@ -267,15 +267,20 @@ __device__ __forceinline__ int wave_chol_inv16(double (&A)[4], double (&Bv)[4]) 
     rs = rs * fma(-0.5 * piv * rs, rs, 1.5);
     rs = rs * fma(-0.5 * piv * rs, rs, 1.5);
     const double bk = bkr * rs;                                      // final row kk of L^-1
-    const double lck = rowk * rs;                                    // L[cc][kk]
+    const double lck = cc > kk ? rowk * rs : 0.0;                    // L[cc][kk], trailing columns
+    // branch-free updates (selects, no exec-mask branches): the masked factors leave every
+    // element outside the trailing block unchanged (fma(-0, x, a) = a); register blocks q
+    // whose rows all lie above kk have nothing left to update
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      if (4 * q + 3 < kk) continue;                                  // (compile time)
       const int r = gg + 4 * q;
       const double lrk = colv[q] * rs;                               // L[r][kk]
-      if (cc == kk && r >= kk) A[q] = lrk;
-      else if (cc > kk && r > kk) A[q] = fma(-lrk, lck, A[q]);
-      if (r == kk) Bv[q] = bk;
-      else if (r > kk) Bv[q] = fma(-lrk, bk, Bv[q]);
+      const double lrt = r > kk ? lrk : 0.0;
+      const double upd = fma(-lrt, lck, A[q]);
+      A[q] = (cc == kk && r >= kk) ? lrk : upd;
+      const double bu = fma(-lrt, bk, Bv[q]);
+      Bv[q] = r == kk ? bk : bu;
     }
   }
   return bad;
