@@ -199,6 +199,15 @@ int pq_gram_xy_batched(const double* panel, int64_t ldp, int32_t n, const double
 int pq_window_geomean(const double* panel, int64_t ldp, int32_t n, const int32_t* rows,
                       const int32_t* tlen, int32_t tmax, int32_t batch, double* mu,
                       int64_t mu_stride, void* stream);
+/* The same for the dates of slide groups (the layout of pq_window_moments_grouped): the
+ * first window's sum of log(1 + x) directly, the later ones by the rows that enter / leave
+ * (T + 2 (G - 1) logarithms per column and group instead of G T).  Replaces
+ * pq_window_geomean for the daily mean-variance backtest (src/optimization.py:157-177,
+ * per rebalance date of src/backtest.py:209-230).                                        */
+int pq_window_geomean_grouped(const double* panel, int64_t ldp, int32_t n, const int32_t* gdates,
+                              int32_t ngroups, const int32_t* urows, int32_t umax,
+                              const int32_t* uoff, const int32_t* tlen, double* mu,
+                              int64_t mu_stride, void* stream);
 
 /* Reset x, z, y, Px, iterations, status and set the initial rho (rho0, or rho0_rel times
  * the mean diagonal of P_eff) for problems idx[].                                      */

@@ -130,6 +130,8 @@ _EXPORTS = {
     "pq_last_error": ([], ctypes.c_char_p),
     "pq_window_mean": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_dp], c_int32),
     "pq_window_geomean": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_dp, c_int64, c_dp], c_int32),
+    "pq_window_geomean_grouped": ([c_dp, c_int64, c_int32, c_dp, c_int32, c_dp, c_int32, c_dp, c_dp, c_dp,
+                                   c_int64, c_dp], c_int32),
     "pq_cov_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_int32, c_dp, c_int64,
                         c_dp, c_int32, c_int64, c_dp], c_int32),
     "pq_cov_slide_batched": ([c_dp, c_int64, c_int32, c_dp, c_dp, c_int32, c_int32, c_int32, c_dp, c_int64,

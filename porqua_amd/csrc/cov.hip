@@ -102,6 +102,37 @@ __global__ __launch_bounds__(256) void k_window_moments_grp(const double* panel,
   }
 }
 
+// Geometric window means of a slide group's dates (src/mean_estimation.py:39-48, the
+// k_window_mean geo arithmetic: exp(sum log(1 + x) / T) - 1) in one sliding pass over the
+// group's union rows: the first window's log sum directly, each later one by the rows that
+// enter and leave -- T + 2 (G - 1) logarithms per column and group instead of G T.
+__global__ __launch_bounds__(256) void k_window_geomean_grp(const double* panel, int64_t ldp, int n,
+                                                            const int32_t* gdates, const int32_t* urows,
+                                                            int umax, const int32_t* uoff,
+                                                            const int32_t* tlen, double* mu,
+                                                            int64_t mu_stride) {
+  const int g = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int d0 = gdates[g], d1 = gdates[g + 1];
+  const int32_t* ur = urows + (int64_t)g * umax;
+  const int T = tlen[d0];
+  auto lx = [&](int u) { return log(1.0 + panel[(int64_t)ur[u] * ldp + j]); };
+  int lo = uoff[d0], hi = lo + T;
+  double s = 0.0;
+#pragma unroll 8
+  for (int u = lo; u < hi; ++u) s += lx(u);
+  for (int b = d0;; ) {
+    mu[(int64_t)b * mu_stride + j] = exp(s / T) - 1.0;
+    if (++b >= d1) break;
+    const int nlo = uoff[b], nhi = nlo + T;
+    for (int u = hi; u < nhi; ++u) s += lx(u);    // entering
+    for (int u = lo; u < nlo; ++u) s -= lx(u);    // leaving
+    lo = nlo;
+    hi = nhi;
+  }
+}
+
 __device__ __forceinline__ void tri_index(int t, int& I, int& J) {
   // t enumerates lower tiles row by row: (0,0),(1,0),(1,1),(2,0),...
   I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
@@ -562,6 +593,20 @@ extern "C" int pq_window_moments_grouped(const double* panel, int64_t ldp, int32
                      (hipStream_t)stream, panel, ldp, n, gdates, urows, umax, uoff, tlen, mu, mu_stride, dg,
                      dg_stride);
   PQ_CHECK_LAUNCH("pq_window_moments_grouped");
+  return 0;
+}
+
+extern "C" int pq_window_geomean_grouped(const double* panel, int64_t ldp, int32_t n, const int32_t* gdates,
+                                         int32_t ngroups, const int32_t* urows, int32_t umax,
+                                         const int32_t* uoff, const int32_t* tlen, double* mu,
+                                         int64_t mu_stride, void* stream) {
+  PQ_CHECK_ARG(panel && gdates && urows && uoff && tlen && mu, "pq_window_geomean_grouped: null pointer");
+  PQ_CHECK_ARG(n > 0 && umax > 0 && ngroups >= 0, "pq_window_geomean_grouped: bad sizes n=%d umax=%d ngroups=%d",
+               n, umax, ngroups);
+  if (ngroups == 0) return 0;
+  hipLaunchKernelGGL(pq::k_window_geomean_grp, dim3((n + 255) / 256, ngroups), dim3(256), 0,
+                     (hipStream_t)stream, panel, ldp, n, gdates, urows, umax, uoff, tlen, mu, mu_stride);
+  PQ_CHECK_LAUNCH("pq_window_geomean_grouped");
   return 0;
 }
 

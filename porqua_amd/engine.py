@@ -1451,6 +1451,18 @@ class Panel:
                                                  dg.stride(0), _stream()), "pq_window_moments_grouped")
         return mu, dg
 
+    def window_geomeans_grouped(self, groups: "GroupPlan", tlen, out=None):
+        """Geometric window means (MeanEstimator.estimate_geometric) of every date of a
+        GroupPlan in one sliding pass per group (pq_window_geomean_grouped) -> (B, round_up(n, 64))."""
+        lib = _lib.load()
+        B = int(tlen.shape[0])
+        mu = out if out is not None else torch.zeros((B, round_up(self.n, 64)), dtype=F64, device=self.device)
+        _lib.check(lib.pq_window_geomean_grouped(_ptr(self.R), self.R.stride(0), self.n, _ptr(groups.gdates),
+                                                 groups.ngroups, _ptr(groups.urows), groups.umax,
+                                                 _ptr(groups.uoff), _ptr(tlen), _ptr(mu), mu.stride(0),
+                                                 _stream()), "pq_window_geomean_grouped")
+        return mu
+
     def rows_to_device(self, rows, tlen):
         r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int32)).to(self.device)
         t = torch.from_numpy(np.ascontiguousarray(tlen, dtype=np.int32)).to(self.device)

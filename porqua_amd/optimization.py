@@ -180,6 +180,9 @@ class MeanVariance(Optimization):
             mu = stage.panel.window_nanmeans(mrows, mtlen, geometric=True)
             if bool(torch.isnan(mu[:, :stage.n]).any().item()):
                 return None
+        elif lowrank and mrows is stage.rows and stage.group_plan().ok:
+            # the full windows of slide groups: one sliding log-sum pass per group
+            mu = stage.panel.window_geomeans_grouped(stage.group_plan(), stage.tlen)
         else:
             mu = stage.panel.window_means(mrows, mtlen, geometric=True)
         sf = me.spec.get("scalefactor")

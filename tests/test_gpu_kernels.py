@@ -187,6 +187,28 @@ def test_gemv_batched_matches_torch(device, m, n, B, trans, offset):
     assert torch.allclose(got, ref, rtol=1e-13, atol=1e-12), float((got - ref).abs().max())
 
 
+
+@pytest.mark.parametrize("stride", [1, 21])
+def test_geomean_grouped_matches_per_window(device, stride):
+    """pq_window_geomean_grouped (sliding log sums over slide-group windows) against the
+    per-window kernel and numpy's (1 + X).prod() ** (1 / T) - 1 (src/mean_estimation.py:39-48),
+    daily and monthly rebalancing."""
+    n, T = 300, 120
+    D = T + 40 * stride + 10
+    dates, R, _, _ = factor_panel(D, n, seed=7)
+    reb = dates[T + 3::stride][:40]
+    rows, tlen = engine.window_rows(dates, reb, T)
+    pan = engine.Panel(R, None, device=device)
+    r_d, t_d = pan.rows_to_device(rows, tlen)
+    gp = engine.GroupPlan(rows, tlen, device)
+    assert gp.ok and gp.ngroups < len(reb)
+    mg = pan.window_geomeans_grouped(gp, t_d).cpu().numpy()
+    mw = pan.window_means(r_d, t_d, geometric=True).cpu().numpy()
+    assert _rel(mg[:, :n], mw[:, :n]) <= 1e-12
+    for b in range(len(reb)):
+        Xw = R[rows[b, :tlen[b]]]
+        assert _rel(mg[b, :n], (1.0 + Xw).prod(0) ** (1.0 / tlen[b]) - 1.0) <= 1e-11
+
 @pytest.mark.parametrize("stride", [1, 21])
 def test_gram_xy_grouped_matches_per_window(device, stride):
     """pq_gram_xy_grouped (X'y, y'y and diag(X'X) of slide-group windows by entering / leaving
