@@ -1750,6 +1750,17 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
     double sum = 0.0;
     for (int j = hl; j < n; j += PPT) sum += cr[j] * wk.xs[j];
     sum = block_sum(sum, red);
+    // a vertex whose bound variables overshoot its equality row (the round before fixed
+    // several free variables at their upper bounds at once, e.g. two weights past 1 under a
+    // budget of 1): no free variable can restore the row, so the variables at a bound that
+    // push it past its value are released (uniform: every thread holds the sum)
+    if (vtx && r == r0 && has_box && sum > ug[r] + ptol * (1.0 + fabs(ug[r]))) {
+      for (int i = hl; i < n; i += PPT) {
+        const int f = wk.fl[i];
+        if ((f == 2 && cr[i] > 0.0) || (f == 1 && cr[i] < 0.0 && lb[i] != ub[i])) wk.fl[i] = 0;
+      }
+      bad = 1;
+    }
     if (hl == 0) {
       if (lg[r] != ug[r]) {
         const int a = (int)R[R_ACT + r];

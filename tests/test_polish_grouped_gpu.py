@@ -214,3 +214,31 @@ def test_inner_primal_steps_same_optimum_fewer_rounds(device):
     assert np.array_equal(outa[:, _lib.PQ_OUT_NFREE], outb[:, _lib.PQ_OUT_NFREE])
     ra, rb = outa[:, _lib.PQ_OUT_ROUNDS], outb[:, _lib.PQ_OUT_ROUNDS]
     assert rb.mean() <= ra.mean(), (ra.mean(), rb.mean())
+
+
+def test_vertex_overshoot_is_released(device):
+    """The drop-in's mean-variance problem (config-3 panel, q = -mu geometric: nearly linear,
+    ~3 free assets per date): a round that fixes two weights past their upper bound of 1 at
+    once leaves a vertex whose bound values overshoot the budget; the post releases them
+    (k_pg_post) instead of repeating that infeasible active set until the hand-off.  Every date
+    stays in the pipeline and matches the per-date polish from the eps_abs point."""
+    from porqua_amd.workloads import MinVarianceBacktest
+    wl = MinVarianceBacktest(D=4749, device=device)
+    n = wl.n
+    wl.qb.q[:, :n] = -wl.pan.window_geomeans_grouped(wl.gplan, wl.tlen_d)[:, :n]
+    ws = engine.Workspace(wl.qb, dense=False)
+    res = engine.solve_lowrank(wl.qb, wl.lr, wl.settings, ws=ws, groups=wl.gplan, sync_free=True, sf_rounds=4)
+    torch.cuda.synchronize()
+    fb = getattr(ws, "pg_fallback", None)
+    assert fb is None or fb.numel() == 0, fb
+    sa = res.status.cpu().numpy()
+    assert np.all(sa == _lib.PQ_SOLVED)
+    oa = res.obj.cpu().numpy().copy()
+    ws0 = engine.Workspace(wl.qb, dense=False)
+    import dataclasses
+    r0 = engine.solve_lowrank(wl.qb, wl.lr, dataclasses.replace(wl.settings, eps_grouped=0.0), ws=ws0,
+                              groups=wl.gplan, grouped_polish=False)
+    torch.cuda.synchronize()
+    o0 = r0.obj.cpu().numpy()
+    assert np.all(r0.status.cpu().numpy() == _lib.PQ_SOLVED)
+    assert np.max(np.abs(oa - o0) / np.maximum(np.abs(o0), 1e-30)) <= 1e-8
