@@ -39,6 +39,24 @@ from .optimization_data import OptimizationData
 from .portfolio import Portfolio, Strategy
 from .selection import Selection
 
+# page-locked weight panels kept for reuse: (rows, n) -> (tensor, weakref to the numpy view
+# handed out last).  Pinning tens of MB costs milliseconds per backtest; a panel is reused
+# only once nothing (no Portfolio row view) references the previous backtest's array.
+_PINNED: dict = {}
+
+
+def _pinned_panel(rows: int, n: int):
+    import weakref
+    import torch
+    ent = _PINNED.get((rows, n))
+    if ent is not None and ent[1]() is None:
+        t = ent[0]
+    else:
+        t = torch.empty((rows, n), dtype=torch.float64, pin_memory=True)
+    W = t.numpy()
+    _PINNED[(rows, n)] = (t, weakref.ref(W))
+    return t, W
+
 
 class BacktestData:
     def __init__(self):
@@ -423,8 +441,10 @@ class Backtest:
             return False, None, None, None, None
         # the weight panel lands in page-locked host memory (one DMA, no pageable bounce; the
         # Portfolio objects keep views of its rows)
-        Wt = torch.empty((hi - lo, n), dtype=torch.float64, pin_memory=True) if dev.type == "cuda" else None
-        W = Wt.numpy() if Wt is not None else np.zeros((hi - lo, n))
+        if dev.type == "cuda":
+            Wt, W = _pinned_panel(hi - lo, n)
+        else:
+            Wt, W = None, np.zeros((hi - lo, n))
         ST = np.zeros(hi - lo, dtype=np.int32)
         OBJ = np.zeros(hi - lo)
         split_panel = None
@@ -444,6 +464,24 @@ class Backtest:
             chunk = min(chunk, max(1, (1 << 35) // per))
         path = "lp-ipm" if lad else "dense"
         ok = True
+        # the lazy Portfolio objects of a single-rank, single-chunk run without append_fun are
+        # built while the device solves (views of W's rows, read only after the solve); phase C
+        # keeps those of the solved dates
+        self._prebuilt = None
+        import torch.distributed as _td
+        single = not (_td.is_available() and _td.is_initialized())
+
+        def prebuild():
+            if single and bs.settings.get("append_fun") is None:
+                keys = list(st["universe"])
+                gc_was = gc.isenabled()
+                gc.disable()
+                try:
+                    self._prebuilt = [Portfolio._from_row(d, keys, W[i])
+                                      for i, d in enumerate(st["rebdates"][lo:hi])]
+                finally:
+                    if gc_was:
+                        gc.enable()
         for s in range(lo, hi, chunk):
             e = min(hi, s + chunk)
             if lad:
@@ -502,7 +540,8 @@ class Backtest:
                     # (dates still pending after them take the host-driven rounds)
                     sf = stage.lowrank.mu is not None
                     res = engine.solve_lowrank(qb, stage.lowrank, settings, groups=stage.group_plan(),
-                                               sync_free=sf, sf_rounds=4 if sf else None)
+                                               sync_free=sf, sf_rounds=4 if sf else None,
+                                               host_work=prebuild if (sf and s == lo and e == hi) else None)
                 else:
                     res = engine.solve(qb, settings)
                 if Wt is not None:
@@ -534,8 +573,15 @@ class Backtest:
         # creates reference cycles, so the collector is paused for it
         gc_was = gc.isenabled()
         gc.disable()
+        pre = getattr(self, "_prebuilt", None)
+        self._prebuilt = None
+        if pre is not None and len(pre) != len(rebdates):
+            pre = None
         try:
             for i, d in enumerate(rebdates):
+                if pre is not None and append_fun is None and solved[i]:
+                    portfolios.append(pre[i])   # built during the solve (_solve_shard)
+                    continue
                 if append_fun is None and solved[i]:
                     # the weights stay a row of W until read (Portfolio._from_row); the dict is
                     # == pd.Series(w, index=universe).to_dict() (Python floats)

@@ -888,7 +888,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
                   fuse: bool = True, grouped_polish: bool = True, gcap: bool = True,
                   eig: "EigCap | None" = None, wide_polish: bool = True, sync_free: bool = False,
-                  graphs: "StageGraphs | None" = None, sf_rounds: int | None = None) -> BatchResult:
+                  graphs: "StageGraphs | None" = None, sf_rounds: int | None = None,
+                  host_work=None) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -900,7 +901,9 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     usual host-driven repairs must run (an adaptive-rho refactorisation: the whole solve is
     redone the host-driven way; dates still pending, handed back, or rejected: the remaining
     rounds, the per-date polish and the ADMM retry, exactly as without it).  With ``graphs``
-    (StageGraphs) the sync-free stages are captured once and replayed."""
+    (StageGraphs) the sync-free stages are captured once and replayed.  ``host_work`` (a
+    callable, sync-free only): the caller's host work that needs no result, run while the
+    device works, just before the flag read."""
     if sync_free and not (gcap and eig is None and groups is not None and grouped_polish and polish):
         sync_free = False
     tl = _Timeline(events, graphs if sync_free else None)
@@ -1142,6 +1145,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     admm_rounds(None, 0, SS_admm)
     if sync_free:
         pg.update(tl("polish", polish_sync_free))
+        if host_work is not None:
+            host_work()
         if not bool(ws._sf_flag.item()):   # the one host sync of the step: nothing left to repair
             return _lowrank_result(qb, ws, cnt, "group")
         if bool((ws.status == _lib.PQ_NEED_REFACTOR).any() | (ws.status == _lib.PQ_UNSOLVED).any()):
