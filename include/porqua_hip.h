@@ -91,6 +91,10 @@ typedef struct pq_settings {
    * that bound and the reduced system solved again inside the same round, at most this many
    * times (0: one solve per round, the checks of the round's end fix them) */
   int32_t polish_inner;
+  /* ADMM: the convergence test is skipped before this iteration (0: tested from the first).
+   * The loose stop before the grouped polish uses it so that an early dip of the residuals
+   * (ADMM's are not monotone) cannot end the iterations before the active set is predicted */
+  int32_t min_iter;
 } pq_settings;
 
 /* Low-rank description of P for T < n (the backtest path): P_eff = p_scale[b] *

@@ -81,7 +81,7 @@ class PQSettings(ctypes.Structure):
         ("max_iter", c_int32), ("adapt_interval", c_int32), ("polish", c_int32),
         ("polish_rounds", c_int32), ("refine_iters", c_int32),
         ("polish_fix_rel", ctypes.c_double),
-        ("polish_inner", ctypes.c_int32),
+        ("polish_inner", ctypes.c_int32), ("min_iter", ctypes.c_int32),
     ]
 
 

@@ -509,7 +509,7 @@ __global__ __launch_bounds__(AT) void k_admm(pq_problem pb, pq_state st, const i
     pc.stamp(5);
     const double eps_p = s.eps_abs + s.eps_rel * fmax(mv[1], mv[2]);
     const double eps_d = s.eps_abs + s.eps_rel * fmax(mv[4], fmax(mv[5], mv[6]));
-    if (mv[0] <= eps_p && mv[3] <= eps_d) {
+    if (it >= s.min_iter && mv[0] <= eps_p && mv[3] <= eps_d) {
       status = PQ_SOLVED;
       break;
     }

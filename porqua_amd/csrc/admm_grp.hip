@@ -656,7 +656,7 @@ __global__ __launch_bounds__(GT) void k_admm_grp(pq_lowrank lr, pq_problem pb, p
       const double eps_p = s.eps_abs + s.eps_rel * fmax(mv[1], mv[2]);
       const double eps_d = s.eps_abs + s.eps_rel * fmax(mv[4], fmax(mv[5], mv[6]));
       double rnew = rho;
-      if (mv[0] <= eps_p && mv[3] <= eps_d) {
+      if (it >= s.min_iter && mv[0] <= eps_p && mv[3] <= eps_d) {
         stat = PQ_SOLVED;
       } else if (s.adapt_interval > 0 && it % s.adapt_interval == 0) {
         const double rp = mv[0] / (fmax(mv[1], mv[2]) + 1e-30);

@@ -100,11 +100,16 @@ class Settings:
     # inner primal steps (polish_inner) the rounds stay cheap from a looser point
     # (profiles/r04t_eg*.log, one box, polish_inner = 1): 0.2 / 0.3 -> 461k / 466k (9 / 8
     # iterations, 2.2 / 2.3 rounds, at most 4, largest free set 88); 0.5 and 1.0 stop after 4
-    # iterations, where the free sets outgrow the LDS solve and every date takes the per-date
-    # fallback (144k).  0.2 keeps a factor 2.5 from that cliff.  Tracking (uncentred) windows keep eps_abs: their free
+    # iterations -- ADMM's residuals are not monotone: they dip below 0.5 at iteration 4 and
+    # stay above 0.3 until 8 -- where the free sets outgrow the LDS solve and every date takes
+    # the per-date fallback (144k).  The loose stop therefore also waits for min_iter_grouped
+    # iterations: 0.3 with at least 8 -> 536k (r04O_eg25*.log: 0.25, the same 8 iterations),
+    # and a larger eps cannot fall off that cliff.  Tracking (uncentred) windows keep eps_abs: their free
     # sets mostly exceed the LDS solve -- config 2 53.0k at 2e-3, 45.0k at 1e-2 from the loose
     # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
-    eps_grouped: float = 0.2
+    eps_grouped: float = 0.3
+    min_iter_grouped: int = 8   # (host-side) the loose stop's pq_settings.min_iter
+    min_iter: int = 0           # pq_settings.min_iter: no convergence test before this iteration
     # grouped polish: variables with x - lb < polish_fix_rel * max(x - lb) at the ADMM point
     # also start fixed at lb (besides OSQP's z - lb < -y): the loose ADMM point leaves small
     # positive weights that the first rounds would only fix later.  Numpy model of config 3
@@ -1138,6 +1143,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
             and st_.eps_grouped > max(st_.eps_abs, st_.eps_rel)):
         sl = st_.to_c()
         sl.eps_abs = sl.eps_rel = st_.eps_grouped
+        sl.min_iter = max(int(st_.min_iter), int(st_.min_iter_grouped))
         SS_admm = ctypes.byref(sl)
     if sync_free and not (grouped and ldk >= 64 and s.polish):
         sync_free = False

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # (C type, ctypes mirror, last field)
 STRUCTS = [("pq_problem", _lib.PQProblem, "box_stride"), ("pq_state", _lib.PQState, "work_stride"),
-           ("pq_settings", _lib.PQSettings, "polish_inner"), ("pq_lowrank", _lib.PQLowRank, "dg_stride"),
+           ("pq_settings", _lib.PQSettings, "min_iter"), ("pq_lowrank", _lib.PQLowRank, "dg_stride"),
            ("pq_gcap", _lib.PQGcap, None), ("pq_pg_wide", _lib.PQPgWide, "refine_steps")]
 
 

@@ -34,7 +34,7 @@ def main():
     if not watch:
         return
     ws = engine.Workspace(wl.qb, dense=False)
-    s_adm = dataclasses.replace(st, polish=0, eps_abs=st.eps_grouped, eps_rel=st.eps_grouped)
+    s_adm = dataclasses.replace(st, polish=0, eps_abs=st.eps_grouped, eps_rel=st.eps_grouped, min_iter=st.min_iter_grouped)
     engine.solve_lowrank(wl.qb, wl.lr, s_adm, ws=ws, groups=wl.gplan, polish=False)
     lib = _lib.load()
     s = st.to_c()

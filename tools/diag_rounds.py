@@ -33,7 +33,7 @@ def main():
     import dataclasses
     st = wl.settings
     ws = engine.Workspace(wl.qb, dense=False)
-    s_adm = dataclasses.replace(st, polish=0, eps_abs=st.eps_grouped, eps_rel=st.eps_grouped)   # the loose stop
+    s_adm = dataclasses.replace(st, polish=0, eps_abs=st.eps_grouped, eps_rel=st.eps_grouped, min_iter=st.min_iter_grouped)   # the loose stop
     engine.solve_lowrank(wl.qb, wl.lr, s_adm, ws=ws, groups=wl.gplan, polish=False)
     lib = _lib.load()
     s = st.to_c()
