@@ -209,6 +209,32 @@ def test_backtest_lowrank_path_matches_oracle(device, kind):
         assert abs(W[i].sum() - 1) < 1e-7 and W[i].min() > -1e-7 and W[i].max() < 0.1 + 1e-7
 
 
+def test_backtests_keep_their_weights_across_runs(device):
+    """The batched path's page-locked weight panel is reused only when no Portfolio of the
+    previous backtest still views it, and its lazy Portfolio objects are built while the
+    device solves: a second backtest (other risk aversion) must not change the first one's
+    weights, read before or after it, and a repeated run gives the same weights."""
+    n, D, width = 300, 160, 60
+    X, y = _synthetic(n, D, seed=12)
+    rebdates = [str(d.date()) for d in X.index[width + 5:width + 5 + 24]]
+    bt1 = Backtest()
+    bt1.run(_service(MeanVariance(solver_name="mi355x"), X, y, rebdates, {"upper": 0.1}, width=width))
+    first_read = dict(bt1.strategy.portfolios[0].weights)        # one portfolio read early
+    bt2 = Backtest()
+    bt2.run(_service(MeanVariance(solver_name="mi355x", risk_aversion=50.0), X, y, rebdates, {"upper": 0.1},
+                     width=width))
+    W1 = bt1.strategy.get_weights_df().to_numpy(dtype=float)
+    W2 = bt2.strategy.get_weights_df().to_numpy(dtype=float)
+    assert np.abs(W1 - W2).max() > 1e-3                          # different problems
+    assert bt1.strategy.portfolios[0].weights == first_read
+    del bt2
+    bt3 = Backtest()                                              # reuses bt2's released panel
+    bt3.run(_service(MeanVariance(solver_name="mi355x"), X, y, rebdates, {"upper": 0.1}, width=width))
+    W3 = bt3.strategy.get_weights_df().to_numpy(dtype=float)
+    assert np.abs(W3 - W1).max() < 1e-9
+    assert np.array_equal(bt1.strategy.get_weights_df().to_numpy(dtype=float), W1)
+
+
 def test_nearest_pd_higham_on_device_matches_reference(device):
     """nearestPD (src/helper_functions.py:29-58) on the device: the projection and the
     eigenvalue shifts on the hand-written block-Jacobi eigensolver, the PD tests on K2.  Checked against the
