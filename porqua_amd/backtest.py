@@ -535,10 +535,10 @@ class Backtest:
                 OBJ[s - lo:e - lo] = (res.obj + const).cpu().numpy()
             else:
                 if stage.lowrank is not None:
-                    # centred windows (the mean-variance family: no wide polish rounds): the
-                    # sync-free stages -- one ADMM launch, four polish rounds, one flag read
-                    # (dates still pending after them take the host-driven rounds)
-                    sf = stage.lowrank.mu is not None
+                    # the sync-free stages -- one ADMM launch, four polish rounds, one flag read
+                    # (dates still pending after them, handed back or needing the wide rounds
+                    # take the host-driven path); PQ_SF_CENTRED_ONLY=1: centred windows only
+                    sf = stage.lowrank.mu is not None or os.environ.get("PQ_SF_CENTRED_ONLY", "0") != "1"
                     res = engine.solve_lowrank(qb, stage.lowrank, settings, groups=stage.group_plan(),
                                                sync_free=sf, sf_rounds=4 if sf else None,
                                                host_work=prebuild if (sf and s == lo and e == hi) else None)

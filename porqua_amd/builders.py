@@ -64,8 +64,19 @@ def bibfn_selection_data(bs, rebdate: str, **kwargs) -> pd.Series:
     return pd.Series(np.ones(data.shape[1], dtype=int), index=data.columns, name="binary")
 
 
+def _upto(data, rebdate, width):
+    """data[data.index <= rebdate].tail(width): on a sorted index the rows up to the date are a
+    prefix, so the window is one positional slice (no copy of the whole prefix first)."""
+    idx = data.index
+    if isinstance(idx, pd.DatetimeIndex) and idx.is_monotonic_increasing:
+        end = int(idx.searchsorted(pd.Timestamp(rebdate), side="right"))
+        return data.iloc[max(0, end - width) if width is not None else 0:end]
+    out = data[idx <= rebdate]
+    return out.tail(width) if width is not None else out
+
+
 def _trailing(data: pd.DataFrame, rebdate, width):
-    out = data[data.index <= rebdate].tail(width)
+    out = _upto(data, rebdate, width)
     return out[out.index.dayofweek < 5]
 
 
@@ -75,7 +86,7 @@ def bibfn_return_series(bs, rebdate: str, **kwargs) -> None:
     if data is None:
         raise ValueError("Return series data is missing.")
     ids = bs.selection.selected
-    out = data[data.index <= rebdate].tail(kwargs.get("width"))[ids]
+    out = _upto(data, rebdate, kwargs.get("width"))[ids]
     bs.optimization_data["return_series"] = out[out.index.dayofweek < 5]
 
 

@@ -109,6 +109,12 @@ class Settings:
     # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
     eps_grouped: float = 0.3
     min_iter_grouped: int = 8   # (host-side) the loose stop's pq_settings.min_iter
+    # (host-side) the same loose stop for uncentred (tracking) windows on the group capacitance;
+    # 0: off (they stop at eps_abs / eps_rel).  Measured on config 2 (profiles/r04T_*.log): off /
+    # 1e-2 / 3e-2 / 1e-1 -> 161k / 151k / 142k / 114k QPs/s (20 / 17 / 15 / 13 iterations, 2.7 /
+    # 3.1 / 3.5 / 4.0 rounds): the tracking rounds (free sets of 160..220) cost more than the
+    # ADMM iterations they replace
+    eps_grouped_tracking: float = 0.0
     min_iter: int = 0           # pq_settings.min_iter: no convergence test before this iteration
     # grouped polish: variables with x - lb < polish_fix_rel * max(x - lb) at the ADMM point
     # also start fixed at lb (besides OSQP's z - lb < -y): the loose ADMM point leaves small
@@ -1139,10 +1145,11 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     SS_main = SS
     SS_admm = SS
     st_ = settings or Settings()
-    if (gc is not None and lr.mu is not None and polish and s.polish and grouped_polish and ldk >= 64
-            and st_.eps_grouped > max(st_.eps_abs, st_.eps_rel)):
+    eps_loose = st_.eps_grouped if lr.mu is not None else st_.eps_grouped_tracking
+    if (gc is not None and polish and s.polish and grouped_polish and ldk >= 64
+            and eps_loose > max(st_.eps_abs, st_.eps_rel)):
         sl = st_.to_c()
-        sl.eps_abs = sl.eps_rel = st_.eps_grouped
+        sl.eps_abs = sl.eps_rel = eps_loose
         sl.min_iter = max(int(st_.min_iter), int(st_.min_iter_grouped))
         SS_admm = ctypes.byref(sl)
     if sync_free and not (grouped and ldk >= 64 and s.polish):

@@ -32,6 +32,12 @@ class Selection:
         return self._filtered
 
     def get_selected(self, filter_names: Optional[list] = None) -> pd.Index:
+        names = list(self.filtered.keys()) if filter_names is None else list(filter_names)
+        if len(names) == 1:   # one binary Series (the usual selection): the same rows, no frame
+            v = self.filtered[names[0]]
+            if isinstance(v, pd.Series) and v.name == "binary" and v.index.is_unique:
+                v = v.dropna()
+                return v.index[v.to_numpy() == 1]
         df = self.df_binary(filter_names)
         return df[df.eq(1).all(axis=1)].index
 
