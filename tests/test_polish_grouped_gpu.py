@@ -242,3 +242,22 @@ def test_vertex_overshoot_is_released(device):
     o0 = r0.obj.cpu().numpy()
     assert np.all(r0.status.cpu().numpy() == _lib.PQ_SOLVED)
     assert np.max(np.abs(oa - o0) / np.maximum(np.abs(o0), 1e-30)) <= 1e-8
+
+
+def test_loose_stop_waits_for_min_iter(device):
+    """pq_settings.min_iter: the loose ADMM stop before the grouped polish is not taken before
+    Settings.min_iter_grouped iterations even when the residuals already pass a very loose eps
+    (ADMM's early residuals dip and rise again); the answers stay the certified optimum."""
+    import dataclasses
+    qb, lr, gp = _problem(device, 1000, 252, 48, 1.0)
+    d = engine.Settings()
+    assert d.min_iter_grouped >= 1
+    xa, sa, oa, *_ = _solve(qb, lr, gp, True)
+    ws = engine.Workspace(qb, dense=False)
+    res = engine.solve_lowrank(qb, lr, dataclasses.replace(d, eps_grouped=10.0), ws=ws, groups=gp)
+    torch.cuda.synchronize()
+    it = res.iters.cpu().numpy()
+    assert it.min() >= d.min_iter_grouped, it.min()
+    assert np.all(res.status.cpu().numpy() == _lib.PQ_SOLVED)
+    ob = res.obj.cpu().numpy()
+    assert np.max(np.abs(ob - oa) / np.maximum(np.abs(oa), 1e-30)) <= 1e-9
