@@ -381,3 +381,30 @@ def test_sparse_columns_of_group_rows():
     qb2 = engine.QPBatch.from_dense(None, None, n=n, A=np.ones((1, n)), b=np.ones(1), G=np.ones((4, n)),
                                     h=np.full(4, 0.5), lb=np.zeros(n), ub=np.ones(n), device=torch.device("cpu"))
     assert engine._sparse_columns(qb2)[2] == 0     # 5 nonzeros per column: dense reads
+
+
+def test_trailing_window_slice_matches_the_boolean_mask():
+    """builders._upto (one positional slice on a sorted DatetimeIndex) returns exactly
+    data[data.index <= rebdate].tail(width) (src/builders.py:188-251), for dates inside,
+    before and after the panel, dates between rows, any width, and an unsorted index."""
+    import pandas as pd
+    from porqua_amd import builders
+    idx = pd.bdate_range("2020-01-01", periods=300)
+    df = pd.DataFrame(np.arange(600.0).reshape(300, 2), index=idx, columns=["a", "b"])
+    for data in (df, df.iloc[::-1], df["a"]):
+        for date in ("2019-06-01", "2020-01-01", "2020-03-07", str(idx[150].date()), str(idx[-1].date()),
+                     "2030-01-01"):
+            for width in (1, 21, 252, 1000, None):
+                ref = data[data.index <= date]
+                ref = ref.tail(width) if width is not None else ref
+                assert builders._upto(data, date, width).equals(ref), (date, width)
+
+
+def test_single_binary_filter_selection():
+    import pandas as pd
+    from porqua_amd.selection import Selection
+    s = Selection()
+    s.add_filtered("data", pd.Series([1, 0, 1, 1], index=list("abcd"), name="binary"))
+    assert list(s.selected) == ["a", "c", "d"] and isinstance(s.selected, pd.Index)
+    s.add_filtered("more", pd.Series([1, 1, 0, 1], index=list("abcd"), name="binary"))
+    assert list(s.selected) == ["a", "d"]
