@@ -362,16 +362,25 @@ __device__ __forceinline__ void form_from_group(const pq_lowrank& lr, const pq_p
   if (t == 0) R[R_FORMED] = 1.0;
 }
 
+// KF = PG_KMAX: the LDS solve's free sets (and the group form); KF = PG_KBIG: the free sets
+// of k_pg_big (PG_KMAX < k <= PG_KBIG), formed here the same way -- every window chunk
+// gathered once for all tiles -- instead of one window pass per 64 x 64 tile
+template <int KF>
 __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
                                                 int ldk, const int32_t* gdates, int ngroups,
                                                 const int32_t* urows_all, const int32_t* ucnt_all,
                                                 const int32_t* uoff, int umax, const double* scr) {
-  __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPIT];
+  constexpr int FPITK = KF + 4;                        // LDS pitch (doubles)
+  constexpr int NCG = KF / 32;                         // gathered columns per thread and row
+  constexpr int NTL = (KF / 16) * (KF / 16 + 1) / 2;   // lower 16 x 16 tiles
+  constexpr int FTWK = (NTL + FNW - 1) / FNW;          // tiles per wave
+  static_assert(KF != PG_KMAX || FTWK == FTW, "k_pg_form tiling");
+  __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPITK];
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;   // wide dates: polish_gw.hip
   const int k = (int)R[R_K];
-  if (k > PG_KMAX || k == 0) return;
+  if (KF == PG_KMAX ? (k > PG_KMAX || k == 0) : (k <= PG_KMAX || k > KF)) return;
   if (R[R_REUSE] != 0.0) {   // P_FF is a principal submatrix of the formed one: nothing to form
     if (R[R_NZB] != 0.0) {   // (the reduced rhs still takes P_FB x_B from pass 0)
       PGWork wk0(st, b, pb.ld);
@@ -388,9 +397,11 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
   if (R[R_NZB] != 0.0)   // rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F  (pass 0 left it in pxb)
     for (int p = t; p < k; p += FT) wk.rF[p] -= ps * wk.pxb[wk.Fl[p]];
-  if (R[R_GFORM] != 0.0) {   // from the group Gram (k_pg_form_grp)
-    form_from_group(lr, pb, st, R, b, k, ldk, gdates, ngroups, urows_all, ucnt_all, uoff, umax, scr, S);
-    return;
+  if constexpr (KF == PG_KMAX) {
+    if (R[R_GFORM] != 0.0) {   // from the group Gram (k_pg_form_grp)
+      form_from_group(lr, pb, st, R, b, k, ldk, gdates, ngroups, urows_all, ucnt_all, uoff, umax, scr, S);
+      return;
+    }
   }
   const int T = lr.tlen[b];
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
@@ -406,57 +417,59 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   const int kp = nt * 16;
   // gather map: thread t -> window row t / 32 of a chunk, free columns (t % 32) + 32 c
   const int gr = t >> 5, gc = t & 31;
-  int col[4];
-  double mc[4];
+  int col[NCG];
+  double mc[NCG];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < NCG; ++c) {
     const int p = gc + 32 * c;
     col[c] = p < k ? wk.Fl[p] : -1;
     mc[c] = (col[c] >= 0 && mu) ? mu[col[c]] : 0.0;
   }
-  double v[4];
+  double v[NCG];
   // unconditional loads (clamped row / column, zeroed by a factor after the load: a conditional
   // load makes the compiler wait for every outstanding load there)
   auto gather = [&](int t0) {
     const int tt = t0 + gr;
     const double* row = lr.panel + (int64_t)rws(tt < T ? tt : 0) * lr.ldp;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < NCG; ++c) {
       const double x = row[col[c] >= 0 ? col[c] : 0];
       v[c] = (x - mc[c]) * ((tt < T && col[c] >= 0) ? 1.0 : 0.0);
     }
   };
   auto put = [&](double* Sb) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (gc + 32 * c < kp) Sb[gr * FPIT + gc + 32 * c] = v[c];
+    for (int c = 0; c < NCG; ++c)
+      if (gc + 32 * c < kp) Sb[gr * FPITK + gc + 32 * c] = v[c];
   };
-  // this wave's tiles (I, J), I >= J, in column-major order of the lower triangle
-  int tI[FTW], tJ[FTW];
+  // this wave's tiles (I, J), I >= J, in column-major order of the lower triangle (from the
+  // wave index made uniform: the tile coordinates stay in scalar registers)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int tI[FTWK], tJ[FTWK];
 #pragma unroll
-  for (int j = 0; j < FTW; ++j) {
-    const int q = w + FNW * j;
+  for (int j = 0; j < FTWK; ++j) {
+    const int q = wu + FNW * j;
     int I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
     while ((I + 1) * (I + 2) / 2 <= q) ++I;
     while (I * (I + 1) / 2 > q) --I;
     tI[j] = I;
     tJ[j] = q - I * (I + 1) / 2;
   }
-  f64x4 acc[FTW];
+  f64x4 acc[FTWK];
 #pragma unroll
-  for (int j = 0; j < FTW; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int j = 0; j < FTWK; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
   auto mma = [&](const double* Sb) {
 #pragma unroll
     for (int kk = 0; kk < FKCH; kk += 4) {
-      const double* r = Sb + (kk + (l >> 4)) * FPIT + (l & 15);
+      const double* r = Sb + (kk + (l >> 4)) * FPITK + (l & 15);
 #pragma unroll
-      for (int j = 0; j < FTW; ++j)
-        if (w + FNW * j < ntile)
+      for (int j = 0; j < FTWK; ++j)
+        if (wu + FNW * j < ntile)
           acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 * tI[j]], r[16 * tJ[j]], acc[j], 0, 0, 0);
     }
   };
   double* S0 = S;
-  double* S1 = S + FKCH * FPIT;
+  double* S1 = S + FKCH * FPITK;
   gather(0);
   put(S0);
   __syncthreads();
@@ -473,10 +486,10 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   for (int i = t; i < pb.n; i += FT) wk.posF[i] = -1;   // positions of the formed free list
   __syncthreads();
   for (int p = t; p < k; p += FT) wk.posF[wk.Fl[p]] = p;
-  if (t == 0) R[R_FORMED] = 1.0;
+  if (t == 0) R[R_FORMED] = 1.0;   // (k_pg_big factors in place and clears it again)
 #pragma unroll
-  for (int j = 0; j < FTW; ++j) {
-    if (w + FNW * j < ntile) {
+  for (int j = 0; j < FTWK; ++j) {
+    if (wu + FNW * j < ntile) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
@@ -1183,11 +1196,9 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
   double* Dt = st.Dt + (int64_t)b * st.Dt_stride;
   const int nbk = (k + TB - 1) / TB;
   const int kp = nbk * TB;
-  // reduced rhs: rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F (pass 0 left the window part in pxb)
-  if (R[R_NZB] != 0.0)
-    for (int p = t; p < k; p += PT) wk.rF[p] -= ps * wk.pxb[wk.Fl[p]];
-  __syncthreads();
-  form_pff(lr, b, wk.Fl, k, nbk, psw, pd, K, ldk, smem);
+  // P_FF (both triangles) and the reduced rhs rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F come
+  // from k_pg_form<PG_KBIG> on the same stream; FormW reads the diagonal 64 x 64 blocks in
+  // full and the other originals from the upper half, which the factor leaves untouched
   const int info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
   if (t == 0) R[R_FORMED] = 0.0;   // the lower tiles now hold L: no reuse of this P_FF
   if (info) {
@@ -1972,7 +1983,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   if (pq::group_form_min() > 0)   // P_FF from one union Gram per polish group (k_pg_form_grp)
     hipLaunchKernelGGL(pq::k_pg_form_grp, dim3(ngroups), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, gdates, urows,
                        ucnt, umax, pass_scratch, pq::group_form_min());
-  hipLaunchKernelGGL(pq::k_pg_form, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk, gdates, ngroups, urows,
+  hipLaunchKernelGGL(pq::k_pg_form<pq::PG_KMAX>, dim3(B), dim3(pq::FT), 0, str, *lr, *pb, *st, rec, ldk, gdates, ngroups, urows,
                      ucnt, uoff, umax, pass_scratch);
   // one workgroup per date, the LDS triangle sized to the free set (more dates per CU when small);
   // the buckets (and the wide rounds) on side streams, joined before the exact-P x passes
@@ -1990,8 +2001,13 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
     pq::launch_solve(i, pq::solve_waves(i), B, on(i), pb, st, rec, s, ldk, i ? KSB[i - 1] : 0);
   }
   if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, on(5))) return -1;   // free sets beyond kmax
-  if (kbig > kmax)
-    hipLaunchKernelGGL(pq::k_pg_big, dim3(B), dim3(pq::PT), 0, on(6), *lr, *pb, *st, rec, *s, ldk, kmax);
+  if (kbig > kmax) {   // free sets of kmax + 1 .. kbig: their P_FF, then the factor and solve
+    static_assert(pq::PG_KBIG == 256, "k_pg_form<PG_KBIG> tiling");
+    const hipStream_t sb = on(6);
+    hipLaunchKernelGGL(pq::k_pg_form<pq::PG_KBIG>, dim3(B), dim3(pq::FT), 0, sb, *lr, *pb, *st, rec, ldk, gdates,
+                       ngroups, urows, ucnt, uoff, umax, pass_scratch);
+    hipLaunchKernelGGL(pq::k_pg_big, dim3(B), dim3(pq::PT), 0, sb, *lr, *pb, *st, rec, *s, ldk, kmax);
+  }
   for (int i = 0; side && i < pq::PgSide::NS; ++i)
     if ((used & (1 << i)) && (hipEventRecord(side->join[i], side->s[i]) != hipSuccess ||
                               hipStreamWaitEvent(str, side->join[i], 0) != hipSuccess)) {
