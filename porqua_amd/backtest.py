@@ -233,18 +233,30 @@ class _PanelUpload:
 
     def __init__(self, frame):
         import threading
+        from . import engine
         self._out = None
         self._err = None
         self._frame = frame
+        # the device is resolved HERE, on the calling thread: torch's current device is per
+        # host thread, so a worker would see device 0 instead of the rank's set_device choice
+        try:
+            self._dev = engine.default_device()
+        except BaseException as ex:   # (no device: surfaces in result(), as on the serial path)
+            self._dev, self._err = None, ex
         self._t = threading.Thread(target=self._run, daemon=True)
         self._t.start()
 
     def _run(self):
         import torch
-        from . import engine
-        try:   # (no device: the error surfaces in result(), where the serial path would raise it too)
+        if self._err is not None:
+            return
+        try:
             R = np.ascontiguousarray(self._frame.to_numpy(dtype=np.float64))
-            self._out = torch.from_numpy(R).to(engine.default_device())
+            if self._dev.type == "cuda":
+                with torch.cuda.device(self._dev):   # the worker's HIP context on the rank's GPU
+                    self._out = torch.from_numpy(R).to(self._dev)
+            else:
+                self._out = torch.from_numpy(R).to(self._dev)
         except BaseException as ex:   # re-raised in the caller's thread
             self._err = ex
 

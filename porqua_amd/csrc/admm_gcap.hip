@@ -878,13 +878,16 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         }
         if (!cin) continue;
         // per-asset data, shared by the lane's dates
-        constexpr int MGR = WIDE ? 1 : (MGC > 0 ? MGC : 1);   // register-resident columns
+        // register-resident columns: MGL of them (0 for the box-only and the wide forms; the
+        // arrays keep one slot so they are never zero-length, but no loop reads past MGL --
+        // an unread slot must not be read: its register is undefined, and 0 * undefined was
+        // folded to garbage that stopped every box-only date after one iteration)
+        constexpr int MGL = WIDE ? 0 : MGC;
+        constexpr int MGR = MGL > 0 ? MGL : 1;
         double2 cg2[MGR];
-        if constexpr (!WIDE) {
 #pragma unroll
-          for (int c = 0; c < MGC; ++c)
-            cg2[c] = c < mg ? *reinterpret_cast<const double2*>(pb.Cg + (int64_t)c * ld + i) : double2{0.0, 0.0};
-        }
+        for (int c = 0; c < MGL; ++c)
+          cg2[c] = c < mg ? *reinterpret_cast<const double2*>(pb.Cg + (int64_t)c * ld + i) : double2{0.0, 0.0};
         int nzr2[2][WIDE ? CNZ : 1];   // wide form: the pair's nonzero rows (-1: none) and values
         double nzv2[2][WIDE ? CNZ : 1];
         if constexpr (WIDE) {
@@ -934,8 +937,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           }
           double cwm[MGR], rgzm[MGR], ygm[MGR], wgm[MGR];
 #pragma unroll
-          for (int c = 0; c < MGR; ++c) {
-            const bool ok = !WIDE && c < mg;
+          for (int c = 0; c < MGL; ++c) {
+            const bool ok = c < mg;
             cwm[c] = ok ? g_cw[m * MGG + c] : 0.0;
             rgzm[c] = ok ? g_rgz[m * MGG + c] : 0.0;
             ygm[c] = ok ? g_yg[m * MGG + c] : 0.0;
@@ -964,14 +967,14 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             double corr = xr - su * mui + gcw;
             double cgi[MGR];
 #pragma unroll
-            for (int c = 0; c < MGR && !WIDE; ++c) {
+            for (int c = 0; c < MGL; ++c) {
               cgi[c] = sel ? cg2[c].y : cg2[c].x;
               corr = fma(cwm[c], cgi[c], corr);
             }
             const double xt = (rr0 - corr) * dinv;
             double pxt = rr0 - sigma * xt - rbi * xt - grgz;
 #pragma unroll
-            for (int c = 0; c < MGR && !WIDE; ++c) {
+            for (int c = 0; c < MGL; ++c) {
               pxt -= cgi[c] * rgzm[c];
               cgy = fma(cgi[c], ygm[c], cgy);
               cgw = fma(cgi[c], wgm[c], cgw);
@@ -1048,10 +1051,16 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       const int it = g_it[g] + 1;
       int stat = PQ_UNSOLVED;
+      // the maxima above are fmax reductions, which drop NaN; muv is a sum over every asset of
+      // mu_i (rhs_i / d) and carries a NaN iterate even where mu = 0 (0 * NaN = NaN), so a
+      // non-finite iterate cannot pass as converged: it fails the date loudly
+      const bool finite = isfinite(muv);
       const double eps_p = s.eps_abs + s.eps_rel * fmax(mv[1], mv[2]);
       const double eps_d = s.eps_abs + s.eps_rel * fmax(mv[4], fmax(mv[5], mv[6]));
       double rn = 0.0;   // this date's rho request (0: none)
-      if (it >= s.min_iter && mv[0] <= eps_p && mv[3] <= eps_d) {
+      if (!finite) {
+        stat = PQ_NON_CONVEX;
+      } else if (it >= s.min_iter && mv[0] <= eps_p && mv[3] <= eps_d) {
         stat = PQ_SOLVED;
       } else if (s.adapt_interval > 0 && it % s.adapt_interval == 0) {
         const double rp = mv[0] / (fmax(mv[1], mv[2]) + 1e-30);

@@ -390,6 +390,7 @@ class StageGraphs:
         self.pool = None
         self._seen = {}
         self._warm = set()
+        self.replays = 0   # replays of a graph captured by an earlier step (tests, diagnostics)
 
     def begin(self):
         self._seen = {}
@@ -401,6 +402,8 @@ class StageGraphs:
         self._seen[name] = k + 1
         key = (name, k)
         hit = self.graphs.get(key)
+        if hit is not None:
+            self.replays += 1
         if hit is None:
             if key not in self._warm:
                 self._warm.add(key)
@@ -971,10 +974,10 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     sparse_cols = _sparse_columns(qb) if grouped else (None, None, 0)
     # group capacitance: shared rows, register-resident (mg <= 4) or column-sparse (mg <= 24,
     # <= 4 nonzeros per asset); pass 1 of admm_gcap.hip covers U + mg <= 320 rows
-    # (box-only problems, mg = 0, keep the per-date capacitance: the group form measured wrong
-    # there -- every date stopped after one iteration, tests/test_gcap_gpu.py)
+    # (box-only problems, mg = 0, included: k_admm_gcap<0> once read an undefined Cg register
+    # and stopped every date after one iteration; fixed, tests/test_gcap_gpu.py)
     gcap_try = (gcap and eig is None and grouped and fuse and qb.shared
-                and (1 <= qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
+                and (qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
                 and groups.ucnt_max + qb.mg <= 320 and groups.corr_max <= 64)
     if band:
         # the band must cover every union the capacitances read: the ADMM's groups and the
@@ -1274,10 +1277,13 @@ def slide_plan(rows, tlen, group: int = 32, smax: int = 64, smin: int = 1):
         s = ((prev[:, :h] < cur[:, :1]) & (col[None, :h] < tp[:, None])).sum(1)
         cand = (tp == tc) & (tc > 1) & (s >= smin) & (s <= smax)
         # windows that are one contiguous run of panel rows (no gap: last - first = T - 1)
-        # overlap exactly when they have the same length -- no element compare needed
+        # of the same length, the current one starting exactly s rows after the previous one,
+        # are that window shifted by s -- no element compare needed.  (Without the start check
+        # a later window starting EARLIER -- descending or shuffled dates -- counts s = 0 and
+        # would pass as identical.)
         last = rows[np.arange(B), np.maximum(tlen - 1, 0)]
         contig = (last - rows[:, 0]) == (tlen - 1)
-        match = cand & contig[:-1] & contig[1:]
+        match = cand & contig[:-1] & contig[1:] & ((cur[:, 0] - prev[:, 0]) == s)
         need = cand & ~match
         for sv in np.unique(s[need]).tolist():   # rows[d][:T-s] == rows[d-1][s:T], per shift value
             sel = np.flatnonzero(need & (s == sv))

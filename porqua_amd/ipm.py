@@ -243,22 +243,24 @@ def active_set_polish(P, q, A, b, G, h, lb, ub, x, y, z, zb, rounds: int = 8):
             return x, y, z, zb, False
         HiC = fac.solve_mat(CF.T[None].contiguous())[0] if m else None
         if m:
-            # Schur complement of the active rows, S = C_F P_FF^-1 C_F' (m x m, SPD; rows that
-            # are dependent make it singular), factored and inverted on K2 with a shift of
-            # 1e-14 of its diagonal (grown by K2's retries when a row is dependent) -- on the
-            # device, no host copy; the refinement step below absorbs the shift
+            # Schur complement of the active rows, S = C_F P_FF^-1 C_F' (m x m, m <= a few
+            # dozen; SPD, singular when active rows are linearly dependent).  Its pseudo-inverse
+            # from a symmetric eigendecomposition on the device (eigenvalues below 1e-12 of the
+            # largest dropped) gives the minimum-norm multipliers: a dependent row's share is
+            # split evenly instead of scaled by 1 / shift (the former shifted Cholesky left x
+            # right -- HiC annihilates that part -- but y / z arbitrarily large)
             S = 0.5 * (CF @ HiC + (CF @ HiC).T)
-            sfac = _NormalFactor(1, m, dev)
-            sfac.factor(S[None], 1e-14 * S.diagonal().abs().amax().clamp(min=1e-300) *
-                        torch.ones((1, m), dtype=F64, device=dev))
+            ev, V = torch.linalg.eigh(S)
+            keep = ev > 1e-12 * ev.abs().max().clamp(min=1e-300)
+            Sp = (V * torch.where(keep, 1.0 / torch.where(keep, ev, torch.ones_like(ev)), torch.zeros_like(ev))) @ V.T
 
         def solve(f, g):
             hf = fac.solve_mat(f[None, :, None].contiguous())[0, :, 0]
             if not m:
                 return hf, torch.zeros(0, dtype=F64, device=dev)
-            r = (CF @ hf - g)[None, :, None].contiguous()
-            lam = sfac.solve_mat(r)
-            lam = (lam + sfac.solve_mat(r - S[None] @ lam))[0, :, 0]   # one refinement step
+            r = CF @ hf - g
+            lam = Sp @ r
+            lam = lam + Sp @ (r - S @ lam)   # one refinement step
             return hf - HiC @ lam, lam
 
         xF, lam = solve(rF, dF)

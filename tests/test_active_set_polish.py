@@ -41,3 +41,29 @@ def test_polish_reaches_the_oracle_optimum(monkeypatch):
     assert np.abs(x.numpy() - exact.x).max() <= 1e-10
     g = pr["P"] @ x.numpy() + pr["q"] + pr["A"].T @ y.numpy() + pr["G"].T @ z.numpy() + zb.numpy()
     assert np.abs(g).max() <= 1e-12 * max(1.0, np.abs(pr["q"]).max()) + 1e-15
+
+
+def test_dependent_active_rows_give_bounded_multipliers(monkeypatch):
+    """Linearly dependent active rows (the budget row twice): x is the single-row optimum and
+    the multipliers are the minimum-norm split of the single row's (each half), not scaled by
+    the reciprocal of a regularising shift."""
+    monkeypatch.setattr(ipm, "_NormalFactor", _DenseFactor)
+    pr = dense_qp(120, T=80, seed=5)
+    cons = {k: pr[k] for k in ("G", "h", "A", "b", "lb", "ub")}
+    rough = solve_qp(pr["P"], pr["q"], tol=1e-7, refine=False, **cons)
+    exact = solve_qp(pr["P"], pr["q"], **cons)
+    T = lambda v: torch.from_numpy(np.asarray(v, dtype=np.float64))
+    A2 = np.vstack([pr["A"], pr["A"]])
+    b2 = np.concatenate([np.atleast_1d(pr["b"]), np.atleast_1d(pr["b"])])
+    y2 = np.concatenate([rough.y, rough.y]) / 2.0
+    x, y, z, zb, ok = ipm.active_set_polish(T(pr["P"]), T(pr["q"]), T(A2), T(b2), T(pr["G"]), T(pr["h"]),
+                                            T(pr["lb"]), T(pr["ub"]), T(rough.x), T(y2), T(rough.z),
+                                            T(rough.z_box))
+    assert ok
+    assert np.abs(x.numpy() - exact.x).max() <= 1e-10
+    me = np.atleast_1d(pr["b"]).size
+    ya, yb = y.numpy()[:me], y.numpy()[me:]
+    assert np.abs(ya - yb).max() <= 1e-9 * max(1.0, np.abs(exact.y).max())
+    assert np.abs((ya + yb) - exact.y).max() <= 1e-8 * max(1.0, np.abs(exact.y).max())
+    g = pr["P"] @ x.numpy() + pr["q"] + A2.T @ y.numpy() + pr["G"].T @ z.numpy() + zb.numpy()
+    assert np.abs(g).max() <= 1e-11 * max(1.0, np.abs(pr["q"]).max()) + 1e-15

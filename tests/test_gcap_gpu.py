@@ -130,27 +130,51 @@ def test_gcap_uncentred_tracking_default_settings(device):
     assert np.abs(xb.sum(1) - 1).max() < 1e-10 and xb.min() > -1e-10
 
 
-def test_gcap_three_general_rows_same_iterates(device):
-    """The kernel's register-resident general-row variant beyond the budget alone (the budget
-    with two sector caps): the same ADMM iterates as the per-date form with one fixed rho."""
-    qb, lr, gp = _problem(device, 600, 150, 40, 0.2, caps=2)
-    assert qb.mg == 3
+@pytest.mark.parametrize("budget,caps", [(False, 0), (True, 2)])
+def test_gcap_general_row_variants_same_iterates(device, budget, caps):
+    """The kernel's general-row variants beyond the budget alone: none (box only, k_admm_gcap<0>;
+    q = -mu so the optimum is not the origin) and the budget with two sector caps (three
+    register-resident rows): the same ADMM iterates as the per-date form with one fixed rho.
+    (Round 4's k_admm_gcap<0> read an undefined Cg register in its epilogue and reported every
+    box-only date SOLVED after one iteration: gpurun_out/r04n_pytest.txt.)"""
+    qb, lr, gp = _problem(device, 600, 150, 40, 0.2, budget=budget, caps=caps)
+    if not budget:
+        qb.q = (-lr.mu * 50.0).contiguous()
+    assert qb.mg == int(budget) + caps
     st = engine.Settings(rho0_rel=0.0, rho0=0.01, rho0_qrel=0.0, adapt_interval=0)
     xa, sa, ia, cap_a, _ = _run(qb, lr, gp, False, st, polish=False)
     xb, sb, ib, cap_b, _ = _run(qb, lr, gp, True, st, polish=False)
     assert cap_a == "band" and cap_b == "group"
     assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED), (sa, sb)
+    assert ia.min() > 1, ia
     assert np.abs(ia - ib).max() <= 1, (ia, ib)
     assert np.abs(xa - xb).max() <= 1e-9, np.abs(xa - xb).max()
 
 
-def test_box_only_problems_keep_the_per_date_capacitance(device):
-    """No general row (box only; q = -mu so the optimum is not the origin): the group form
-    is not taken (it measured wrong there: every date stopped after one iteration), and the
-    per-date form solves every date."""
+def test_box_only_problems_group_form_same_optimum(device):
+    """Box only (mg = 0) with the default settings and the polish: the group form is taken
+    and reaches the per-date form's optimum (weights 1e-8, inside the box)."""
     qb, lr, gp = _problem(device, 600, 150, 40, 0.2, budget=False)
     qb.q = (-lr.mu * 50.0).contiguous()
     assert qb.mg == 0
-    x, st_, it, cap, _ = _run(qb, lr, gp, True, None)
-    assert cap != "group" and np.all(st_ == _lib.PQ_SOLVED) and it.min() > 1
-    assert x.min() > -1e-9 and x.max() < 0.2 + 1e-9
+    xa, sa, ia, cap_a, _ = _run(qb, lr, gp, False, None)
+    xb, sb, ib, cap_b, _ = _run(qb, lr, gp, True, None)
+    assert cap_b == "group"
+    assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED), (sa, sb)
+    assert ib.min() > 1, ib
+    assert np.abs(xa - xb).max() <= 1e-8, np.abs(xa - xb).max()
+    assert xb.min() > -1e-9 and xb.max() < 0.2 + 1e-9
+
+
+def test_gcap_nan_iterate_is_not_solved(device):
+    """A date whose data carries a NaN (here its q) cannot pass the convergence test: the
+    residual maxima are fmax reductions, which drop NaN, so the kernel checks a NaN-carrying
+    sum and fails the date (PQ_NON_CONVEX, found = False) while its group's other dates solve."""
+    qb, lr, gp = _problem(device, 600, 150, 40, 0.2, budget=True)
+    qb.q = (-lr.mu * 5.0).contiguous()
+    qb.q[7, 3] = float("nan")
+    st = engine.Settings(rho0_rel=0.0, rho0=0.01, rho0_qrel=0.0, adapt_interval=0)
+    _, sb, _, cap_b, _ = _run(qb, lr, gp, True, st, polish=False)
+    assert cap_b == "group"
+    assert sb[7] == _lib.PQ_NON_CONVEX, sb
+    assert np.all(np.delete(sb, 7) == _lib.PQ_SOLVED), sb

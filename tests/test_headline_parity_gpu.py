@@ -1,7 +1,8 @@
 """Parity at the headline configuration: bench.py's exact problem (BASELINE.json configs[2]:
 n = 1000, T = 252, all 4749 daily dates of the seed-20240314 panel, long-only
 min-variance, budget + box [0, 1]) solved through the same path the bench times (window
-moments -> band Gram -> capacitance + K2 -> grouped fused ADMM -> window polish), then
+moments -> band Gram -> capacitance + K2 -> grouped fused ADMM -> window polish), both
+eager and as the replayed HIP-graph step bench.py times (graph=True), then
 
   * 32 evenly spaced dates against the oracle optima in tests/golden/headline_c3.npz
     (oracle.qp_ipm, tools/capture_headline.py): weights <= 1e-5 L-inf, objective <= 1e-6
@@ -26,12 +27,21 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "headline_c3.npz")
 
 
-@pytest.fixture(scope="module")
-def solved(device):
-    wl = MinVarianceBacktest(device=device)
+@pytest.fixture(scope="module", params=["eager", "graph"])
+def solved(device, request):
+    """``graph``: exactly what bench.py times -- graph=True, prepare() (the eager step and the
+    capturing step), then a REPLAYED step: sync-free rounds capped at the first step's count,
+    every stage a replayed HIP graph.  ``eager``: the host-checked solve."""
+    graph = request.param == "graph"
+    wl = MinVarianceBacktest(device=device, graph=graph)
     assert wl.use_lr and wl.grouped and not wl.with_cov     # the path bench.py times
+    if graph:
+        wl.prepare()
+        assert wl.graphs is not None and wl.sf_rounds is not None
     res = wl.step()
     torch.cuda.synchronize()
+    if graph:
+        assert wl.graphs.replays > 0, "the checked step was not a graph replay"
     return wl, res
 
 

@@ -325,7 +325,7 @@ def test_planners_match_their_contracts_on_random_calendars():
     """window_rows (vs the oracle's per-date restatement of src/builders.py:208-211),
     slide_plan (vs a per-date loop) and GroupPlan (every date's window is its union slice
     [uoff, uoff + T), unions within umax) on calendars with weekends, gaps, repeated
-    rebalance dates and short histories."""
+    rebalance dates, descending or shuffled rebalance dates and short histories."""
     import torch
     rng = np.random.default_rng(11)
     for trial in range(30):
@@ -341,6 +341,10 @@ def test_planners_match_their_contracts_on_random_calendars():
         reb = cal[int(rng.integers(0, min(len(cal) - 1, T + 3))):][::int(rng.choice([1, 1, 3, 21]))]
         if trial % 4 == 0:
             reb = np.repeat(reb, int(rng.integers(1, 4)))
+        if trial % 5 == 1:     # descending rebalance dates: a later window starts earlier
+            reb = reb[::-1].copy()
+        elif trial % 5 == 3:   # shuffled (the slide plan must not take them as identical)
+            reb = reb[rng.permutation(len(reb))]
         rows, tlen = engine.window_rows(cal, reb, T)
         for b in range(0, len(reb), max(1, len(reb) // 17)):
             assert np.array_equal(rows[b, :tlen[b]], rp.window_rows(cal, reb[b], T))
@@ -408,3 +412,23 @@ def test_single_binary_filter_selection():
     assert list(s.selected) == ["a", "c", "d"] and isinstance(s.selected, pd.Index)
     s.add_filtered("more", pd.Series([1, 1, 0, 1], index=list("abcd"), name="binary"))
     assert list(s.selected) == ["a", "d"]
+
+
+def test_panel_upload_resolves_the_device_on_the_calling_thread(monkeypatch):
+    """_PanelUpload asks for the device on the caller's thread (torch's current device is
+    per host thread: a worker would see device 0, not the rank's set_device choice) and copies
+    to that device on the worker."""
+    import threading
+    from porqua_amd import backtest as bt
+    seen = []
+
+    def fake_device():
+        seen.append(threading.current_thread())
+        return torch.device("cpu")
+
+    monkeypatch.setattr(engine, "default_device", fake_device)
+    frame = pd.DataFrame(np.arange(12.0).reshape(4, 3))
+    up = bt._PanelUpload(frame)
+    out = up.result()
+    assert seen == [threading.current_thread()]
+    assert out.device.type == "cpu" and np.array_equal(out.numpy(), frame.to_numpy())
