@@ -44,6 +44,12 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 matrix spec
 
 
+CPU_PATH_TEXT = {   # the reference's per-QP arithmetic the cpu_baseline leg restates
+    "config2": "P = 2 X'X, q = -2 X'y (LeastSquares) + isPD/nearestPD of P",
+    "config3": "np.cov + isPD/nearestPD, P = 2 Sigma, + isPD/nearestPD of P",
+    "config4": "P = 2 X'X, q = -2 X'y (LeastSquares, 20 sector caps) + isPD/nearestPD of P",
+    "config5": "np.cov + isPD/nearestPD, P = 2 lam Sigma, q = -geometric mean, + isPD/nearestPD of P",
+}
 WORKLOAD_TEXT = {
     "config2": "config2: SPTR index replication, LS tracking (P=2 X'X, q=-2 X'y), budget + box [0,1], n=494 "
                "usa-shaped panel on the real SPTR calendar, every daily rebalance date (4544)",
@@ -246,15 +252,22 @@ def main():
     # CPU baseline first, in a child process, before this process touches the GPU (its
     # process pool forks; bench.py itself never forks after HIP initialisation)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and wname == "config3":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import subprocess
-        cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--n", str(args.n), "--window", str(args.window),
-               "--dates", str(args.dates), "--budget", str(args.cpu_budget)]
-        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+        # bounded samples: the per-QP reference cost grows with n^3 (nearestPD's SVD + eigvals:
+        # ~0.3 s at n = 494, ~2 s at 1000, ~40 s at 3000, minutes at 5000 on one core), so the
+        # n >= 3000 legs time one QP per worker and one serial QP
+        cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--workload", wname, "--n", str(args.n),
+               "--window", str(args.window), "--dates", str(args.dates), "--budget", str(args.cpu_budget)]
+        cmd += {"config2": ["--serial-dates", "8", "--pool-rounds", "8"],
+                "config4": ["--serial-dates", "1", "--pool-rounds", "1"],
+                "config5": ["--serial-dates", "1", "--pool-rounds", "1"]}.get(wname, [])
+        # progress lines pass through on stderr (the n = 5000 legs run for minutes)
+        r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, text=True, timeout=1500)
         if r.returncode == 0 and r.stdout.strip():
             cpu = json.loads(r.stdout.strip().splitlines()[-1])
         else:
-            print("cpu baseline failed:", r.stderr[-2000:], file=sys.stderr)
+            print("cpu baseline failed: rc", r.returncode, file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -531,6 +544,24 @@ def main():
                                                    "from the panel rows (torch), not by the engine")},
         "cpu_baseline": None,
     }
+    if cpu is not None:
+        legs = {"serial": cpu["serial"], "pool": cpu["pool"]}
+        best = max(legs, key=lambda k: legs[k]["qps"])
+        b = legs[best]
+        cores = b["workers"] if best == "pool" else b["blas_threads"]
+        out["cpu_baseline"] = {
+            "value": b["qps"], "unit": "QPs/s", "cores": cores, "kind": "port",
+            "sample": (f"better of (a) serial, {cpu['serial']['dates']} dates with {cpu['serial']['blas_threads']} "
+                       f"BLAS threads: {cpu['serial']['qps']:.3f} QPs/s and (b) pool of {cpu['pool']['workers']} "
+                       f"single-threaded processes, {cpu['pool']['dates']} dates: {cpu['pool']['qps']:.3f} QPs/s "
+                       f"(evenly spaced QPs of the same inputs; full per-QP reference path at n={n}: "
+                       f"{CPU_PATH_TEXT[wname]} + dense IPM, cvxopt coneqp algorithm, tol 1e-7; "
+                       f"qpsolvers unavailable)"),
+            "leg": best, "cpu_model": cpu["cpu_model"], "host_cores": cpu["host_cores"],
+            "serial": cpu["serial"], "pool": cpu["pool"],
+            "solver_only_no_nearestPD": {"serial_qps": cpu.get("serial_solver_only", {}).get("qps"),
+                                         "pool_qps": cpu.get("pool_solver_only", {}).get("qps")},
+            "speedup": qps / b["qps"]}
     if wname == "config2" and world == 1 and not args.no_dropin:
         out["end_to_end"] = dropin_config2(wl, T)
     if wname != "config3":   # the next-row and drop-in legs below are config-3 (n = 1000 min-variance) lines
@@ -624,23 +655,6 @@ def main():
             "path": bt.stats["path"],
             "note": "host DataFrame in, Portfolio objects out: panel upload, window staging, device solve "
                     "and weight download included; q = -mu (geometric) instead of the step's q = 0"}
-    if cpu is not None:
-        legs = {"serial": cpu["serial"], "pool": cpu["pool"]}
-        best = max(legs, key=lambda k: legs[k]["qps"])
-        b = legs[best]
-        cores = b["workers"] if best == "pool" else b["blas_threads"]
-        out["cpu_baseline"] = {
-            "value": b["qps"], "unit": "QPs/s", "cores": cores, "kind": "port",
-            "sample": (f"better of (a) serial, {cpu['serial']['dates']} dates with {cpu['serial']['blas_threads']} "
-                       f"BLAS threads: {cpu['serial']['qps']:.3f} QPs/s and (b) pool of {cpu['pool']['workers']} "
-                       f"single-threaded processes, {cpu['pool']['dates']} dates: {cpu['pool']['qps']:.3f} QPs/s "
-                       f"(evenly spaced dates of the same panel; full per-date reference path at n={n}: np.cov + "
-                       f"isPD/nearestPD + dense IPM, cvxopt coneqp algorithm, tol 1e-7; qpsolvers unavailable)"),
-            "leg": best, "cpu_model": cpu["cpu_model"], "host_cores": cpu["host_cores"],
-            "serial": cpu["serial"], "pool": cpu["pool"],
-            "solver_only_no_nearestPD": {"serial_qps": cpu["serial_solver_only"]["qps"],
-                                         "pool_qps": cpu["pool_solver_only"]["qps"]},
-            "speedup": qps / b["qps"]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -16,9 +16,23 @@ Two ways of running it, as BASELINE.md §3 plans, and the better one is the deno
   (b) pool: one single-threaded worker process per host core, dates spread over them.
 A solver-only variant (no nearestPD: the IPM takes the PSD P as it is) is timed beside it.
 
+Workloads (``--workload``, the same synthetic inputs bench.py's GPU legs solve):
+  config3  min-variance above, n = 1000 (the headline);
+  config2  LeastSquares SPTR replication on the usa-shaped panel (n = 494, daily dates):
+           P = 2 X'X, q = -2 X'y (src/optimization.py:206-226, uncentred), budget + box;
+  config4  the same tracking objective at n = 3000 with the 20 sector caps G x <= 0.15
+           (src/constraints.py:66-94, 114-167);
+  config5  MeanVariance lambda sweep at n = 5000: Sigma by np.cov + nearestPD
+           (src/covariance.py:40-56), P = 2 lam Sigma, q = -geometric mean
+           (src/optimization.py:157-174, src/mean_estimation.py:39-48), budget + box;
+each followed by the solve's own isPD / nearestPD of P (src/qp_problems.py:189-191), as the
+reference runs it.  Samples are bounded by the per-QP cost: n = 3000 / 5000 QPs take tens of
+seconds to minutes each on one core (nearestPD's SVD + eigvals dominate), so those legs time
+one QP per worker.
+
 Run as a CHILD process (``python -m oracle.cpu_baseline ...``), before the bench touches the
 GPU; the pool's workers are spawned (fresh interpreters, single-threaded BLAS); prints one
-JSON object.
+JSON object on stdout and progress lines on stderr.
 """
 from __future__ import annotations
 
@@ -29,7 +43,7 @@ import time
 import numpy as np
 
 from .qp_ipm import solve_qp
-from .ref_pipeline import cov_pearson, is_pd, nearest_pd
+from .ref_pipeline import cov_pearson, is_pd, mean_geometric, nearest_pd
 
 
 def blas_threads() -> int:
@@ -57,6 +71,77 @@ def reference_date(X: np.ndarray, ub: float = 1.0, shrink: float = 0.0, repair: 
     return sol
 
 
+def reference_ls(X: np.ndarray, y: np.ndarray, G=None, h=None, repair: bool = True):
+    """LeastSquares tracking date (src/optimization.py:206-226: P = 2 X'X uncentred, q = -2 X'y),
+    budget + long-only box (+ G x <= h), the solve's PD repair (src/qp_problems.py:189-191)."""
+    n = X.shape[1]
+    P = 2.0 * (X.T @ X)
+    q = -2.0 * (X.T @ y)
+    if repair and not is_pd(P):
+        P = _nearest_pd(P)
+    return solve_qp(P, q, G=G, h=h, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n),
+                    tol=1e-7, refine=False)
+
+
+def reference_mv(X: np.ndarray, lam: float, repair: bool = True):
+    """MeanVariance date of the lambda sweep (src/optimization.py:157-174): Covariance.estimate
+    (np.cov + isPD / nearestPD), P = 2 lam Sigma, q = -geometric mean, then the solve's repair."""
+    n = X.shape[1]
+    S = cov_pearson(X)
+    if repair and not is_pd(S):
+        S = _nearest_pd(S)
+    P = 2.0 * lam * S
+    q = -mean_geometric(X)
+    if repair and not is_pd(P):
+        P = _nearest_pd(P)
+    return solve_qp(P, q, A=np.ones((1, n)), b=np.ones(1), lb=np.zeros(n), ub=np.ones(n), tol=1e-7, refine=False)
+
+
+class Workload:
+    """The synthetic inputs of one bench workload (built identically in every pool worker)
+    and its per-QP reference call.  ``units``: the QP ids to sample (row index of the
+    rebalance day, or (row, lambda index) for the sweep)."""
+
+    def __init__(self, name: str, n: int, T: int, dates: int, seed: int, root: str = "."):
+        from porqua_amd.synthetic import factor_panel, usa_panel
+        self.name, self.T = name, T
+        self.G = self.h = None
+        if name == "config2":
+            g = np.load(os.path.join(root, "tests", "golden", "sptr.npz"), allow_pickle=False)
+            _, self.R, self.y = usa_panel(g["days"], g["returns"], n_assets=n)
+            self.units = list(range(T - 1, self.R.shape[0]))
+        elif name == "config4":
+            _, self.R, self.y, sec = factor_panel(T - 1 + dates, n, n_sectors=20)
+            self.G = np.stack([(sec == k).astype(float) for k in range(20)])
+            self.h = np.full(20, 0.15)
+            self.units = list(range(T - 1, T - 1 + dates))
+        elif name == "config5":
+            stride, n_lam = 21, 64
+            self.R = factor_panel(T - 1 + stride * dates, n)[1]
+            self.lams = np.logspace(-1, 2, n_lam)
+            ends = np.arange(T - 1, T - 1 + stride * dates, stride)
+            self.units = [(int(e), k) for e in ends for k in range(n_lam)]
+        else:
+            self.R = factor_panel(T - 1 + dates, n, seed=seed)[1]
+            self.units = list(range(T - 1, T - 1 + dates))
+
+    def sample(self, k: int):
+        """k evenly spaced QPs of the workload (for the sweep: spread over dates AND lambdas)."""
+        pos = np.linspace(0, len(self.units) - 1, max(1, k)).astype(int)
+        if self.name == "config5":   # stride through the (date, lambda) grid so lambdas vary too
+            pos = (np.arange(k) * (len(self.units) // max(1, k) + 1)) % len(self.units)
+        return [self.units[i] for i in pos]
+
+    def solve(self, u, repair: bool = True):
+        T = self.T
+        if self.name in ("config2", "config4"):
+            return reference_ls(self.R[u - T + 1:u + 1], self.y[u - T + 1:u + 1], self.G, self.h, repair)
+        if self.name == "config5":
+            e, k = u
+            return reference_mv(self.R[e - T + 1:e + 1], float(self.lams[k]), repair)
+        return reference_date(self.R[u - T + 1:u + 1], repair=repair)
+
+
 def _nearest_pd(A: np.ndarray) -> np.ndarray:
     """nearest_pd, retrying once with LAPACK gesvd when gesdd (numpy's SVD) does not converge
     -- the same repair, so the timed work is unchanged."""
@@ -76,45 +161,82 @@ def _nearest_pd(A: np.ndarray) -> np.ndarray:
         return A3
 
 
-def time_reference(R: np.ndarray, ends, T: int, budget_s: float = 20.0, max_dates: int = 8, repair=True):
-    """Run the per-date reference path on dates ``ends`` (row index of the rebalance day)
-    until ``budget_s`` seconds or ``max_dates`` dates; returns (qps, dates_done, seconds)."""
+def time_reference(wl: "Workload", units, budget_s: float = 20.0, max_dates: int = 8, repair=True):
+    """Run the per-QP reference path on ``units`` until ``budget_s`` seconds or ``max_dates``
+    QPs; returns (qps, dates_done, seconds)."""
     t0 = time.perf_counter()
     done = 0
-    for e in ends:
-        reference_date(R[e - T + 1:e + 1], repair=repair)
-        done += 1
-        if done >= max_dates or time.perf_counter() - t0 > budget_s:
-            break
+    with _Heartbeat("serial" + ("" if repair else " solver-only")):
+        for u in units:
+            wl.solve(u, repair=repair)
+            done += 1
+            _progress(f"serial {done}/{min(len(units), max_dates)} ({time.perf_counter() - t0:.1f} s)")
+            if done >= max_dates or time.perf_counter() - t0 > budget_s:
+                break
     dt = time.perf_counter() - t0
     return done / dt, done, dt
+
+
+def _progress(msg: str):
+    import sys
+    print(f"[cpu_baseline] {msg}", file=sys.stderr, flush=True)
+
+
+class _Heartbeat:
+    """A progress line every ``every`` seconds while a leg runs (one n = 5000 QP takes minutes
+    on a core, and a run that prints nothing for minutes looks hung)."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        import threading
+        self.what, self.every = what, every
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self._stop.wait(self.every):
+            _progress(f"{self.what}: running ({time.perf_counter() - t0:.0f} s)")
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join()
 
 
 _POOL = {}
 
 
-def _pool_init(n_dates, n, T, seed):
-    from porqua_amd.synthetic import factor_panel
-    _POOL["R"] = factor_panel(n_dates, n, seed=seed)[1]
-    _POOL["T"] = T
+def _pool_init(name, n, T, dates, seed, root):
+    _POOL["wl"] = Workload(name, n, T, dates, seed, root)
 
 
 def _pool_date(args):
-    e, repair = args
-    R, T = _POOL["R"], _POOL["T"]
-    reference_date(R[e - T + 1:e + 1], repair=repair)
-    return e
+    u, repair = args
+    _POOL["wl"].solve(u, repair=repair)
+    return 1
 
 
-def time_pool(n_dates, n, T, ends, workers, seed, repair=True):
-    """(b): ``workers`` single-threaded processes over ``ends``; returns (qps, done, seconds)
-    timed from the first submitted date to the last result (pool start-up excluded)."""
+def time_pool(name, n, T, dates, seed, units, workers, repair=True, root="."):
+    """(b): ``workers`` single-threaded processes over ``units``; returns (qps, done, seconds)
+    timed from the first submitted QP to the last result (pool start-up and the workers'
+    panel construction excluded).  Progress lines while it runs (a long leg stays visibly
+    alive)."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")   # fresh interpreters: no BLAS thread state copied by fork
-    with ctx.Pool(workers, initializer=_pool_init, initargs=(n_dates, n, T, seed)) as pool:
-        pool.map(_pool_date, [(ends[0], False)] * workers)     # warm: panel built, BLAS loaded
+    with ctx.Pool(workers, initializer=_pool_init, initargs=(name, n, T, dates, seed, root)) as pool:
+        # warm: panel built, BLAS loaded (the solver-only path, cheap next to the repair)
+        with _Heartbeat("pool warm-up"):
+            pool.map(_pool_date, [(units[0], False)] * workers)
         t0 = time.perf_counter()
-        done = len(pool.map(_pool_date, [(e, repair) for e in ends], chunksize=1))
+        done = 0
+        with _Heartbeat("pool" + ("" if repair else " solver-only")):
+            for _ in pool.imap_unordered(_pool_date, [(u, repair) for u in units], chunksize=1):
+                done += 1
+                _progress(f"pool{'' if repair else ' solver-only'} {done}/{len(units)} "
+                          f"({time.perf_counter() - t0:.1f} s)")
         dt = time.perf_counter() - t0
     return done / dt, done, dt
 
@@ -143,29 +265,32 @@ def host_cores() -> int:
 def main():
     import argparse
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5"], default="config3")
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--window", type=int, default=252)
     ap.add_argument("--dates", type=int, default=4749)
     ap.add_argument("--seed", type=int, default=20240314)
     ap.add_argument("--serial-dates", type=int, default=6)
-    ap.add_argument("--pool-rounds", type=int, default=2, help="dates per worker in the pool leg")
+    ap.add_argument("--pool-rounds", type=int, default=2, help="QPs per worker in the pool leg")
     ap.add_argument("--workers", type=int, default=0)
     ap.add_argument("--budget", type=float, default=20.0)
+    ap.add_argument("--no-solver-only", action="store_true", help="skip the solver-only legs")
     a = ap.parse_args()
-    from porqua_amd.synthetic import factor_panel
-    T, D, n = a.window, a.dates, a.n
-    n_rows = T - 1 + D
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    T, n = a.window, a.n
     workers = a.workers or host_cores()
-    R = factor_panel(n_rows, n, seed=a.seed)[1]
-    sample = np.linspace(T - 1, n_rows - 1, max(a.serial_dates, workers * a.pool_rounds)).astype(int)
-    out = {"host_cores": host_cores(), "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count()}
-    qs, ds, ss = time_reference(R, sample[:a.serial_dates], T, budget_s=a.budget, max_dates=a.serial_dates)
+    wl = Workload(a.workload, n, T, a.dates, a.seed, root)
+    sample = wl.sample(max(a.serial_dates, workers * a.pool_rounds))
+    out = {"workload": a.workload, "n": n, "host_cores": host_cores(), "cpu_model": cpu_model(),
+           "os_cpu_count": os.cpu_count()}
+    qs, ds, ss = time_reference(wl, sample[:a.serial_dates], budget_s=a.budget, max_dates=a.serial_dates)
     out["serial"] = {"qps": qs, "dates": ds, "seconds": ss, "blas_threads": blas_threads()}
-    qo, do, so = time_reference(R, sample[:a.serial_dates], T, budget_s=a.budget, max_dates=a.serial_dates,
-                                repair=False)
-    out["serial_solver_only"] = {"qps": qo, "dates": do, "seconds": so}
-    del R
-    pool_ends = sample[:workers * a.pool_rounds]
+    if not a.no_solver_only:
+        qo, do, so = time_reference(wl, sample[:a.serial_dates], budget_s=a.budget, max_dates=a.serial_dates,
+                                    repair=False)
+        out["serial_solver_only"] = {"qps": qo, "dates": do, "seconds": so}
+    del wl
+    pool_units = sample[:workers * a.pool_rounds]
     for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
         os.environ[k] = "1"
     try:
@@ -173,10 +298,11 @@ def main():
         threadpool_limits(1)
     except Exception:
         pass
-    qp, dp, sp = time_pool(n_rows, n, T, pool_ends, workers, a.seed)
+    qp, dp, sp = time_pool(a.workload, n, T, a.dates, a.seed, pool_units, workers, root=root)
     out["pool"] = {"qps": qp, "dates": dp, "seconds": sp, "workers": workers, "threads_per_worker": 1}
-    qpo, dpo, spo = time_pool(n_rows, n, T, pool_ends, workers, a.seed, repair=False)
-    out["pool_solver_only"] = {"qps": qpo, "dates": dpo, "seconds": spo, "workers": workers}
+    if not a.no_solver_only:
+        qpo, dpo, spo = time_pool(a.workload, n, T, a.dates, a.seed, pool_units, workers, repair=False, root=root)
+        out["pool_solver_only"] = {"qps": qpo, "dates": dpo, "seconds": spo, "workers": workers}
     print(json.dumps(out), flush=True)
 
 

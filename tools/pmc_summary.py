@@ -69,9 +69,15 @@ def main():
         wr = write.get(k, 0.0) * 1024.0
         e = {"calls_per_step": calls[k], "read_bytes_per_step": rd, "write_bytes_per_step": wr,
              "hbm_bytes_per_step": rd + wr}
+        e["hbm_bytes_first_dispatch"] = 2.0 * f1[k] * 1024.0 + w1.get(k, 0.0) * 1024.0
         if k in stats:
             e["trace_avg_ns"] = float(stats[k]["AverageNs"])
             e["trace_calls"] = int(stats[k]["Calls"])
+            # HBM bytes actually moved per launch (the step's first dispatch) over the trace's
+            # average launch duration: the kernel's measured HBM rate (approximate for kernels
+            # whose dispatches differ within a step, e.g. the polish rounds)
+            e["measured_hbm_gbs"] = e["hbm_bytes_first_dispatch"] / e["trace_avg_ns"]
+            e["measured_hbm_frac"] = e["measured_hbm_gbs"] / 8000.0
         out["kernels"][k] = e
     kern = bench_pmc["roofline"]["kernel"].split()[0]
     adm = out["kernels"].get(kern)
