@@ -115,6 +115,9 @@ class Settings:
     # 3.1 / 3.5 / 4.0 rounds): the tracking rounds (free sets of 160..220) cost more than the
     # ADMM iterations they replace
     eps_grouped_tracking: float = 0.0
+    # (host-side) the loose stop also on the per-problem capacitance (grouped ADMM without the
+    # group capacitance: the lambda sweep, whose problems of a date differ in P's scale)
+    eps_grouped_percap: bool = False
     min_iter: int = 0           # pq_settings.min_iter: no convergence test before this iteration
     # grouped polish: variables with x - lb < polish_fix_rel * max(x - lb) at the ADMM point
     # also start fixed at lb (besides OSQP's z - lb < -y): the loose ADMM point leaves small
@@ -1149,8 +1152,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     SS_admm = SS
     st_ = settings or Settings()
     eps_loose = st_.eps_grouped if lr.mu is not None else st_.eps_grouped_tracking
-    if (gc is not None and polish and s.polish and grouped_polish and ldk >= 64
-            and eps_loose > max(st_.eps_abs, st_.eps_rel)):
+    if ((gc is not None or (st_.eps_grouped_percap and grouped and eig is None)) and polish and s.polish
+            and grouped_polish and ldk >= 64 and eps_loose > max(st_.eps_abs, st_.eps_rel)):
         sl = st_.to_c()
         sl.eps_abs = sl.eps_rel = eps_loose
         sl.min_iter = max(int(st_.min_iter), int(st_.min_iter_grouped))

@@ -97,6 +97,7 @@ class MeanVarianceSweep:
         qb.p_scale = 2.0 * lam_p
         self.qb = qb
         self.mu_p = torch.zeros((B, ld), dtype=torch.float64, device=dev)
+        self.dg_c = torch.zeros((nd, ld), dtype=torch.float64, device=dev)   # diag(Xc'Xc) per date
         self.lr = engine.LowRank(panel, self.rp_d, self.tp_d, mu=self.mu_p,
                                  w_scale=1.0 / (self.tp_d.to(torch.float64) - 1.0),
                                  dg=torch.zeros((B, ld), dtype=torch.float64, device=dev))
@@ -128,7 +129,10 @@ class MeanVarianceSweep:
                 pan.window_means(self.r_d, self.t_d, geometric=True, out=self.mu_q)
             torch.neg(self.mu_q.repeat_interleave(L, dim=0), out=self.qb.q)
             self.mu_p.copy_(self.mu_c.repeat_interleave(L, dim=0))
-            self.lr.refresh()
+            # diag(Xc'Xc) once per DATE (its window is every lambda's), then repeated to the
+            # problems: one window pass per date instead of one per (date, lambda)
+            pan.window_sumsq(self.r_d, self.t_d, self.mu_c, out=self.dg_c)
+            self.lr.dg.copy_(self.dg_c.repeat_interleave(L, dim=0))
         tl("moments", moments)
         eig = None
         if self.use_eig:
