@@ -288,8 +288,8 @@ def main():
         wl = ReplicationBacktest(g["days"], g["returns"], T=T, rank=rank, world=world, device=dev,
                                  settings=settings, n=n)
     elif wname == "config5":
-        from porqua_amd.sweep import SWEEP_RHO0_QREL
-        settings = engine.Settings.from_params(dict({"rho0_qrel": SWEEP_RHO0_QREL}, **ov))
+        from porqua_amd.sweep import SWEEP_SETTINGS
+        settings = engine.Settings.from_params(dict(SWEEP_SETTINGS, **ov))
         wl = SweepBacktest(n=n, T=T, dates=args.dates, rank=rank, world=world, device=dev, settings=settings)
     else:
         settings = engine.Settings.from_params(dict(kv.split("=", 1) for kv in args.set))

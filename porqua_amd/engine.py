@@ -148,7 +148,10 @@ class Settings:
             for f in dataclasses.fields(cls):
                 for key in (f.name, "admm_" + f.name):
                     if key in params and params[key] is not None:
-                        setattr(s, f.name, type(getattr(s, f.name))(params[key]))
+                        v, typ = params[key], type(getattr(s, f.name))
+                        if typ is bool and isinstance(v, str):   # "0" / "false" from --set KEY=VALUE
+                            v = v.strip().lower() not in ("0", "false", "no", "off", "")
+                        setattr(s, f.name, typ(v))
         return s
 
 

@@ -43,6 +43,15 @@ EIG_MIN_PER_DATE = 192   # factor='auto': eigen form from this many problems per
 # QPs/s), 60 -> 26, 100 -> problems fall to the eps_retry ADMM; 30 keeps a factor 3 from both
 # cliffs.  (A single mean-variance backtest at risk aversion 1 is faster at 10.)
 SWEEP_RHO0_QREL = 30.0
+# The sweep's settings: the rho floor above, and the loose ADMM stop before the grouped polish
+# on its per-problem capacitance (Settings.eps_grouped_percap; the problems of a date differ in
+# P's scale, so they cannot share the group capacitance the loose stop was tuned on).
+# Measured at the config-5 shape (profiles/r05c_*, r05d_*): eps 2e-3 (no loose stop) / 0.3 /
+# 0.5 / 1.0 -> 58.6k / 94.2k / 100.1k / 67.4k QPs/s (24.6 / 13.2 / 11.6 / 8.0 ADMM iterations,
+# 2.06 / 2.63 / 2.83 / 3.48 polish rounds; at 1.0 the free sets outgrow the LDS solve and dates
+# fall back to the per-date polish after resuming ADMM); min_iter_grouped 6 / 8 / 10 changes
+# nothing at 0.3
+SWEEP_SETTINGS = {"rho0_qrel": SWEEP_RHO0_QREL, "eps_grouped": 0.5, "eps_grouped_percap": True}
 
 
 class MeanVarianceSweep:
@@ -108,7 +117,7 @@ class MeanVarianceSweep:
         self.k_ld = k_ld
         self.pdate = torch.arange(nd, dtype=torch.int32, device=dev).repeat_interleave(L)
         self.gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax) if (group and B) else None
-        self.settings = settings if settings is not None else engine.Settings(rho0_qrel=SWEEP_RHO0_QREL)
+        self.settings = settings if settings is not None else engine.Settings.from_params(SWEEP_SETTINGS)
         self.ws = ws if ws is not None else engine.Workspace(qb, dense=False)
 
     def solve(self, events: list | None = None):
