@@ -402,8 +402,9 @@ def main():
         # the group's M_U^-1, and per date the ADMM state read + written (x, Px, z, y, rhs: 10
         # n-vectors) plus q and mu read -- amortised per date-iteration over the mean group
         kern = "k_admm_gcap"
-        u_mean = float(gplan.ucnt.double().mean().item())
-        g_mean = float(gplan.sizes.mean())
+        gp_used = getattr(ws, "gcap_groups", None) or gplan   # the plan the ADMM ran (32-date groups)
+        u_mean = float(gp_used.ucnt.double().mean().item())
+        g_mean = float(gp_used.sizes.mean())
         k_u = u_mean + qb.mg
         it_bytes = (2 * 8.0 * u_mean * n + 8.0 * k_u * (k_u + 1) / 2) / g_mean + 12 * 8.0 * n
         admm_bytes = it_bytes * total_iters
@@ -443,8 +444,9 @@ def main():
     n_factor = D * args.steps + res.refactors * args.steps
     factor_flops = factor_flops_per * n_factor
     if use_lr and res.capacitance == "group":   # one M_U (k = U + mg) per slide group
-        k_u = float(gplan.ucnt.double().mean().item()) + qb.mg
-        factor_flops = k_u ** 3 * gplan.ngroups * args.steps
+        gp_used = getattr(ws, "gcap_groups", None) or gplan
+        k_u = float(gp_used.ucnt.double().mean().item()) + qb.mg
+        factor_flops = k_u ** 3 * gp_used.ngroups * args.steps
 
     # polish (K4) algorithmic flops per step: per problem and active-set round the P_FF Gram
     # of the free columns over the window (|F|^2 T) and its Cholesky (|F|^3 / 3), plus the

@@ -103,6 +103,7 @@ class PQGcap(ctypes.Structure):
         ("M", c_dp), ("Minv", c_dp), ("k_ld", c_int32), ("M_stride", c_int64),
         ("aq", c_dp), ("aq_stride", c_int64),
         ("hinv", c_dp), ("ldh", c_int32),
+        ("gmax", c_int32),
     ]
 
 

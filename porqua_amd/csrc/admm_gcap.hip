@@ -137,23 +137,29 @@ __global__ __launch_bounds__(256) void k_gcap_assemble(pq_lowrank lr, pq_problem
 // Then per date: mu'mu, a'q, H_b (m + 1 x m + 1) assembled in LDS, its Cholesky, and H_b^-1
 // column by column (lane t solves for column t, x in LDS).
 constexpr int PT_PREP = 512;    // 8 waves: a row of G_U / a GEMM tile / a date per wave; two
-                                // workgroups per CU (44 KB of LDS each): all 475 groups of the
-                                // config-3 batch in one round instead of two
+                                // workgroups per CU (44 KB of LDS each) for 16-date groups: all
+                                // 475 groups of the config-3 batch in one round instead of two
 constexpr int PW_PREP = PT_PREP / 64;
+constexpr int HWP = 33;         // pitch of a wave's own H_b (16 < m + 1 <= 32, the 32-date groups)
 
-__global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
-                                                   pq_settings s, const int32_t* idx, const double* band,
-                                                   int64_t ldo, int r0, const double* pc, int64_t ldpc) {
+template <int NB>
+__global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq_problem pb, pq_state st,
+                                                   pq_gcap gc, pq_settings s, const int32_t* idx,
+                                                   const double* band, int64_t ldo, int r0, const double* pc,
+                                                   int64_t ldpc) {
+  constexpr int CG = CG_MAX * NB;   // dates per group
   __shared__ int s_w[CU_MAX];
   // a_b: row u, column (date) g.  q_b = M_U^-1 a_b goes straight to its output rows (gc.aq),
-  // and the rare LDS Cholesky of H_b (m + 1 > 16) reuses this array once the GEMM is done:
-  // 44 KB of LDS instead of 151 KB, two workgroups per CU
-  __shared__ __attribute__((aligned(16))) double s_a[(CK_MAX + 16) * CG_MAX];
+  // and the LDS inverses of H_b (m + 1 > 16) reuse this array once the GEMM is done:
+  // 44 KB of LDS per 16 dates instead of 151 KB
+  __shared__ __attribute__((aligned(16))) double s_a[(CK_MAX + 16) * CG];
   constexpr int HP = CH_MAX + 1;
-  static_assert(CH_MAX * HP <= (CK_MAX + 16) * CG_MAX, "H_b does not fit in the a_b array");
+  static_assert(CH_MAX * HP <= (CK_MAX + 16) * CG, "H_b does not fit in the a_b array");
   double* const H = s_a;
-  __shared__ double s_mm[CG_MAX], s_aq[CG_MAX], s_sr[CMGW];
-  __shared__ int s_off[CG_MAX], s_T[CG_MAX];
+  // waves that invert an H_b of 16 < m + 1 <= 32 in their own part of the array
+  constexpr int NWS = ((CK_MAX + 16) * CG / (33 * HWP)) < PW_PREP ? ((CK_MAX + 16) * CG / (33 * HWP)) : PW_PREP;
+  __shared__ double s_mm[CG], s_aq[CG], s_sr[CMGW];
+  __shared__ int s_off[CG], s_T[CG];
   const int slot = xcd_slot(blockIdx.x, gridDim.x);
   const int grp = idx ? idx[slot] : slot;
   const int d0 = gc.gdates[grp];
@@ -162,14 +168,14 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
   const int kU = U + mg, k_ld = gc.k_ld;
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   for (int u = t; u < U; u += PT_PREP) s_w[u] = gc.urows[(int64_t)grp * gc.umax + u] - r0;
-  if (t < CG_MAX) {
+  if (t < CG) {
     s_off[t] = t < G ? gc.uoff[d0 + t] : 0;
     s_T[t] = t < G ? lr.tlen[d0 + t] : 1;
   }
   const GConst g = gconst(lr, pb, s, d0, gc.grho[grp]);   // c, d, rho uniform in the group
   if (t < mg) s_sr[t] = sqrt(crho(pb.lg[t], pb.ug[t], g.rho, s));
   const int ktile = (kU + 15) >> 4;
-  for (int e = t; e < (CK_MAX + 16) * CG_MAX; e += PT_PREP) s_a[e] = 0.0;
+  for (int e = t; e < (CK_MAX + 16) * CG; e += PT_PREP) s_a[e] = 0.0;
   __syncthreads();
   // ---- A: a_b for every date (wave per union row; the row of G_U in registers).  Uncentred
   //      windows (lr.mu null, LeastSquares): no mean column, a_b = q_b = 0 and H_b's last
@@ -191,7 +197,7 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
         if (v >= lo && v < hi) sum += gv[j];
       }
       sum = wave_sum(sum);
-      if (l == 0) s_a[u * CG_MAX + gg] = g.sqc * sum / s_T[gg];
+      if (l == 0) s_a[u * CG + gg] = g.sqc * sum / s_T[gg];
     }
   }
   for (int e = w; centred && e < mg * G; e += PW_PREP) {   // general rows: sqrt(R_r) Cg_r mu_b = sqrt(R_r) (1/T) sum PC
@@ -199,7 +205,7 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
     double sum = 0.0;
     for (int tt = l; tt < s_T[gg]; tt += 64) sum += pc[(int64_t)s_w[s_off[gg] + tt] * ldpc + r];
     sum = wave_sum(sum);
-    if (l == 0) s_a[(U + r) * CG_MAX + gg] = s_sr[r] * sum / s_T[gg];
+    if (l == 0) s_a[(U + r) * CG + gg] = s_sr[r] * sum / s_T[gg];
   }
   __syncthreads();
   // ---- B: Q = M_U^-1 A (MFMA; A rows from the full symmetric M_U^-1, B from LDS) -----------
@@ -211,30 +217,37 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
       const int row = tile * 16 + m;
       const bool rv = row < kU;
       const double* mrow = Mi + (int64_t)(rv ? row : 0) * k_ld;
-      f64x4 z = f64x4{0.0, 0.0, 0.0, 0.0};
+      f64x4 z[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) z[nb] = f64x4{0.0, 0.0, 0.0, 0.0};
       for (int k0 = 0; k0 < kU4; k0 += 8) {
         const int kk = k0 + 2 * kq;
         const bool kin = kk < kU, kin1 = kk + 1 < kU;
-        const double b0 = s_a[kk * CG_MAX + m];   // rows >= kU of s_a are zero
-        const double b1 = s_a[(kk + 1) * CG_MAX + m];
         double2 av = double2{0.0, 0.0};
         if (rv && kin1) av = *reinterpret_cast<const double2*>(mrow + kk);
         else if (rv && kin) av.x = mrow[kk];
-        z = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, b0, z, 0, 0, 0);
-        z = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, b1, z, 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const double b0 = s_a[kk * CG + m + 16 * nb];   // rows >= kU of s_a are zero
+          const double b1 = s_a[(kk + 1) * CG + m + 16 * nb];
+          z[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, b0, z[nb], 0, 0, 0);
+          z[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, b1, z[nb], 0, 0, 0);
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int u = tile * 16 + kq + 4 * r;
-        if (u < kU && m < G) gc.aq[(int64_t)(d0 + m) * gc.aq_stride + k_ld + u] = z[r];   // q_b
-      }
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int u = tile * 16 + kq + 4 * r, md = m + 16 * nb;
+          if (u < kU && md < G) gc.aq[(int64_t)(d0 + md) * gc.aq_stride + k_ld + u] = z[nb][r];   // q_b
+        }
     }
   }
   // ---- a out (q_b's padding rows zero); mu'mu and a'q per date (wave per date) ----------------
   for (int e = t; e < G * k_ld; e += PT_PREP) {
     const int gg = e / k_ld, u = e % k_ld;
     double* A = gc.aq + (int64_t)(d0 + gg) * gc.aq_stride;
-    A[u] = u < kU ? s_a[u * CG_MAX + gg] : 0.0;
+    A[u] = u < kU ? s_a[u * CG + gg] : 0.0;
     if (u >= kU) A[k_ld + u] = 0.0;
   }
   __syncthreads();   // (q_b rows written above are read back below)
@@ -245,7 +258,7 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
       const double* mu = lr.mu + (int64_t)(d0 + gg) * lr.mu_stride;
       for (int i = l; i < n; i += 64) mm = fma(mu[i], mu[i], mm);
     }
-    for (int u = l; u < kU; u += 64) aq = fma(s_a[u * CG_MAX + gg], q_at(gg, u), aq);
+    for (int u = l; u < kU; u += 64) aq = fma(s_a[u * CG + gg], q_at(gg, u), aq);
     mm = wave_sum(mm);
     aq = wave_sum(aq);
     if (l == 0) {
@@ -298,52 +311,113 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
       if (r < mh && cc < mh) Hi[(int64_t)r * gc.ldh + cc] = hi[q];
     }
   }
-  // m + 1 > 16: the whole workgroup per date, H in LDS
+  // 16 < m + 1 <= 32 (the outer dates of a 32-date group): one wave per date, its H_b in its
+  // own part of the a_b array, inverted in place by the symmetric sweep operator (below) with
+  // no workgroup barrier -- a wave's LDS operations complete in order, and every lane loads its
+  // elements' old values before any lane stores
+  __syncthreads();   // the a_b array is free (GEMM done, a / q written, mu'mu and a'q in s_mm / s_aq)
+  if (w < NWS) {
+    double* Hw = s_a + w * 33 * HWP;   // H_b (32 x 32 at most, pitch HWP), then the pivot row's copy
+    double* rk = Hw + 32 * HWP;
+    for (int gg = w; gg < G; gg += NWS) {
+      const int mh = U - s_T[gg] + 1;
+      const int b = d0 + gg;
+      if (mh <= 16 || mh > 32) continue;
+      // lane j < mh owns column j of H: the pivot row is copied first, then every lane updates
+      // its own column row by row (no lane writes what another reads)
+      for (int e = l; e < mh * mh; e += 64) Hw[(e / mh) * HWP + e % mh] = h_entry(gg, e / mh, e % mh);
+      int bad = 0;
+      for (int k = 0; k < mh; ++k) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (l < mh) rk[l] = Hw[k * HWP + l];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const double dk = rk[k];
+        if (!(dk > 0.0) || !isfinite(dk)) {   // uniform over the wave
+          bad = 1;
+          break;
+        }
+        const double dinv = 1.0 / dk;
+        if (l < mh) {
+          const int j = l;
+          const double rkj = rk[j];
+          for (int i = 0; i < mh; ++i) {
+            const double rki = rk[i];   // (symmetric: a_ik = a_ki)
+            double v;
+            if (i == k) v = j == k ? -dinv : rkj * dinv;
+            else if (j == k) v = rki * dinv;
+            else v = fma(-rki * dinv, rkj, Hw[i * HWP + j]);
+            Hw[i * HWP + j] = v;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (bad) {
+        if (l == 0) st.status[b] = PQ_NON_CONVEX;
+      } else {
+        double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
+        const int ldh = gc.ldh;
+        for (int e = l; e < ldh * ldh; e += 64) {
+          const int i = e / ldh, j = e % ldh;
+          Hi[e] = (i < mh && j < mh) ? -0.5 * (Hw[i * HWP + j] + Hw[j * HWP + i]) : 0.0;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  // m + 1 > 32 (monthly or sparser rebalancing: up to 63 union rows outside a window): the
+  // whole workgroup per date, H in LDS, inverted in place by the symmetric sweep operator --
+  // every pivot a_kk (a Schur-complement diagonal, > 0 for SPD H) turns row / column k into
+  // multipliers and updates the rest by a rank-1 term; after all pivots the array holds -H^-1.
+  // mh^3 FMAs over the 512 threads and two barriers per pivot, no global memory in the loop
+  // (the former column-by-column substitutions read the output column from global memory in
+  // their dependent inner loops: 1.5 ms for a 13-date monthly batch)
+  double* const rk = s_a + CH_MAX * HP;   // the pivot row (old values), beside H
+  static_assert(CH_MAX * HP + CH_MAX <= (CK_MAX + 16) * CG, "H_b and its pivot row do not fit");
   for (int gg = 0; gg < G; ++gg) {
     const int b = d0 + gg;
     const int mh = U - s_T[gg] + 1;
-    if (mh <= 16) continue;   // uniform
+    if (mh <= 32) continue;   // uniform
     __syncthreads();
     for (int e = t; e < mh * mh; e += PT_PREP) H[(e / mh) * HP + e % mh] = h_entry(gg, e / mh, e % mh);
-    __syncthreads();
-    for (int k = 0; k < mh; ++k) {   // right-looking Cholesky in LDS (lower)
-      const double dk = H[k * HP + k];
-      if (!(dk > 0.0) || !isfinite(dk)) break;   // uniform: every thread reads the same dk
-      const double sd = sqrt(dk);
+    int bad = 0;
+    for (int k = 0; k < mh; ++k) {
       __syncthreads();
-      if (t > k && t < mh) H[t * HP + k] /= sd;
-      if (t == 0) H[k * HP + k] = sd;
+      if (t < mh) rk[t] = H[k * HP + t];
       __syncthreads();
-      const int rem = mh - 1 - k;
-      for (int e = t; e < rem * rem; e += PT_PREP) {
-        const int i = k + 1 + e / rem, j = k + 1 + e % rem;
-        if (j <= i) H[i * HP + j] -= H[i * HP + k] * H[j * HP + k];
+      const double dk = rk[k];
+      if (!(dk > 0.0) || !isfinite(dk)) {   // uniform: every thread reads the same pivot
+        bad = 1;
+        break;
       }
-      __syncthreads();
+      const double dinv = 1.0 / dk;
+      for (int e = t; e < mh * mh; e += PT_PREP) {
+        const int i = e / mh, j = e - i * mh;
+        const double aik = rk[i] * dinv;   // (symmetric: a_ik = a_ki)
+        double v;
+        if (i == k) v = j == k ? -dinv : rk[j] * dinv;
+        else if (j == k) v = aik;
+        else v = fma(-aik, rk[j], H[i * HP + j]);
+        H[i * HP + j] = v;
+      }
     }
-    int bad = 0;   // a failed pivot leaves H[k][k] unscaled and non-positive
-    for (int k = 0; k < mh; ++k) bad |= !(H[k * HP + k] > 0.0) || !isfinite(H[k * HP + k]);
     if (bad) {
       if (t == 0) st.status[b] = PQ_NON_CONVEX;
       continue;
     }
+    __syncthreads();
     double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
     const int ldh = gc.ldh;
-    if (t < mh) {   // column t of H^-1: L L' x = e_t, solved in place in column t of the output
-      for (int i = 0; i < mh; ++i) {
-        double v = (i == t) ? 1.0 : 0.0;
-        for (int j = 0; j < i; ++j) v -= H[i * HP + j] * Hi[(int64_t)j * ldh + t];
-        Hi[(int64_t)i * ldh + t] = v / H[i * HP + i];
-      }
-      for (int i = mh - 1; i >= 0; --i) {
-        double v = Hi[(int64_t)i * ldh + t];
-        for (int j = i + 1; j < mh; ++j) v -= H[j * HP + i] * Hi[(int64_t)j * ldh + t];
-        Hi[(int64_t)i * ldh + t] = v / H[i * HP + i];
-      }
-    }
-    for (int e = t; e < ldh * ldh; e += PT_PREP) {   // outside the mh x mh block
+    for (int e = t; e < ldh * ldh; e += PT_PREP) {
       const int i = e / ldh, j = e % ldh;
-      if (i >= mh || j >= mh) Hi[e] = 0.0;
+      Hi[e] = (i < mh && j < mh) ? -0.5 * (H[i * HP + j] + H[j * HP + i]) : 0.0;   // (symmetrised)
     }
   }
 }
@@ -353,26 +427,37 @@ __global__ __launch_bounds__(PT_PREP, 2) void k_gcap_prep(pq_lowrank lr, pq_prob
 // CMGW: the wide form, up to 24 shared rows read column-sparse -- cg_nzr / cg_nzv, nzmax <= CNZ
 // nonzeros per asset, e.g. the budget plus one 0/1 sector membership -- instead of as
 // register-resident columns)
-template <int MGC>
-__global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
+// NB: MFMA column blocks of 16 dates -- NB = 2 takes up to 32 dates per group with one
+// 512-thread workgroup per CU (the CU's union rows streamed once per pass for all of them:
+// half the union traffic and half the group factorisations of two 16-date groups); NB = 1 is
+// the 256-thread, 16-date form (two workgroups per CU).  The wide form is NB = 1 only (its
+// per-(date, row) LDS would not fit twice).
+template <int MGC, int NB>
+__global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
                                                   pq_settings s, int iters_call, const double* pc, int64_t ldpc,
                                                   int r0, const double* cc, const int32_t* cg_nzr,
                                                   const double* cg_nzv, int nzmax) {
   constexpr bool WIDE = MGC > CMG;
+  static_assert(NB == 1 || (NB == 2 && !WIDE), "k_admm_gcap: 32-date groups for mg <= 4 only");
   constexpr int MGG = WIDE ? CMGW : 8;
-  __shared__ __attribute__((aligned(16))) double WU[(CU_MAX + 4) * CG_MAX];
+  constexpr int CTN = CT * NB, CNWN = CTN / 64, CHWN = CTN / 32;   // threads, waves, half-waves
+  constexpr int CG = CG_MAX * NB;                                   // dates per group
+  constexpr int CTP1N = (CP1_ROWS / 16 + CNWN - 1) / CNWN;          // pass-1 row tiles per wave
+  constexpr int CTP2N = ((CK_MAX + 15) / 16 + CNWN - 1) / CNWN;     // GEMM row tiles per wave
+  static_assert(CTP1N * CNWN * 16 >= CP1_ROWS && CTP2N * CNWN * 16 >= CK_MAX, "k_admm_gcap tiling");
+  __shared__ __attribute__((aligned(16))) double WU[(CU_MAX + 4) * CG];
   double* const UT = WU;
-  __shared__ double g_muv[CG_MAX], g_su[CG_MAX], g_dinv[CG_MAX], g_rn[CG_MAX], g_qmax[CG_MAX], g_coef[CG_MAX];
-  __shared__ double g_y[CG_MAX * CH_MAX];   // y_b = H_b^-1 s_b of every date
+  __shared__ double g_muv[CG], g_su[CG], g_dinv[CG], g_rn[CG], g_qmax[CG], g_coef[CG];
+  __shared__ double g_y[CG * CH_MAX];   // y_b = H_b^-1 s_b of every date
   constexpr int NPART = 5;                    // per wave and date: 4 maxima, mu.V
-  __shared__ double g_part[CNW * CG_MAX * NPART];
-  __shared__ double g_gm[CG_MAX * 3];
+  __shared__ double g_part[CNWN * CG * NPART];
+  __shared__ double g_gm[CG * 3];
   // per (date, row); the rows' bounds and rho are shared by the group's dates
-  __shared__ double g_zg[CG_MAX * MGG], g_yg[CG_MAX * MGG], g_cgv[CG_MAX * MGG], g_cgx[CG_MAX * MGG],
-      g_wg[CG_MAX * MGG], g_cw[CG_MAX * MGG], g_rgz[CG_MAX * MGG], g_cmu[CG_MAX * MGG];
+  __shared__ double g_zg[CG * MGG], g_yg[CG * MGG], g_cgv[CG * MGG], g_cgx[CG * MGG],
+      g_wg[CG * MGG], g_cw[CG * MGG], g_rgz[CG * MGG], g_cmu[CG * MGG];
   __shared__ double g_rg[MGG], g_lg[MGG], g_ug[MGG];
   double* const g_zt = g_rgz;   // Cg x~ of (date, row): read, then overwritten by rho z~, by one lane
-  __shared__ int g_act[CG_MAX], g_it[CG_MAX], g_end[CG_MAX], g_stat[CG_MAX], g_off[CG_MAX], g_T[CG_MAX];
+  __shared__ int g_act[CG], g_it[CG], g_end[CG], g_stat[CG], g_off[CG], g_T[CG];
   __shared__ int s_urow[CU_MAX];
   __shared__ double s_sr[MGG];
   __shared__ double s_rho;
@@ -397,20 +482,20 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   // a group beyond pass 1's rows (U + mg > CP1_ROWS) or the MFMA N cannot be solved here:
   // its dates fail loudly (status NON_CONVEX, found = False) instead of dropping rows
   // (uniform exit, before any barrier; GroupPlan never builds such a group)
-  if (kU > CP1_ROWS || U > CU_MAX || G > CG_MAX || kU > k_ld) {
-    for (int g = t; g < G; g += CT) st.status[d0 + g] = PQ_NON_CONVEX;
+  if (kU > CP1_ROWS || U > CU_MAX || G > CG || kU > k_ld) {
+    for (int g = t; g < G; g += CTN) st.status[d0 + g] = PQ_NON_CONVEX;
     return;
   }
 
   // ---- setup -------------------------------------------------------------------------------
-  for (int u = t; u < CU_MAX; u += CT) s_urow[u] = u < U ? gc.urows[(int64_t)grp * gc.umax + u] : 0;
-  for (int e = t; e < (CU_MAX + 4) * CG_MAX; e += CT) UT[e] = 0.0;
+  for (int u = t; u < CU_MAX; u += CTN) s_urow[u] = u < U ? gc.urows[(int64_t)grp * gc.umax + u] : 0;
+  for (int e = t; e < (CU_MAX + 4) * CG; e += CTN) UT[e] = 0.0;
   if (t == 0) s_rho = gc.grho[grp];
   __syncthreads();
   const double rho = s_rho;
   const GConst gk = gconst(lr, pb, s, d0, rho);
   if (t < mg) s_sr[t] = sqrt(crho(pb.lg[t], pb.ug[t], rho, s));
-  if (t < CG_MAX) {
+  if (t < CG) {
     const int g = t;
     int act = 0;
     if (g < G) {
@@ -426,7 +511,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
     g_act[g] = act;
   }
-  for (int e = t; e < CG_MAX * MGG; e += CT) {
+  for (int e = t; e < CG * MGG; e += CTN) {
     const int g = e / MGG, r = e % MGG;
     double zg = 0, yg = 0;
     if (g < G && r < mg) {
@@ -463,7 +548,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   (void)zb_h; (void)yb_h; (void)R_h; (void)X_h
 
   // ---- prologue: Cg x, the first rhs, mu.V, Cg.V, Cg.mu (admm_grp.hip's next_rhs, fused) --
-  for (int g = hg; g < G; g += CHW) {
+  for (int g = hg; g < G; g += CHWN) {
     if (!g_act[g]) continue;
     const int hb = d0 + g;
     GC_HPTRS;
@@ -539,43 +624,59 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int hbase = (hg & 1) * 32;
 #pragma clang diagnostic pop
     (void)hbase;
-    // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs) ----------------------
+    // ---- pass 1: W = X_union V (V = rhs / d, W scaled after the MFMAs); each loaded union
+    //      row pair feeds the NB column blocks' MFMAs ------------------------------------------
     {
       const int z0 = loop_zero();
-      const int kq = l >> 4, m = (l & 15) + z0;
-      const double* Vp = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride + ld : nullptr;
-      const double wsc1 = m < G ? g_dinv[m] : 1.0;
-      f64x4 c[CTP1];
-      const double* arow[CTP1];
-      bool tv[CTP1], aval[CTP1];
+      const int kq = l >> 4, m0 = (l & 15) + z0;
+      const double* Vp[NB];
+      double wsc1[NB];
 #pragma unroll
-      for (int j = 0; j < CTP1; ++j) {
-        c[j] = f64x4{0.0, 0.0, 0.0, 0.0};
-        const int u = (w + CNW * j) * 16 + m;
-        tv[j] = w + CNW * j < ntile;
+      for (int nb = 0; nb < NB; ++nb) {
+        const int m = m0 + 16 * nb;
+        Vp[nb] = (m < G) ? st.work + (int64_t)(d0 + m) * st.work_stride + ld : nullptr;
+        wsc1[nb] = m < G ? g_dinv[m] : 1.0;
+      }
+      f64x4 c[CTP1N][NB];
+      const double* arow[CTP1N];
+      bool tv[CTP1N], aval[CTP1N];
+#pragma unroll
+      for (int j = 0; j < CTP1N; ++j) {
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) c[j][nb] = f64x4{0.0, 0.0, 0.0, 0.0};
+        const int u = (w + CNWN * j) * 16 + m0;
+        tv[j] = w + CNWN * j < ntile;
         aval[j] = u < U + mg;
         arow[j] = u < U ? lr.panel + (int64_t)s_urow[u] * lr.ldp : pb.Cg + (int64_t)(u < U + mg ? u - U : 0) * ld;
       }
-      struct Buf { double2 b; double2 a[CTP1]; double bs; };
+      struct Buf { double2 b[NB]; double2 a[CTP1N]; double bs[NB]; };
       // unconditional loads from clamped addresses, no select on a loaded register (see pass 2's
       // load): rows past U + mg and tiles past ntile produce output rows nobody reads, and the
       // columns past n meet a zero V (scaled by 0, after the load)
-      const double* Vq = Vp ? Vp : st.work + (int64_t)d0 * st.work_stride + ld;
+      const double* Vq[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) Vq[nb] = Vp[nb] ? Vp[nb] : st.work + (int64_t)d0 * st.work_stride + ld;
       auto load = [&](Buf& f, int k0) {
         const int kk = k0 + 2 * kq;
         const bool kin = kk + 1 < n;
         const int kc = kin ? kk : 0;
-        f.b = *reinterpret_cast<const double2*>(Vq + kc);
 #pragma unroll
-        for (int j = 0; j < CTP1; ++j) f.a[j] = *reinterpret_cast<const double2*>(arow[j] + kc);
-        f.bs = (Vp && kin) ? 1.0 : 0.0;
+        for (int nb = 0; nb < NB; ++nb) {
+          f.b[nb] = *reinterpret_cast<const double2*>(Vq[nb] + kc);
+          f.bs[nb] = (Vp[nb] && kin) ? 1.0 : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < CTP1N; ++j) f.a[j] = *reinterpret_cast<const double2*>(arow[j] + kc);
       };
       auto mma = [&](const Buf& f) {   // (no branch in the loop: every tile multiplies)
-        const double bx = f.b.x * f.bs, by = f.b.y * f.bs;
 #pragma unroll
-        for (int j = 0; j < CTP1; ++j) {
-          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].x, bx, c[j], 0, 0, 0);
-          c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].y, by, c[j], 0, 0, 0);
+        for (int nb = 0; nb < NB; ++nb) {
+          const double bx = f.b[nb].x * f.bs[nb], by = f.b[nb].y * f.bs[nb];
+#pragma unroll
+          for (int j = 0; j < CTP1N; ++j) {
+            c[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].x, bx, c[j][nb], 0, 0, 0);
+            c[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].y, by, c[j][nb], 0, 0, 0);
+          }
         }
       };
       Buf f0, f1;
@@ -588,18 +689,22 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       // B operand of the group GEMM in place: rows < U = sqrt(c) W, rows U + r = sqrt(R_r) Cg_r V
 #pragma unroll
-      for (int j = 0; j < CTP1; ++j) {
-        const int tile = w + CNW * j;
+      for (int j = 0; j < CTP1N; ++j) {
+        const int tile = w + CNWN * j;
         if (tv[j]) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int u = tile * 16 + kq + 4 * r;
-            if (u < U) {
-              WU[u * CG_MAX + m] = gk.sqc * wsc1 * c[j][r];
-            } else if (u < U + mg) {   // Cg V of date m
-              const double cgv = wsc1 * c[j][r];
-              if (m < G) g_cgv[m * MGG + (u - U)] = cgv;
-              WU[u * CG_MAX + m] = s_sr[u - U] * cgv;
+          for (int nb = 0; nb < NB; ++nb) {
+            const int m = m0 + 16 * nb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int u = tile * 16 + kq + 4 * r;
+              if (u < U) {
+                WU[u * CG + m] = gk.sqc * wsc1[nb] * c[j][nb][r];
+              } else if (u < U + mg) {   // Cg V of date m
+                const double cgv = wsc1[nb] * c[j][nb][r];
+                if (m < G) g_cgv[m * MGG + (u - U)] = cgv;
+                WU[u * CG + m] = s_sr[u - U] * cgv;
+              }
             }
           }
         }
@@ -614,14 +719,15 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     {
       const int z0 = loop_zero();
       const int kq = l >> 4, m = (l & 15) + z0;
-      f64x4 z[CTP2];
-      const double* mrow[CTP2];
-      bool zv[CTP2], rv[CTP2];
+      f64x4 z[CTP2N][NB];
+      const double* mrow[CTP2N];
+      bool zv[CTP2N], rv[CTP2N];
 #pragma unroll
-      for (int j = 0; j < CTP2; ++j) {
-        z[j] = f64x4{0.0, 0.0, 0.0, 0.0};
-        const int row = (w + CNW * j) * 16 + m;
-        zv[j] = w + CNW * j < ktile;
+      for (int j = 0; j < CTP2N; ++j) {
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) z[j][nb] = f64x4{0.0, 0.0, 0.0, 0.0};
+        const int row = (w + CNWN * j) * 16 + m;
+        zv[j] = w + CNWN * j < ktile;
         rv[j] = row < kU;
         mrow[j] = Mi + (int64_t)(rv[j] ? row : 0) * k_ld;
       }
@@ -630,31 +736,34 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       // unconditional loads from clamped addresses (see pass 2's load): rows / columns >= kU of
       // M^-1 (k_ld padding) are never read, rows past kU and tiles past ktile produce output
       // rows nobody reads, and B is zero past kU
-      auto loadA = [&](double2 (&a)[CTP2], int k0) {
+      auto loadA = [&](double2 (&a)[CTP2N], int k0) {
         const int kk = k0 + 2 * kq;
         const int k0c = kk < kU ? kk : 0, k1c = kk + 1 < kU ? kk + 1 : 0;
 #pragma unroll
-        for (int j = 0; j < CTP2; ++j) {
-          const int ts = zv[j] ? (w + CNW * j) * 16 : 0;
+        for (int j = 0; j < CTP2N; ++j) {
+          const int ts = zv[j] ? (w + CNWN * j) * 16 : 0;
           const bool left = kk < ts;   // strictly left of the diagonal block: kk + 1 < ts <= row
           const double* mc = Mi + (ts + m);
           a[j].x = *(left ? mrow[j] + kk : mc + (int64_t)k0c * k_ld);
           a[j].y = *(left ? mrow[j] + kk + 1 : mc + (int64_t)k1c * k_ld);
         }
       };
-      auto mmaA = [&](const double2 (&a)[CTP2], int k0) {
+      auto mmaA = [&](const double2 (&a)[CTP2N], int k0) {
         const int kk = k0 + 2 * kq;
-        const double b0 = kk < kU ? WU[kk * CG_MAX + m] : 0.0;
-        const double b1 = kk + 1 < kU ? WU[(kk + 1) * CG_MAX + m] : 0.0;
 #pragma unroll
-        for (int j = 0; j < CTP2; ++j) {
-          if (zv[j]) {
-            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].x, b0, z[j], 0, 0, 0);
-            z[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].y, b1, z[j], 0, 0, 0);
+        for (int nb = 0; nb < NB; ++nb) {
+          const double b0 = kk < kU ? WU[kk * CG + m + 16 * nb] : 0.0;
+          const double b1 = kk + 1 < kU ? WU[(kk + 1) * CG + m + 16 * nb] : 0.0;
+#pragma unroll
+          for (int j = 0; j < CTP2N; ++j) {
+            if (zv[j]) {
+              z[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].x, b0, z[j][nb], 0, 0, 0);
+              z[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].y, b1, z[j][nb], 0, 0, 0);
+            }
           }
         }
       };
-      double2 a0[CTP2], a1[CTP2];
+      double2 a0[CTP2N], a1[CTP2N];
       loadA(a0, 0);
       for (int k0 = 0; k0 < kU4; k0 += 16) {
         loadA(a1, k0 + 8);
@@ -664,21 +773,23 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       __syncthreads();   // every wave is done reading B
 #pragma unroll
-      for (int j = 0; j < CTP2; ++j) {
-        const int tile = w + CNW * j;
+      for (int j = 0; j < CTP2N; ++j) {
+        const int tile = w + CNWN * j;
         if (zv[j]) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int u = tile * 16 + kq + 4 * r;
-            if (u < kU) WU[u * CG_MAX + m] = z[j][r];
-          }
+          for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int u = tile * 16 + kq + 4 * r;
+              if (u < kU) WU[u * CG + m + 16 * nb] = z[j][nb][r];
+            }
         }
       }
     }
     __syncthreads();
     CSTAMP(1);
     // ---- per date: s, y = H^-1 s (half-wave per date) -------------------------------------------
-    for (int g = hg; g < G; g += CHW) {
+    for (int g = hg; g < G; g += CHWN) {
       if (!g_act[g]) continue;
       const int b = d0 + g;
       const int T = g_T[g], off = g_off[g];
@@ -687,7 +798,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const double* A = gc.aq + (int64_t)b * gc.aq_stride;
       const double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
       double az = 0.0;
-      for (int u = hl; u < kU; u += 32) az = fma(A[u], WU[u * CG_MAX + g], az);
+      for (int u = hl; u < kU; u += 32) az = fma(A[u], WU[u * CG + g], az);
       az = csum32(az);
       // s: lane j < m holds s_j = z'_{C_j}; lane m (or the last) holds s_mu
       double sj[2];
@@ -697,7 +808,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         double v = 0.0;
         if (j < m) {
           const int cj = j < off ? j : j + T;
-          v = WU[cj * CG_MAX + g];
+          v = WU[cj * CG + g];
         } else if (j == m) {
           v = sct * (g_muv[g] - az / d);
         }
@@ -710,7 +821,25 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       const int ldh = gc.ldh;
       const double* hr0 = Hi + (int64_t)(hl < ldh ? hl : ldh - 1) * ldh;
       const double* hr1 = Hi + (int64_t)(hl + 32 < ldh ? hl + 32 : ldh - 1) * ldh;
-      for (int j = 0; j < mh; ++j) {
+      // 8 steps' row loads issued together, then their FMAs: with the monthly windows' mh up
+      // to 64 a load-wait per step (~1 us from L2) dominated the iteration
+      int j0 = 0;
+      for (; j0 + 8 <= mh; j0 += 8) {
+        double h0[8], h1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          h0[u] = hr0[j0 + u];
+          h1[u] = hr1[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + u;
+          const double sv = __shfl(j < 32 ? sj[0] : sj[1], hbase + (j & 31), 64);
+          yi[0] = fma(h0[u], sv, yi[0]);
+          yi[1] = fma(h1[u], sv, yi[1]);
+        }
+      }
+      for (int j = j0; j < mh; ++j) {
         const double sv = __shfl(j < 32 ? sj[0] : sj[1], hbase + (j & 31), 64);
         yi[0] = fma(hr0[j], sv, yi[0]);
         yi[1] = fma(hr1[j], sv, yi[1]);
@@ -733,37 +862,61 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     //      sqrt(R) base on general rows (in place of z' in WU) -------------------------------------
     {
       const int z0 = loop_zero();
-      const int kq = l >> 4, gl = (l & 15) + z0;
+      const int kq = l >> 4, gl0 = (l & 15) + z0;
       const int T0 = g_T[0];
       const int NH = g_off[G - 1], NE = NH + (U - T0);
-      const bool gact = gl < G && g_act[gl];
-      const int offg = gl < G ? g_off[gl] : 0;
-      for (int tile = w; tile < ktile; tile += CNW) {
-        const int ua = tile * 16 + gl;   // A row of this lane
-        f64x4 z = f64x4{0.0, 0.0, 0.0, 0.0};
+      bool gact[NB];
+      int offg[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int gl = gl0 + 16 * nb;
+        gact[nb] = gl < G && g_act[gl];
+        offg[nb] = gl < G ? g_off[gl] : 0;
+      }
+      for (int tile = w; tile < ktile; tile += CNWN) {
+        const int ua = tile * 16 + gl0;   // A row of this lane
+        f64x4 z[NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) z[nb] = f64x4{0.0, 0.0, 0.0, 0.0};
+        // unconditional loads (clamped row / column; rows past kU unused, B zero past NE), the
+        // next step's issued before this step's MFMA: NE reaches ~130 for monthly windows
+        auto edge_a = [&](int e0) -> double {
+          const int e = e0 + kq;
+          const int cu = e < NH ? e : T0 + (e - NH);
+          return Mi[(int64_t)(e < NE ? cu : 0) * k_ld + (ua < kU ? ua : 0)];
+        };
+        double av_next = edge_a(0);
         for (int e0 = 0; e0 < NE; e0 += 4) {
           const int e = e0 + kq;
           const int cu = e < NH ? e : T0 + (e - NH);   // union row of edge e
-          // unconditional load (clamped row / column; rows past kU unused, B zero past NE)
-          const double av = Mi[(int64_t)(e < NE ? cu : 0) * k_ld + (ua < kU ? ua : 0)];
-          double bv = 0.0;
-          if (e < NE && gact) {
-            if (e < NH) bv = e < offg ? g_y[gl * CH_MAX + e] : 0.0;
-            else bv = cu >= offg + T0 ? g_y[gl * CH_MAX + (cu - T0)] : 0.0;
+          const double av = av_next;
+          av_next = edge_a(e0 + 4);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const int gl = gl0 + 16 * nb;
+            double bv = 0.0;
+            if (e < NE && gact[nb]) {
+              if (e < NH) bv = e < offg[nb] ? g_y[gl * CH_MAX + e] : 0.0;
+              else bv = cu >= offg[nb] + T0 ? g_y[gl * CH_MAX + (cu - T0)] : 0.0;
+            }
+            z[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, z[nb], 0, 0, 0);
           }
-          z = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, z, 0, 0, 0);
         }
         // lane holds rows tile * 16 + kq + 4 r of date gl
-        if (gact) {
-          const double coef = g_coef[gl];
-          const double* Q = gc.aq + (int64_t)(d0 + gl) * gc.aq_stride + k_ld;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int u = tile * 16 + kq + 4 * r;
-            if (u < kU) {
-              const double v = WU[u * CG_MAX + gl] - z[r] + coef * Q[u];
-              if (u < U) UT[u * CG_MAX + gl] = gk.sqc * v;
-              else g_cw[gl * MGG + (u - U)] = s_sr[u - U] * v;
+        for (int nb = 0; nb < NB; ++nb) {
+          const int gl = gl0 + 16 * nb;
+          if (gact[nb]) {
+            const double coef = g_coef[gl];
+            const double* Q = gc.aq + (int64_t)(d0 + gl) * gc.aq_stride + k_ld;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int u = tile * 16 + kq + 4 * r;
+              if (u < kU) {
+                const double v = WU[u * CG + gl] - z[nb][r] + coef * Q[u];
+                if (u < U) UT[u * CG + gl] = gk.sqc * v;
+                else g_cw[gl * MGG + (u - U)] = s_sr[u - U] * v;
+              }
             }
           }
         }
@@ -772,12 +925,12 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (MGC > 0) {
       __syncthreads();
       // Cg x~ = Cg V - (PC' Ut - su Cg mu + Cg Cg' cw) / d, then the general rows' z / y
-      for (int g = hg; g < G; g += CHW) {
+      for (int g = hg; g < G; g += CHWN) {
         if (!g_act[g]) continue;
         const double dinv = g_dinv[g], su = g_su[g];
         for (int r = 0; r < mg; ++r) {
           double a = 0.0;
-          for (int u = hl; u < U; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * CG_MAX + g], a);
+          for (int u = hl; u < U; u += 32) a = fma(pc[(int64_t)(s_urow[u] - r0) * ldpc + r], UT[u * CG + g], a);
           a = csum32(a);
           double cwv = 0.0;
           for (int r2 = 0; r2 < mg; ++r2) cwv = fma(cc[r * mg + r2], g_cw[g * MGG + r2], cwv);
@@ -816,32 +969,39 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     //      contiguous bytes per date), and the per-asset data (box, Cg columns) once per
     //      lane for all its dates.  Per-date maxima / sums: lane partials, reduced over the
     //      16 lanes of a date, then NP slots per wave in LDS ---------------------------------
+    // With NB = 2 the waves split by column block (waves 0-3: dates 0-15, waves 4-7: dates
+    // 16-31), wave w + 4 walking the same asset blocks as wave w at the same time, so the union
+    // rows it loads come from L1 / L2 right after wave w's: 4 dates per lane as in the 16-date
+    // form (8 per lane spilled the epilogue's registers)
     {
       const int z0 = loop_zero();
       const int kq = l >> 4, ia = (l & 15) + z0;
       const int Uk = (U + 3) & ~3;
+      const int cb = w / CNW, wb = w - cb * CNW;   // column block of this wave, wave within it
 #ifndef PQ_GCAP_PS
 #define PQ_GCAP_PS 4
 #endif
       constexpr int PS = PQ_GCAP_PS;   // union rows per pass-2 load step (x 4 lanes)
-      bool mact[4];
+      // the lane's dates: slot r -> date 16 cb + kq + 4 r
+      constexpr int NR = 4;
+      bool mact[NR];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = kq + 4 * r;
+      for (int r = 0; r < NR; ++r) {
+        const int m = 16 * cb + kq + 4 * r;
         mact[r] = m < G && g_act[m];
       }
       const bool box_shared = pb.box_stride == 0;
       // per date of the lane: |x-z|, max(|x|, |z|), |dual res|, max(|Px|, |C'y|) (|q|: prologue;
       // Cg V: next pass 1, as extra MFMA rows)
-      double mv[4][4];
-      double muv[4];
+      double mv[NR][4];
+      double muv[NR];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < NR; ++r) {
         muv[r] = 0.0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) mv[r][e] = 0.0;
       }
-      for (int p = w; p * 32 < n; p += CNW) {
+      for (int p = wb; p * 32 < n; p += CNW) {
         const int i = p * 32 + 2 * ia;   // this lane's asset pair (n even: i < n => i + 1 < n)
         const bool cin = i < n;
         f64x4 ce = f64x4{0.0, 0.0, 0.0, 0.0}, co = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -863,7 +1023,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
           for (int h = 0; h < PS; ++h) {
             const int u = u0 + 4 * h + kq;
-            const double av = u < U ? UT[u * CG_MAX + ia] : 0.0;   // Ut'[date ia][u]
+            const double av = u < U ? UT[u * CG + 16 * cb + ia] : 0.0;   // Ut'[date 16 cb + ia][u]
             ce = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].x, ce, 0, 0, 0);
             co = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f.a[h].y, co, 0, 0, 0);
           }
@@ -907,10 +1067,10 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
           rb2 = double2{crho(lo2.x, up2.x, rho, s), crho(lo2.y, up2.y, rho, s)};
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
+        for (int r = 0; r < NR; ++r) {
           __builtin_amdgcn_sched_barrier(0);   // one date's loads live at a time (VGPR budget)
           if (!mact[r]) continue;
-          const int m = kq + 4 * r;
+          const int m = 16 * cb + kq + 4 * r;
           const int bm = d0 + m;
           const double su = g_su[m], dinv = g_dinv[m];
           double2 lo = lo2, up = up2, rb = rb2;
@@ -1017,16 +1177,16 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
       // reduce over the 16 lanes of each date (lanes kq * 16 + 0..15), then one slot per wave
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < NR; ++r) {
 #pragma unroll
         for (int sh = 1; sh < 16; sh <<= 1) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) mv[r][e] = fmax(mv[r][e], __shfl_xor(mv[r][e], sh, 64));
           muv[r] += __shfl_xor(muv[r], sh, 64);
         }
-        const int m = kq + 4 * r;
+        const int m = 16 * cb + kq + 4 * r;
         if (ia == 0) {
-          double* pp = g_part + (w * CG_MAX + m) * NPART;
+          double* pp = g_part + (w * CG + m) * NPART;
 #pragma unroll
           for (int e = 0; e < 4; ++e) pp[e] = mv[r][e];
           pp[4] = muv[r];
@@ -1041,8 +1201,8 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       // mv: |Cx-z| max(|Cx|,|z|) - |dres| max(|Px|,|C'y|) - |q| (the 7-slot form of admm_grp)
       double mv[7] = {g_gm[g * 3], fmax(g_gm[g * 3 + 1], g_gm[g * 3 + 2]), 0.0, 0.0, 0.0, 0.0, g_qmax[g]};
       double muv = 0.0;
-      for (int ww = 0; ww < CNW; ++ww) {
-        const double* pp = g_part + (ww * CG_MAX + g) * NPART;
+      for (int ww = (g / 16) * CNW; ww < (g / 16 + 1) * CNW; ++ww) {   // the waves of g's column block
+        const double* pp = g_part + (ww * CG + g) * NPART;
         mv[0] = fmax(mv[0], pp[0]);
         mv[1] = fmax(mv[1], pp[1]);
         mv[3] = fmax(mv[3], pp[2]);
@@ -1116,7 +1276,7 @@ __global__ __launch_bounds__(CT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
   }
   if (t == 0) gc.grho[grp] = s_rho;
-  for (int e = t; e < CG_MAX * MGG; e += CT) {
+  for (int e = t; e < CG * MGG; e += CTN) {
     const int g = e / MGG, r = e % MGG;
     if (g < G && r < mg) {
       const int b = d0 + g;
@@ -1147,8 +1307,14 @@ static int gcap_check(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap*
   // (a group with ucnt[g] + mg beyond k_ld or pass 1 fails its dates in k_admm_gcap; U <= umax <= 320)
   PQ_CHECK_ARG(gc->k_ld % 64 == 0 && gc->k_ld >= 64 && gc->k_ld <= 384,
                "%s: need 64 <= k_ld <= 384, a multiple of 64 (k_ld=%d)", who, gc->k_ld);
+  PQ_CHECK_ARG(gc->gmax >= 0 && gc->gmax <= pq::CG_MAX * 2, "%s: gmax must be in [0, %d] (gmax=%d)", who,
+               pq::CG_MAX * 2, gc->gmax);
   return 0;
 }
+
+// column blocks of the group kernels: 2 (32-date groups, one 512-thread workgroup per CU) when
+// the plan has groups of more than 16 dates
+static int gcap_nb(const pq_gcap* gc) { return gc->gmax > pq::CG_MAX ? 2 : 1; }
 
 extern "C" int pq_gcap_assemble(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap* gc,
                                 const pq_settings* s, const double* band, int64_t ldo, int32_t r0,
@@ -1173,8 +1339,12 @@ extern "C" int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(gc->umax <= pq::CU_MAX && pb->mg <= pq::CMGW, "pq_gcap_prepare: union or general rows too many");
   const int grid = idx ? nidx : gc->ngroups;   // one workgroup per group (idx: group subset)
   if (grid <= 0) return 0;
-  hipLaunchKernelGGL(pq::k_gcap_prep, dim3(grid), dim3(pq::PT_PREP), 0, (hipStream_t)stream, *lr, *pb, *st, *gc, *s, idx,
-                     band, ldo, r0, pc, ldpc);
+  if (gcap_nb(gc) == 2)
+    hipLaunchKernelGGL(pq::k_gcap_prep<2>, dim3(grid), dim3(pq::PT_PREP), 0, (hipStream_t)stream, *lr, *pb, *st, *gc,
+                       *s, idx, band, ldo, r0, pc, ldpc);
+  else
+    hipLaunchKernelGGL(pq::k_gcap_prep<1>, dim3(grid), dim3(pq::PT_PREP), 0, (hipStream_t)stream, *lr, *pb, *st, *gc,
+                       *s, idx, band, ldo, r0, pc, ldpc);
   PQ_CHECK_LAUNCH("pq_gcap_prepare");
   return 0;
 }
@@ -1195,18 +1365,35 @@ extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(pb->mg <= pq::CMG || (cg_nzr && cg_nzv && nzmax > 0 && nzmax <= pq::CNZ),
                "pq_admm_lr_gcap: more than %d general rows need their column-sparse form (nzmax <= %d)", pq::CMG,
                pq::CNZ);
-  if (pb->mg == 0)
-    hipLaunchKernelGGL(pq::k_admm_gcap<0>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
-                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
-  else if (pb->mg == 1)   // the budget row alone (the usual case): one general row in registers
-    hipLaunchKernelGGL(pq::k_admm_gcap<1>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb, *st,
-                       *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
-  else if (pb->mg <= pq::CMG)
-    hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMG>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
-                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, nullptr, nullptr, 0);
-  else   // budget + sector caps: column-sparse rows
-    hipLaunchKernelGGL(pq::k_admm_gcap<pq::CMGW>, dim3(gc->ngroups), dim3(pq::CT), 0, (hipStream_t)stream, *lr, *pb,
-                       *st, *gc, *s, iters_this_call, pc, ldpc, r0, cc, cg_nzr, cg_nzv, nzmax);
+  const dim3 grid(gc->ngroups);
+  const hipStream_t str = (hipStream_t)stream;
+  if (gcap_nb(gc) == 2) {   // 32-date groups: the register-resident general-row forms only
+    PQ_CHECK_ARG(pb->mg <= pq::CMG, "pq_admm_lr_gcap: groups of more than 16 dates need mg <= %d", pq::CMG);
+    const dim3 blk(pq::CT * 2);
+    if (pb->mg == 0)
+      hipLaunchKernelGGL((pq::k_admm_gcap<0, 2>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc, ldpc,
+                         r0, cc, nullptr, nullptr, 0);
+    else if (pb->mg == 1)
+      hipLaunchKernelGGL((pq::k_admm_gcap<1, 2>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc, ldpc,
+                         r0, cc, nullptr, nullptr, 0);
+    else
+      hipLaunchKernelGGL((pq::k_admm_gcap<pq::CMG, 2>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc,
+                         ldpc, r0, cc, nullptr, nullptr, 0);
+  } else {
+    const dim3 blk(pq::CT);
+    if (pb->mg == 0)
+      hipLaunchKernelGGL((pq::k_admm_gcap<0, 1>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc, ldpc,
+                         r0, cc, nullptr, nullptr, 0);
+    else if (pb->mg == 1)   // the budget row alone (the usual case): one general row in registers
+      hipLaunchKernelGGL((pq::k_admm_gcap<1, 1>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc, ldpc,
+                         r0, cc, nullptr, nullptr, 0);
+    else if (pb->mg <= pq::CMG)
+      hipLaunchKernelGGL((pq::k_admm_gcap<pq::CMG, 1>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc,
+                         ldpc, r0, cc, nullptr, nullptr, 0);
+    else   // budget + sector caps: column-sparse rows
+      hipLaunchKernelGGL((pq::k_admm_gcap<pq::CMGW, 1>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc,
+                         ldpc, r0, cc, cg_nzr, cg_nzv, nzmax);
+  }
   PQ_CHECK_LAUNCH("pq_admm_lr_gcap");
   return 0;
 }

@@ -13,6 +13,7 @@ raises ``PorquaHipError``.
 """
 from __future__ import annotations
 
+import os
 import ctypes
 import dataclasses
 from dataclasses import dataclass
@@ -804,7 +805,8 @@ def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan"
                            ucnt=groups.ucnt.data_ptr(), uoff=groups.uoff.data_ptr(), umax=groups.umax,
                            gidx=groups.gidx.data_ptr(), grho=buf["grho"].data_ptr(), M=buf["M"].data_ptr(),
                            Minv=buf["Minv"].data_ptr(), k_ld=k_ld, M_stride=k_ld * k_ld,
-                           aq=buf["aq"].data_ptr(), aq_stride=2 * k_ld, hinv=buf["hinv"].data_ptr(), ldh=ldh)
+                           aq=buf["aq"].data_ptr(), aq_stride=2 * k_ld, hinv=buf["hinv"].data_ptr(), ldh=ldh,
+                           gmax=int(groups.sizes.max()) if G else 0)
     # the factor sees each M_U as a k x k "problem" (identity padding beyond its U + mg rows)
     buf["pb"] = _lib.PQProblem(n=kmax, ld=k_ld, batch=G, mg=0, P=buf["M"].data_ptr(), P_stride=k_ld * k_ld,
                                q=qb.q.data_ptr(), q_stride=qb.q.stride(0), Cg=qb.Cg.data_ptr(),
@@ -985,12 +987,21 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     gcap_try = (gcap and eig is None and grouped and fuse and qb.shared
                 and (qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
                 and groups.ucnt_max + qb.mg <= 320 and groups.corr_max <= 64)
+    # the group capacitance's own plan: up to 32 dates per group for register-resident general
+    # rows (GroupPlan.gcap_plan); the polish keeps its 16-date groups (polish_plan)
+    gplan = groups
+    if gcap_try and qb.mg <= 4:
+        g32 = groups.gcap_plan()
+        if g32.ucnt_max + qb.mg <= 320 and g32.corr_max <= 64:
+            gplan = g32
     if band:
         # the band must cover every union the capacitances read: the ADMM's groups and the
         # polish's (wide rounds)
-        wmin = max(groups.span_max, groups.polish_plan().span_max) if (gcap_try or (grouped and wide_polish)) else 0
+        wmin = (max(gplan.span_max, groups.polish_plan().span_max) if (gcap_try or (grouped and wide_polish))
+                else 0)
         bd = tl("gram", lambda: _band_setup(qb, lr, strm, w_min=wmin))
-    gc = _gcap_setup(qb, lr, ws, groups, settings or Settings()) if (gcap_try and bd is not None) else None
+    gc = _gcap_setup(qb, lr, ws, gplan, settings or Settings()) if (gcap_try and bd is not None) else None
+    ws.gcap_groups = gplan if gc is not None else None   # (the bench's roofline reads the plan used)
 
     def refactor_groups():
         """Group capacitance: one M_U per group (current group rho), its inverse, and every
@@ -1319,6 +1330,9 @@ class SlidePlan:
 
 
 GROUP_MAX_DATES = 16     # MFMA N of the grouped ADMM (admm_grp.hip GMAX)
+# dates per group of the group-capacitance ADMM with its two MFMA column blocks (admm_gcap.hip,
+# NB = 2: one 512-thread workgroup per CU); PQ_GCAP_GMAX=16 keeps the 16-date groups (A/B)
+GCAP_MAX_DATES = int(os.environ.get("PQ_GCAP_GMAX", "32"))
 GROUP_MAX_UNION = 320    # union rows per group (admm_grp.hip UMAXG)
 
 
@@ -1340,6 +1354,8 @@ class GroupPlan:
         self._host = (rows, tlen, device, umax, smax, breaks, cus, gmax)
         self._polish_full = polish_full
         self._polish_plan = None
+        self._gcap_plan = None
+        self._gmin = gmin
         # balance: one group per CU per round (one 512-thread workgroup fits a CU), as few
         # rounds as gmax allows, groups as even as possible within them
         rounds = max(1, -(-B // (gmax * cus)))
@@ -1439,6 +1455,23 @@ class GroupPlan:
             if full:
                 self._polish_full = False
         return self._polish_plan if self._polish_plan is not None else self
+
+    def gcap_plan(self) -> "GroupPlan":
+        """The plan of the group-capacitance ADMM (admm_gcap.hip) for register-resident general
+        rows (mg <= 4): CU-balanced groups of up to GCAP_MAX_DATES dates (its 32-date form: one
+        workgroup per CU streams one union for all of them -- half the union traffic and half the
+        group factorisations of two 16-date groups; config 3: 475 groups of 10 -> 250 of 19).
+        This plan itself when that changes nothing (small batches, GCAP_MAX_DATES <= 16)."""
+        if self._gcap_plan is None:
+            rows, tlen, device, umax, smax, breaks, cus, gmax0 = self._host
+            g = self
+            if GCAP_MAX_DATES > gmax0 and self.ngroups > 0:
+                g32 = GroupPlan(rows, tlen, device, gmax=min(GCAP_MAX_DATES, 32), umax=umax, smax=smax, cus=cus,
+                                gmin=self._gmin, breaks=breaks)
+                if g32.ok and g32.ngroups < self.ngroups and int(g32.sizes.max()) > gmax0:
+                    g = g32
+            self._gcap_plan = g
+        return self._gcap_plan
 
     def device_index(self):
         """(group of each date as int64, dates per group as FP64) on the device, built once."""

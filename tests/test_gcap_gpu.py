@@ -23,7 +23,7 @@ from porqua_amd.synthetic import factor_panel
 pytestmark = pytest.mark.gpu
 
 
-def _problem(device, n, T, D, ub, stride=1, centred=True, budget=True, caps=0):
+def _problem(device, n, T, D, ub, stride=1, centred=True, budget=True, caps=0, cus=256):
     ends = list(range(T + 5, T + 5 + D * stride, stride))
     dates, R, y, sec = factor_panel(max(ends) + 1, n)
     rows, tlen = engine.window_rows(dates, dates[ends], T)
@@ -44,7 +44,7 @@ def _problem(device, n, T, D, ub, stride=1, centred=True, budget=True, caps=0):
         xty, _ = pan.gram_xy(r_d, t_d)
         qb.q = (-2.0 * xty).contiguous()
         lr = engine.LowRank(pan, r_d, t_d, mu=None)
-    gp = engine.GroupPlan(rows, tlen, device)
+    gp = engine.GroupPlan(rows, tlen, device, cus=cus)
     return qb, lr, gp
 
 
@@ -59,7 +59,8 @@ def _run(qb, lr, gp, gcap, settings, polish=True):
             res.capacitance, res.refactors)
 
 
-@pytest.mark.parametrize("n,T,D,ub,stride", [(1000, 252, 48, 1.0, 1), (400, 120, 40, 0.05, 1), (300, 60, 30, 0.2, 3)])
+@pytest.mark.parametrize("n,T,D,ub,stride", [(1000, 252, 48, 1.0, 1), (400, 120, 40, 0.05, 1), (300, 60, 30, 0.2, 3),
+                                              (600, 252, 13, 0.2, 21)])
 def test_gcap_same_iterates_with_one_rho(device, n, T, D, ub, stride):
     qb, lr, gp = _problem(device, n, T, D, ub, stride)
     # one fixed rho, no adaptation: the per-date and the group form are the same iteration
@@ -92,7 +93,8 @@ def test_gcap_group_rho_adaptation(device):
     assert np.abs(xa - xb).max() <= 1e-8
 
 
-@pytest.mark.parametrize("n,T,D,ub,stride", [(1000, 252, 48, 1.0, 1), (494, 252, 40, 1.0, 1), (300, 60, 30, 0.2, 3)])
+@pytest.mark.parametrize("n,T,D,ub,stride", [(1000, 252, 48, 1.0, 1), (494, 252, 40, 1.0, 1), (300, 60, 30, 0.2, 3),
+                                              (494, 252, 13, 1.0, 21)])
 def test_gcap_uncentred_same_iterates_with_one_rho(device, n, T, D, ub, stride):
     """The ADMM iterates themselves (no polish): the tracking P = 2 X'X has rank T < n, so
     the optimum can be a face and polished points of two exact solvers need not coincide."""
@@ -178,3 +180,55 @@ def test_gcap_nan_iterate_is_not_solved(device):
     assert cap_b == "group"
     assert sb[7] == _lib.PQ_NON_CONVEX, sb
     assert np.all(np.delete(sb, 7) == _lib.PQ_SOLVED), sb
+
+
+@pytest.mark.parametrize("centred,mg_caps", [(True, 0), (False, 0), (True, 2)])
+def test_gcap_32_date_groups_same_iterates(device, centred, mg_caps):
+    """The 32-date form (two MFMA column blocks, one 512-thread workgroup per group; the plan
+    GroupPlan.gcap_plan builds CU-balanced groups of up to 32 dates -- here 19, with cus = 16):
+    the same ADMM iterates as the per-date form with one fixed rho, centred and uncentred
+    windows, the budget alone and with two sector caps."""
+    qb, lr, gp = _problem(device, 600, 120, 300, 0.2, centred=centred, caps=mg_caps, cus=16)
+    g32 = gp.gcap_plan()
+    assert g32 is not gp and int(g32.sizes.max()) > 16 and int(gp.sizes.max()) <= 16
+    st = engine.Settings(rho0_rel=0.0, rho0=0.01, rho0_qrel=0.0, adapt_interval=0, eps_grouped=0.0)
+    ws = engine.Workspace(qb, dense=False)
+    ra = engine.solve_lowrank(qb, lr, st, ws=ws, groups=gp, gcap=False, polish=False)
+    xa, sa, ia = ra.x.cpu().numpy().copy(), ra.status.cpu().numpy().copy(), ra.iters.cpu().numpy().copy()
+    ws2 = engine.Workspace(qb, dense=False)
+    rb = engine.solve_lowrank(qb, lr, st, ws=ws2, groups=gp, gcap=True, polish=False)
+    torch.cuda.synchronize()
+    assert rb.capacitance == "group" and ws2.gcap_groups is g32
+    xb, sb, ib = rb.x.cpu().numpy(), rb.status.cpu().numpy(), rb.iters.cpu().numpy()
+    assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED), (sa, sb)
+    assert np.abs(ia - ib).max() <= 1, (ia, ib)
+    # rounding differences between the per-date and any group form grow with the iterations:
+    # on this problem with the caps the 16-date form differs from the per-date one by 1.2e-9
+    # and the 32-date one by 1.6e-9 (tools/diag_gcap32.py, profiles/r05k_diag_gcap32.log)
+    tol = (1e-9 if not mg_caps else 3e-9) if centred else 1e-8
+    assert np.abs(xa - xb).max() <= tol, np.abs(xa - xb).max()
+
+
+def test_gcap_32_date_groups_polished_optimum(device):
+    """Default settings, the whole solve (loose ADMM stop, grouped polish on its 16-date plan):
+    the 32-date group form reaches the optimum of the 16-date one."""
+    import porqua_amd.engine as eng
+    qb, lr, gp = _problem(device, 1000, 252, 400, 1.0, cus=16)
+    assert int(gp.gcap_plan().sizes.max()) > 16
+    ws = engine.Workspace(qb, dense=False)
+    rb = engine.solve_lowrank(qb, lr, None, ws=ws, groups=gp)
+    xb, sb = rb.x.cpu().numpy().copy(), rb.status.cpu().numpy().copy()
+    assert ws.gcap_groups is gp.gcap_plan()
+    old = eng.GCAP_MAX_DATES
+    try:
+        eng.GCAP_MAX_DATES = 16
+        qb2, lr2, gp2 = _problem(device, 1000, 252, 400, 1.0, cus=16)
+        ws2 = engine.Workspace(qb2, dense=False)
+        ra = engine.solve_lowrank(qb2, lr2, None, ws=ws2, groups=gp2)
+        assert ws2.gcap_groups is gp2
+    finally:
+        eng.GCAP_MAX_DATES = old
+    torch.cuda.synchronize()
+    xa, sa = ra.x.cpu().numpy(), ra.status.cpu().numpy()
+    assert np.all(sa == _lib.PQ_SOLVED) and np.all(sb == _lib.PQ_SOLVED)
+    assert np.abs(xa - xb).max() <= 1e-8, np.abs(xa - xb).max()

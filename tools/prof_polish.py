@@ -23,8 +23,12 @@ def main():
     cfg4 = "--config4" in sys.argv   # n = 3000 tracking LS with 20 sector caps (tools/bench_configs.py)
     lsq = "--lsq494" in sys.argv     # config 2's shape: n = 494 tracking LS, budget + long-only box
     n, T, D = (3000 if cfg4 else (494 if lsq else 1000)), 252, int(args[0]) if args else (2000 if cfg4 else 4749)
-    dates, R, y, sec = factor_panel(T - 1 + D, n, n_sectors=20 if cfg4 else 10)
-    rows, tlen = engine.window_rows(dates, dates[T - 1:T - 1 + D], T)
+    stride = 1   # --stride=S: rebalance every S rows (21: the monthly run of the reference notebook)
+    for a in sys.argv:
+        if a.startswith("--stride="):
+            stride = int(a.split("=")[1])
+    dates, R, y, sec = factor_panel(T - 1 + (D - 1) * stride + 1, n, n_sectors=20 if cfg4 else 10)
+    rows, tlen = engine.window_rows(dates, dates[T - 1:T - 1 + (D - 1) * stride + 1:stride], T)
     pan = engine.Panel(R, y if (cfg4 or lsq) else None)
     r_d, t_d = pan.rows_to_device(rows, tlen)
     G = np.stack([(sec == g).astype(float) for g in range(20)]) if cfg4 else None
