@@ -95,6 +95,11 @@ typedef struct pq_settings {
    * The loose stop before the grouped polish uses it so that an early dip of the residuals
    * (ADMM's are not monotone) cannot end the iterations before the active set is predicted */
   int32_t min_iter;
+  /* grouped polish: when a round's answer is rejected anyway, variables at a bound whose
+   * multiplier is within polish_release_rel * (problem scale) of the wrong sign are released
+   * too (0: only the wrong-sign ones) -- the next round's free set anticipates the shift, and
+   * the solve's inner primal step fixes those that were right after all */
+  double polish_release_rel;
 } pq_settings;
 
 /* Low-rank description of P for T < n (the backtest path): P_eff = p_scale[b] *

@@ -82,6 +82,7 @@ class PQSettings(ctypes.Structure):
         ("polish_rounds", c_int32), ("refine_iters", c_int32),
         ("polish_fix_rel", ctypes.c_double),
         ("polish_inner", ctypes.c_int32), ("min_iter", ctypes.c_int32),
+        ("polish_release_rel", ctypes.c_double),
     ]
 
 

@@ -208,38 +208,61 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
     if (l == 0) s_a[(U + r) * CG + gg] = s_sr[r] * sum / s_T[gg];
   }
   __syncthreads();
-  // ---- B: Q = M_U^-1 A (MFMA; A rows from the full symmetric M_U^-1, B from LDS) -----------
+  // ---- B: Q = M_U^-1 A (MFMA; A rows from the full symmetric M_U^-1, B from LDS).  All row
+  //      tiles of a wave in one k loop, the next step's A loads in flight during this step's
+  //      MFMAs (unconditional loads from clamped addresses: rows / columns >= kU are M_U^-1's
+  //      identity padding, multiplied by the zero rows of s_a) ------------------------------------
   const double* Mi = gc.Minv + (int64_t)grp * gc.M_stride;
   {
+    constexpr int QT = (CK_MAX / 16 + 1 + PW_PREP - 1) / PW_PREP;   // row tiles per wave (<= 21 tiles)
     const int kq = l >> 4, m = l & 15;
     const int kU4 = (kU + 7) & ~7;
-    for (int tile = w; tile < ktile; tile += PW_PREP) {
-      const int row = tile * 16 + m;
-      const bool rv = row < kU;
-      const double* mrow = Mi + (int64_t)(rv ? row : 0) * k_ld;
-      f64x4 z[NB];
+    f64x4 z[QT][NB];
+    const double* mrow[QT];
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) z[nb] = f64x4{0.0, 0.0, 0.0, 0.0};
-      for (int k0 = 0; k0 < kU4; k0 += 8) {
-        const int kk = k0 + 2 * kq;
-        const bool kin = kk < kU, kin1 = kk + 1 < kU;
-        double2 av = double2{0.0, 0.0};
-        if (rv && kin1) av = *reinterpret_cast<const double2*>(mrow + kk);
-        else if (rv && kin) av.x = mrow[kk];
+    for (int j = 0; j < QT; ++j) {
+      const int row = (w + PW_PREP * j) * 16 + m;
+      mrow[j] = Mi + (int64_t)(row < k_ld ? row : 0) * k_ld;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
-          const double b0 = s_a[kk * CG + m + 16 * nb];   // rows >= kU of s_a are zero
-          const double b1 = s_a[(kk + 1) * CG + m + 16 * nb];
-          z[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, b0, z[nb], 0, 0, 0);
-          z[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, b1, z[nb], 0, 0, 0);
+      for (int nb = 0; nb < NB; ++nb) z[j][nb] = f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    auto loadq = [&](double2 (&a)[QT], int k0) {
+      const int kk = k0 + 2 * kq;
+      const int kc = kk + 1 < k_ld ? kk : 0;
+#pragma unroll
+      for (int j = 0; j < QT; ++j) a[j] = *reinterpret_cast<const double2*>(mrow[j] + kc);
+    };
+    auto mmaq = [&](const double2 (&a)[QT], int k0) {
+      const int kk = k0 + 2 * kq;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const double b0 = s_a[kk * CG + m + 16 * nb];   // rows >= kU of s_a are zero
+        const double b1 = s_a[(kk + 1) * CG + m + 16 * nb];
+#pragma unroll
+        for (int j = 0; j < QT; ++j) {
+          z[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].x, b0, z[j][nb], 0, 0, 0);
+          z[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j].y, b1, z[j][nb], 0, 0, 0);
         }
       }
+    };
+    double2 qa0[QT], qa1[QT];
+    loadq(qa0, 0);
+    for (int k0 = 0; k0 < kU4; k0 += 16) {
+      loadq(qa1, k0 + 8);
+      mmaq(qa0, k0);
+      loadq(qa0, k0 + 16);
+      if (k0 + 8 < kU4) mmaq(qa1, k0 + 8);
+    }
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+      const int tile = w + PW_PREP * j;
+      if (tile * 16 >= kU) continue;
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int u = tile * 16 + kq + 4 * r, md = m + 16 * nb;
-          if (u < kU && md < G) gc.aq[(int64_t)(d0 + md) * gc.aq_stride + k_ld + u] = z[nb][r];   // q_b
+          if (u < kU && md < G) gc.aq[(int64_t)(d0 + md) * gc.aq_stride + k_ld + u] = z[j][nb][r];   // q_b
         }
     }
   }

@@ -1692,6 +1692,7 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
   const double sc = R[R_SC];
   const double dtol = s.dual_tol * sc;
   const double ptol = 1e-12;
+  const double soft = s.polish_release_rel > 0.0 ? s.polish_release_rel * sc : 0.0;
   // vertex (k == 0, set up with at most one active equality row r0): its multiplier is the
   // middle of the interval in which every bound variable's multiplier has the right sign,
   //   at lb: g0_i + lam c_i >= 0,  at ub: g0_i + lam c_i <= 0   (g0 = P x + q)
@@ -1753,6 +1754,8 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
         else if (!isinf(ubi) && xi > ubi + ptol * (1.0 + fabs(ubi))) { wk.fl[i] = 2; bad = 1; }
       } else if (f == 1 && lbi != ubi && -gi > dtol) { wk.fl[i] = 0; bad = 1; }
       else if (f == 2 && -gi < -dtol) { wk.fl[i] = 0; bad = 1; }
+      else if (soft > 0.0 && f == 1 && lbi != ubi && -gi > dtol - soft) wk.fl[i] = 5;   // near the sign
+      else if (soft > 0.0 && f == 2 && -gi < soft - dtol) wk.fl[i] = 6;                  // (resolved below)
     }
   }
   // general rows: Cg x, activity checks (lane 0 decides, as the reference kernel's lane 0)
@@ -1786,6 +1789,11 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
     }
   }
   bad = block_max((double)bad, red) > 0.5;
+  if (soft > 0.0)   // a rejected round also releases the near-sign variables; an accepted one keeps them
+    for (int i = hl; i < n; i += PPT) {
+      const int f = wk.fl[i];
+      if (f >= 5) wk.fl[i] = bad ? 0 : f - 4;
+    }
   if (vtx && hl == 0) {   // the next round starts from it (setup's R_SOL), or the scoring uses it
     R[R_LAM + r0] = lam0;
     R[R_SOL] = lam0;

@@ -136,6 +136,9 @@ class Settings:
     # eps_grouped 0.3 (profiles/r04t_eg3_in{1,2}.log): 1 / 2 -> 466k / 457k QPs/s (2.29 / 2.11
     # rounds; the second step costs more in the solve buckets than the rounds it saves)
     polish_inner: int = 1
+    # grouped polish: a rejected round also releases the variables at a bound whose multiplier
+    # is within this fraction of the problem scale of the wrong sign (0: off; see pq_settings)
+    polish_release_rel: float = 0.0
 
     def to_c(self) -> _lib.PQSettings:
         names = {f[0] for f in _lib.PQSettings._fields_}
@@ -1011,8 +1014,14 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         _lib.check(lib.pq_gcap_assemble(L_, P_, GC_, SS, bd["band"].data_ptr(), bd["ldo"], bd["r0"],
                                         bd["pc"].data_ptr(), bd["pc"].stride(0), bd["cc"].data_ptr(), strm),
                    "pq_gcap_assemble")
-        _lib.check(lib.pq_factor_batched(ctypes.byref(g["pb"]), ctypes.byref(g["st"]), None, 0, SSM, 2, strm),
-                   "pq_factor_batched(M_U)")
+        if GCAP_FACTOR == "large":   # (experiment) many workgroups per M_U: K2L, one tile each
+            if g.get("W") is None:
+                g["W"] = torch.empty_like(g["M"])
+            _lib.check(lib.pq_factor_large(ctypes.byref(g["pb"]), ctypes.byref(g["st"]), None, 0, SSM, 2,
+                                           g["W"].data_ptr(), g["W"].stride(0), strm), "pq_factor_large(M_U)")
+        else:
+            _lib.check(lib.pq_factor_batched(ctypes.byref(g["pb"]), ctypes.byref(g["st"]), None, 0, SSM, 2, strm),
+                       "pq_factor_batched(M_U)")
         _lib.check(lib.pq_gcap_prepare(L_, P_, S_, GC_, SS, None, 0, bd["band"].data_ptr(), bd["ldo"], bd["r0"],
                                        bd["pc"].data_ptr(), bd["pc"].stride(0), strm), "pq_gcap_prepare")
 
@@ -1333,6 +1342,7 @@ GROUP_MAX_DATES = 16     # MFMA N of the grouped ADMM (admm_grp.hip GMAX)
 # dates per group of the group-capacitance ADMM with its two MFMA column blocks (admm_gcap.hip,
 # NB = 2: one 512-thread workgroup per CU); PQ_GCAP_GMAX=16 keeps the 16-date groups (A/B)
 GCAP_MAX_DATES = int(os.environ.get("PQ_GCAP_GMAX", "32"))
+GCAP_FACTOR = os.environ.get("PQ_GCAP_FACTOR", "batched")   # (A/B) "large": K2L for the group factor
 GROUP_MAX_UNION = 320    # union rows per group (admm_grp.hip UMAXG)
 
 
