@@ -464,6 +464,16 @@ class Backtest:
             if lb is None or ub is None:
                 return False, None, None, None, None   # the split needs a box (serial path raises)
             split_panel = engine.Panel(torch.cat([panel.R, -panel.R], 1).contiguous(), None, device=dev)
+        # turnover + leverage: the segment split on the ADMM engine (porqua_amd/l1seg.py) when the
+        # box holds 0 and x0 and P has no ridge (checked per chunk); else the per-asset-block IPM
+        seg_sd, seg_panel, seg_mg = None, None, 0
+        if l1both is not None and lb is not None and ub is not None:
+            from . import l1seg
+            seg_sd = l1seg.segment_data(l1both.x0, lb, ub, cost=l1both.cost, to_budget=l1both.to_budget,
+                                        lev_budget=l1both.lev_budget)
+            if seg_sd is not None:
+                seg_mg = mg + (seg_sd["to_budget"] is not None and np.isfinite(seg_sd["to_budget"])) + \
+                    bool(np.isfinite(seg_sd["lev_budget"]))
         if lad:
             if l1term is not None or l1both is not None:
                 return False, None, None, None, None
@@ -510,6 +520,9 @@ class Backtest:
             # triangle only (engine.lowrank_shape_ok: same test as solve_lowrank's)
             stage.prefer_lowrank = (bs.settings.get("lowrank", True)
                                     and engine.lowrank_shape_ok(n, int(stage.rows_host.shape[1]), mg))
+            if seg_sd is not None:   # the segment split's window form: 3n variables, seg_mg rows
+                stage.prefer_lowrank = (bs.settings.get("lowrank", True)
+                                        and engine.lowrank_shape_ok(3 * n, int(stage.rows_host.shape[1]), seg_mg))
             obj = opt.objective_batch(stage)
             if obj is None:
                 ok = False
@@ -526,7 +539,22 @@ class Backtest:
             qq = torch.zeros((e - s, qb.ld), dtype=torch.float64, device=dev)
             qq[:, :n] = q[:, :n]
             qb.q = qq
-            if l1both is not None:   # turnover + leverage: the per-asset-block IPM (porqua_amd/ipm_l1.py)
+            seg_go = (seg_sd is not None and stage.lowrank is not None
+                      and (pdiag is None or not bool((pdiag != 0).any())))
+            if seg_go:   # turnover + leverage: the segment split (porqua_amd/l1seg.py) on the window path
+                from . import l1seg
+                from .l1split import split_settings
+                if seg_panel is None:
+                    seg_panel = engine.Panel(torch.cat([panel.R] * 3, 1).contiguous(), None, device=dev)
+                qb3, lr3, const = l1seg.segment_batch(qb, stage.lowrank, seg_sd, seg_panel, GhAb["A"], GhAb["b"],
+                                                      GhAb["G"], GhAb["h"])
+                kind = "budget" if (seg_sd["to_budget"] is not None or np.isfinite(seg_sd["lev_budget"])) else "cost"
+                res = engine.solve_lowrank(qb3, lr3, split_settings(settings, opt.params, kind),
+                                           groups=stage.group_plan())
+                path = "l1-segments"
+                W[s - lo:e - lo] = l1seg.merge_batch(res.x, n, seg_sd["lb"]).cpu().numpy()
+                OBJ[s - lo:e - lo] = (res.obj + const).cpu().numpy()
+            elif l1both is not None:   # turnover + leverage: the per-asset-block IPM (porqua_amd/ipm_l1.py)
                 from .ipm_l1 import l1_ipm_batched, window_rows as l1_rows
                 UW, pdv = l1_rows(stage, scale, pdiag, Pm, n)
                 res = l1_ipm_batched(UW, pdv, q[:, :n].contiguous(), l1both, A=GhAb["A"], b=GhAb["b"],

@@ -366,3 +366,57 @@ def test_device_backtest_turnover_and_leverage_window_path():
         assert np.abs(W[i] - o.x[:n]).max() < 1e-6, (i, np.abs(W[i] - o.x[:n]).max())
         assert np.abs(W[i]).sum() <= 1.2 + 1e-7 and np.abs(W[i] - w0).sum() <= 0.5 + 1e-7
         assert abs(W[i].sum() - 1) < 1e-8 and W[i].min() > -0.02 - 1e-8 and W[i].max() < 0.05 + 1e-8
+
+
+@pytest.mark.gpu
+def test_device_backtest_turnover_and_leverage_segment_split():
+    """Turnover budget + leverage with a Pearson covariance (no ridge): the batched backtest
+    takes the segment split on the ADMM engine (porqua_amd/l1seg.py; window path over
+    [R, R, R], 3n = 300 > T + 3), 12 daily dates, long-short box, x0 with short positions;
+    three dates against the oracle IPM on the reference's linearised problem
+    (src/qp_problems.py:40-118).  n = 100 < T = 150: P = 2 Sigma is positive definite, so
+    the optimum is unique and the weights are compared."""
+    import pandas as pd
+    from oracle import ref_pipeline as rp
+    from oracle.qp_ipm import solve_qp
+    from porqua_amd.backtest import Backtest
+    from porqua_amd.builders import OptimizationItemBuilder
+    from porqua_amd.optimization import MeanVariance
+    from porqua_amd.qp_problems import QuadraticProgram
+    from porqua_amd.synthetic import factor_panel
+    n, D, width = 100, 180, 150
+    dates, R, yv, _ = factor_panel(D, n, seed=13)
+    idx = pd.DatetimeIndex(dates)
+    X = pd.DataFrame(R, index=idx, columns=[f"a{i}" for i in range(n)])
+    y = pd.DataFrame({"bm": yv}, index=idx)
+    rebdates = [str(d.date()) for d in idx[width + 5:width + 17]]
+    w0 = np.random.default_rng(4).dirichlet(np.ones(n)) * 1.3 - 0.3 / n
+    x0 = dict(zip(X.columns, w0))
+
+    def add_l1(bs, rebdate, **kw):
+        bs.optimization.constraints.add_l1("turnover", rhs=0.5, x0=x0)
+        bs.optimization.constraints.add_l1("leverage", rhs=1.25)
+
+    opt = MeanVariance(solver_name="mi355x", risk_aversion=1.0)
+    bs = _service(opt, X, y, rebdates, extra=OptimizationItemBuilder(bibfn=add_l1), width=width,
+                  box_kw={"box_type": "LongShort", "lower": -0.04, "upper": 0.08})
+    bs.settings["static_builders"] = True
+    bt = Backtest()
+    bt.run(bs)
+    assert bt.stats["path"] == "l1-segments" and bt.stats["solved"] == len(rebdates)
+    W = bt.strategy.get_weights_df().to_numpy(dtype=float)
+    for i in (0, 6, len(rebdates) - 1):
+        e = X.index.get_loc(pd.Timestamp(rebdates[i]))
+        Xw = R[e - width + 1:e + 1]
+        P, q = 2 * rp.cov_pearson(Xw), -rp.mean_geometric(Xw, None, None, None)
+        qp = QuadraticProgram(P=P, q=q, A=np.ones((1, n)), b=np.ones(1), G=None, h=None,
+                              lb=np.full(n, -0.04), ub=np.full(n, 0.08), params={"solver_name": "cvxopt"})
+        qp.linearize_turnover_constraint(w0, 0.5)
+        qp.linearize_leverage_constraint(N=n, leverage_budget=1.25)
+        o = solve_qp(qp["P"], qp["q"], G=qp["G"], h=qp["h"], A=qp["A"], b=qp["b"], lb=qp["lb"], ub=qp["ub"])
+        f = lambda x: 0.5 * x @ P @ x + q @ x                # noqa: E731
+        fo, fw = f(o.x[:n]), f(W[i])
+        assert abs(fw - fo) <= 1e-6 * max(abs(fo), 1e-6), (i, fw, fo)
+        assert np.abs(W[i] - o.x[:n]).max() < 1e-5, (i, np.abs(W[i] - o.x[:n]).max())
+        assert np.abs(W[i]).sum() <= 1.25 + 1e-7 and np.abs(W[i] - w0).sum() <= 0.5 + 1e-7
+        assert abs(W[i].sum() - 1) < 1e-8 and W[i].min() > -0.04 - 1e-8 and W[i].max() < 0.08 + 1e-8
