@@ -464,10 +464,14 @@ class Backtest:
             if lb is None or ub is None:
                 return False, None, None, None, None   # the split needs a box (serial path raises)
             split_panel = engine.Panel(torch.cat([panel.R, -panel.R], 1).contiguous(), None, device=dev)
-        # turnover + leverage: the segment split on the ADMM engine (porqua_amd/l1seg.py) when the
-        # box holds 0 and x0 and P has no ridge (checked per chunk); else the per-asset-block IPM
+        # turnover + leverage: the per-asset-block IPM by default; settings['l1_segments'] takes the
+        # segment split on the ADMM engine (porqua_amd/l1seg.py) when the box holds 0 and x0 and P
+        # has no ridge (checked per chunk).  Measured at the config-3 shape (turnover 0.5, leverage
+        # 1.3): the split's ADMM needs ~490 iterations (P is singular along s1 - s2 per asset), 1.4k
+        # QPs/s against the IPM's 2.1k (profiles/r05s_bench_l1_both_seg.log), so it is opt-in
         seg_sd, seg_panel, seg_mg = None, None, 0
-        if l1both is not None and lb is not None and ub is not None:
+        if (l1both is not None and lb is not None and ub is not None
+                and bs.settings.get("l1_segments", False)):
             from . import l1seg
             seg_sd = l1seg.segment_data(l1both.x0, lb, ub, cost=l1both.cost, to_budget=l1both.to_budget,
                                         lev_budget=l1both.lev_budget)

@@ -401,6 +401,7 @@ def test_device_backtest_turnover_and_leverage_segment_split():
     bs = _service(opt, X, y, rebdates, extra=OptimizationItemBuilder(bibfn=add_l1), width=width,
                   box_kw={"box_type": "LongShort", "lower": -0.04, "upper": 0.08})
     bs.settings["static_builders"] = True
+    bs.settings["l1_segments"] = True
     bt = Backtest()
     bt.run(bs)
     assert bt.stats["path"] == "l1-segments" and bt.stats["solved"] == len(rebdates)
