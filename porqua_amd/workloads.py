@@ -113,6 +113,11 @@ class MinVarianceBacktest:
             self.sf_rounds = max(2, int(res.out[:, engine._lib.PQ_OUT_ROUNDS].max().item()))
         return res
 
+    @property
+    def graph_replays(self) -> int:
+        """Stage graphs replayed so far (tests, diagnostics)."""
+        return self.graphs.replays if self.graphs is not None else 0
+
     def prepare(self):
         """Graph mode: the first (eager, cache-filling) step and the capturing step, outside
         any timed region -- afterwards every step replays the captured stages."""

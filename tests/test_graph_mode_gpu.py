@@ -23,7 +23,9 @@ def test_graph_mode_matches_host_driven_solve(device):
     assert graph.graphs is not None and len(graph.graphs.graphs) >= 4
     for _ in range(2):
         ev = []
+        n0 = graph.graph_replays
         r1 = graph.step(ev)
+        assert graph.graph_replays > n0
         torch.cuda.synchronize()
         assert {"moments", "factor", "admm", "polish"} <= {e[0] for e in ev}
         assert np.abs((r1.x - x0).cpu().numpy()).max() <= 1e-12

@@ -41,7 +41,7 @@ def solved(device, request):
     res = wl.step()
     torch.cuda.synchronize()
     if graph:
-        assert wl.graphs.replays > 0, "the checked step was not a graph replay"
+        assert wl.graph_replays > 0, "the checked step was not a graph replay"
     return wl, res
 
 
