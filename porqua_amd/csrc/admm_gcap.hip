@@ -136,11 +136,92 @@ __global__ __launch_bounds__(256) void k_gcap_assemble(pq_lowrank lr, pq_problem
 // MFMA GEMM over the group's dates (the ADMM's z' = M_U^-1 B loop) instead of a symv per date.
 // Then per date: mu'mu, a'q, H_b (m + 1 x m + 1) assembled in LDS, its Cholesky, and H_b^-1
 // column by column (lane t solves for column t, x in LDS).
+// ---- H_b^-1 for 16 < m + 1 <= 32 in one wave's registers: 2 x 2 blocks of 16 ----------------
+// Matrices in the MFMA C layout (lane (g4 = l >> 4, cc = l & 15), register q holds
+// X[g4 + 4q][cc]).  Register s of X is also the A operand slice s of X' and the B operand
+// slice s of X, so sum_s mfma(X[s], Y[s]) = X' Y; a transpose goes through the wave's own
+// 16 x 17 LDS tile (wave-local ordering, no workgroup barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void c_transpose(const double (&X)[4], double (&Xt)[4], double* tile) {
+  const int l = lane_id(), cc = l & 15, g4 = l >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tile[(g4 + 4 * q) * 17 + cc] = X[q];
+  wave_lds_sync();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Xt[q] = tile[cc * 17 + g4 + 4 * q];
+  wave_lds_sync();   // (the tile is reused by the next transpose)
+}
+// acc -/+= X' Y
+__device__ __forceinline__ f64x4 c_xty(const double (&X)[4], const double (&Y)[4], f64x4 acc) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[q], Y[q], acc, 0, 0, 0);
+  return acc;
+}
+// H (mh x mh, 16 < mh <= 32, identity padding to 32) given element-wise by h(i, j): H^-1 by
+// the blocked Cholesky  L = [[L1, 0], [L21, L2]],  L21 = H21 L1^-T,  L2 L2' = H22 - L21 L21',
+// L^-1 = [[W1, 0], [X21, W2]] with X21 = -W2 L21 W1, and H^-1 = L^-T L^-1:
+//   (H^-1)_11 = W1'W1 + X21'X21,  (H^-1)_21 = W2'X21,  (H^-1)_22 = W2'W2.
+// Two 16-step register chains (wave_chol_inv16) and 32 MFMAs instead of mh sweep steps
+// through LDS.  Writes the ldh x ldh output (zeros outside mh x mh); returns 1 (uniform) when
+// a pivot is not positive (nothing written).
+template <typename HF>
+__device__ __forceinline__ int wave_inv32(const HF& h, int mh, double* Hi, int ldh, double* tile) {
+  const int l = lane_id(), cc = l & 15, g4 = l >> 4;
+  double A[4], W1[4], h12[4], S[4], W2[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = g4 + 4 * q;
+    A[q] = h(r, cc);
+    W1[q] = r == cc ? 1.0 : 0.0;
+    h12[q] = 16 + cc < mh ? h(r, 16 + cc) : 0.0;                                  // H12 = H21'
+    S[q] = (16 + r < mh && 16 + cc < mh) ? h(16 + r, 16 + cc) : (r == cc ? 1.0 : 0.0);   // H22
+    W2[q] = r == cc ? 1.0 : 0.0;
+  }
+  if (wave_chol_inv16(A, W1)) return 1;
+  double W1t[4], L21[4], L21t[4];
+  c_transpose(W1, W1t, tile);
+  f64x4 acc = c_xty(h12, W1t, f64x4{0.0, 0.0, 0.0, 0.0});                            // L21 = H21 W1'
+#pragma unroll
+  for (int q = 0; q < 4; ++q) L21[q] = acc[q];
+  c_transpose(L21, L21t, tile);
+  acc = c_xty(L21t, L21t, f64x4{0.0, 0.0, 0.0, 0.0});                                // L21 L21'
+#pragma unroll
+  for (int q = 0; q < 4; ++q) S[q] -= acc[q];
+  if (wave_chol_inv16(S, W2)) return 1;
+  double T1[4], W2t[4], X21[4];
+  acc = c_xty(L21t, W1, f64x4{0.0, 0.0, 0.0, 0.0});                                  // T1 = L21 W1
+#pragma unroll
+  for (int q = 0; q < 4; ++q) T1[q] = acc[q];
+  c_transpose(W2, W2t, tile);
+  acc = c_xty(W2t, T1, f64x4{0.0, 0.0, 0.0, 0.0});                                   // W2 T1
+#pragma unroll
+  for (int q = 0; q < 4; ++q) X21[q] = -acc[q];
+  const f64x4 i11 = c_xty(X21, X21, c_xty(W1, W1, f64x4{0.0, 0.0, 0.0, 0.0}));
+  const f64x4 i21 = c_xty(W2, X21, f64x4{0.0, 0.0, 0.0, 0.0});
+  const f64x4 i22 = c_xty(W2, W2, f64x4{0.0, 0.0, 0.0, 0.0});
+  for (int e = l; e < ldh * ldh; e += 64)   // entries outside the mh x mh block
+    if (e / ldh >= mh || e % ldh >= mh) Hi[e] = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = g4 + 4 * q;
+    Hi[(int64_t)r * ldh + cc] = i11[q];
+    if (16 + r < mh) {
+      Hi[(int64_t)(16 + r) * ldh + cc] = i21[q];
+      Hi[(int64_t)cc * ldh + 16 + r] = i21[q];
+      if (16 + cc < mh) Hi[(int64_t)(16 + r) * ldh + 16 + cc] = i22[q];
+    }
+  }
+  return 0;
+}
+
 constexpr int PT_PREP = 512;    // 8 waves: a row of G_U / a GEMM tile / a date per wave; two
                                 // workgroups per CU (44 KB of LDS each) for 16-date groups: all
                                 // 475 groups of the config-3 batch in one round instead of two
 constexpr int PW_PREP = PT_PREP / 64;
-constexpr int HWP = 33;         // pitch of a wave's own H_b (16 < m + 1 <= 32, the 32-date groups)
 
 template <int NB>
 __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq_problem pb, pq_state st,
@@ -156,8 +237,7 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
   constexpr int HP = CH_MAX + 1;
   static_assert(CH_MAX * HP <= (CK_MAX + 16) * CG, "H_b does not fit in the a_b array");
   double* const H = s_a;
-  // waves that invert an H_b of 16 < m + 1 <= 32 in their own part of the array
-  constexpr int NWS = ((CK_MAX + 16) * CG / (33 * HWP)) < PW_PREP ? ((CK_MAX + 16) * CG / (33 * HWP)) : PW_PREP;
+  static_assert(PW_PREP * 16 * 17 <= (CK_MAX + 16) * CG, "the waves' transpose tiles do not fit");
   __shared__ double s_mm[CG], s_aq[CG], s_sr[CMGW];
   __shared__ int s_off[CG], s_T[CG];
   const int slot = xcd_slot(blockIdx.x, gridDim.x);
@@ -305,10 +385,21 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
   };
   // m + 1 <= 16 (the slide groups' usual case): one wave per date, H in registers (MFMA C
   // layout), Cholesky + L^-1 in one shuffle chain (wave_chol_inv16), H^-1 = L^-T L^-1 by four
-  // 16x16x4 MFMAs -- no LDS, no barriers
+  // 16x16x4 MFMAs -- no LDS, no barriers.  16 < m + 1 <= 32 (the outer dates of a 32-date
+  // group): the same in 2 x 2 blocks of 16 (wave_inv32; its transposes use the wave's own
+  // tile of the a_b array, free since the barrier above).  Formerly the symmetric sweep
+  // operator through LDS, mh steps of a lane-per-column loop with wave barriers
+  double* tile = s_a + w * (16 * 17);
   for (int gg = w; gg < G; gg += PW_PREP) {
     const int mh = U - s_T[gg] + 1;
-    if (mh > 16) continue;
+    const int b = d0 + gg;
+    if (mh > 32) continue;
+    if (mh > 16) {
+      auto hf = [&](int i, int j) -> double { return h_entry(gg, i, j); };
+      if (wave_inv32(hf, mh, gc.hinv + (int64_t)b * gc.ldh * gc.ldh, gc.ldh, tile) && l == 0)
+        st.status[b] = PQ_NON_CONVEX;   // not SPD to rounding: no group form for it
+      continue;
+    }
     const int cc = l & 15, g4 = l >> 4;
     double A[4], Bv[4];
 #pragma unroll
@@ -317,7 +408,6 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
       A[q] = (r < mh && cc < mh) ? h_entry(gg, r, cc) : (r == cc ? 1.0 : 0.0);
       Bv[q] = (r == cc) ? 1.0 : 0.0;
     }
-    const int b = d0 + gg;
     if (wave_chol_inv16(A, Bv)) {
       if (l == 0) st.status[b] = PQ_NON_CONVEX;   // not SPD to rounding: no group form for it
       continue;
@@ -332,67 +422,6 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
     for (int q = 0; q < 4; ++q) {
       const int r = g4 + 4 * q;
       if (r < mh && cc < mh) Hi[(int64_t)r * gc.ldh + cc] = hi[q];
-    }
-  }
-  // 16 < m + 1 <= 32 (the outer dates of a 32-date group): one wave per date, its H_b in its
-  // own part of the a_b array, inverted in place by the symmetric sweep operator (below) with
-  // no workgroup barrier -- a wave's LDS operations complete in order, and every lane loads its
-  // elements' old values before any lane stores
-  __syncthreads();   // the a_b array is free (GEMM done, a / q written, mu'mu and a'q in s_mm / s_aq)
-  if (w < NWS) {
-    double* Hw = s_a + w * 33 * HWP;   // H_b (32 x 32 at most, pitch HWP), then the pivot row's copy
-    double* rk = Hw + 32 * HWP;
-    for (int gg = w; gg < G; gg += NWS) {
-      const int mh = U - s_T[gg] + 1;
-      const int b = d0 + gg;
-      if (mh <= 16 || mh > 32) continue;
-      // lane j < mh owns column j of H: the pivot row is copied first, then every lane updates
-      // its own column row by row (no lane writes what another reads)
-      for (int e = l; e < mh * mh; e += 64) Hw[(e / mh) * HWP + e % mh] = h_entry(gg, e / mh, e % mh);
-      int bad = 0;
-      for (int k = 0; k < mh; ++k) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (l < mh) rk[l] = Hw[k * HWP + l];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const double dk = rk[k];
-        if (!(dk > 0.0) || !isfinite(dk)) {   // uniform over the wave
-          bad = 1;
-          break;
-        }
-        const double dinv = 1.0 / dk;
-        if (l < mh) {
-          const int j = l;
-          const double rkj = rk[j];
-          for (int i = 0; i < mh; ++i) {
-            const double rki = rk[i];   // (symmetric: a_ik = a_ki)
-            double v;
-            if (i == k) v = j == k ? -dinv : rkj * dinv;
-            else if (j == k) v = rki * dinv;
-            else v = fma(-rki * dinv, rkj, Hw[i * HWP + j]);
-            Hw[i * HWP + j] = v;
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (bad) {
-        if (l == 0) st.status[b] = PQ_NON_CONVEX;
-      } else {
-        double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
-        const int ldh = gc.ldh;
-        for (int e = l; e < ldh * ldh; e += 64) {
-          const int i = e / ldh, j = e % ldh;
-          Hi[e] = (i < mh && j < mh) ? -0.5 * (Hw[i * HWP + j] + Hw[j * HWP + i]) : 0.0;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   // m + 1 > 32 (monthly or sparser rebalancing: up to 63 union rows outside a window): the
