@@ -176,7 +176,7 @@ PQ_DEVFN int tile_chol_inv64(double* T, double* X, int nvalid) {
     __syncthreads();
     // trailing update A_ij -= L_ip L_jp' for p < j <= i (lower 16x16 tiles, round-robin over waves)
     const int m = 3 - p, ntr = m * (m + 1) / 2;
-    for (int tt = w; tt < ntr; tt += 4) {
+    for (int tt = w; w < 4 && tt < ntr; tt += 4) {   // (waves 4.. of k_factor_sk: no tiles)
       int ii = 0;
       while ((ii + 1) * (ii + 2) / 2 <= tt) ++ii;
       const int jj = tt - ii * (ii + 1) / 2;

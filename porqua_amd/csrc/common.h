@@ -47,8 +47,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
 // Row / column of accumulator element (m, n, r) inside the 64x64 tile for this lane.
+// (wave_id() & 3, threadIdx.x & 255 below: a 512-thread workgroup runs the tile GEMM as two
+// 256-thread teams, k_factor_sk; the identity for the 256-thread workgroups)
 __device__ __forceinline__ int acc_row(int m, int r) {
-  return (wave_id() >> 1) * 32 + m * 16 + (lane_id() >> 4) + 4 * r;
+  return ((wave_id() & 3) >> 1) * 32 + m * 16 + (lane_id() >> 4) + 4 * r;
 }
 __device__ __forceinline__ int acc_col(int n) {
   return (wave_id() & 1) * 32 + n * 16 + (lane_id() & 15);
@@ -58,7 +60,7 @@ __device__ __forceinline__ int acc_col(int n) {
 // SA[k][i] holds A[i][k]; SB[k][j] holds B[k][j]; both with pitch LDW.
 __device__ __forceinline__ void mma_lds(Acc& acc, const double* SA, const double* SB, int kdepth) {
   const int l = lane_id();
-  const int w = wave_id();
+  const int w = wave_id() & 3;
   const int i0 = (w >> 1) * 32 + (l & 15);
   const int j0 = (w & 1) * 32 + (l & 15);
   const int kr = l >> 4;
@@ -83,28 +85,28 @@ struct Stage4 {
 };
 
 __device__ __forceinline__ void load_ki(Stage4& s, const double* G, int64_t ld, int k0, int i0) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & (NTHR - 1);
   const int k = t >> 4, i = (t & 15) * 4;
   const double2* p = reinterpret_cast<const double2*>(G + (int64_t)(k0 + k) * ld + i0 + i);
   double2 a = p[0], b = p[1];
   s.v[0] = a.x; s.v[1] = a.y; s.v[2] = b.x; s.v[3] = b.y;
 }
 __device__ __forceinline__ void store_ki(const Stage4& s, double* S) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & (NTHR - 1);
   const int k = t >> 4, i = (t & 15) * 4;
   double2* p = reinterpret_cast<double2*>(S + k * LDW + i);
   p[0] = double2{s.v[0], s.v[1]};
   p[1] = double2{s.v[2], s.v[3]};
 }
 __device__ __forceinline__ void load_ik(Stage4& s, const double* G, int64_t ld, int k0, int i0) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & (NTHR - 1);
   const int i = t >> 2, k = (t & 3) * 4;
   const double2* p = reinterpret_cast<const double2*>(G + (int64_t)(i0 + i) * ld + k0 + k);
   double2 a = p[0], b = p[1];
   s.v[0] = a.x; s.v[1] = a.y; s.v[2] = b.x; s.v[3] = b.y;
 }
 __device__ __forceinline__ void store_ik(const Stage4& s, double* S) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & (NTHR - 1);
   const int i = t >> 2, k = (t & 3) * 4;
 #pragma unroll
   for (int e = 0; e < 4; ++e) S[(k + e) * LDW + i] = s.v[e];
