@@ -27,7 +27,7 @@
 //
 // Replaces qpsolvers.solve_problem (src/qp_problems.py:211-214) for the batched backtest,
 // like pq_admm_lr_grouped.
-#include "common.h"
+#include "chol_dev.h"   // (common.h; tile_chol_inv64 for the H_b of m + 1 > 32)
 #include "capi_util.h"
 
 namespace pq {
@@ -231,12 +231,11 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
   constexpr int CG = CG_MAX * NB;   // dates per group
   __shared__ int s_w[CU_MAX];
   // a_b: row u, column (date) g.  q_b = M_U^-1 a_b goes straight to its output rows (gc.aq),
-  // and the LDS inverses of H_b (m + 1 > 16) reuse this array once the GEMM is done:
-  // 44 KB of LDS per 16 dates instead of 151 KB
-  __shared__ __attribute__((aligned(16))) double s_a[(CK_MAX + 16) * CG];
-  constexpr int HP = CH_MAX + 1;
-  static_assert(CH_MAX * HP <= (CK_MAX + 16) * CG, "H_b does not fit in the a_b array");
-  double* const H = s_a;
+  // and the inversions of H_b (m + 1 > 16) reuse this array once the GEMM is done (at least
+  // the two 64 x 65 tiles of an H_b of m + 1 > 32 and its inverse factor: 65 KB of LDS per
+  // 16 dates, two workgroups per CU)
+  __shared__ __attribute__((aligned(16))) double s_a[(CK_MAX + 16) * CG > 2 * TB * DP ? (CK_MAX + 16) * CG : 2 * TB * DP];
+  static_assert(CH_MAX <= TB, "H_b larger than a 64 x 64 tile");
   static_assert(PW_PREP * 16 * 17 <= (CK_MAX + 16) * CG, "the waves' transpose tiles do not fit");
   __shared__ double s_mm[CG], s_aq[CG], s_sr[CMGW];
   __shared__ int s_off[CG], s_T[CG];
@@ -425,51 +424,46 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
     }
   }
   // m + 1 > 32 (monthly or sparser rebalancing: up to 63 union rows outside a window): the
-  // whole workgroup per date, H in LDS, inverted in place by the symmetric sweep operator --
-  // every pivot a_kk (a Schur-complement diagonal, > 0 for SPD H) turns row / column k into
-  // multipliers and updates the rest by a rank-1 term; after all pivots the array holds -H^-1.
-  // mh^3 FMAs over the 512 threads and two barriers per pivot, no global memory in the loop
-  // (the former column-by-column substitutions read the output column from global memory in
-  // their dependent inner loops: 1.5 ms for a 13-date monthly batch)
-  double* const rk = s_a + CH_MAX * HP;   // the pivot row (old values), beside H
-  static_assert(CH_MAX * HP + CH_MAX <= (CK_MAX + 16) * CG, "H_b and its pivot row do not fit");
+  // whole workgroup per date, H (identity padding to 64) in LDS, factored and inverted by
+  // tile_chol_inv64 (16-column register chains + MFMA panel / trailing / inverse tiles, as
+  // the factor's diagonal blocks), then H^-1 = L^-T L^-1 as ten 16 x 16 MFMA tiles over the
+  // waves.  Formerly the symmetric sweep operator: mh pivots of two barriers each (~110 us
+  // per date of a 13-date monthly batch)
+  double* const T64 = s_a;               // H, then L (pitch DP)
+  double* const X64 = s_a + TB * DP;     // X[c][r] = (L^-1)[r][c] (pitch DP)
   for (int gg = 0; gg < G; ++gg) {
     const int b = d0 + gg;
     const int mh = U - s_T[gg] + 1;
     if (mh <= 32) continue;   // uniform
     __syncthreads();
-    for (int e = t; e < mh * mh; e += PT_PREP) H[(e / mh) * HP + e % mh] = h_entry(gg, e / mh, e % mh);
-    int bad = 0;
-    for (int k = 0; k < mh; ++k) {
-      __syncthreads();
-      if (t < mh) rk[t] = H[k * HP + t];
-      __syncthreads();
-      const double dk = rk[k];
-      if (!(dk > 0.0) || !isfinite(dk)) {   // uniform: every thread reads the same pivot
-        bad = 1;
-        break;
-      }
-      const double dinv = 1.0 / dk;
-      for (int e = t; e < mh * mh; e += PT_PREP) {
-        const int i = e / mh, j = e - i * mh;
-        const double aik = rk[i] * dinv;   // (symmetric: a_ik = a_ki)
-        double v;
-        if (i == k) v = j == k ? -dinv : rk[j] * dinv;
-        else if (j == k) v = aik;
-        else v = fma(-aik, rk[j], H[i * HP + j]);
-        H[i * HP + j] = v;
-      }
+    for (int e = t; e < TB * TB; e += PT_PREP) {
+      const int i = e >> 6, j = e & 63;
+      T64[i * DP + j] = (i < mh && j < mh) ? h_entry(gg, i, j) : (i == j ? 1.0 : 0.0);
     }
-    if (bad) {
+    if (tile_chol_inv64(T64, X64, mh)) {   // (uniform; all threads, waves 4.. idle)
       if (t == 0) st.status[b] = PQ_NON_CONVEX;
       continue;
     }
-    __syncthreads();
+    // (H^-1)[i][j] = sum_r (L^-1)[r][i] (L^-1)[r][j] = sum_r X[i][r] X[j][r]: lower 16 x 16 tiles
     double* Hi = gc.hinv + (int64_t)b * gc.ldh * gc.ldh;
     const int ldh = gc.ldh;
-    for (int e = t; e < ldh * ldh; e += PT_PREP) {
-      const int i = e / ldh, j = e % ldh;
-      Hi[e] = (i < mh && j < mh) ? -0.5 * (H[i * HP + j] + H[j * HP + i]) : 0.0;   // (symmetrised)
+    const int cc = l & 15, g4 = l >> 4;
+    for (int tt = w; tt < 10; tt += PW_PREP) {
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= tt) ++I;
+      const int J = tt - I * (I + 1) / 2;
+      f64x4 acc = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+      for (int k0 = 0; k0 < TB; k0 += 4)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X64[(16 * I + cc) * DP + k0 + g4], X64[(16 * J + cc) * DP + k0 + g4],
+                                                  acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // element (16 I + g4 + 4q, 16 J + cc) and its mirror
+        const int i = 16 * I + g4 + 4 * q, j = 16 * J + cc;
+        const bool in = i < mh && j < mh;
+        if (i < ldh && j < ldh) Hi[(int64_t)i * ldh + j] = in ? acc[q] : 0.0;
+        if (I != J && i < ldh && j < ldh) Hi[(int64_t)j * ldh + i] = in ? acc[q] : 0.0;
+      }
     }
   }
 }
