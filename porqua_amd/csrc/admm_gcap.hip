@@ -227,7 +227,7 @@ template <int NB>
 __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq_problem pb, pq_state st,
                                                    pq_gcap gc, pq_settings s, const int32_t* idx,
                                                    const double* band, int64_t ldo, int r0, const double* pc,
-                                                   int64_t ldpc) {
+                                                   int64_t ldpc, int skip) {
   constexpr int CG = CG_MAX * NB;   // dates per group
   __shared__ int s_w[CU_MAX];
   // a_b: row u, column (date) g.  q_b = M_U^-1 a_b goes straight to its output rows (gc.aq),
@@ -236,6 +236,7 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
   // 16 dates, two workgroups per CU)
   __shared__ __attribute__((aligned(16))) double s_a[(CK_MAX + 16) * CG > 2 * TB * DP ? (CK_MAX + 16) * CG : 2 * TB * DP];
   static_assert(CH_MAX <= TB, "H_b larger than a 64 x 64 tile");
+  __shared__ double s_pref[PW_PREP * (CU_MAX + 64 + 1)];   // a wave's prefix sums of one G_U row
   static_assert(PW_PREP * 16 * 17 <= (CK_MAX + 16) * CG, "the waves' transpose tiles do not fit");
   __shared__ double s_mm[CG], s_aq[CG], s_sr[CMGW];
   __shared__ int s_off[CG], s_T[CG];
@@ -260,24 +261,39 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
   //      windows (lr.mu null, LeastSquares): no mean column, a_b = q_b = 0 and H_b's last
   //      row / column is the unit vector ------------------------------------------------------
   const bool centred = lr.mu != nullptr;
-  for (int u = w; centred && u < U; u += PW_PREP) {
+  // a_b[u] over the window [off_b, off_b + T_b) of the union is a difference of two prefix
+  // sums of G_U's row u: per row one wave scan of its U entries into the wave's own LDS row,
+  // then lane b (a date) reads its two prefixes -- instead of a masked wave reduction per
+  // (row, date): 32 of them per row, 75 % of this kernel (330 of 440 us at config 3).  (The
+  // prefix before a window sums at most its < 64 outside rows: the rounding is that of the
+  // direct sum's order of magnitude)
+  double* const Sw = s_pref + w * (CU_MAX + 64 + 1);
+  for (int u = w; centred && !(skip & 1) && u < U; u += PW_PREP) {
     double gv[CU_MAX / 64];
 #pragma unroll
     for (int j = 0; j < CU_MAX / 64; ++j) {
       const int v = l + 64 * j;
       gv[j] = v < U ? band_at(band, ldo, s_w[u], s_w[v]) : 0.0;
     }
-    for (int gg = 0; gg < G; ++gg) {
-      const int lo = s_off[gg], hi = lo + s_T[gg];
-      double sum = 0.0;
+    double run = 0.0;
 #pragma unroll
-      for (int j = 0; j < CU_MAX / 64; ++j) {
-        const int v = l + 64 * j;
-        if (v >= lo && v < hi) sum += gv[j];
+    for (int j = 0; j < CU_MAX / 64; ++j) {   // inclusive scan of each 64-entry block
+      double x = gv[j];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(x, o, 64);
+        if (l >= o) x += y;
       }
-      sum = wave_sum(sum);
-      if (l == 0) s_a[u * CG + gg] = g.sqc * sum / s_T[gg];
+      Sw[64 * j + l + 1] = run + x;          // Sw[v] = sum of the entries before v
+      run += readlane_f64(x, 63);
     }
+    if (l == 0) Sw[0] = 0.0;
+    wave_lds_sync();
+    if (l < G) {
+      const int lo = s_off[l], T = s_T[l];
+      s_a[u * CG + l] = g.sqc * (Sw[lo + T] - Sw[lo]) / T;
+    }
+    wave_lds_sync();   // (the next row overwrites Sw)
   }
   for (int e = w; centred && e < mg * G; e += PW_PREP) {   // general rows: sqrt(R_r) Cg_r mu_b = sqrt(R_r) (1/T) sum PC
     const int r = e / G, gg = e % G;
@@ -326,7 +342,7 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
     };
     double2 qa0[QT], qa1[QT];
     loadq(qa0, 0);
-    for (int k0 = 0; k0 < kU4; k0 += 16) {
+    for (int k0 = 0; !(skip & 2) && k0 < kU4; k0 += 16) {
       loadq(qa1, k0 + 8);
       mmaq(qa0, k0);
       loadq(qa0, k0 + 16);
@@ -389,7 +405,7 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
   // tile of the a_b array, free since the barrier above).  Formerly the symmetric sweep
   // operator through LDS, mh steps of a lane-per-column loop with wave barriers
   double* tile = s_a + w * (16 * 17);
-  for (int gg = w; gg < G; gg += PW_PREP) {
+  for (int gg = w; !(skip & 4) && gg < G; gg += PW_PREP) {
     const int mh = U - s_T[gg] + 1;
     const int b = d0 + gg;
     if (mh > 32) continue;
@@ -469,6 +485,9 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
 }
 
 // ---- the ADMM iterations -------------------------------------------------------------------
+#ifndef PQ_GCAP_SKIP1
+#define PQ_GCAP_SKIP1 1   // pass 1 skips the MFMAs of row tiles past the union (0: every tile multiplies)
+#endif
 // MGC: general rows compiled in (0 for box-only problems: no Cg registers in the epilogue;
 // CMGW: the wide form, up to 24 shared rows read column-sparse -- cg_nzr / cg_nzv, nzmax <= CNZ
 // nonzeros per asset, e.g. the budget plus one 0/1 sector membership -- instead of as
@@ -686,12 +705,13 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
       f64x4 c[CTP1N][NB];
       const double* arow[CTP1N];
       bool tv[CTP1N], aval[CTP1N];
+      const int wu = __builtin_amdgcn_readfirstlane(w);   // (tv: wave-uniform, a scalar branch)
 #pragma unroll
       for (int j = 0; j < CTP1N; ++j) {
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) c[j][nb] = f64x4{0.0, 0.0, 0.0, 0.0};
         const int u = (w + CNWN * j) * 16 + m0;
-        tv[j] = w + CNWN * j < ntile;
+        tv[j] = wu + CNWN * j < ntile;
         aval[j] = u < U + mg;
         arow[j] = u < U ? lr.panel + (int64_t)s_urow[u] * lr.ldp : pb.Cg + (int64_t)(u < U + mg ? u - U : 0) * ld;
       }
@@ -714,12 +734,16 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
         for (int j = 0; j < CTP1N; ++j) f.a[j] = *reinterpret_cast<const double2*>(arow[j] + kc);
       };
-      auto mma = [&](const Buf& f) {   // (no branch in the loop: every tile multiplies)
+      // tiles past ntile (wave-uniform) skip their MFMAs: 18 row tiles of a 284-row union over
+      // 8 waves leave two SIMDs 5 tiles and two 4 instead of 6 each (the loads stay
+      // unconditional, from clamped addresses)
+      auto mma = [&](const Buf& f) {
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
           const double bx = f.b[nb].x * f.bs[nb], by = f.b[nb].y * f.bs[nb];
 #pragma unroll
           for (int j = 0; j < CTP1N; ++j) {
+            if (PQ_GCAP_SKIP1 && !tv[j]) continue;
             c[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].x, bx, c[j][nb], 0, 0, 0);
             c[j][nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(f.a[j].y, by, c[j][nb], 0, 0, 0);
           }
@@ -1385,12 +1409,18 @@ extern "C" int pq_gcap_prepare(const pq_lowrank* lr, const pq_problem* pb, pq_st
   PQ_CHECK_ARG(gc->umax <= pq::CU_MAX && pb->mg <= pq::CMGW, "pq_gcap_prepare: union or general rows too many");
   const int grid = idx ? nidx : gc->ngroups;   // one workgroup per group (idx: group subset)
   if (grid <= 0) return 0;
+  // PQ_PREP_SKIP (timing experiments only; wrong results): bit 0 skips a_b, bit 1 the
+  // M_U^-1 A GEMM, bit 2 the per-date H_b^-1 of m + 1 <= 32
+  static const int skip = [] {
+    const char* e = getenv("PQ_PREP_SKIP");
+    return e ? atoi(e) : 0;
+  }();
   if (gcap_nb(gc) == 2)
     hipLaunchKernelGGL(pq::k_gcap_prep<2>, dim3(grid), dim3(pq::PT_PREP), 0, (hipStream_t)stream, *lr, *pb, *st, *gc,
-                       *s, idx, band, ldo, r0, pc, ldpc);
+                       *s, idx, band, ldo, r0, pc, ldpc, skip);
   else
     hipLaunchKernelGGL(pq::k_gcap_prep<1>, dim3(grid), dim3(pq::PT_PREP), 0, (hipStream_t)stream, *lr, *pb, *st, *gc,
-                       *s, idx, band, ldo, r0, pc, ldpc);
+                       *s, idx, band, ldo, r0, pc, ldpc, skip);
   PQ_CHECK_LAUNCH("pq_gcap_prepare");
   return 0;
 }
