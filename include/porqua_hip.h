@@ -408,7 +408,8 @@ int pq_polish_w_batched(const pq_lowrank* lr, const pq_problem* pb, pq_state* st
  * pass_scratch = ngroups * PQ_PG_PASS_SCRATCH doubles for their partial products.
  * Replaces, with pq_polish_w_batched, the accuracy of qpsolvers (src/qp_problems.py:211-214). */
 #define PQ_PG_RECORD 384
-#define PQ_PG_PASS_SCRATCH 20816   /* doubles per group: 4 x 324 x 16 + 4 x 16 + 16 */
+#define PQ_PG_PASS_SCRATCH 123537  /* doubles per group: 4 x 324 x 16 + 4 x 16 + 16 (window passes)
+                                      + 320 x 320 + 320 + 1 (the big group form's Gram)      */
 #define PQ_PG_PENDING 0
 #define PQ_PG_DONE 1
 #define PQ_PG_FALLBACK 2

@@ -26,7 +26,7 @@ PQ_DUAL_INFEASIBLE = -4
 PQ_NON_CONVEX = -5
 
 PQ_PG_RECORD = 384                   # doubles per problem of the grouped polish record
-PQ_PG_PASS_SCRATCH = 20816           # doubles per slide group of the split polish window passes
+PQ_PG_PASS_SCRATCH = 123537          # doubles per slide group of the split polish window passes
 PQ_PG_PENDING, PQ_PG_DONE, PQ_PG_FALLBACK, PQ_PG_SKIP = range(4)
 PQ_PG_STATE = 3                      # record field holding the state
 PQ_PG_K, PQ_PG_SC, PQ_PG_W = 0, 5, 320   # record fields: free count, problem scale, wide round

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(PT) void k_pg_init(pq_lowrank lr, pq_problem pb, pq
     R[R_REUSE] = 0;
   }
 #ifdef PQ_PROFILE
-  if (t >= 8 && t < 20) R[t] = 0.0;
+  if (t >= 8 && t < 32) R[t] = 0.0;
 #endif
 }
 
@@ -289,6 +289,16 @@ constexpr int GLD = PG_KMAX;
 constexpr int64_t GS_COL = (int64_t)GLD * GLD, GS_MU = GS_COL + GLD, GS_CS = GS_MU + GLD, GS_N = GS_CS + GLD;
 static_assert(GS_N + 1 <= PQ_PG_PASS_SCRATCH, "group form scratch exceeds the pass scratch");
 constexpr int GMO = 32;   // union rows outside a date's window (the per-date correction)
+// big group form (k_pg_form_grp_big, uncentred windows, free sets of PG_KMAX + 1 .. PG_KBIG):
+// the Gram of the group's union rows over the union of its forming dates' free lists (at most
+// KBG columns), pitch KBG, in the group's pass scratch after the window passes' region
+// (GB_OFF doubles: QSCR, checked below), with the union free list and its length beside it
+constexpr int KBG = 320;   // 16-date unions of config 2's free sets: 261 mean, 313 max (r05G_diag_union.log)
+constexpr int64_t GB_OFF = 20816;
+constexpr int64_t GB_COL = GB_OFF + (int64_t)KBG * KBG, GB_N = GB_COL + KBG, GB_END = GB_N + 1;
+static_assert(GB_END <= PQ_PG_PASS_SCRATCH, "big group form scratch exceeds the pass scratch");
+constexpr int GBS = 4;    // workgroups per group of the big Gram (its lower tiles split between them)
+constexpr int FKB = 8;    // union rows per staged chunk of the big Gram
 
 // P_FF of date b from its group's Gram G (centred by mu_g over the union rows U):
 //   sum_{t in W} (x_t - mu)(x_t - mu)' = G_FF - sum_{o in U \ W} x~_o x~_o'
@@ -403,14 +413,27 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
       return;
     }
   }
-  const int T = lr.tlen[b];
-  const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  // big free sets from the group Gram (k_pg_form_grp_big, uncentred windows): P_FF =
+  // G_FF - X_o,F' X_o,F over the union rows o outside the window (at most GMO), the same tile
+  // MFMAs over those rows instead of the window's T, the accumulators starting at -G_FF
+  const bool from_g = KF == PG_KBIG && R[R_GFORM] != 0.0;   // (uniform)
+  const int grp_g = from_g ? (int)R[R_GFORM] - 1 : 0;
+  const double* Gb = scr + (int64_t)grp_g * PQ_PG_PASS_SCRATCH;
+  const int Tw = lr.tlen[b];
+  const int T = from_g ? ucnt_all[grp_g] - Tw : Tw;   // rows accumulated
+  const double* mu = (lr.mu && !from_g) ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
   // the window's row indices in LDS: a gather's row address is then one LDS read away, not a
   // dependent global load
   __shared__ int s_rws[GMAXT];
   const int32_t* g_rws = lr.rows + (int64_t)b * lr.tmax;
-  const bool lds_rows = T <= GMAXT;   // (uniform; longer windows read the indices from memory)
-  for (int tt = t; lds_rows && tt < T; tt += FT) s_rws[tt] = g_rws[tt];
+  const bool lds_rows = from_g || T <= GMAXT;   // (uniform; longer windows read the indices from memory)
+  if (from_g) {   // the union rows outside [off, off + Tw)
+    const int off = uoff[b];
+    const int32_t* ur = urows_all + (int64_t)grp_g * umax;
+    for (int tt = t; tt < T; tt += FT) s_rws[tt] = ur[tt < off ? tt : tt + Tw];
+  } else {
+    for (int tt = t; lds_rows && tt < T; tt += FT) s_rws[tt] = g_rws[tt];
+  }
   __syncthreads();
   auto rws = [&](int tt) -> int { return lds_rows ? s_rws[tt] : g_rws[tt]; };
   const int nt = (k + 15) >> 4, ntile = nt * (nt + 1) / 2;
@@ -458,6 +481,30 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   f64x4 acc[FTWK];
 #pragma unroll
   for (int j = 0; j < FTWK; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+  if (from_g) {   // acc = -G_FF: the union position of each free variable, then the tiles' entries
+    __shared__ int s_gp[KF];
+    const int nc = (int)Gb[GB_N];
+    for (int p = t; p < k; p += FT) {   // (the union list is ascending)
+      const int i = wk.Fl[p];
+      int a = 0, z = nc;
+      while (z - a > 1) {
+        const int mid = (a + z) >> 1;
+        if ((int)Gb[GB_COL + mid] <= i) a = mid; else z = mid;
+      }
+      s_gp[p] = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FTWK; ++j) {
+      if (wu + FNW * j < ntile) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
+          acc[j][r] = (gi < k && gj < k) ? -Gb[GB_OFF + (int64_t)s_gp[gi] * KBG + s_gp[gj]] : 0.0;
+        }
+      }
+    }
+  }
   auto mma = [&](const double* Sb) {
 #pragma unroll
     for (int kk = 0; kk < FKCH; kk += 4) {
@@ -474,7 +521,7 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   put(S0);
   __syncthreads();
   int buf = 0;
-  for (int t0 = 0; t0 < T; t0 += FKCH) {
+  for (int t0 = 0; t0 < T; t0 += FKCH) {   // (T = 0, from the group Gram alone: no chunk)
     const bool more = t0 + FKCH < T;
     if (more) gather(t0 + FKCH);
     mma(buf ? S1 : S0);
@@ -493,7 +540,7 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
-        const double v = psw * acc[j][r] + (gi == gj ? pd : 0.0);
+        const double v = psw * (from_g ? -acc[j][r] : acc[j][r]) + (gi == gj ? pd : 0.0);
         K[(int64_t)gi * ldk + gj] = v;
         if (tI[j] != tJ[j]) K[(int64_t)gj * ldk + gi] = v;   // both triangles: column reads in the solve
       }
@@ -664,6 +711,163 @@ __global__ __launch_bounds__(FT) void k_pg_form_grp(pq_lowrank lr, pq_problem pb
   if (t < nc) Gs[GS_CS + t] = csum;
   if (t == 0) Gs[GS_N] = nc;
   if (t < G && s_on[t]) rec[(int64_t)(d0 + t) * PGR + R_GFORM] = grp + 1;   // the date's group, + 1
+}
+
+// ---------------------------------------------------------------------------------------
+// big group form: GBS workgroups per polish group with at least min_dates dates that form a
+// free set of PG_KMAX + 1 .. PG_KBIG this round on an uncentred window (the tracking
+// objectives: pending, not reusing K, at most GMO union rows outside the window).  Each merges
+// the dates' free lists in column order (identically) and, when the union stays within KBG
+// columns, computes its share of the lower 16 x 16 tiles of the union rows' Gram over it,
+// X_U,F' X_U,F, into the group's pass scratch (pitch KBG); k_pg_form<PG_KBIG> then forms each
+// date's P_FF = G_FF - X_o,F' X_o,F from it with its outside rows only (about U - T = 15 rows
+// instead of T = 252 per date and round).  Otherwise the dates keep R_GFORM = 0 and form alone.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(FT) void k_pg_form_grp_big(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                        const int32_t* gdates, const int32_t* urows_all,
+                                                        const int32_t* ucnt_all, int umax, double* scr,
+                                                        int min_dates) {
+  constexpr int FPB = KBG + 4;                               // LDS pitch (doubles)
+  constexpr int NTB = (KBG / 16) * (KBG / 16 + 1) / 2;        // lower tiles of a full union
+  constexpr int TPW = ((NTB + GBS - 1) / GBS + FNW - 1) / FNW;   // tiles per wave
+  constexpr int NCB = KBG / 64;                              // gathered columns per thread and row
+  static_assert(FT == 64 * FKB, "k_pg_form_grp_big: one staged row per wave");
+  __shared__ __attribute__((aligned(16))) double S[2 * FKB * FPB];
+  __shared__ int s_col[KBG], s_on[16], s_wcnt[FNW], s_ncol;
+  const int slot = xcd_slot(blockIdx.x, gridDim.x);   // the GBS parts of a group on one XCD (its L2)
+  const int grp = slot / GBS, part = slot - grp * GBS;
+  const int d0 = gdates[grp], G = gdates[grp + 1] - d0, U = ucnt_all[grp];
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int n = pb.n, ld = pb.ld;
+  if (lr.mu != nullptr) return;   // (uniform) centred windows: the small form's corrections only
+  if (t < 16) {
+    int on = 0;
+    if (t < G) {
+      const double* R = rec + (int64_t)(d0 + t) * PGR;
+      const int k = (int)R[R_K];
+      on = R[R_STATE] == PQ_PG_PENDING && R[R_W] == 0.0 && R[R_REUSE] == 0.0 && k > PG_KMAX && k <= PG_KBIG &&
+           U - lr.tlen[d0 + t] <= GMO;
+    }
+    s_on[t] = on;
+  }
+  if (t == 0) s_ncol = 0;
+  __syncthreads();
+  int non = 0;
+  for (int g = 0; g < G; ++g) non += s_on[g];
+  if (non < min_dates) return;   // uniform
+  // ---- union of the forming dates' free lists, in column order (as k_pg_form_grp) -----------
+  for (int cb = 0; cb < n; cb += FT) {
+    const int i = cb + t;
+    bool f = false;
+    {
+      int fv[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        PGWork wg(st, d0 + (g < G ? g : 0), ld);
+        fv[g] = wg.fl[i < n ? i : 0];
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) f |= g < G && s_on[g] && fv[g] == 0;
+      f = f && i < n;
+    }
+    const unsigned long long bal = __ballot(f);
+    if (l == 0) s_wcnt[w] = __popcll(bal);
+    __syncthreads();
+    int pos = s_ncol;
+    for (int ww = 0; ww < w; ++ww) pos += s_wcnt[ww];
+    pos += __popcll(bal & ((1ull << l) - 1ull));
+    if (f && pos < KBG) s_col[pos] = i;
+    __syncthreads();
+    if (t == 0)
+      for (int ww = 0; ww < FNW; ++ww) s_ncol += s_wcnt[ww];
+    __syncthreads();
+  }
+  const int nc = s_ncol;
+  if (nc > KBG) return;   // uniform: the dates form alone
+  __shared__ int ur[GMAXT];
+  for (int u = t; u < U && u < GMAXT; u += FT) ur[u] = urows_all[(int64_t)grp * umax + u];
+  __syncthreads();
+  const int nt = (nc + 15) >> 4, ntile = nt * (nt + 1) / 2;
+  const int kp = nt * 16;
+  const int q0 = (part * ntile) / GBS, q1 = ((part + 1) * ntile) / GBS;   // this part's tiles
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  int tI[TPW], tJ[TPW];
+  bool tv[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int q = q0 + wu + FNW * j;
+    tv[j] = q < q1;
+    int I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= q) ++I;
+    while (I * (I + 1) / 2 > q) --I;
+    tI[j] = I;
+    tJ[j] = q - I * (I + 1) / 2;
+  }
+  // gather map: wave w -> staged row w of a chunk, columns l + 64 c
+  int col[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const int p = l + 64 * c;
+    col[c] = p < nc ? s_col[p] : -1;
+  }
+  double v[NCB];
+  auto gather = [&](int t0) {   // unconditional loads from clamped addresses (as k_pg_form)
+    const int tt = t0 + w;
+    const double* row = lr.panel + (int64_t)ur[tt < U ? tt : 0] * lr.ldp;
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      const double x = row[col[c] >= 0 ? col[c] : 0];
+      v[c] = x * ((tt < U && col[c] >= 0) ? 1.0 : 0.0);
+    }
+  };
+  auto put = [&](double* Sb) {
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+      if (l + 64 * c < kp) Sb[w * FPB + l + 64 * c] = v[c];
+  };
+  f64x4 acc[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc[j] = f64x4{0.0, 0.0, 0.0, 0.0};
+  auto mma = [&](const double* Sb) {
+#pragma unroll
+    for (int kk = 0; kk < FKB; kk += 4) {
+      const double* r = Sb + (kk + (l >> 4)) * FPB + (l & 15);
+#pragma unroll
+      for (int j = 0; j < TPW; ++j)
+        if (tv[j]) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 * tI[j]], r[16 * tJ[j]], acc[j], 0, 0, 0);
+    }
+  };
+  double* S0 = S;
+  double* S1 = S + FKB * FPB;
+  gather(0);
+  put(S0);
+  __syncthreads();
+  int buf = 0;
+  for (int t0 = 0; t0 < U; t0 += FKB) {
+    const bool more = t0 + FKB < U;
+    if (more) gather(t0 + FKB);
+    mma(buf ? S1 : S0);
+    if (more) put(buf ? S0 : S1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  double* Gs = scr + (int64_t)grp * PQ_PG_PASS_SCRATCH;
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    if (tv[j]) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
+        Gs[GB_OFF + (int64_t)gi * KBG + gj] = acc[j][r];
+        if (tI[j] != tJ[j]) Gs[GB_OFF + (int64_t)gj * KBG + gi] = acc[j][r];
+      }
+    }
+  }
+  if (part == 0) {
+    for (int c = t; c < nc; c += FT) Gs[GB_COL + c] = s_col[c];
+    if (t == 0) Gs[GB_N] = nc;
+    if (t < G && s_on[t]) rec[(int64_t)(d0 + t) * PGR + R_GFORM] = grp + 1;   // the date's group, + 1
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1112,6 +1316,15 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
     }
     __syncthreads();
     const int nv = s_flag;
+#ifdef PQ_PROFILE
+    if (t == 0) {   // inner-step counters: solves, steps taken, violators, steps over WMA rows
+      R[20] += 1.0;
+      R[21] += (nv > 0 && nv < k) ? 1.0 : 0.0;
+      R[22] += (nv < k) ? (double)nv : 0.0;
+      R[23] += (nv > 0 && nv < k && ma + nv > WMA) ? 1.0 : 0.0;
+      R[24] += (double)k;
+    }
+#endif
     if (nv == 0 || nv == k) break;   // uniform: feasible, or nothing left free (the rounds decide)
     const int k2 = k - nv;
     for (int p = t; p < k2; p += T) {
@@ -1196,11 +1409,22 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
   double* Dt = st.Dt + (int64_t)b * st.Dt_stride;
   const int nbk = (k + TB - 1) / TB;
   const int kp = nbk * TB;
+#ifdef PQ_PROFILE
+  long long tb_last_ = wall_clock64();
+#define BSTAMP(k_)                                                         \
+  do {                                                                     \
+    __syncthreads();                                                       \
+    if (t == 0) { const long long n_ = wall_clock64(); R[25 + (k_)] += (double)(n_ - tb_last_); tb_last_ = n_; } \
+  } while (0)
+#else
+#define BSTAMP(k_) do { } while (0)
+#endif
   // P_FF (both triangles) and the reduced rhs rF = -q_F - p_scale (w_scale Xc'Xc x_B)_F come
   // from k_pg_form<PG_KBIG> on the same stream; FormW reads the diagonal 64 x 64 blocks in
   // full and the other originals from the upper half, which the factor leaves untouched
   const int info = wg_cholesky<false>(FormW{K, ldk, k, delta}, K, ldk, nbk, k, Dt, smem);
   if (t == 0) R[R_FORMED] = 0.0;   // the lower tiles now hold L: no reuse of this P_FF
+  BSTAMP(0);
   if (info) {
     if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
@@ -1221,7 +1445,9 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
   double* rl = dAv + WMA;
   double* wl = rl + WMA;
   int* s_al = reinterpret_cast<int*>(wl + WMA);
-  static_assert(5 * PG_KBIG + 6 * TB + 16 + WMA * WMA + 5 * WMA + WMA <= CHOL_LDS, "k_pg_big LDS layout");
+  constexpr int YC_OFF = 2048;   // the residual's per-wave column partials (PW x PG_KBIG)
+  static_assert(5 * PG_KBIG + 6 * TB + 16 + WMA * WMA + 5 * WMA + WMA <= YC_OFF &&
+                YC_OFF + PW * PG_KBIG <= CHOL_LDS, "k_pg_big LDS layout");
   __syncthreads();   // the factor is done with smem
   if (t < ma) {
     s_al[t] = (int)R[R_AL + t];
@@ -1270,19 +1496,50 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
   }
   for (int p = t; p < kp; p += PT) sx[p] = p < k ? wk.solx[p] : 0.0;
   __syncthreads();
+  BSTAMP(1);
   // ---- proximal iterative refinement (polish_w.hip, compact mode) ------------------------------
   for (int itr = 0; itr < s.refine_iters; ++itr) {
-    for (int p = w; p < k; p += PW) {   // rx = rF - P_FF x - C_aF' lam
-      double sum = 0.0;
-      for (int qq = l; qq < k; qq += 64) sum += pc_at(K, ldk, p, qq) * sx[qq];
-      sum = wave_sum(sum);
-      if (l == 0) {
-        double v = wk.rF[p] - sum;
-        for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + wk.Fl[p]] * lamv[a];
+    {   // rx = rF - P_FF x - C_aF' lam.  P_FF x in one coalesced pass over the stored originals
+        // (the diagonal 64-blocks in full, the off-diagonal blocks in the upper half): row i's
+        // entries give (P x)_i by a wave sum, and its upper off-diagonal entries also add
+        // K[i][j] x_i to (P x)_j in lane registers (column 64 c + lane), combined over the waves
+        // in LDS -- instead of reading the lower off-diagonal originals down the columns of the
+        // upper half (64 cache lines per load: 103 of 344 us per date-round, r05G_diag_union.log)
+      double* ycol = smem + YC_OFF;
+      double yc[PG_KBIG / 64];
+#pragma unroll
+      for (int c = 0; c < PG_KBIG / 64; ++c) yc[c] = 0.0;
+      for (int i = w; i < k; i += PW) {
+        const int bi = i >> 6;
+        const double xi = sx[i];
+        const double* Ki = K + (int64_t)i * ldk;
+        double sacc = 0.0;
+#pragma unroll
+        for (int c = 0; c < PG_KBIG / 64; ++c) {
+          if (c < bi || 64 * c >= k) continue;   // (wave-uniform)
+          const int j = 64 * c + l;
+          const double v = Ki[j < k ? j : i] * (j < k ? 1.0 : 0.0);   // (clamped, unconditional)
+          sacc = fma(v, sx[j], sacc);
+          if (c > bi) yc[c] = fma(v, xi, yc[c]);
+        }
+        sacc = wave_sum(sacc);
+        if (l == 0) rx[i] = sacc;
+      }
+#pragma unroll
+      for (int c = 0; c < PG_KBIG / 64; ++c) ycol[w * PG_KBIG + 64 * c + l] = yc[c];
+      __syncthreads();
+      for (int p = t; p < kp; p += PT) {
+        double v = 0.0;
+        if (p < k) {
+          double y = rx[p];
+#pragma unroll
+          for (int ww = 0; ww < PW; ++ww) y += ycol[ww * PG_KBIG + p];
+          v = wk.rF[p] - y;
+          for (int a = 0; a < ma; ++a) v -= Cg[(int64_t)s_al[a] * ld + wk.Fl[p]] * lamv[a];
+        }
         rx[p] = v;
       }
     }
-    for (int p = k + t; p < kp; p += PT) rx[p] = 0.0;
     for (int a = w; a < ma; a += PW) {   // rl = dA - C_aF x
       const double* c = Cg + (int64_t)s_al[a] * ld;
       double sum = 0.0;
@@ -1297,6 +1554,7 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
     double rm = 0.0;
     for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
     if (t < ma) rm = fmax(rm, fabs(rl[t]));
+    BSTAMP(2);
     if (block_max(rm, red) <= 1e-13 * sc) break;
     fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
     for (int a = w; a < ma; a += PW) {   // wl = U' t1 - rl
@@ -1329,6 +1587,7 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
     for (int p = t; p < k; p += PT) sx[p] += dx[p];
     if (t < ma) lamv[t] += wl[t];
     __syncthreads();
+    BSTAMP(3);
   }
   // ---- expand: xs = x_B off F, x_F on F; general multipliers by row ------------------------
   for (int ii = t; ii < n; ii += PT) wk.xs[ii] = wk.xb[ii];
@@ -1343,6 +1602,12 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
     R[R_LAM + s_al[t]] = lamv[t];
     R[R_SOL + t] = lamv[t];
   }
+  BSTAMP(4);
+  if (t == 0) {
+    R[30] += 1.0;
+    R[31] += (double)k;
+  }
+#undef BSTAMP
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1917,6 +2182,16 @@ static int group_form_min() {
   return v;
 }
 
+// the big group form (k_pg_form_grp_big) for groups with at least this many forming dates;
+// PQ_PG_GFORM_BIG overrides, 0 = off (A/B)
+static int group_form_big_min() {
+  static const int v = [] {
+    const char* e = getenv("PQ_PG_GFORM_BIG");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 // free sets beyond the LDS solve inside the pipeline (k_pg_big); PQ_PG_BIG=0 hands them to the
 // per-date kernel as before (A/B)
 static int pg_big() {
@@ -1967,7 +2242,7 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
                                        const int32_t* ucnt, const int32_t* uoff, int32_t umax, const pq_settings* s,
                                        double* pass_scratch, const pq_pg_wide* wide, void* stream) {
   PQ_CHECK_ARG(lr && pb && st && s && rec && pass_scratch, "pq_polish_grouped_round: null argument");
-  static_assert(pq::QSCR == PQ_PG_PASS_SCRATCH, "PQ_PG_PASS_SCRATCH out of date");
+  static_assert(pq::QSCR == pq::GB_OFF && pq::GB_END == PQ_PG_PASS_SCRATCH, "PQ_PG_PASS_SCRATCH out of date");
   PQ_CHECK_ARG(gdates && urows && ucnt && uoff && umax > 0 && umax <= pq::QU,
                "pq_polish_grouped_round: group plan missing (umax <= %d)", pq::QU);
   PQ_CHECK_ARG(pb->n % 2 == 0 && lr->ldp % 2 == 0, "pq_polish_grouped_round: needs even n and panel stride");
@@ -2012,6 +2287,9 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
   if (kbig > kmax) {   // free sets of kmax + 1 .. kbig: their P_FF, then the factor and solve
     static_assert(pq::PG_KBIG == 256, "k_pg_form<PG_KBIG> tiling");
     const hipStream_t sb = on(6);
+    if (pq::group_form_big_min() > 0 && lr->mu == nullptr)   // from one union Gram per polish group
+      hipLaunchKernelGGL(pq::k_pg_form_grp_big, dim3(ngroups * pq::GBS), dim3(pq::FT), 0, sb, *lr, *pb, *st, rec,
+                         gdates, urows, ucnt, umax, pass_scratch, pq::group_form_big_min());
     hipLaunchKernelGGL(pq::k_pg_form<pq::PG_KBIG>, dim3(B), dim3(pq::FT), 0, sb, *lr, *pb, *st, rec, ldk, gdates,
                        ngroups, urows, ucnt, uoff, umax, pass_scratch);
     hipLaunchKernelGGL(pq::k_pg_big, dim3(B), dim3(pq::PT), 0, sb, *lr, *pb, *st, rec, *s, ldk, kmax);

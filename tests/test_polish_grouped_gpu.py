@@ -140,6 +140,38 @@ def test_large_free_sets_are_solved_inside_the_pipeline(device):
     assert np.array_equal(outa[:, _lib.PQ_OUT_NFREE], k)
 
 
+def test_large_free_sets_from_the_group_gram(device):
+    """Uncentred windows with free sets of 129..256 (config 2's SPTR tracking on the usa-shaped
+    panel, 24 consecutive daily dates: about 190 of 494 assets free): the pipeline forms each
+    date's P_FF from one Gram of its polish group's union rows over the union of the group's
+    free lists minus the date's outside rows (k_pg_form_grp_big + k_pg_form<256>) instead of
+    from its whole window, and gives the per-date kernel's answers to rounding."""
+    import dataclasses
+    from tests.conftest import load_golden
+    from porqua_amd.workloads import ReplicationBacktest
+    g = load_golden("sptr")
+    wl = ReplicationBacktest(g["days"], g["returns"], n_rows=252 + 23, device=device)
+    xty, _ = wl.pan.gram_xy(wl.rows_d, wl.tlen_d)
+    torch.mul(xty, -2.0, out=wl.qb.q)
+    qb, lr, gp = wl.qb, wl.lr, wl.gplan
+    xa, sa, oa, ya, za, outa, _ = _solve(qb, lr, gp, False, settings=wl.settings)
+    st = dataclasses.replace(wl.settings, eps_grouped=0.0, polish_fix_rel=0.0, polish_inner=0)
+    ws = engine.Workspace(qb, dense=False)
+    res = engine.solve_lowrank(qb, lr, st, ws=ws, groups=gp, grouped_polish=True, wide_polish=False)
+    torch.cuda.synchronize()
+    rec = ws.pg_record().cpu().numpy()
+    xb, sb, ob, outb = (res.x.cpu().numpy(), res.status.cpu().numpy(), res.obj.cpu().numpy(),
+                        res.out.cpu().numpy())
+    assert np.all(sa == _lib.PQ_SOLVED) and np.array_equal(sa, sb)
+    k = outb[:, _lib.PQ_OUT_NFREE]
+    assert ((k > 128) & (k <= 256)).mean() >= 0.5, k
+    assert np.all(rec[:, _lib.PQ_PG_STATE] == _lib.PQ_PG_DONE)
+    assert (rec[:, 348] > 0).any()   # R_GFORM: some date's last round formed from its group's Gram
+    assert np.abs(xa - xb).max() <= 1e-10, np.abs(xa - xb).max()
+    assert np.abs(oa - ob).max() <= 1e-12 * max(1.0, np.abs(oa).max()) + 1e-15
+    assert np.array_equal(outa[:, _lib.PQ_OUT_NFREE], k)
+
+
 def test_loose_admm_stop_before_the_pipeline(device):
     """Settings.eps_grouped (centred windows, default 0.3 with at least min_iter_grouped iterations): the ADMM stops early and the
     pipeline's rounds finish the job -- the same optimum as from the eps_abs point, fewer

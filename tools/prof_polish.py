@@ -87,6 +87,15 @@ def main():
         pp = ws.pg_record()[:, 16:19].cpu().numpy() * 10e-3
         for i, nm in enumerate(["potrf: diag chain (+ deferred MFMA update)", "potrf: panel trsm", "potrf: (unused)"]):
             print("  %-20s %8.1f us" % (nm, pp[:, i].mean()))
+        bb = ws.pg_record()[:, 25:32].cpu().numpy()
+        nb = max(bb[:, 5].sum(), 1)
+        print("  k_pg_big: %d date-rounds, mean k %.1f; us per date-round:" % (bb[:, 5].sum(), bb[:, 6].sum() / nb))
+        for i, nm in enumerate(["factor (wg_cholesky)", "U + S", "residual", "solves + update", "expand"]):
+            print("    %-22s %8.1f us" % (nm, bb[:, i].sum() * 10e-3 / nb))
+        ic = ws.pg_record()[:, 20:25].cpu().numpy()
+        print("  inner steps: solve calls %.0f, steps taken %.0f, violators per step %.2f, steps with ma + nv > 8: %.0f,"
+              " mean k at the check %.1f" % (ic[:, 0].sum(), ic[:, 1].sum(), ic[:, 2].sum() / max(ic[:, 1].sum(), 1),
+                                             ic[:, 3].sum(), ic[:, 4].sum() / max(ic[:, 0].sum(), 1)))
     for name, a, b in ev:
         print("stage", name, "%.1f ms" % a.elapsed_time(b))
     out = res.out.cpu().numpy()
