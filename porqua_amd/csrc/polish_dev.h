@@ -138,8 +138,14 @@ __device__ void fwd_solve(const double* K, int64_t ld, const double* Dt, int nbk
     for (int i0 = 4 * w; i0 < TB; i0 += 4 * PW) {
       const int i = i0 + g4;
       const double* row = K + (int64_t)(I * TB + i) * ld;
-      double s = 0.0;
-      for (int c = c16; c < I * TB; c += 16) s = fma(row[c], y[c], s);
+      double s = 0.0, s2 = 0.0;   // (two chains; the loop unrolled so its loads issue together)
+#pragma unroll 4
+      for (int c = c16; c < I * TB; c += 32) {
+        const bool in2 = c + 16 < I * TB;   // (clamped, unconditional second load)
+        s = fma(row[c], y[c], s);
+        s2 = fma(row[in2 ? c + 16 : c], in2 ? y[c + 16] : 0.0, s2);
+      }
+      s += s2;
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
       if (c16 == 0) t64[i] = r[I * TB + i] - s;
@@ -165,9 +171,14 @@ __device__ void bwd_solve(const double* K, int64_t ld, const double* Dt, int nbk
   const int t = threadIdx.x, w = wave_id(), l = lane_id();
   for (int I = nbk - 1; I >= 0; --I) {
     // t_I = y_I - sum_{r >= 64(I+1)} L[r][64I + i] x[r]   (lanes over i, waves split r)
-    double s = 0.0;
-    for (int r = (I + 1) * TB + w; r < nbk * TB; r += PW) s += K[(int64_t)r * ld + I * TB + l] * x[r];
-    part[w * TB + l] = s;
+    double s = 0.0, s2 = 0.0;   // (two chains; unrolled so the row loads issue together)
+#pragma unroll 4
+    for (int r = (I + 1) * TB + w; r < nbk * TB; r += 2 * PW) {
+      const bool in2 = r + PW < nbk * TB;   // (clamped, unconditional second load)
+      s = fma(K[(int64_t)r * ld + I * TB + l], x[r], s);
+      s2 = fma(K[(int64_t)(in2 ? r + PW : r) * ld + I * TB + l], in2 ? x[r + PW] : 0.0, s2);
+    }
+    part[w * TB + l] = s + s2;
     __syncthreads();
     if (t < TB) t64[t] = y[I * TB + t] - (part[t] + part[TB + t] + part[2 * TB + t] + part[3 * TB + t]);
     __syncthreads();

@@ -1509,21 +1509,42 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
       double yc[PG_KBIG / 64];
 #pragma unroll
       for (int c = 0; c < PG_KBIG / 64; ++c) yc[c] = 0.0;
-      for (int i = w; i < k; i += PW) {
-        const int bi = i >> 6;
-        const double xi = sx[i];
-        const double* Ki = K + (int64_t)i * ldk;
-        double sacc = 0.0;
+      // RU rows per wave in flight: all their loads unconditional from clamped addresses (a
+      // load under a branch makes the compiler wait for every outstanding load at the join),
+      // the entries outside the stored part zeroed by a factor after the load
+      constexpr int RU = 4;
+      constexpr int NCB = PG_KBIG / 64;
+      for (int i0 = w; i0 < k; i0 += RU * PW) {
+        double sacc[RU], xv[RU], kv[RU][NCB];
 #pragma unroll
-        for (int c = 0; c < PG_KBIG / 64; ++c) {
-          if (c < bi || 64 * c >= k) continue;   // (wave-uniform)
-          const int j = 64 * c + l;
-          const double v = Ki[j < k ? j : i] * (j < k ? 1.0 : 0.0);   // (clamped, unconditional)
-          sacc = fma(v, sx[j], sacc);
-          if (c > bi) yc[c] = fma(v, xi, yc[c]);
+        for (int u = 0; u < RU; ++u) {
+          const int i = i0 + u * PW, ic = i < k ? i : k - 1;
+          xv[u] = sx[ic];
+          const double* Ki = K + (int64_t)ic * ldk;
+#pragma unroll
+          for (int c = 0; c < NCB; ++c) {
+            const int j = 64 * c + l;
+            kv[u][c] = Ki[j < k ? j : ic];
+          }
         }
-        sacc = wave_sum(sacc);
-        if (l == 0) rx[i] = sacc;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const int i = i0 + u * PW, bi = i >> 6;
+          const bool iv = i < k;
+          sacc[u] = 0.0;
+#pragma unroll
+          for (int c = 0; c < NCB; ++c) {
+            const int j = 64 * c + l;
+            const double v = kv[u][c] * ((iv && c >= bi && j < k) ? 1.0 : 0.0);
+            sacc[u] = fma(v, sx[j < kp ? j : 0], sacc[u]);
+            yc[c] = fma(v * (c > bi ? 1.0 : 0.0), xv[u], yc[c]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+          const double v = wave_sum(sacc[u]);
+          if (l == 0 && i0 + u * PW < k) rx[i0 + u * PW] = v;
+        }
       }
 #pragma unroll
       for (int c = 0; c < PG_KBIG / 64; ++c) ycol[w * PG_KBIG + 64 * c + l] = yc[c];
