@@ -537,11 +537,15 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
 #pragma unroll
   for (int j = 0; j < FTWK; ++j) {
     if (wu + FNW * j < ntile) {
+      // k_pg_big (KF = PG_KBIG) reads the diagonal 64-blocks in full and the off-diagonal
+      // originals from the upper half only (its factor overwrites the lower off-diagonal
+      // blocks with L): those lower writes are skipped
+      const bool lower = KF != PG_KBIG || (tI[j] >> 2) == (tJ[j] >> 2);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gi = 16 * tI[j] + (l >> 4) + 4 * r, gj = 16 * tJ[j] + (l & 15);
         const double v = psw * (from_g ? -acc[j][r] : acc[j][r]) + (gi == gj ? pd : 0.0);
-        K[(int64_t)gi * ldk + gj] = v;
+        if (lower) K[(int64_t)gi * ldk + gj] = v;
         if (tI[j] != tJ[j]) K[(int64_t)gj * ldk + gi] = v;   // both triangles: column reads in the solve
       }
     }

@@ -116,6 +116,15 @@ class Settings:
     # 3.1 / 3.5 / 4.0 rounds): the tracking rounds (free sets of 160..220) cost more than the
     # ADMM iterations they replace
     eps_grouped_tracking: float = 0.0
+    # (host-side) small batches of tracking windows (at most small_batch dates, e.g. the
+    # reference notebook's 13-date monthly run) take the loose stop at this eps when
+    # eps_grouped_tracking is 0: there the GPU runs a handful of slide groups, so an ADMM
+    # iteration costs one group's latency while a polish round stays cheap.  Measured on the
+    # 13-date monthly run (profiles/r05N_monthly_grid.log): off / 3e-3 / 1e-2 / 3e-2 / 0.1 / 0.3
+    # -> 10.3 / 10.4 / 9.5 / 9.6 / 10.0 / 9.5 ms, the same weights to 4e-11.  Off with
+    # eps_grouped = 0 (no loose stop at all)
+    eps_grouped_tracking_small: float = 1e-2
+    small_batch: int = 64
     # (host-side) the loose stop also on the per-problem capacitance (grouped ADMM without the
     # group capacitance: the lambda sweep, whose problems of a date differ in P's scale)
     eps_grouped_percap: bool = False
@@ -1175,6 +1184,8 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     SS_admm = SS
     st_ = settings or Settings()
     eps_loose = st_.eps_grouped if lr.mu is not None else st_.eps_grouped_tracking
+    if lr.mu is None and eps_loose <= 0.0 and st_.eps_grouped > 0.0 and qb.batch <= st_.small_batch:
+        eps_loose = st_.eps_grouped_tracking_small   # (eps_grouped = 0: every loose stop off)
     if ((gc is not None or (st_.eps_grouped_percap and grouped and eig is None)) and polish and s.polish
             and grouped_polish and ldk >= 64 and eps_loose > max(st_.eps_abs, st_.eps_rel)):
         sl = st_.to_c()
