@@ -114,25 +114,16 @@ __global__ __launch_bounds__(256) void k_gcap_assemble(pq_lowrank lr, pq_problem
   __syncthreads();
   const double a1 = g.c / g.d, a2 = g.sqc / g.d;
   double* M = gc.M + (int64_t)grp * gc.M_stride;
-  // row i per wave (uniform), columns over the lanes: every load unconditional from a clamped
-  // address and the block chosen afterwards (a load under a lane-varying branch made the
-  // compiler wait for every outstanding load at the join, once per column step)
   for (int i = w; i < k_ld; i += 4) {
     const int jend = (i / TB + 1) * TB;
     const bool icg = i >= U && i < U + mg;
-    const int ic = i < U ? i : U - 1, ig = icg ? i - U : 0;
     for (int j = l; j < jend; j += 64) {
-      const bool jcg = j >= U && j < U + mg;
-      const int jc = j < U ? j : U - 1, jg = jcg ? j - U : 0;
-      const double bv = band_at(band, ldo, s_w[ic], s_w[jc]);
-      const double pi = mg ? pc[(int64_t)s_w[jc] * ldpc + ig] : 0.0;   // (mg: uniform)
-      const double pj = mg ? pc[(int64_t)s_w[ic] * ldpc + jg] : 0.0;
-      const double cv = mg ? cc[ig * mg + jg] : 0.0;
       double v = (i == j) ? 1.0 : 0.0;
-      if (i < U && j < U) v += a1 * bv;
-      else if (icg && j < U) v += a2 * s_sr[ig] * pi;
-      else if (i < U && jcg) v += a2 * s_sr[jg] * pj;
-      else if (icg && jcg) v += s_sr[ig] * s_sr[jg] / g.d * cv;
+      const bool jcg = j >= U && j < U + mg;
+      if (i < U && j < U) v += a1 * band_at(band, ldo, s_w[i], s_w[j]);
+      else if (icg && j < U) v += a2 * s_sr[i - U] * pc[(int64_t)s_w[j] * ldpc + (i - U)];
+      else if (i < U && jcg) v += a2 * s_sr[j - U] * pc[(int64_t)s_w[i] * ldpc + (j - U)];
+      else if (icg && jcg) v += s_sr[i - U] * s_sr[j - U] / g.d * cc[(i - U) * mg + (j - U)];
       M[(int64_t)i * k_ld + j] = v;
     }
   }
