@@ -917,6 +917,19 @@ def _pg_wide_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPl
     return buf["wide"]
 
 
+def loose_stop_eps(settings: Settings, centred: bool, batch: int) -> float:
+    """The eps of the loose ADMM stop before the grouped polish (0: none): eps_grouped for
+    centred windows, eps_grouped_tracking for uncentred ones, and eps_grouped_tracking_small
+    for uncentred batches of at most small_batch dates when eps_grouped_tracking is 0.
+    eps_grouped = 0 turns every loose stop off."""
+    if centred:
+        return settings.eps_grouped
+    eps = settings.eps_grouped_tracking
+    if eps <= 0.0 and settings.eps_grouped > 0.0 and batch <= settings.small_batch:
+        eps = settings.eps_grouped_tracking_small
+    return eps
+
+
 def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   ws: Workspace | None = None, max_rounds: int = 64, events: list | None = None,
                   polish: bool = True, groups: "GroupPlan | None" = None, band: bool = True,
@@ -1183,9 +1196,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     SS_main = SS
     SS_admm = SS
     st_ = settings or Settings()
-    eps_loose = st_.eps_grouped if lr.mu is not None else st_.eps_grouped_tracking
-    if lr.mu is None and eps_loose <= 0.0 and st_.eps_grouped > 0.0 and qb.batch <= st_.small_batch:
-        eps_loose = st_.eps_grouped_tracking_small   # (eps_grouped = 0: every loose stop off)
+    eps_loose = loose_stop_eps(st_, lr.mu is not None, qb.batch)
     if ((gc is not None or (st_.eps_grouped_percap and grouped and eig is None)) and polish and s.polish
             and grouped_polish and ldk >= 64 and eps_loose > max(st_.eps_abs, st_.eps_rel)):
         sl = st_.to_c()

@@ -432,3 +432,20 @@ def test_panel_upload_resolves_the_device_on_the_calling_thread(monkeypatch):
     out = up.result()
     assert seen == [threading.current_thread()]
     assert out.device.type == "cpu" and np.array_equal(out.numpy(), frame.to_numpy())
+
+
+def test_loose_stop_eps_rule():
+    """engine.loose_stop_eps: centred windows take eps_grouped; tracking windows take
+    eps_grouped_tracking, or eps_grouped_tracking_small for batches of at most small_batch
+    dates (the notebook's monthly run); eps_grouped = 0 turns every loose stop off."""
+    from porqua_amd import engine
+    s = engine.Settings()
+    assert engine.loose_stop_eps(s, True, 4749) == s.eps_grouped
+    assert engine.loose_stop_eps(s, False, 4544) == 0.0
+    assert engine.loose_stop_eps(s, False, 13) == s.eps_grouped_tracking_small > 0.0
+    assert engine.loose_stop_eps(s, False, s.small_batch) == s.eps_grouped_tracking_small
+    assert engine.loose_stop_eps(s, False, s.small_batch + 1) == 0.0
+    off = engine.Settings(eps_grouped=0.0)
+    assert engine.loose_stop_eps(off, False, 13) == 0.0 and engine.loose_stop_eps(off, True, 13) == 0.0
+    own = engine.Settings(eps_grouped_tracking=3e-2)
+    assert engine.loose_stop_eps(own, False, 13) == 3e-2 and engine.loose_stop_eps(own, False, 4544) == 3e-2
