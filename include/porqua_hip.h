@@ -336,7 +336,7 @@ typedef struct pq_gcap {
   double* hinv; int32_t ldh;                                   /* per date: ldh x ldh      */
   int32_t gmax;                 /* dates in the largest group: 0..16 -> 16-date kernels;
                                    17..32 -> the 32-date form (one 512-thread workgroup per
-                                   group; pq_admm_lr_gcap then needs mg <= 4)              */
+                                   group; register-resident or column-sparse general rows) */
 } pq_gcap;
 int pq_gcap_assemble(const pq_lowrank* lr, const pq_problem* pb, const pq_gcap* gc, const pq_settings* s,
                      const double* band, int64_t ldo, int32_t r0, const double* pc, int64_t ldpc,

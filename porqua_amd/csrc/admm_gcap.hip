@@ -503,7 +503,8 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
                                                   int r0, const double* cc, const int32_t* cg_nzr,
                                                   const double* cg_nzv, int nzmax) {
   constexpr bool WIDE = MGC > CMG;
-  static_assert(NB == 1 || (NB == 2 && !WIDE), "k_admm_gcap: 32-date groups for mg <= 4 only");
+  // (NB = 2 with the wide form fits the CU's 160 KiB of LDS with g_part indexed by the date
+  // within its wave's column block: each wave only ever writes its own block's 16 dates)
   constexpr int MGG = WIDE ? CMGW : 8;
   constexpr int CTN = CT * NB, CNWN = CTN / 64, CHWN = CTN / 32;   // threads, waves, half-waves
   constexpr int CG = CG_MAX * NB;                                   // dates per group
@@ -515,7 +516,7 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
   __shared__ double g_muv[CG], g_su[CG], g_dinv[CG], g_rn[CG], g_qmax[CG], g_coef[CG];
   __shared__ double g_y[CG * CH_MAX];   // y_b = H_b^-1 s_b of every date
   constexpr int NPART = 5;                    // per wave and date: 4 maxima, mu.V
-  __shared__ double g_part[CNWN * CG * NPART];
+  __shared__ double g_part[CNWN * CG_MAX * NPART];   // (wave, date of its column block, slot)
   __shared__ double g_gm[CG * 3];
   // per (date, row); the rows' bounds and rho are shared by the group's dates
   __shared__ double g_zg[CG * MGG], g_yg[CG * MGG], g_cgv[CG * MGG], g_cgx[CG * MGG],
@@ -1256,7 +1257,7 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         const int m = 16 * cb + kq + 4 * r;
         if (ia == 0) {
-          double* pp = g_part + (w * CG + m) * NPART;
+          double* pp = g_part + (w * CG_MAX + (m - 16 * cb)) * NPART;
 #pragma unroll
           for (int e = 0; e < 4; ++e) pp[e] = mv[r][e];
           pp[4] = muv[r];
@@ -1272,7 +1273,7 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
       double mv[7] = {g_gm[g * 3], fmax(g_gm[g * 3 + 1], g_gm[g * 3 + 2]), 0.0, 0.0, 0.0, 0.0, g_qmax[g]};
       double muv = 0.0;
       for (int ww = (g / 16) * CNW; ww < (g / 16 + 1) * CNW; ++ww) {   // the waves of g's column block
-        const double* pp = g_part + (ww * CG + g) * NPART;
+        const double* pp = g_part + (ww * CG_MAX + (g & 15)) * NPART;
         mv[0] = fmax(mv[0], pp[0]);
         mv[1] = fmax(mv[1], pp[1]);
         mv[3] = fmax(mv[3], pp[2]);
@@ -1443,8 +1444,7 @@ extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_st
                pq::CNZ);
   const dim3 grid(gc->ngroups);
   const hipStream_t str = (hipStream_t)stream;
-  if (gcap_nb(gc) == 2) {   // 32-date groups: the register-resident general-row forms only
-    PQ_CHECK_ARG(pb->mg <= pq::CMG, "pq_admm_lr_gcap: groups of more than 16 dates need mg <= %d", pq::CMG);
+  if (gcap_nb(gc) == 2) {   // 32-date groups (one 512-thread workgroup per group)
     const dim3 blk(pq::CT * 2);
     if (pb->mg == 0)
       hipLaunchKernelGGL((pq::k_admm_gcap<0, 2>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc, ldpc,
@@ -1452,9 +1452,12 @@ extern "C" int pq_admm_lr_gcap(const pq_lowrank* lr, const pq_problem* pb, pq_st
     else if (pb->mg == 1)
       hipLaunchKernelGGL((pq::k_admm_gcap<1, 2>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc, ldpc,
                          r0, cc, nullptr, nullptr, 0);
-    else
+    else if (pb->mg <= pq::CMG)
       hipLaunchKernelGGL((pq::k_admm_gcap<pq::CMG, 2>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc,
                          ldpc, r0, cc, nullptr, nullptr, 0);
+    else   // budget + sector caps, column-sparse (config 4): the union streamed once for 32 dates
+      hipLaunchKernelGGL((pq::k_admm_gcap<pq::CMGW, 2>), grid, blk, 0, str, *lr, *pb, *st, *gc, *s, iters_this_call, pc,
+                         ldpc, r0, cc, cg_nzr, cg_nzv, nzmax);
   } else {
     const dim3 blk(pq::CT);
     if (pb->mg == 0)

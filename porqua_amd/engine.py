@@ -1012,10 +1012,11 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     gcap_try = (gcap and eig is None and grouped and fuse and qb.shared
                 and (qb.mg <= 4 or (qb.mg <= 24 and sparse_cols[2] > 0))
                 and groups.ucnt_max + qb.mg <= 320 and groups.corr_max <= 64)
-    # the group capacitance's own plan: up to 32 dates per group for register-resident general
-    # rows (GroupPlan.gcap_plan); the polish keeps its 16-date groups (polish_plan)
+    # the group capacitance's own plan: up to 32 dates per group (GroupPlan.gcap_plan), for
+    # register-resident general rows and (GCAP32_WIDE) the column-sparse wide form; the polish
+    # keeps its 16-date groups (polish_plan)
     gplan = groups
-    if gcap_try and qb.mg <= 4:
+    if gcap_try and (qb.mg <= 4 or GCAP32_WIDE):
         g32 = groups.gcap_plan()
         if g32.ucnt_max + qb.mg <= 320 and g32.corr_max <= 64:
             gplan = g32
@@ -1364,6 +1365,9 @@ GROUP_MAX_DATES = 16     # MFMA N of the grouped ADMM (admm_grp.hip GMAX)
 # dates per group of the group-capacitance ADMM with its two MFMA column blocks (admm_gcap.hip,
 # NB = 2: one 512-thread workgroup per CU); PQ_GCAP_GMAX=16 keeps the 16-date groups (A/B)
 GCAP_MAX_DATES = int(os.environ.get("PQ_GCAP_GMAX", "32"))
+# the 32-date groups also for the wide form (column-sparse general rows, config 4's sector
+# caps); PQ_GCAP32_WIDE=0: 16-date groups there (A/B)
+GCAP32_WIDE = os.environ.get("PQ_GCAP32_WIDE", "1") != "0"
 GCAP_FACTOR = os.environ.get("PQ_GCAP_FACTOR", "batched")   # (A/B) "large": K2L for the group factor
 GROUP_MAX_UNION = 320    # union rows per group (admm_grp.hip UMAXG)
 
