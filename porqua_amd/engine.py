@@ -125,6 +125,13 @@ class Settings:
     # eps_grouped = 0 (no loose stop at all)
     eps_grouped_tracking_small: float = 1e-2
     small_batch: int = 64
+    # (host-side) tracking windows with more than 4 general rows (the column-sparse wide form,
+    # e.g. config 4's sector caps) take the loose stop at this eps when eps_grouped_tracking is
+    # 0: their polish finishes in about one wide round, so ADMM iterations are the cost.
+    # Measured on config 4 (profiles/r05Q_grid.log): off / 3e-3 / 1e-2 / 3e-2 -> 119-123k /
+    # 124k / 129k / 113k QPs/s (20 / 19 / 17 / 15 iterations; 3e-2 hands dates to the per-date
+    # polish); config 2 (one general row) keeps eps_abs (round 4: 161k off, 151k at 1e-2)
+    eps_grouped_tracking_wide: float = 1e-2
     # (host-side) the loose stop also on the per-problem capacitance (grouped ADMM without the
     # group capacitance: the lambda sweep, whose problems of a date differ in P's scale)
     eps_grouped_percap: bool = False
@@ -917,16 +924,20 @@ def _pg_wide_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPl
     return buf["wide"]
 
 
-def loose_stop_eps(settings: Settings, centred: bool, batch: int) -> float:
+def loose_stop_eps(settings: Settings, centred: bool, batch: int, mg: int = 1) -> float:
     """The eps of the loose ADMM stop before the grouped polish (0: none): eps_grouped for
-    centred windows, eps_grouped_tracking for uncentred ones, and eps_grouped_tracking_small
-    for uncentred batches of at most small_batch dates when eps_grouped_tracking is 0.
-    eps_grouped = 0 turns every loose stop off."""
+    centred windows, eps_grouped_tracking for uncentred ones; when that is 0,
+    eps_grouped_tracking_small for uncentred batches of at most small_batch dates and
+    eps_grouped_tracking_wide for more than 4 general rows (the wide form).  eps_grouped = 0
+    turns every loose stop off."""
     if centred:
         return settings.eps_grouped
     eps = settings.eps_grouped_tracking
-    if eps <= 0.0 and settings.eps_grouped > 0.0 and batch <= settings.small_batch:
-        eps = settings.eps_grouped_tracking_small
+    if eps <= 0.0 and settings.eps_grouped > 0.0:
+        if batch <= settings.small_batch:
+            eps = settings.eps_grouped_tracking_small
+        elif mg > 4:
+            eps = settings.eps_grouped_tracking_wide
     return eps
 
 
@@ -1197,7 +1208,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     SS_main = SS
     SS_admm = SS
     st_ = settings or Settings()
-    eps_loose = loose_stop_eps(st_, lr.mu is not None, qb.batch)
+    eps_loose = loose_stop_eps(st_, lr.mu is not None, qb.batch, qb.mg)
     if ((gc is not None or (st_.eps_grouped_percap and grouped and eig is None)) and polish and s.polish
             and grouped_polish and ldk >= 64 and eps_loose > max(st_.eps_abs, st_.eps_rel)):
         sl = st_.to_c()

@@ -437,7 +437,8 @@ def test_panel_upload_resolves_the_device_on_the_calling_thread(monkeypatch):
 def test_loose_stop_eps_rule():
     """engine.loose_stop_eps: centred windows take eps_grouped; tracking windows take
     eps_grouped_tracking, or eps_grouped_tracking_small for batches of at most small_batch
-    dates (the notebook's monthly run); eps_grouped = 0 turns every loose stop off."""
+    dates (the notebook's monthly run), or eps_grouped_tracking_wide with more than 4 general
+    rows (config 4's sector caps); eps_grouped = 0 turns every loose stop off."""
     from porqua_amd import engine
     s = engine.Settings()
     assert engine.loose_stop_eps(s, True, 4749) == s.eps_grouped
@@ -447,5 +448,8 @@ def test_loose_stop_eps_rule():
     assert engine.loose_stop_eps(s, False, s.small_batch + 1) == 0.0
     off = engine.Settings(eps_grouped=0.0)
     assert engine.loose_stop_eps(off, False, 13) == 0.0 and engine.loose_stop_eps(off, True, 13) == 0.0
+    assert engine.loose_stop_eps(s, False, 9749, mg=21) == s.eps_grouped_tracking_wide > 0.0
+    assert engine.loose_stop_eps(s, False, 9749, mg=4) == 0.0
+    assert engine.loose_stop_eps(off, False, 9749, mg=21) == 0.0
     own = engine.Settings(eps_grouped_tracking=3e-2)
     assert engine.loose_stop_eps(own, False, 13) == 3e-2 and engine.loose_stop_eps(own, False, 4544) == 3e-2
