@@ -109,7 +109,9 @@ class Settings:
     # sets mostly exceed the LDS solve -- config 2 53.0k at 2e-3, 45.0k at 1e-2 from the loose
     # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
     eps_grouped: float = 0.3
-    min_iter_grouped: int = 8   # (host-side) the loose stop's pq_settings.min_iter
+    # (host-side) the loose stop's pq_settings.min_iter.  Round 5 (profiles/r05T_config3_miniter_grid.log):
+    # 6 / 7 / 8 / 9 -> the same 8 iterations below 9 (eps 0.3 is first met at 8), 9 slower (569k)
+    min_iter_grouped: int = 8
     # (host-side) the same loose stop for uncentred (tracking) windows on the group capacitance;
     # 0: off (they stop at eps_abs / eps_rel).  Measured on config 2 (profiles/r04T_*.log): off /
     # 1e-2 / 3e-2 / 1e-1 -> 161k / 151k / 142k / 114k QPs/s (20 / 17 / 15 / 13 iterations, 2.7 /
