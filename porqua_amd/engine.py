@@ -132,7 +132,9 @@ class Settings:
     # 0: their polish finishes in about one wide round, so ADMM iterations are the cost.
     # Measured on config 4 (profiles/r05Q_grid.log): off / 3e-3 / 1e-2 / 3e-2 -> 119-123k /
     # 124k / 129k / 113k QPs/s (20 / 19 / 17 / 15 iterations; 3e-2 hands dates to the per-date
-    # polish); config 2 (one general row) keeps eps_abs (round 4: 161k off, 151k at 1e-2;
+    # polish); around it (profiles/r05U_config4_eps_wide_grid.log) 1e-2 / 1.5e-2 / 2e-2 ->
+    # 130-131k / 122-124k / 128-131k (1.00 / 1.12 / 1.05 rounds: 1e-2 the steadiest); config 2
+    # (one general row) keeps eps_abs (round 4: 161k off, 151k at 1e-2;
     # round 5, profiles/r05S_config2_loose_grid.log: off / 3e-3 / 1e-2 -> 227k / 226-230k /
     # 214-217k: its rounds of free sets of ~190 still cost more than the iterations saved)
     eps_grouped_tracking_wide: float = 1e-2
