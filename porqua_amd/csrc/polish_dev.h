@@ -165,6 +165,61 @@ __device__ void fwd_solve(const double* K, int64_t ld, const double* Dt, int nbk
   }
 }
 
+// fwd_solve for two right-hand sides at once (y = L^-1 r, y2 = L^-1 r2): one pass over L's
+// rows and the block inverses instead of two.  t64: 2*64, y64p: 2*4*64 LDS scratch.
+__device__ void fwd_solve2(const double* K, int64_t ld, const double* Dt, int nbk, const double* r,
+                           const double* r2, double* y, double* y2, double* t64, double* y64p) {
+  const int t = threadIdx.x, w = wave_id(), l = lane_id();
+  const int g4 = l >> 4, c16 = l & 15;
+  for (int I = 0; I < nbk; ++I) {
+    for (int i0 = 4 * w; i0 < TB; i0 += 4 * PW) {
+      const int i = i0 + g4;
+      const double* row = K + (int64_t)(I * TB + i) * ld;
+      double s = 0.0, s2 = 0.0, u = 0.0, u2 = 0.0;
+#pragma unroll 4
+      for (int c = c16; c < I * TB; c += 32) {
+        const bool in2 = c + 16 < I * TB;   // (clamped, unconditional second load)
+        const double a = row[c], b = row[in2 ? c + 16 : c];
+        s = fma(a, y[c], s);
+        u = fma(a, y2[c], u);
+        s2 = fma(b, in2 ? y[c + 16] : 0.0, s2);
+        u2 = fma(b, in2 ? y2[c + 16] : 0.0, u2);
+      }
+      s += s2;
+      u += u2;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        u += __shfl_xor(u, o, 64);
+      }
+      if (c16 == 0) {
+        t64[i] = r[I * TB + i] - s;
+        t64[TB + i] = r2[I * TB + i] - u;
+      }
+    }
+    __syncthreads();
+    {  // y_I = Dinv_I t_I for both
+      const double* D = Dt + (int64_t)I * TB * TB;
+      const int o = t & 63, part = t >> 6;
+      double v = 0.0, v2 = 0.0;
+#pragma unroll
+      for (int c = part * 16; c < part * 16 + 16; ++c) {
+        const double d = D[c * TB + o];   // Dinv[o][c] = Dt[c][o]
+        v = fma(d, t64[c], v);
+        v2 = fma(d, t64[TB + c], v2);
+      }
+      y64p[part * TB + o] = v;
+      y64p[4 * TB + part * TB + o] = v2;
+    }
+    __syncthreads();
+    if (t < TB) {
+      y[I * TB + t] = (y64p[t] + y64p[TB + t]) + (y64p[2 * TB + t] + y64p[3 * TB + t]);
+      y2[I * TB + t] = (y64p[4 * TB + t] + y64p[5 * TB + t]) + (y64p[6 * TB + t] + y64p[7 * TB + t]);
+    }
+    __syncthreads();
+  }
+}
+
 // x = L^-T y ; part[] is 4*64 LDS scratch.
 __device__ void bwd_solve(const double* K, int64_t ld, const double* Dt, int nbk, const double* y,
                           double* x, double* t64, double* part, double* part_out) {

@@ -1460,43 +1460,54 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
   }
   __syncthreads();
   // ---- U = L^-1 C_aF', S = U'U + delta I (tiny Cholesky, one thread) -------------------------
-  for (int a = 0; a < ma; ++a) {
-    const double* cr = Cg + (int64_t)s_al[a] * ld;
-    for (int p = t; p < kp; p += PT) rx[p] = p < k ? cr[wk.Fl[p]] : 0.0;
-    __syncthreads();
-    fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
-    for (int p = t; p < kp; p += PT) U[(int64_t)a * ld + p] = t1[p];
-    __syncthreads();
-  }
-  for (int e = w; e < ma * ma; e += PW) {
-    const int ii = e / ma, jj = e % ma;
-    if (jj > ii) continue;
-    double sum = 0.0;
-    for (int p = l; p < k; p += 64) sum += U[(int64_t)ii * ld + p] * U[(int64_t)jj * ld + p];
-    sum = wave_sum(sum);
-    if (l == 0) Sm[ii * WMA + jj] = sum + (ii == jj ? delta : 0.0);
-  }
-  __syncthreads();
-  if (t == 0) {
-    int sbad = 0;
-    for (int c = 0; c < ma && !sbad; ++c) {
-      double d = Sm[c * WMA + c];
-      for (int m = 0; m < c; ++m) d -= Sm[c * WMA + m] * Sm[c * WMA + m];
-      if (!(d > 0.0) || !isfinite(d)) { sbad = 1; break; }
-      d = sqrt(d);
-      Sm[c * WMA + c] = d;
-      for (int r = c + 1; r < ma; ++r) {
-        double v = Sm[r * WMA + c];
-        for (int m = 0; m < c; ++m) v -= Sm[r * WMA + m] * Sm[c * WMA + m];
-        Sm[r * WMA + c] = v / d;
-      }
+  // With one active row (the budget: the usual case) U's forward solve is deferred into the
+  // first refinement step's, as the second right-hand side of one pass over L and Dt
+  const bool defer_u = ma == 1;   // (uniform)
+  constexpr int CR_OFF = YC_OFF + PW * PG_KBIG, U1_OFF = CR_OFF + PG_KBIG, T2_OFF = U1_OFF + PG_KBIG,
+                Y2_OFF = T2_OFF + 2 * TB;
+  static_assert(Y2_OFF + 8 * TB <= CHOL_LDS, "k_pg_big LDS layout (two-right-hand-side solve)");
+  auto factor_s = [&]() -> bool {   // S = U'U + delta I and its Cholesky; true: not PD (uniform)
+    for (int e = w; e < ma * ma; e += PW) {
+      const int ii = e / ma, jj = e % ma;
+      if (jj > ii) continue;
+      double sum = 0.0;
+      for (int p = l; p < k; p += 64) sum += U[(int64_t)ii * ld + p] * U[(int64_t)jj * ld + p];
+      sum = wave_sum(sum);
+      if (l == 0) Sm[ii * WMA + jj] = sum + (ii == jj ? delta : 0.0);
     }
-    red[0] = sbad;
-  }
-  __syncthreads();
-  if (red[0] != 0.0) {
-    if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
-    return;
+    __syncthreads();
+    if (t == 0) {
+      int sbad = 0;
+      for (int c = 0; c < ma && !sbad; ++c) {
+        double d = Sm[c * WMA + c];
+        for (int m = 0; m < c; ++m) d -= Sm[c * WMA + m] * Sm[c * WMA + m];
+        if (!(d > 0.0) || !isfinite(d)) { sbad = 1; break; }
+        d = sqrt(d);
+        Sm[c * WMA + c] = d;
+        for (int r = c + 1; r < ma; ++r) {
+          double v = Sm[r * WMA + c];
+          for (int m = 0; m < c; ++m) v -= Sm[r * WMA + m] * Sm[c * WMA + m];
+          Sm[r * WMA + c] = v / d;
+        }
+      }
+      red[0] = sbad;
+    }
+    __syncthreads();
+    return red[0] != 0.0;
+  };
+  if (!defer_u) {
+    for (int a = 0; a < ma; ++a) {
+      const double* cr = Cg + (int64_t)s_al[a] * ld;
+      for (int p = t; p < kp; p += PT) rx[p] = p < k ? cr[wk.Fl[p]] : 0.0;
+      __syncthreads();
+      fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+      for (int p = t; p < kp; p += PT) U[(int64_t)a * ld + p] = t1[p];
+      __syncthreads();
+    }
+    if (factor_s()) {
+      if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+      return;
+    }
   }
   for (int p = t; p < kp; p += PT) sx[p] = p < k ? wk.solx[p] : 0.0;
   __syncthreads();
@@ -1581,7 +1592,22 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
     if (t < ma) rm = fmax(rm, fabs(rl[t]));
     BSTAMP(2);
     if (block_max(rm, red) <= 1e-13 * sc) break;
-    fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+    if (defer_u && itr == 0) {   // t1 = L^-1 rx and U = L^-1 C_aF' in one pass, then S
+      double* cr2 = smem + CR_OFF;
+      double* u1 = smem + U1_OFF;
+      const double* cr = Cg + (int64_t)s_al[0] * ld;
+      for (int p = t; p < kp; p += PT) cr2[p] = p < k ? cr[wk.Fl[p]] : 0.0;
+      __syncthreads();
+      fwd_solve2(K, ldk, Dt, nbk, rx, cr2, t1, u1, smem + T2_OFF, smem + Y2_OFF);
+      for (int p = t; p < kp; p += PT) U[p] = u1[p];
+      __syncthreads();
+      if (factor_s()) {
+        if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
+        return;
+      }
+    } else {
+      fwd_solve(K, ldk, Dt, nbk, rx, t1, t64, y64p);
+    }
     for (int a = w; a < ma; a += PW) {   // wl = U' t1 - rl
       double sum = 0.0;
       for (int p = l; p < k; p += 64) sum += U[(int64_t)a * ld + p] * t1[p];
