@@ -45,12 +45,16 @@ FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 matrix spec
 
 
 CPU_PATH_TEXT = {   # the reference's per-QP arithmetic the cpu_baseline leg restates
+    "config1": "P = 2 X'X, q = -2 X'y (LeastSquares) + isPD/nearestPD of P",
     "config2": "P = 2 X'X, q = -2 X'y (LeastSquares) + isPD/nearestPD of P",
     "config3": "np.cov + isPD/nearestPD, P = 2 Sigma, + isPD/nearestPD of P",
     "config4": "P = 2 X'X, q = -2 X'y (LeastSquares, 20 sector caps) + isPD/nearestPD of P",
     "config5": "np.cov + isPD/nearestPD, P = 2 lam Sigma, q = -geometric mean, + isPD/nearestPD of P",
 }
 WORKLOAD_TEXT = {
+    "config1": "config1: SPTR index replication, LS tracking (P=2 X'X, q=-2 X'y), budget + box [0,1], n=494 "
+               "usa-shaped panel on the real SPTR calendar, the reference notebook's MONTHLY rebalancing "
+               "(every 21st date from the first full window: 217 dates)",
     "config2": "config2: SPTR index replication, LS tracking (P=2 X'X, q=-2 X'y), budget + box [0,1], n=494 "
                "usa-shaped panel on the real SPTR calendar, every daily rebalance date (4544)",
     "config3": "config3: long-only min-variance (P=2*Pearson cov, budget + box [0,1]), daily rebalance",
@@ -61,10 +65,11 @@ WORKLOAD_TEXT = {
 }
 
 
-def dropin_config2(wl, T):
-    """Config 2 through the reference API (rank 0, N = 1, outside the timed region):
-    Backtest.run(bs) with LeastSquares(solver_name='mi355x') on the same panel and dates, from
-    the host DataFrames to the Portfolio objects (upload, staging, download included)."""
+def dropin_config2(wl, T, reb=None, runs=1):
+    """Configs 1 / 2 through the reference API (rank 0, N = 1, outside the timed region):
+    Backtest.run(bs) with LeastSquares(solver_name='mi355x') on the same panel and dates (or the
+    rebalance dates ``reb``), from the host DataFrames to the Portfolio objects (upload,
+    staging, download included); the median of ``runs`` runs after one warm-up run."""
     import pandas as pd
     from porqua_amd.backtest import Backtest, BacktestService
     from porqua_amd.builders import (OptimizationItemBuilder, SelectionItemBuilder, bibfn_bm_series,
@@ -74,7 +79,8 @@ def dropin_config2(wl, T):
     idx = pd.DatetimeIndex(wl.dates_rank)
     X = pd.DataFrame(wl.R_rank, index=idx, columns=[f"u{i:03d}" for i in range(wl.n)])
     y = pd.DataFrame({"SPTR": wl.y_rank}, index=idx)
-    reb = [str(d.date()) for d in idx[wl.ends_local]]
+    if reb is None:
+        reb = [str(d.date()) for d in idx[wl.ends_local]]
 
     def run():
         svc = BacktestService(
@@ -91,11 +97,15 @@ def dropin_config2(wl, T):
         torch.cuda.synchronize()
         return bt
     run()
-    t = time.perf_counter()
-    bt = run()
-    t = time.perf_counter() - t
+    ts = []
+    for _ in range(runs):
+        t = time.perf_counter()
+        bt = run()
+        ts.append(time.perf_counter() - t)
+    t = float(np.median(ts))
     return {"api": "porqua_amd.backtest.Backtest.run(bs), LeastSquares(solver_name='mi355x')",
-            "qps": len(reb) / t, "s": t, "dates": len(reb), "solved": bt.stats["solved"], "path": bt.stats["path"],
+            "qps": len(reb) / t, "s": t, "runs_s": [round(r, 5) for r in ts], "dates": len(reb),
+            "solved": bt.stats["solved"], "path": bt.stats["path"],
             "note": "host DataFrames in, Portfolio objects out: panel upload, window staging, device solve and "
                     "weight download included"}
 
@@ -107,8 +117,10 @@ def parse():
                          "them itself, one child process per GPU, before anything touches the GPU")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5"], default="config3",
-                    help="config3: n=1000 long-only min-variance (the metric's configuration); config2: SPTR "
+    ap.add_argument("--workload", choices=["config1", "config2", "config3", "config4", "config5"], default="config3",
+                    help="config3: n=1000 long-only min-variance (the metric's configuration); config1: the SPTR "
+                         "replication at the notebook's monthly rebalancing (every 21st date, 217 QPs; "
+                         "BASELINE configs[0..1]); config2: SPTR "
                          "replication, n=494 LS tracking on the usa-shaped panel, all 4544 daily dates (BASELINE "
                          "configs[1]; strong scaling: the fixed date set split over the ranks); config4: n=3000 "
                          "tracking LS with 20 sector caps (configs[3], 'dates sharded'); config5: n=5000 "
@@ -238,10 +250,10 @@ def main():
         sys.exit(run_ranks(plan, sys.argv[1:]))
     wname = args.workload
     cfg4 = wname == "config4"
-    if wname in ("config2", "config5"):
+    if wname in ("config1", "config2", "config5"):
         args.strong = True                 # a fixed problem set split over the ranks
     if args.n is None:
-        args.n = {"config2": 494, "config4": 3000, "config5": 5000}.get(wname, 1000)
+        args.n = {"config1": 494, "config2": 494, "config4": 3000, "config5": 5000}.get(wname, 1000)
     if args.dates is None:
         args.dates = {"config4": 9749, "config5": 64}.get(wname, 4749)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -259,7 +271,8 @@ def main():
         # n >= 3000 legs time one QP per worker and one serial QP
         cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--workload", wname, "--n", str(args.n),
                "--window", str(args.window), "--dates", str(args.dates), "--budget", str(args.cpu_budget)]
-        cmd += {"config2": ["--serial-dates", "8", "--pool-rounds", "8"],
+        cmd += {"config1": ["--serial-dates", "8", "--pool-rounds", "8"],
+                "config2": ["--serial-dates", "8", "--pool-rounds", "8"],
                 "config4": ["--serial-dates", "1", "--pool-rounds", "1"],
                 "config5": ["--serial-dates", "1", "--pool-rounds", "1"]}.get(wname, [])
         # progress lines pass through on stderr (the n = 5000 legs run for minutes)
@@ -282,11 +295,11 @@ def main():
         settings = engine.Settings.from_params(dict({"rho0_rel": 0.1, "rho0_qrel": 0.0}, **ov))
         wl = TrackingBacktest(n=n, T=T, D=args.dates, rank=rank, world=world, device=dev, settings=settings,
                               strong=args.strong)
-    elif wname == "config2":
+    elif wname in ("config1", "config2"):
         g = np.load(os.path.join(ROOT, "tests", "golden", "sptr.npz"), allow_pickle=False)
         settings = engine.Settings.from_params(dict({"rho0_rel": 0.2, "rho0_qrel": 0.0}, **ov))
         wl = ReplicationBacktest(g["days"], g["returns"], T=T, rank=rank, world=world, device=dev,
-                                 settings=settings, n=n)
+                                 settings=settings, n=n, stride=21 if wname == "config1" else 1)
     elif wname == "config5":
         from porqua_amd.sweep import SWEEP_SETTINGS
         settings = engine.Settings.from_params(dict(SWEEP_SETTINGS, **ov))
@@ -483,7 +496,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": ("synthetic usa-shaped panel (494 assets loading on the real SPTR returns, seed 20240101; "
-                 "usa_returns absent) on the real SPTR calendar" if wname == "config2" else
+                 "usa_returns absent) on the real SPTR calendar" if wname in ("config1", "config2") else
                  "synthetic (factor-model panel, seed 20240314; usa_returns absent)"),
         "config": {"workload": WORKLOAD_TEXT[wname], "n_assets": n, "window": T,
                    "dates_per_gpu": D, "global_batch": D_all,
@@ -566,6 +579,15 @@ def main():
             "speedup": qps / b["qps"]}
     if wname == "config2" and world == 1 and not args.no_dropin:
         out["end_to_end"] = dropin_config2(wl, T)
+    if wname == "config1" and world == 1 and not args.no_dropin:
+        # the monthly run through the reference API, and the notebook's own 13-date run
+        # (example/backtest.ipynb: dates[dates > start][::21]; start 2022-06-01 on this calendar,
+        # which ends in 2023, so that the run has the notebook's 13 dates)
+        out["end_to_end"] = dropin_config2(wl, T, runs=5)
+        d = np.asarray(wl.dates_rank).astype("datetime64[D]")
+        nb13 = [str(r) for r in d[d > np.datetime64("2022-06-01")][::21]]
+        out["end_to_end_notebook13"] = dict(dropin_config2(wl, T, reb=nb13, runs=9),
+                                            rebdates=f"{nb13[0]} .. {nb13[-1]} (every 21st date after 2022-06-01)")
     if wname != "config3":   # the next-row and drop-in legs below are config-3 (n = 1000 min-variance) lines
         if rank == 0:
             print(json.dumps(out), flush=True)

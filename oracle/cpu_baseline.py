@@ -20,6 +20,7 @@ Workloads (``--workload``, the same synthetic inputs bench.py's GPU legs solve):
   config3  min-variance above, n = 1000 (the headline);
   config2  LeastSquares SPTR replication on the usa-shaped panel (n = 494, daily dates):
            P = 2 X'X, q = -2 X'y (src/optimization.py:206-226, uncentred), budget + box;
+  config1  the same at the notebook's monthly rebalancing (every 21st date);
   config4  the same tracking objective at n = 3000 with the 20 sector caps G x <= 0.15
            (src/constraints.py:66-94, 114-167);
   config5  MeanVariance lambda sweep at n = 5000: Sigma by np.cov + nearestPD
@@ -106,10 +107,10 @@ class Workload:
         from porqua_amd.synthetic import factor_panel, usa_panel
         self.name, self.T = name, T
         self.G = self.h = None
-        if name == "config2":
+        if name in ("config1", "config2"):   # monthly (every 21st row) / daily rebalancing
             g = np.load(os.path.join(root, "tests", "golden", "sptr.npz"), allow_pickle=False)
             _, self.R, self.y = usa_panel(g["days"], g["returns"], n_assets=n)
-            self.units = list(range(T - 1, self.R.shape[0]))
+            self.units = list(range(T - 1, self.R.shape[0], 21 if name == "config1" else 1))
         elif name == "config4":
             _, self.R, self.y, sec = factor_panel(T - 1 + dates, n, n_sectors=20)
             self.G = np.stack([(sec == k).astype(float) for k in range(20)])
@@ -134,7 +135,7 @@ class Workload:
 
     def solve(self, u, repair: bool = True):
         T = self.T
-        if self.name in ("config2", "config4"):
+        if self.name in ("config1", "config2", "config4"):
             return reference_ls(self.R[u - T + 1:u + 1], self.y[u - T + 1:u + 1], self.G, self.h, repair)
         if self.name == "config5":
             e, k = u
@@ -265,7 +266,7 @@ def host_cores() -> int:
 def main():
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5"], default="config3")
+    ap.add_argument("--workload", choices=["config1", "config2", "config3", "config4", "config5"], default="config3")
     ap.add_argument("--n", type=int, default=1000)
     ap.add_argument("--window", type=int, default=252)
     ap.add_argument("--dates", type=int, default=4749)

@@ -495,8 +495,9 @@ __global__ __launch_bounds__(PT_PREP, 2 / NB) void k_gcap_prep(pq_lowrank lr, pq
 // NB: MFMA column blocks of 16 dates -- NB = 2 takes up to 32 dates per group with one
 // 512-thread workgroup per CU (the CU's union rows streamed once per pass for all of them:
 // half the union traffic and half the group factorisations of two 16-date groups); NB = 1 is
-// the 256-thread, 16-date form (two workgroups per CU).  The wide form is NB = 1 only (its
-// per-(date, row) LDS would not fit twice).
+// the 256-thread, 16-date form (two workgroups per CU).  The wide form runs NB = 2 as well:
+// its per-(date, row) LDS (g_part) is indexed by the date within its wave's column block, so
+// k_admm_gcap<CMGW, 2> fits the CU's 160 KiB.
 template <int MGC, int NB>
 __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_admm_gcap(pq_lowrank lr, pq_problem pb, pq_state st, pq_gcap gc,
                                                   pq_settings s, int iters_call, const double* pc, int64_t ldpc,

@@ -250,8 +250,9 @@ __device__ __forceinline__ double row_bcast16(double v, int k) {
 // update and the inverse's row operations in registers.  On return A holds L (lower, column
 // layout as above; the strictly upper part is stale) and Bv = L^-1; returns 1 when a pivot is
 // not positive (uniform), 0 otherwise.
-__device__ __forceinline__ int wave_chol_inv16(double (&A)[4], double (&Bv)[4]) {
-  const int l = lane_id();
+// (l: the lane id; callers that inline several chains pass one rebuilt from loop_zero(), so
+// the chain's per-lane masks are not hoisted and held live across all of them)
+__device__ __forceinline__ int wave_chol_inv16(double (&A)[4], double (&Bv)[4], const int l) {
   const int cc = l & 15, gg = l >> 4;
   int bad = 0;
 #pragma unroll
@@ -286,6 +287,9 @@ __device__ __forceinline__ int wave_chol_inv16(double (&A)[4], double (&Bv)[4]) 
     }
   }
   return bad;
+}
+__device__ __forceinline__ int wave_chol_inv16(double (&A)[4], double (&Bv)[4]) {
+  return wave_chol_inv16(A, Bv, lane_id());
 }
 
 // XCD-contiguous block order: the hardware deals workgroups round-robin over the 8 XCDs

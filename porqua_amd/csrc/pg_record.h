@@ -23,8 +23,16 @@ enum : int {
   R_GFORM = 348,
   // R_KB: the free-set size setup found this round -- the LDS solve's buckets select on it
   // (the solve's inner primal loop lowers R_K while the other buckets may still be reading)
-  R_KB = 349
+  R_KB = 349,
+  // the solve buckets' date lists: record i holds at R_LIST + j the i-th date of bucket j (free
+  // sets <= 48, 64, 80, 96, 128); date 0's record holds the five counts at R_CNT (as 64-bit
+  // integers, appended by k_pg_form's atomics, cleared by k_pg_post<0>)
+  R_LIST = 352, R_CNT = 360
 };
+constexpr int PG_NBUCKET = 5;
+__device__ __forceinline__ int pg_bucket(int kb) {
+  return kb <= 48 ? 0 : kb <= 64 ? 1 : kb <= 80 ? 2 : kb <= 96 ? 3 : 4;
+}
 constexpr int PG_KMAX = 128;   // largest free set of the LDS solve
 constexpr int PG_KBIG = 256;   // largest free set of the grouped large-free-set solve (k_pg_big)
 constexpr int PG_MGMAX = 32;   // general rows
@@ -33,7 +41,8 @@ constexpr int PG_MGMAX = 32;   // general rows
 // variables as bordered rows (at most PG_WMB of them)
 constexpr int PG_WMB = 8;
 constexpr int PG_WG_MAX = 24;   // general rows of the wide mode
-static_assert(R_FXL + PG_WMB <= R_GFORM && R_KB < PQ_PG_RECORD, "PQ_PG_RECORD too small");
+static_assert(R_FXL + PG_WMB <= R_GFORM && R_KB < R_LIST && R_LIST + 5 <= R_CNT && R_CNT + 5 <= PQ_PG_RECORD,
+              "PQ_PG_RECORD too small");
 
 struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl
   double *xs, *xb, *g, *Px, *rF, *solx, *pxb, *U;
@@ -60,5 +69,9 @@ __device__ __forceinline__ int pk(int r, int c) { return ((r * (r + 1)) >> 1) + 
 }  // namespace pq
 
 // wide rounds (polish_gw.hip), launched by pq_polish_grouped_round
+// the register-tile solve (polish_rt.hip) of the free-set buckets <= 48 .. <= 16 nbmax (nbmax
+// in 3..6), one launch
+int pq_pg_solve_rt_launch(int nbmax, int B, hipStream_t str, const pq_problem* pb, pq_state* st, double* rec,
+                          const pq_settings* s, int ldk);
 int pq_pg_wide_launch(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, double* rec, const pq_settings* s,
                       const pq_pg_wide* wd, hipStream_t stream);

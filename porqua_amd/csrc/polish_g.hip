@@ -339,32 +339,60 @@ __device__ __forceinline__ void form_from_group(const pq_lowrank& lr, const pq_p
     s_d[p] = (mu ? mu[i] : 0.0) - s_gmu[a];
   }
   __syncthreads();
-  // outside rows x~_o (F columns) into S, pitch k; s = union column sums - outside rows
+  // outside rows x~_o (F columns) into S, pitch kp (zero beyond k, and whole zero rows up to a
+  // multiple of 4: the MFMA operands below read them unconditionally); s = union column sums -
+  // outside rows
   const int32_t* ur = urows_all + (int64_t)grp * umax;
-  for (int e = t; e < mo * k; e += FT) {
-    const int o = e / k, p = e - o * k;
+  const int nt = (k + 15) >> 4, kp = 16 * nt, mo4 = (mo + 3) & ~3;
+  for (int e = t; e < mo4 * kp; e += FT) {
+    const int o = e / kp, p = e - o * kp;
     const int u = o < off ? o : o + T;
-    S[e] = lr.panel[(int64_t)ur[u] * lr.ldp + wk.Fl[p]] - s_gmu[s_pi[p]];
+    S[e] = (o < mo && p < k) ? lr.panel[(int64_t)ur[u] * lr.ldp + wk.Fl[p]] - s_gmu[s_pi[p]] : 0.0;
   }
   __syncthreads();
   for (int p = t; p < k; p += FT) {
     double v = Gs[GS_CS + s_pi[p]];
-    for (int o = 0; o < mo; ++o) v -= S[o * k + p];
+    for (int o = 0; o < mo; ++o) v -= S[o * kp + p];
     s_s[p] = v;
   }
   __syncthreads();
+  // the lower 16 x 16 tiles, FTW per wave: acc = G_FF - X_o,F' X_o,F by MFMA over the outside
+  // rows (4 per step), then the centring terms, into K (both triangles) -- instead of one
+  // thread per entry summing its mo products from LDS
   double* K = st.K + (int64_t)b * st.K_stride;
   const double Td = (double)T;
-  for (int e = t; e < k * k; e += FT) {
-    const int p = e / k, q = e - p * k;
-    if (q > p) continue;
-    double v = Gs[(int64_t)s_pi[p] * GLD + s_pi[q]];
-    for (int o = 0; o < mo; ++o) v = fma(-S[o * k + p], S[o * k + q], v);
-    v -= s_d[p] * s_s[q] + s_s[p] * s_d[q];
-    v = fma(Td * s_d[p], s_d[q], v);
-    const double val = psw * v + (p == q ? pd : 0.0);
-    K[(int64_t)p * ldk + q] = val;
-    K[(int64_t)q * ldk + p] = val;
+  const int l = lane_id(), wu = __builtin_amdgcn_readfirstlane(wave_id());
+  const int ntile = nt * (nt + 1) / 2;
+#pragma unroll
+  for (int j = 0; j < FTW; ++j) {
+    const int q = wu + FNW * j;
+    if (q >= ntile) break;   // (uniform)
+    int I = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+    while ((I + 1) * (I + 2) / 2 <= q) ++I;
+    while (I * (I + 1) / 2 > q) --I;
+    const int J = q - I * (I + 1) / 2;
+    const int gj = 16 * J + (l & 15), pj = s_pi[gj < k ? gj : 0];
+    f64x4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = 16 * I + (l >> 4) + 4 * r;
+      acc[r] = Gs[(int64_t)s_pi[gi < k ? gi : 0] * GLD + pj];
+    }
+    for (int o0 = 0; o0 < mo4; o0 += 4) {
+      const double* so = S + (o0 + (l >> 4)) * kp + (l & 15);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-so[16 * I], so[16 * J], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = 16 * I + (l >> 4) + 4 * r;
+      if (gi < k && gj < k && gj <= gi) {
+        double v = acc[r] - (s_d[gi] * s_s[gj] + s_s[gi] * s_d[gj]);
+        v = fma(Td * s_d[gi], s_d[gj], v);
+        const double val = psw * v + (gi == gj ? pd : 0.0);
+        K[(int64_t)gi * ldk + gj] = val;
+        K[(int64_t)gj * ldk + gi] = val;
+      }
+    }
   }
   for (int i = t; i < pb.n; i += FT) wk.posF[i] = -1;   // positions of the formed free list
   __syncthreads();
@@ -390,6 +418,14 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;   // wide dates: polish_gw.hip
   const int k = (int)R[R_K];
+  if (KF == PG_KMAX && threadIdx.x == 0) {   // the date joins its solve bucket's list
+    const int kb = (int)R[R_KB], kmax = ldk < PG_KMAX ? ldk : PG_KMAX;
+    if (kb >= 1 && kb <= kmax) {
+      const int bk = pg_bucket(kb);
+      const unsigned long long i = atomicAdd(reinterpret_cast<unsigned long long*>(rec + R_CNT) + bk, 1ull);
+      rec[(int64_t)i * PGR + R_LIST + bk] = (double)b;
+    }
+  }
   if (KF == PG_KMAX ? (k > PG_KMAX || k == 0) : (k <= PG_KMAX || k > KF)) return;
   if (R[R_REUSE] != 0.0) {   // P_FF is a principal submatrix of the formed one: nothing to form
     if (R[R_NZB] != 0.0) {   // (the reduced rhs still takes P_FB x_B from pass 0)
@@ -1068,9 +1104,10 @@ __device__ __forceinline__ void b_bwd(const double* Lp, int k, double* y, double
   }
 }
 
+// the solve of date b (k_pg_solve's grid-stride loop body)
 template <int KS, int NW>
-__global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s,
-                                                      int ldk, int klo, int inner) {
+__device__ __forceinline__ void pg_solve_date(int b, const pq_problem& pb, const pq_state& st, double* rec,
+                                              const pq_settings& s, int ldk, int klo, int inner) {
   constexpr int T = 64 * NW;
   constexpr int NP = KS * (KS + 1) / 2;
   __shared__ double Lp[NP];
@@ -1081,7 +1118,6 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
   __shared__ int s_flag;
   double* t1 = sc4;
   double* t2 = sc4 + KS;
-  const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;
   const int kb = (int)R[R_KB];   // (the bucket key: R_K may already be lowered by this kernel)
@@ -1375,6 +1411,19 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
 #undef WSTAMP
 }
 
+// Workgroup i solves the i-th date of the bucket's list (k_pg_form appends them): the dates
+// are dispatched first and the surplus workgroups only read the count and exit -- with one
+// workgroup per date, most of them read the record and exited, and each of those still needed
+// the full LDS triangle to be dispatched, so with the other buckets filling the CUs they
+// trickled in behind the dates
+template <int KS, int NW>
+__global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s,
+                                                      int ldk, int klo, int inner) {
+  const int i = blockIdx.x, bk = pg_bucket(KS);
+  if ((unsigned long long)i >= reinterpret_cast<const unsigned long long*>(rec + R_CNT)[bk]) return;
+  pg_solve_date<KS, NW>((int)rec[(int64_t)i * PGR + R_LIST + bk], pb, st, rec, s, ldk, klo, inner);
+}
+
 // ---------------------------------------------------------------------------------------
 // solve for the free sets beyond the LDS solve, PG_KMAX < k <= ldk (the tracking windows of
 // configs 1/2: 160..220 free assets at n = 494), one 256-thread workgroup per date inside the
@@ -1591,6 +1640,9 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
     for (int p = t; p < k; p += PT) rm = fmax(rm, fabs(rx[p]));
     if (t < ma) rm = fmax(rm, fabs(rl[t]));
     BSTAMP(2);
+    // (with defer_u this break can come before U and S exist: the starting point then already
+    // solves the regularised KKT system to 1e-13 of the problem scale and is kept as it is --
+    // no step is taken, so S's Cholesky, which only guards the step, is not needed)
     if (block_max(rm, red) <= 1e-13 * sc) break;
     if (defer_u && itr == 0) {   // t1 = L^-1 rx and U = L^-1 C_aF' in one pass, then S
       double* cr2 = smem + CR_OFF;
@@ -1978,6 +2030,8 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
                                                 const double* scr) {
   const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
+  if (MODE == 0 && b == 0 && threadIdx.x < PG_NBUCKET)   // this round's solve-bucket lists start empty
+    reinterpret_cast<unsigned long long*>(rec + R_CNT)[threadIdx.x] = 0ull;
   if (!(R[R_STATE] == PQ_PG_PENDING && (MODE == 1 || R[R_NZB] != 0.0))) return;
   int lo = 0, hi = ngroups;   // group of date b: gdates[grp] <= b < gdates[grp + 1]
   while (hi - lo > 1) {
@@ -2253,6 +2307,17 @@ static int pg_big() {
   return v;
 }
 
+// buckets (48, 64, 80, 96 in order) taken by the register-tile solve (polish_rt.hip) instead of
+// the LDS solve: 4 (default, up to 96) or 3 (up to 80); PQ_PG_RT overrides (0 = the LDS solve
+// for every bucket, A/B)
+static int solve_rt() {
+  static const int v = [] {
+    const char* e = getenv("PQ_PG_RT");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 // waves per date of the solve, per free-set bucket (48, 64, 80, 96, 128): PQ_PG_SOLVE_NW
 // (1, 2 or 4) overrides all buckets
 static int solve_waves(int bucket) {
@@ -2329,11 +2394,15 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
     used |= 1 << i;
     return side->s[i];
   };
-  for (int i = 0; i < 5; ++i) {
+  // the LDS solve's buckets beyond the register solve's (largest free sets first), and the
+  // register solve's buckets in one launch
+  const int nrt = pq::solve_rt() <= 0 ? 0 : (pq::solve_rt() >= 4 ? 4 : 3);   // register buckets 0 .. nrt - 1
+  for (int i = 4; i >= nrt; --i) {
     static const int KSB[5] = {48, 64, 80, 96, 128};
-    if (i >= 2 && kmax <= KSB[i - 1]) break;
+    if (i >= 2 && kmax <= KSB[i - 1]) continue;
     pq::launch_solve(i, pq::solve_waves(i), B, on(i), pb, st, rec, s, ldk, i ? KSB[i - 1] : 0);
   }
+  if (nrt > 0 && pq_pg_solve_rt_launch(nrt + 2, B, on(0), pb, st, rec, s, ldk)) return -1;
   if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, on(5))) return -1;   // free sets beyond kmax
   if (kbig > kmax) {   // free sets of kmax + 1 .. kbig: their P_FF, then the factor and solve
     static_assert(pq::PG_KBIG == 256, "k_pg_form<PG_KBIG> tiling");

@@ -119,13 +119,13 @@ class Settings:
     # ADMM iterations they replace
     eps_grouped_tracking: float = 0.0
     # (host-side) small batches of tracking windows (at most small_batch dates, e.g. the
-    # reference notebook's 13-date monthly run) take the loose stop at this eps when
-    # eps_grouped_tracking is 0: there the GPU runs a handful of slide groups, so an ADMM
-    # iteration costs one group's latency while a polish round stays cheap.  Measured on the
-    # 13-date monthly run (profiles/r05N_monthly_grid.log): off / 3e-3 / 1e-2 / 3e-2 / 0.1 / 0.3
-    # -> 10.3 / 10.4 / 9.5 / 9.6 / 10.0 / 9.5 ms, the same weights to 4e-11.  Off with
-    # eps_grouped = 0 (no loose stop at all)
-    eps_grouped_tracking_small: float = 1e-2
+    # reference notebook's 13-date monthly run) take the loose stop at this eps when it is > 0
+    # and eps_grouped_tracking is 0.  Off by default: the first grid on the 13-date monthly run
+    # (profiles/r05N_monthly_grid.log: off / 3e-3 / 1e-2 / 3e-2 / 0.1 / 0.3 -> 10.3 / 10.4 / 9.5 /
+    # 9.6 / 10.0 / 9.5 ms) did not hold up when re-measured as medians of five
+    # (profiles/r05V_monthly_grid.log: 1e-2 9.84 ms, off 9.78 ms).  The rule keys on the batch
+    # of one solve call, so in a chunked backtest only a short last chunk would take it
+    eps_grouped_tracking_small: float = 0.0
     small_batch: int = 64
     # (host-side) tracking windows with more than 4 general rows (the column-sparse wide form,
     # e.g. config 4's sector caps) take the loose stop at this eps when eps_grouped_tracking is
@@ -933,14 +933,14 @@ def _pg_wide_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPl
 def loose_stop_eps(settings: Settings, centred: bool, batch: int, mg: int = 1) -> float:
     """The eps of the loose ADMM stop before the grouped polish (0: none): eps_grouped for
     centred windows, eps_grouped_tracking for uncentred ones; when that is 0,
-    eps_grouped_tracking_small for uncentred batches of at most small_batch dates and
-    eps_grouped_tracking_wide for more than 4 general rows (the wide form).  eps_grouped = 0
-    turns every loose stop off."""
+    eps_grouped_tracking_small (when > 0; default off) for uncentred batches of at most
+    small_batch dates, else eps_grouped_tracking_wide for more than 4 general rows (the wide
+    form).  eps_grouped = 0 turns every loose stop off."""
     if centred:
         return settings.eps_grouped
     eps = settings.eps_grouped_tracking
     if eps <= 0.0 and settings.eps_grouped > 0.0:
-        if batch <= settings.small_batch:
+        if batch <= settings.small_batch and settings.eps_grouped_tracking_small > 0.0:
             eps = settings.eps_grouped_tracking_small
         elif mg > 4:
             eps = settings.eps_grouped_tracking_wide

@@ -164,13 +164,13 @@ class _LSTrackingBatch:
     rebalance dates are the slice's rows T - 1 .. T - 2 + D.  q is formed inside ``step``
     (the X'y window products are part of the per-date objective)."""
 
-    def _setup(self, dates, R, y, T, D, device, settings, G=None, h=None):
+    def _setup(self, dates, R, y, T, D, device, settings, G=None, h=None, stride=1):
         self.T = T
         self.device = dev = device or engine.default_device()
         self.D = D
         self.n = n = R.shape[1]
         self.R_rank, self.y_rank, self.dates_rank = R, y, dates
-        self.ends_local = np.arange(T - 1, T - 1 + D)
+        self.ends_local = T - 1 + stride * np.arange(D)
         self.rows, self.tlen = engine.window_rows(dates, dates[self.ends_local], T)
         self.pan = engine.Panel(R, y, device=dev)
         self.rows_d, self.tlen_d = self.pan.rows_to_device(self.rows, self.tlen)
@@ -249,28 +249,31 @@ class TrackingBacktest(_LSTrackingBatch):
 
 
 class ReplicationBacktest(_LSTrackingBatch):
-    """Config 2 on one device (BASELINE.json configs[1]): the reference notebook's SPTR index
-    replication (example/backtest.ipynb: LeastSquares, budget + LongOnly box, width 252) on
-    the usa-shaped panel (synthetic.usa_panel: 494 assets on the last 4795 real SPTR dates;
-    usa_returns itself is absent from the reference tree), rebalanced on EVERY date from the
-    first full window on: 4795 - 251 = 4544 daily QPs.  ``sptr_days`` / ``sptr``: the real
-    SPTR series (tests/golden/sptr.npz, captured from the reference's data/SPTR.csv).
+    """Configs 1 / 2 on one device (BASELINE.json configs[0..1]): the reference notebook's SPTR
+    index replication (example/backtest.ipynb: LeastSquares, budget + LongOnly box, width 252)
+    on the usa-shaped panel (synthetic.usa_panel: 494 assets on the last 4795 real SPTR dates;
+    usa_returns itself is absent from the reference tree), rebalanced every ``stride`` rows
+    from the first full window on: stride 1 = every date (config 2's 4795 - 251 = 4544 daily
+    QPs), stride 21 = the notebook's monthly rebalancing (``dates[::21]``, 217 QPs over the
+    panel).  ``sptr_days`` / ``sptr``: the real SPTR series (tests/golden/sptr.npz, captured
+    from the reference's data/SPTR.csv).
 
     Multi-GPU: the fixed set of dates is split into contiguous blocks (strong scaling,
     backtest.shard_range); each rank uploads only the panel rows its windows touch."""
 
     def __init__(self, sptr_days, sptr, T: int = 252, rank: int = 0, world: int = 1, device=None,
-                 settings: engine.Settings | None = None, n: int = 494, n_rows: int = 4795):
+                 settings: engine.Settings | None = None, n: int = 494, n_rows: int = 4795, stride: int = 1):
         from .backtest import shard_range
         from .synthetic import usa_panel
         days, R, y = usa_panel(sptr_days, sptr, n_assets=n, n_rows=n_rows)
-        total = len(days) - (T - 1)
+        total = (len(days) - (T - 1) + stride - 1) // stride
         self.global_dates = total
         lo, hi = shard_range(total, rank, world)
-        self.row_offset = lo
+        self.row_offset = lo * stride
+        r0, r1 = lo * stride, (hi - 1) * stride + T if hi > lo else lo * stride
         # LeastSquares' tracking rho (porqua_amd/optimization.py: rho0_rel 0.2, no |q| floor)
-        self._setup(days[lo:hi + T - 1], R[lo:hi + T - 1], y[lo:hi + T - 1], T, hi - lo, device,
-                    settings or engine.Settings(rho0_rel=0.2, rho0_qrel=0.0))
+        self._setup(days[r0:r1], R[r0:r1], y[r0:r1], T, hi - lo, device,
+                    settings or engine.Settings(rho0_rel=0.2, rho0_qrel=0.0), stride=stride)
         if self.D and int(self.tlen.min()) != T:
             raise ValueError("ReplicationBacktest: the SPTR calendar slice has a short window")
 

@@ -436,16 +436,19 @@ def test_panel_upload_resolves_the_device_on_the_calling_thread(monkeypatch):
 
 def test_loose_stop_eps_rule():
     """engine.loose_stop_eps: centred windows take eps_grouped; tracking windows take
-    eps_grouped_tracking, or eps_grouped_tracking_small for batches of at most small_batch
-    dates (the notebook's monthly run), or eps_grouped_tracking_wide with more than 4 general
-    rows (config 4's sector caps); eps_grouped = 0 turns every loose stop off."""
+    eps_grouped_tracking, or eps_grouped_tracking_small (off by default) for batches of at
+    most small_batch dates (the notebook's monthly run), or eps_grouped_tracking_wide with more
+    than 4 general rows (config 4's sector caps); eps_grouped = 0 turns every loose stop off."""
     from porqua_amd import engine
     s = engine.Settings()
     assert engine.loose_stop_eps(s, True, 4749) == s.eps_grouped
     assert engine.loose_stop_eps(s, False, 4544) == 0.0
-    assert engine.loose_stop_eps(s, False, 13) == s.eps_grouped_tracking_small > 0.0
-    assert engine.loose_stop_eps(s, False, s.small_batch) == s.eps_grouped_tracking_small
-    assert engine.loose_stop_eps(s, False, s.small_batch + 1) == 0.0
+    assert s.eps_grouped_tracking_small == 0.0 and engine.loose_stop_eps(s, False, 13) == 0.0
+    assert engine.loose_stop_eps(s, False, 13, mg=21) == s.eps_grouped_tracking_wide   # small wide batch
+    sm = engine.Settings(eps_grouped_tracking_small=1e-2)
+    assert engine.loose_stop_eps(sm, False, 13) == 1e-2
+    assert engine.loose_stop_eps(sm, False, sm.small_batch) == 1e-2
+    assert engine.loose_stop_eps(sm, False, sm.small_batch + 1) == 0.0
     off = engine.Settings(eps_grouped=0.0)
     assert engine.loose_stop_eps(off, False, 13) == 0.0 and engine.loose_stop_eps(off, True, 13) == 0.0
     assert engine.loose_stop_eps(s, False, 9749, mg=21) == s.eps_grouped_tracking_wide > 0.0

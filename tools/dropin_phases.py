@@ -34,6 +34,7 @@ def timed(owner, name, label):
         ACC[label] += time.perf_counter() - t0
         CNT[label] += 1
         return r
+    wrap.__wrapped_orig__ = fn
     setattr(owner, name, wrap)
 
 
@@ -72,6 +73,35 @@ def main():
         print(f"  {k:48s} {v / runs * 1e3:8.2f} ms  ({CNT[k] // runs} calls)")
         named += v / runs
     print(f"  {'(rest: service build, result copies, glue)':48s} {(tot - named) * 1e3:8.2f} ms")
+    # the top-level phases of Backtest.run (no inner brackets: each phase's host work and
+    # the device time it waits for), and the service build that the bench line also times
+    for owner, name in ((engine.Panel, "__init__"), (bt_mod.BatchStage, "__init__"), (engine.QPBatch, "from_dense"),
+                        (bt_mod.BatchStage, "group_plan"), (engine, "solve_lowrank"), (Backtest, "_finish_batched"),
+                        (opt_cls, "objective_batch"), (bt_mod.BacktestService, "prepare_rebalancing"),
+                        (engine, "window_rows")):
+        setattr(owner, name, getattr(owner, name).__wrapped_orig__ if hasattr(getattr(owner, name), "__wrapped_orig__")
+                else getattr(owner, name))
+    ACC.clear()
+    CNT.clear()
+    top = [(Backtest, "_stage_batched", "A stage (host: builders, windows, constraints)"),
+           (bt_mod._PanelUpload, "result", "B0 wait for the panel upload"),
+           (Backtest, "_solve_shard", "B solve shard (incl. the upload wait)"),
+           (Backtest, "_finish_batched", "C finish (Portfolio objects)")]
+    for owner, name, label in top:
+        timed(owner, name, label)
+    t_make = 0.0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(runs):
+        tm = time.perf_counter()
+        svc = make()
+        t_make += time.perf_counter() - tm
+        Backtest().run(svc)
+    torch.cuda.synchronize()
+    tot = (time.perf_counter() - t0) / runs
+    print(f"top-level split: {tot * 1e3:.2f} ms per run (service build {t_make / runs * 1e3:.2f} ms)", flush=True)
+    for k, v in sorted(ACC.items()):
+        print(f"  {k:48s} {v / runs * 1e3:8.2f} ms  ({CNT[k] // runs} calls)")
     # the device solve of one more run, stage by stage (HIP events) with its iteration and
     # round counts: where the drop-in's solve differs from the bench step's
     from porqua_amd import _lib
