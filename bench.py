@@ -453,7 +453,11 @@ def main():
     # potrf + trtri + lauum (k^3), plus the per-date capacitance SYRK (2 k^2 n) unless the
     # band Gram (one row-band SYRK per panel, stage "gram") supplies it
     factor_flops_per = (kld ** 3 + (0.0 if band else 2.0 * kld * kld * n)) if use_lr else ld ** 3
-    gram_flops = 2.0 * (T - 1 + D) * T * n * args.steps if band else None
+    # the row-band SYRK of the panel (stage "gram", k_band_gram): x_r . x_{r-j} for the band's
+    # W offsets of each of its rows -- 2 n W flop per row (the group path's band is as wide as
+    # the widest slide-group union)
+    bshape = getattr(ws, "band_shape", None) if use_lr else None
+    gram_flops = 2.0 * n * bshape[0] * bshape[1] * args.steps if bshape else None
     n_factor = D * args.steps + res.refactors * args.steps
     factor_flops = factor_flops_per * n_factor
     if use_lr and res.capacitance == "group":   # one M_U (k = U + mg) per slide group
@@ -541,7 +545,9 @@ def main():
             "factor_tflops": factor_flops / tk.get("factor", float("nan")) / 1e12,
             "polish_tflops": polish_flops / tk["polish"] / 1e12 if tk.get("polish") else None,
             "polish_flops_note": "sum over problems of rounds x (|F|^2 T + |F|^3/3) + 4 T n (two P x window passes)",
-            "gram_tflops": gram_flops / tk["gram"] / 1e12 if band and tk.get("gram") else None,
+            "gram_tflops": gram_flops / tk["gram"] / 1e12 if gram_flops and tk.get("gram") else None,
+            "gram_flops_note": ("2 n W flop per panel row of the band (rows x W: %d x %d)" % tuple(bshape))
+            if bshape else None,
             "capacitance": res.capacitance or None,
             "fp64_peak_tflops": FP64_PEAK_TFLOPS,
             "mfma_busy_fraction_pmc": mfma_busy,

@@ -25,11 +25,22 @@ enum : int {
   // (the solve's inner primal loop lowers R_K while the other buckets may still be reading)
   R_KB = 349,
   // the solve buckets' date lists: record i holds at R_LIST + j the i-th date of bucket j (free
-  // sets <= 48, 64, 80, 96, 128); date 0's record holds the five counts at R_CNT (as 64-bit
-  // integers, appended by k_pg_form's atomics, cleared by k_pg_post<0>)
+  // sets <= 48, 64, 80, 96, 128, and PG_BIGB: the large free sets of k_pg_big); date 0's record
+  // holds the counts at R_CNT (as 64-bit integers, appended by k_pg_form's atomics, cleared by
+  // k_pg_post<0>)
   R_LIST = 352, R_CNT = 360
 };
-constexpr int PG_NBUCKET = 5;
+constexpr int PG_NBUCKET = 6;
+constexpr int PG_BIGB = 5;
+__device__ __forceinline__ unsigned long long pg_count(const double* rec, int bk) {
+  return reinterpret_cast<const unsigned long long*>(rec + R_CNT)[bk];
+}
+__device__ __forceinline__ int pg_listed(const double* rec, int bk, int i) {
+  return (int)rec[(int64_t)i * PGR + R_LIST + bk];
+}
+// grid of a grid-stride kernel over at most B items: the workgroups that fit on the device at
+// once (occupancy x CUs, queried once per kernel and device), at most B
+int resident_grid(const void* kernel, int block, int B);
 __device__ __forceinline__ int pg_bucket(int kb) {
   return kb <= 48 ? 0 : kb <= 64 ? 1 : kb <= 80 ? 2 : kb <= 96 ? 3 : 4;
 }
@@ -41,7 +52,7 @@ constexpr int PG_MGMAX = 32;   // general rows
 // variables as bordered rows (at most PG_WMB of them)
 constexpr int PG_WMB = 8;
 constexpr int PG_WG_MAX = 24;   // general rows of the wide mode
-static_assert(R_FXL + PG_WMB <= R_GFORM && R_KB < R_LIST && R_LIST + 5 <= R_CNT && R_CNT + 5 <= PQ_PG_RECORD,
+static_assert(R_FXL + PG_WMB <= R_GFORM && R_KB < R_LIST && R_LIST + 6 <= R_CNT && R_CNT + 6 <= PQ_PG_RECORD,
               "PQ_PG_RECORD too small");
 
 struct PGWork {   // per-date work layout: xs | xb | g | Px | Fl | rF | solx | pxb | U | fl

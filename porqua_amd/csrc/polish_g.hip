@@ -404,24 +404,23 @@ __device__ __forceinline__ void form_from_group(const pq_lowrank& lr, const pq_p
 // of k_pg_big (PG_KMAX < k <= PG_KBIG), formed here the same way -- every window chunk
 // gathered once for all tiles -- instead of one window pass per 64 x 64 tile
 template <int KF>
-__global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
-                                                int ldk, const int32_t* gdates, int ngroups,
-                                                const int32_t* urows_all, const int32_t* ucnt_all,
-                                                const int32_t* uoff, int umax, const double* scr) {
+__device__ __forceinline__ void pg_form_date(int b, const pq_lowrank& lr, const pq_problem& pb, const pq_state& st,
+                                             double* rec, int ldk, const int32_t* gdates, int ngroups,
+                                             const int32_t* urows_all, const int32_t* ucnt_all,
+                                             const int32_t* uoff, int umax, const double* scr) {
   constexpr int FPITK = KF + 4;                        // LDS pitch (doubles)
   constexpr int NCG = KF / 32;                         // gathered columns per thread and row
   constexpr int NTL = (KF / 16) * (KF / 16 + 1) / 2;   // lower 16 x 16 tiles
   constexpr int FTWK = (NTL + FNW - 1) / FNW;          // tiles per wave
   static_assert(KF != PG_KMAX || FTWK == FTW, "k_pg_form tiling");
   __shared__ __attribute__((aligned(16))) double S[2 * FKCH * FPITK];
-  const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;   // wide dates: polish_gw.hip
   const int k = (int)R[R_K];
   if (KF == PG_KMAX && threadIdx.x == 0) {   // the date joins its solve bucket's list
-    const int kb = (int)R[R_KB], kmax = ldk < PG_KMAX ? ldk : PG_KMAX;
-    if (kb >= 1 && kb <= kmax) {
-      const int bk = pg_bucket(kb);
+    const int kb = (int)R[R_KB], kmax = ldk < PG_KMAX ? ldk : PG_KMAX, kbig = ldk < PG_KBIG ? ldk : PG_KBIG;
+    if (kb >= 1 && kb <= kbig) {
+      const int bk = kb <= kmax ? pg_bucket(kb) : PG_BIGB;
       const unsigned long long i = atomicAdd(reinterpret_cast<unsigned long long*>(rec + R_CNT) + bk, 1ull);
       rec[(int64_t)i * PGR + R_LIST + bk] = (double)b;
     }
@@ -584,6 +583,26 @@ __global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq
         if (lower) K[(int64_t)gi * ldk + gj] = v;
         if (tI[j] != tJ[j]) K[(int64_t)gj * ldk + gi] = v;   // both triangles: column reads in the solve
       }
+    }
+  }
+}
+
+// KF = PG_KMAX: one workgroup per date (and the bucket lists' appends); KF = PG_KBIG: a
+// resident grid striding over the large free sets' list (most backtests have none: one
+// workgroup per date needed its 66 KB of LDS only to exit, behind the solves on the CUs)
+template <int KF>
+__global__ __launch_bounds__(FT) void k_pg_form(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                int ldk, const int32_t* gdates, int ngroups,
+                                                const int32_t* urows_all, const int32_t* ucnt_all,
+                                                const int32_t* uoff, int umax, const double* scr) {
+  if constexpr (KF == PG_KMAX) {
+    pg_form_date<KF>(blockIdx.x, lr, pb, st, rec, ldk, gdates, ngroups, urows_all, ucnt_all, uoff, umax, scr);
+  } else {
+    const int cnt = (int)pg_count(rec, PG_BIGB);
+    for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+      pg_form_date<KF>(pg_listed(rec, PG_BIGB, i), lr, pb, st, rec, ldk, gdates, ngroups, urows_all, ucnt_all,
+                       uoff, umax, scr);
+      __syncthreads();   // (LDS reused by the next date)
     }
   }
 }
@@ -1411,17 +1430,18 @@ __device__ __forceinline__ void pg_solve_date(int b, const pq_problem& pb, const
 #undef WSTAMP
 }
 
-// Workgroup i solves the i-th date of the bucket's list (k_pg_form appends them): the dates
-// are dispatched first and the surplus workgroups only read the count and exit -- with one
+// A resident grid strides over the bucket's list of dates (k_pg_form appends them) -- with one
 // workgroup per date, most of them read the record and exited, and each of those still needed
 // the full LDS triangle to be dispatched, so with the other buckets filling the CUs they
 // trickled in behind the dates
 template <int KS, int NW>
 __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st, double* rec, pq_settings s,
                                                       int ldk, int klo, int inner) {
-  const int i = blockIdx.x, bk = pg_bucket(KS);
-  if ((unsigned long long)i >= reinterpret_cast<const unsigned long long*>(rec + R_CNT)[bk]) return;
-  pg_solve_date<KS, NW>((int)rec[(int64_t)i * PGR + R_LIST + bk], pb, st, rec, s, ldk, klo, inner);
+  const int bk = pg_bucket(KS), cnt = (int)pg_count(rec, bk);
+  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    pg_solve_date<KS, NW>(pg_listed(rec, bk, i), pb, st, rec, s, ldk, klo, inner);
+    __syncthreads();   // (LDS reused by the next date)
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1436,10 +1456,9 @@ __global__ __launch_bounds__(64 * NW) void k_pg_solve(pq_problem pb, pq_state st
 // (exact P x, checks, scoring) then treat the date like every other.  The factor overwrites
 // the lower tiles of K, so the date's next round forms again (R_FORMED = 0).
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
-                                                 pq_settings s, int ldk, int kmin) {
+__device__ __forceinline__ void pg_big_date(int b, const pq_lowrank& lr, const pq_problem& pb, const pq_state& st,
+                                            double* rec, const pq_settings& s, int ldk, int kmin) {
   __shared__ __attribute__((aligned(16))) double smem[CHOL_LDS];   // exactly 80 KiB: 2 per CU
-  const int b = blockIdx.x;
   double* R = rec + (int64_t)b * PGR;
   if (R[R_STATE] != PQ_PG_PENDING || R[R_W] != 0.0) return;
   const int k = (int)R[R_K];
@@ -1711,6 +1730,16 @@ __global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, 
     R[31] += (double)k;
   }
 #undef BSTAMP
+}
+
+// a resident grid striding over the large free sets' list (k_pg_form<PG_KBIG>'s)
+__global__ __launch_bounds__(PT, 2) void k_pg_big(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
+                                                 pq_settings s, int ldk, int kmin) {
+  const int cnt = (int)pg_count(rec, PG_BIGB);
+  for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+    pg_big_date(pg_listed(rec, PG_BIGB, i), lr, pb, st, rec, s, ldk, kmin);
+    __syncthreads();   // (LDS reused by the next date)
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2335,11 +2364,14 @@ static void launch_solve_ks(int nw, int B, hipStream_t str, const pq_problem* pb
                             const pq_settings* s, int ldk, int klo) {
   const int inner = s->polish_inner > 0 ? s->polish_inner : 0;
   if (nw == 1)
-    hipLaunchKernelGGL((k_pg_solve<KS, 1>), dim3(B), dim3(64), 0, str, *pb, *st, rec, *s, ldk, klo, inner);
+    hipLaunchKernelGGL((k_pg_solve<KS, 1>), dim3(resident_grid((const void*)k_pg_solve<KS, 1>, 64, B)), dim3(64), 0,
+                       str, *pb, *st, rec, *s, ldk, klo, inner);
   else if (nw == 2)
-    hipLaunchKernelGGL((k_pg_solve<KS, 2>), dim3(B), dim3(128), 0, str, *pb, *st, rec, *s, ldk, klo, inner);
+    hipLaunchKernelGGL((k_pg_solve<KS, 2>), dim3(resident_grid((const void*)k_pg_solve<KS, 2>, 128, B)), dim3(128),
+                       0, str, *pb, *st, rec, *s, ldk, klo, inner);
   else
-    hipLaunchKernelGGL((k_pg_solve<KS, 4>), dim3(B), dim3(256), 0, str, *pb, *st, rec, *s, ldk, klo, inner);
+    hipLaunchKernelGGL((k_pg_solve<KS, 4>), dim3(resident_grid((const void*)k_pg_solve<KS, 4>, 256, B)), dim3(256),
+                       0, str, *pb, *st, rec, *s, ldk, klo, inner);
 }
 static void launch_solve(int bucket, int nw, int B, hipStream_t str, const pq_problem* pb, pq_state* st,
                          double* rec, const pq_settings* s, int ldk, int klo) {
@@ -2394,6 +2426,22 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
     used |= 1 << i;
     return side->s[i];
   };
+  // free sets of kmax + 1 .. kbig first (their P_FF, then the factor and solve): the longest
+  // solves when there are any, and a resident grid that only reads an empty list when there are
+  // none -- launched after the other buckets, its workgroups waited for their CUs to drain
+  if (kbig > kmax) {
+    static_assert(pq::PG_KBIG == 256, "k_pg_form<PG_KBIG> tiling");
+    const hipStream_t sb = on(6);
+    if (pq::group_form_big_min() > 0 && lr->mu == nullptr)   // from one union Gram per polish group
+      hipLaunchKernelGGL(pq::k_pg_form_grp_big, dim3(ngroups * pq::GBS), dim3(pq::FT), 0, sb, *lr, *pb, *st, rec,
+                         gdates, urows, ucnt, umax, pass_scratch, pq::group_form_big_min());
+    hipLaunchKernelGGL(pq::k_pg_form<pq::PG_KBIG>, dim3(pq::resident_grid((const void*)pq::k_pg_form<pq::PG_KBIG>,
+                                                                          pq::FT, B)),
+                       dim3(pq::FT), 0, sb, *lr, *pb, *st, rec, ldk, gdates, ngroups, urows, ucnt, uoff, umax,
+                       pass_scratch);
+    hipLaunchKernelGGL(pq::k_pg_big, dim3(pq::resident_grid((const void*)pq::k_pg_big, pq::PT, B)), dim3(pq::PT), 0,
+                       sb, *lr, *pb, *st, rec, *s, ldk, kmax);
+  }
   // the LDS solve's buckets beyond the register solve's (largest free sets first), and the
   // register solve's buckets in one launch
   const int nrt = pq::solve_rt() <= 0 ? 0 : (pq::solve_rt() >= 4 ? 4 : 3);   // register buckets 0 .. nrt - 1
@@ -2402,18 +2450,11 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
     if (i >= 2 && kmax <= KSB[i - 1]) continue;
     pq::launch_solve(i, pq::solve_waves(i), B, on(i), pb, st, rec, s, ldk, i ? KSB[i - 1] : 0);
   }
-  if (nrt > 0 && pq_pg_solve_rt_launch(nrt + 2, B, on(0), pb, st, rec, s, ldk)) return -1;
+  // (side stream 1: the streams are dealt round-robin over the process's hardware queues, four
+  // by default, so stream 0 shared one with the <= 128 bucket's stream 4 and the register
+  // solve waited for that kernel to finish)
+  if (nrt > 0 && pq_pg_solve_rt_launch(nrt + 2, B, on(1), pb, st, rec, s, ldk)) return -1;
   if (wide && pq_pg_wide_launch(lr, pb, st, rec, s, wide, on(5))) return -1;   // free sets beyond kmax
-  if (kbig > kmax) {   // free sets of kmax + 1 .. kbig: their P_FF, then the factor and solve
-    static_assert(pq::PG_KBIG == 256, "k_pg_form<PG_KBIG> tiling");
-    const hipStream_t sb = on(6);
-    if (pq::group_form_big_min() > 0 && lr->mu == nullptr)   // from one union Gram per polish group
-      hipLaunchKernelGGL(pq::k_pg_form_grp_big, dim3(ngroups * pq::GBS), dim3(pq::FT), 0, sb, *lr, *pb, *st, rec,
-                         gdates, urows, ucnt, umax, pass_scratch, pq::group_form_big_min());
-    hipLaunchKernelGGL(pq::k_pg_form<pq::PG_KBIG>, dim3(B), dim3(pq::FT), 0, sb, *lr, *pb, *st, rec, ldk, gdates,
-                       ngroups, urows, ucnt, uoff, umax, pass_scratch);
-    hipLaunchKernelGGL(pq::k_pg_big, dim3(B), dim3(pq::PT), 0, sb, *lr, *pb, *st, rec, *s, ldk, kmax);
-  }
   for (int i = 0; side && i < pq::PgSide::NS; ++i)
     if ((used & (1 << i)) && (hipEventRecord(side->join[i], side->s[i]) != hipSuccess ||
                               hipStreamWaitEvent(str, side->join[i], 0) != hipSuccess)) {
@@ -2428,4 +2469,26 @@ extern "C" int pq_polish_grouped_round(const pq_lowrank* lr, const pq_problem* p
                      pass_scratch);
   PQ_CHECK_LAUNCH("pq_polish_grouped_round");
   return 0;
+}
+
+// occupancy x CUs of a kernel, cached per (kernel, device); B when the query fails
+int pq::resident_grid(const void* kernel, int block, int B) {
+  struct Entry { const void* k; int dev, n; };
+  static Entry cache[64];
+  static int used = 0;
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return B;
+  std::lock_guard<std::mutex> lock(mu);
+  for (int i = 0; i < used; ++i)
+    if (cache[i].k == kernel && cache[i].dev == dev) return cache[i].n < B ? cache[i].n : B;
+  int per = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per <= 0 || cus <= 0) {
+    (void)hipGetLastError();
+    return B;
+  }
+  const int n = per * cus;
+  if (used < 64) cache[used++] = Entry{kernel, dev, n};
+  return n < B ? n : B;
 }

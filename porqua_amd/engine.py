@@ -783,7 +783,7 @@ def _band_setup(qb: QPBatch, lr: LowRank, strm, w_min: int = 0):
         C = qb.Cg[0, :mg, :n]
         return (C @ C.T).contiguous() if mg else torch.zeros((1, 1), dtype=F64, device=dev)
     cc = _cached(qb, "_c_cc", _tkey(qb.Cg), cgram, keep=(qb.Cg,))
-    return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc, "W": W}
+    return {"band": band, "ldo": ldo, "r0": r0, "pc": pc, "cc": cc, "W": W, "nrows": nrows}
 
 
 def _gcap_setup(qb: QPBatch, lr: "LowRank", ws: "Workspace", groups: "GroupPlan", settings: Settings):
@@ -1043,6 +1043,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         wmin = (max(gplan.span_max, groups.polish_plan().span_max) if (gcap_try or (grouped and wide_polish))
                 else 0)
         bd = tl("gram", lambda: _band_setup(qb, lr, strm, w_min=wmin))
+        ws.band_shape = (bd["nrows"], bd["W"]) if bd is not None else None   # (the bench's gram rate)
     gc = _gcap_setup(qb, lr, ws, gplan, settings or Settings()) if (gcap_try and bd is not None) else None
     ws.gcap_groups = gplan if gc is not None else None   # (the bench's roofline reads the plan used)
 
@@ -1340,8 +1341,6 @@ def slide_plan(rows, tlen, group: int = 32, smax: int = 64, smin: int = 1):
         # s = #rows of the previous window before the current window's first row; only
         # s <= smax can join, so the first smax + 1 columns decide it
         h = min(tmax, int(smax) + 1)
-        s = ((prev[:, :h] < cur[:, :1]) & (col[None, :h] < tp[:, None])).sum(1)
-        cand = (tp == tc) & (tc > 1) & (s >= smin) & (s <= smax)
         # windows that are one contiguous run of panel rows (no gap: last - first = T - 1)
         # of the same length, the current one starting exactly s rows after the previous one,
         # are that window shifted by s -- no element compare needed.  (Without the start check
@@ -1349,6 +1348,11 @@ def slide_plan(rows, tlen, group: int = 32, smax: int = 64, smin: int = 1):
         # would pass as identical.)
         last = rows[np.arange(B), np.maximum(tlen - 1, 0)]
         contig = (last - rows[:, 0]) == (tlen - 1)
+        if contig.all():   # (the same count from the window starts alone)
+            s = np.minimum(np.clip(cur[:, 0].astype(np.int64) - prev[:, 0], 0, tp), h)
+        else:
+            s = ((prev[:, :h] < cur[:, :1]) & (col[None, :h] < tp[:, None])).sum(1)
+        cand = (tp == tc) & (tc > 1) & (s >= smin) & (s <= smax)
         match = cand & contig[:-1] & contig[1:] & ((cur[:, 0] - prev[:, 0]) == s)
         need = cand & ~match
         for sv in np.unique(s[need]).tolist():   # rows[d][:T-s] == rows[d-1][s:T], per shift value
@@ -1415,6 +1419,11 @@ class GroupPlan:
         gmax = max(1, min(gmax, max(gmin, -(-B // (rounds * cus)))))
         self.ok = B > 0 and int(tlen.min()) >= 2 and int(tlen.max()) <= umax
         gs, sh = slide_plan(rows, tlen, group=gmax, smax=smax, smin=0)
+        # windows that are runs of consecutive panel rows, each joined one starting exactly its
+        # shift after its predecessor: every union is then a run too (the fast path below; a
+        # shift of a whole window or more joins disjoint windows, whose union has gaps)
+        contig_all = bool(B) and bool(((rows[np.arange(B), np.maximum(tlen - 1, 0)] - rows[:, 0]) == (tlen - 1)).all()
+                                      and ((sh[1:] == 0) | (rows[1:, 0] - rows[:-1, 0] == sh[1:])).all())
         groups = []
         # a slide group whose whole union fits (first window + every later shift <= umax) is
         # one date group; only the others are cut greedily, date by date
@@ -1458,19 +1467,26 @@ class GroupPlan:
             col0 = np.where(isfirst, 0, tlen - shd)
             cum = np.cumsum(shd)
             uoff[:] = cum - cum[gdates[:-1]][gof]                           # sum of shifts since the group start
-            estart = np.concatenate([[0], np.cumsum(cnt)])
-            tot = int(estart[-1])
-            dte = np.repeat(np.arange(B), cnt)
-            k = np.arange(tot) - estart[dte]
-            vals = rows[dte, col0[dte] + k]
-            gstart_e = estart[gdates[:-1]]                                  # first entry of each group
-            pos = np.arange(tot) - gstart_e[gof[dte]]
             cnts = np.add.reduceat(cnt, gdates[:-1]) if self.ngroups else np.zeros(0, np.int64)
             over = cnts > umax
             if over.any():
                 self.ok = False
-            keep = ~over[gof[dte]]
-            urows[gof[dte][keep], pos[keep]] = vals[keep]
+            g0 = gdates[:-1]
+            if contig_all:
+                # every window one run of consecutive panel rows (daily / monthly calendars
+                # without gaps): a group's union is the run from its first window's first row
+                u = np.arange(umax)[None, :]
+                urows[:] = np.where((u < cnts[:, None]) & ~over[:, None], rows[g0, 0][:, None] + u, 0)
+            else:
+                estart = np.concatenate([[0], np.cumsum(cnt)])
+                tot = int(estart[-1])
+                dte = np.repeat(np.arange(B), cnt)
+                k = np.arange(tot) - estart[dte]
+                vals = rows[dte, col0[dte] + k]
+                gstart_e = estart[g0]                                       # first entry of each group
+                pos = np.arange(tot) - gstart_e[gof[dte]]
+                keep = ~over[gof[dte]]
+                urows[gof[dte][keep], pos[keep]] = vals[keep]
             ucnt[:] = np.where(over, 0, cnts)
         self.sizes = np.diff(gdates)
         gidx = np.repeat(np.arange(max(self.ngroups, 0), dtype=np.int32), self.sizes) if B else np.zeros(0, np.int32)
