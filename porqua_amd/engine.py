@@ -1318,6 +1318,8 @@ def window_rows(dates: np.ndarray, rebdates, width: int):
     idx = first.astype(np.int32)[:, None] + j
     if len(wpos) != len(dates):
         idx = wpos[np.minimum(idx, len(wpos) - 1)]
+    if int(tlen.min()) == tmax:   # every window full (the usual backtest): nothing to mask
+        return idx.astype(np.int32, copy=False), tlen
     rows = idx * (j < tlen[:, None])
     return rows.astype(np.int32, copy=False), tlen
 
