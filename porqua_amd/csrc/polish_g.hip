@@ -310,7 +310,7 @@ __device__ __forceinline__ void form_from_group(const pq_lowrank& lr, const pq_p
                                                 double* R, int b, int k, int ldk, const int32_t* gdates,
                                                 int ngroups, const int32_t* urows_all, const int32_t* ucnt_all,
                                                 const int32_t* uoff, int umax, const double* scr, double* S) {
-  __shared__ int s_cu[GLD], s_pi[PG_KMAX];
+  __shared__ int s_cu[GLD], s_pi[PG_KMAX], s_fl[PG_KMAX], s_ou[GMO];
   __shared__ double s_gmu[GLD], s_d[PG_KMAX], s_s[PG_KMAX];
   const int ld = pb.ld;
   const int t = threadIdx.x;
@@ -323,31 +323,43 @@ __device__ __forceinline__ void form_from_group(const pq_lowrank& lr, const pq_p
   const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
   const double psw = ps * (lr.w_scale ? lr.w_scale[b] : 1.0);
   const double* mu = lr.mu ? lr.mu + (int64_t)b * lr.mu_stride : nullptr;
+  const int32_t* ur = urows_all + (int64_t)grp * umax;
+  // the independent reads of every list first (one memory round trip; the date's means at
+  // its free variables one more): union free list and centre, the date's free list, the union
+  // rows outside its window
+  double muF = 0.0;
   for (int c = t; c < nc; c += FT) {
     s_cu[c] = (int)Gs[GS_COL + c];
     s_gmu[c] = Gs[GS_MU + c];
   }
-  __syncthreads();
-  for (int p = t; p < k; p += FT) {   // union position of each free variable (s_cu ascending)
+  for (int p = t; p < k; p += FT) {
     const int i = wk.Fl[p];
+    s_fl[p] = i;
+    muF = mu ? mu[i] : 0.0;   // (k <= PG_KMAX <= FT: one free variable per thread)
+  }
+  for (int o = t; o < mo; o += FT) s_ou[o] = ur[o < off ? o : o + T];
+  __syncthreads();
+  // union position of each free variable (s_cu ascending) and the outside rows' raw values
+  if (t < k) {
+    const int i = s_fl[t];
     int a = 0, z = nc;
     while (z - a > 1) {
       const int mid = (a + z) >> 1;
       if (s_cu[mid] <= i) a = mid; else z = mid;
     }
-    s_pi[p] = a;
-    s_d[p] = (mu ? mu[i] : 0.0) - s_gmu[a];
+    s_pi[t] = a;
+    s_d[t] = muF - s_gmu[a];
+  }
+  const int nt = (k + 15) >> 4, kp = 16 * nt, mo4 = (mo + 3) & ~3;
+  for (int e = t; e < mo4 * kp; e += FT) {   // (zero beyond k, and whole zero rows up to mo4)
+    const int o = e / kp, p = e - o * kp;
+    S[e] = (o < mo && p < k) ? lr.panel[(int64_t)s_ou[o] * lr.ldp + s_fl[p]] : 0.0;
   }
   __syncthreads();
-  // outside rows x~_o (F columns) into S, pitch kp (zero beyond k, and whole zero rows up to a
-  // multiple of 4: the MFMA operands below read them unconditionally); s = union column sums -
-  // outside rows
-  const int32_t* ur = urows_all + (int64_t)grp * umax;
-  const int nt = (k + 15) >> 4, kp = 16 * nt, mo4 = (mo + 3) & ~3;
-  for (int e = t; e < mo4 * kp; e += FT) {
-    const int o = e / kp, p = e - o * kp;
-    const int u = o < off ? o : o + T;
-    S[e] = (o < mo && p < k) ? lr.panel[(int64_t)ur[u] * lr.ldp + wk.Fl[p]] - s_gmu[s_pi[p]] : 0.0;
+  // centred by the union's centre, and s = union column sums - outside rows
+  for (int e = t; e < mo * kp; e += FT) {
+    const int p = e % kp;
+    if (p < k) S[e] -= s_gmu[s_pi[p]];
   }
   __syncthreads();
   for (int p = t; p < k; p += FT) {
@@ -394,9 +406,16 @@ __device__ __forceinline__ void form_from_group(const pq_lowrank& lr, const pq_p
       }
     }
   }
-  for (int i = t; i < pb.n; i += FT) wk.posF[i] = -1;   // positions of the formed free list
-  __syncthreads();
-  for (int p = t; p < k; p += FT) wk.posF[wk.Fl[p]] = p;
+  // positions of the formed free list, in one pass (the free list is ascending: setup builds it
+  // in index order and the solves' inner steps compact it in order)
+  for (int i = t; i < pb.n; i += FT) {
+    int a = 0, z = k;
+    while (z - a > 1) {
+      const int mid = (a + z) >> 1;
+      if (s_fl[mid] <= i) a = mid; else z = mid;
+    }
+    wk.posF[i] = (k > 0 && s_fl[a] == i) ? a : -1;
+  }
   if (t == 0) R[R_FORMED] = 1.0;
 }
 
@@ -693,20 +712,20 @@ __global__ __launch_bounds__(FT) void k_pg_form_grp(pq_lowrank lr, pq_problem pb
     col[c] = p < nc ? s_col[p] : -1;
     mc[c] = p < nc ? s_gm[p] : 0.0;
   }
-  double v[4];
-  auto gather = [&](int t0) {   // (unconditional loads, as k_pg_form's gather)
+  // two chunks' gathers in flight (v1 for the next chunk, v2 for the one after): the chunk
+  // loop is bound by the gather latency, not by its MFMAs
+  double v1[4], v2[4];
+  auto gather = [&](double (&v)[4], int t0) {   // (unconditional loads, as k_pg_form's gather)
     const int tt = t0 + gr;
     const double* row = lr.panel + (int64_t)ur[tt < U ? tt : 0] * lr.ldp;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double x = row[col[c] >= 0 ? col[c] : 0];
-      v[c] = (x - mc[c]) * ((tt < U && col[c] >= 0) ? 1.0 : 0.0);
-    }
+    for (int c = 0; c < 4; ++c) v[c] = row[col[c] >= 0 ? col[c] : 0];
   };
-  auto put = [&](double* Sb) {
+  auto put = [&](const double (&v)[4], double* Sb, int t0) {   // centred and masked on the way to LDS
+    const int tt = t0 + gr;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      if (gc + 32 * c < kp) Sb[gr * FPIT + gc + 32 * c] = v[c];
+      if (gc + 32 * c < kp) Sb[gr * FPIT + gc + 32 * c] = (v[c] - mc[c]) * ((tt < U && col[c] >= 0) ? 1.0 : 0.0);
   };
   int tI[FTW], tJ[FTW];
 #pragma unroll
@@ -738,18 +757,22 @@ __global__ __launch_bounds__(FT) void k_pg_form_grp(pq_lowrank lr, pq_problem pb
   };
   double* S0 = S;
   double* S1 = S + FKCH * FPIT;
-  gather(0);
-  put(S0);
-  __syncthreads();
-  int buf = 0;
-  for (int t0 = 0; t0 < U; t0 += FKCH) {
-    const bool more = t0 + FKCH < U;
-    if (more) gather(t0 + FKCH);
-    mma(buf ? S1 : S0);
-    colsum(buf ? S1 : S0, t0);
-    if (more) put(buf ? S0 : S1);
+  // chunk t0 in LDS buffer sb; vr holds chunk t0 + FKCH (issued a step earlier), vi receives
+  // chunk t0 + 2 FKCH: each gather has two steps of MFMAs and stores to arrive
+  auto step = [&](int t0, double* sb, double* so, double (&vr)[4], double (&vi)[4]) {
+    if (t0 + 2 * FKCH < U) gather(vi, t0 + 2 * FKCH);
+    mma(sb);
+    colsum(sb, t0);
+    if (t0 + FKCH < U) put(vr, so, t0 + FKCH);
     __syncthreads();
-    buf ^= 1;
+  };
+  gather(v1, 0);
+  put(v1, S0, 0);
+  gather(v1, FKCH);
+  __syncthreads();
+  for (int t0 = 0; t0 < U; t0 += 2 * FKCH) {
+    step(t0, S0, S1, v1, v2);
+    if (t0 + FKCH < U) step(t0 + FKCH, S1, S0, v2, v1);
   }
   double* Gs = scr + (int64_t)grp * PQ_PG_PASS_SCRATCH;
 #pragma unroll

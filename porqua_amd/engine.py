@@ -108,10 +108,16 @@ class Settings:
     # and a larger eps cannot fall off that cliff.  Tracking (uncentred) windows keep eps_abs: their free
     # sets mostly exceed the LDS solve -- config 2 53.0k at 2e-3, 45.0k at 1e-2 from the loose
     # point, 50.1k with the resume; config 4 87.9k / 91.8k / 87.6k.  0 or <= eps_abs: off.
-    eps_grouped: float = 0.3
+    # Round 6, with the register-tile polish solve (profiles/r06p_*, r06q_*): (0.3, floor 8) ->
+    # 676-680k QPs/s (ADMM 2.90, polish 2.52-2.61 ms); (0.5 or 1.0, floor 7) -> 694-699k (7
+    # iterations: ADMM 2.56, polish 2.75 ms, 2.27 rounds, at most 4); floor 6 or 5 -> 525-560k
+    # (polish 5.0-5.3 ms: free sets beyond the register solve and up to 5 rounds).  So the loose
+    # stop is in effect a 7-iteration warm start of the polish for the centred windows
+    eps_grouped: float = 0.5
     # (host-side) the loose stop's pq_settings.min_iter.  Round 5 (profiles/r05T_config3_miniter_grid.log):
-    # 6 / 7 / 8 / 9 -> the same 8 iterations below 9 (eps 0.3 is first met at 8), 9 slower (569k)
-    min_iter_grouped: int = 8
+    # 6 / 7 / 8 / 9 -> the same 8 iterations below 9 (eps 0.3 is first met at 8), 9 slower (569k);
+    # round 6: 7 with eps 0.5 (above)
+    min_iter_grouped: int = 7
     # (host-side) the same loose stop for uncentred (tracking) windows on the group capacitance;
     # 0: off (they stop at eps_abs / eps_rel).  Measured on config 2 (profiles/r04T_*.log): off /
     # 1e-2 / 3e-2 / 1e-1 -> 161k / 151k / 142k / 114k QPs/s (20 / 17 / 15 / 13 iterations, 2.7 /

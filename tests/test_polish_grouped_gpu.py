@@ -173,7 +173,7 @@ def test_large_free_sets_from_the_group_gram(device):
 
 
 def test_loose_admm_stop_before_the_pipeline(device):
-    """Settings.eps_grouped (centred windows, default 0.3 with at least min_iter_grouped iterations): the ADMM stops early and the
+    """Settings.eps_grouped (centred windows, default 0.5 with at least min_iter_grouped = 7 iterations): the ADMM stops early and the
     pipeline's rounds finish the job -- the same optimum as from the eps_abs point, fewer
     ADMM iterations, every date SOLVED."""
     qb, lr, gp = _problem(device, 1000, 252, 48, 1.0)

@@ -62,6 +62,9 @@ def main():
         hist = np.histogram(kb[solved], bins=edges)[0]
         line += "; solve buckets " + " ".join(f"<={e}:{c}" for e, c in zip(edges[1:], hist))
         line += f", reused P_FF {int((R[solved, 7] != 0).sum())}"
+        # P_FF of this round: from the group Gram (R_GFORM = 348: polish group + 1) or a window pass
+        formed = solved & (R[:, 7] == 0) & (kb >= 1) & (kb <= 128)
+        line += f", formed from the group Gram {int((R[formed, 348] != 0).sum())} of {int(formed.sum())}"
         if prev_k is not None:
             was = prev_pend
             dk = k[was] - prev_k[was]
