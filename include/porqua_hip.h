@@ -306,6 +306,27 @@ int pq_admm_lr_grouped(const pq_lowrank* lr, const pq_problem* pb, pq_state* st,
  * sector-membership row per asset: nzmax = 2); the per-asset row sums of the updates then
  * read nzmax entries instead of mg.                                                      */
 
+/* Risk-aversion sweep form of the fused pq_admm_lr_grouped (admm_sweep.hip): group g holds
+ * problems [gdates[g], gdates[g+1]) (at most 64) that share ONE window and its centring (the
+ * risk-aversion row of a date: P_b = p_scale[b] w_scale[b] Xc'Xc, own rho and M_b^-1 each).
+ * An iteration is two chip-wide launches -- one workgroup per (group, 256-asset chunk) for
+ * pass 2, the updates, the next rhs and its pass-1 partial (the window chunk read once for
+ * all problems of the group), then one per problem for the M_b^-1 symv -- instead of one
+ * workgroup per group.  Same iterates as the fused pq_admm_lr_grouped up to summation
+ * order; one flag read between blocks of iterations.  Needs tmax <= 256, k_ld <= 256, shared
+ * general rows mg <= 4 with pc / cc (mg > 0), shared box rows, uniform ADMM diagonal, and
+ * scratch_doubles >= pq_sweep_scratch_doubles(n, batch, ngroups).  q_shared != 0: the problems
+ * of a group share q too (q_b = -mu_d for every risk aversion), read from the group's first
+ * problem.  Replaces
+ * qpsolvers.solve_problem (src/qp_problems.py:211-214) for the sweep of
+ * src/optimization.py:168-174 over risk aversions.                                       */
+int pq_admm_lr_sweep(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const double* Minv,
+                     int32_t k_ld, int64_t M_stride, const int32_t* gdates, int32_t ngroups,
+                     const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
+                     int32_t r0, const double* cc, int32_t q_shared, double* scratch, int64_t scratch_doubles,
+                     void* stream);
+int64_t pq_sweep_scratch_doubles(int32_t n, int32_t batch, int32_t ngroups);
+
 /* Group capacitance (admm_gcap.hip): the dates of each slide group (same T, same
  * c = p_scale w_scale, same p_diag, one shared rho grho[g]) share ONE capacitance matrix of
  * the union of their windows, M_U = I + W_U W_U' / d with W_U = [sqrt(c) X_U; sqrt(R) Cg]

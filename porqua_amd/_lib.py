@@ -176,6 +176,10 @@ _EXPORTS = {
                             c_dp, c_int32, c_int64, c_dp, c_int32, c_dp, c_dp, c_dp, c_int32,
                             ctypes.POINTER(PQSettings), c_int32, c_dp, c_int64, c_int32, c_dp, c_dp, c_dp,
                             c_int32, c_dp], c_int32),
+    "pq_admm_lr_sweep": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
+                          c_dp, c_int32, c_int64, c_dp, c_int32, ctypes.POINTER(PQSettings), c_int32, c_dp,
+                          c_int64, c_int32, c_dp, c_int32, c_dp, c_int64, c_dp], c_int32),
+    "pq_sweep_scratch_doubles": ([c_int32, c_int32, c_int32], c_int64),
     "pq_polish_lr_batched": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),
                               c_dp, c_int32, ctypes.POINTER(PQSettings), c_dp], c_int32),
     "pq_lr_capacitance": ([ctypes.POINTER(PQLowRank), ctypes.POINTER(PQProblem), ctypes.POINTER(PQState),

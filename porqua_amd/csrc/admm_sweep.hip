@@ -1,0 +1,815 @@
+// K3, risk-aversion-sweep form: the fused low-rank ADMM of k_admm_grp for groups of up to 64
+// problems that share ONE window (the risk-aversion row of a rebalance date, config 5:
+// P_b = 2 lam_b Sigma_d, q_b = -mu_d).
+//
+// k_admm_grp runs a group's iterations in one 512-thread workgroup: for config 5 that is 256
+// workgroups, one per CU, each streaming the date's 252 x 5000 window twice per iteration with
+// 8 waves -- latency-bound at 0.14 MFMA busy and 0.25 of HBM (profiles/r05t_config5_*).  Here
+// an iteration is two launches over the whole chip:
+//   k_sw_pass  one workgroup per (group, 256-asset chunk): pass 2 of iteration k
+//              (x~raw = X' Ut for the chunk's assets, all 64 problems as MFMA columns), the
+//              x / Px / z / y updates and residual terms of iteration k, the rhs of iteration
+//              k + 1 and its pass-1 partial W_chunk = X_chunk v (MFMA again) -- the window
+//              chunk is read once per iteration for all problems of the group;
+//   k_sw_mid   one workgroup per problem: the convergence test of iteration k from the chunk
+//              partials, W = sum of the chunk partials, u = M_b^-1 kw (the per-problem
+//              capacitance inverse, lower triangle), the pass-2 operand Ut and the general
+//              rows' update of iteration k + 1.
+// The rhs is never stored: k_sw_pass recomputes it from x, z, y (which it reads anyway) and
+// the previous general-row term, with the same expression that produced the pass-1 operand.
+// Per problem-iteration HBM bytes: x, Px, z, y read + write (64 n) + q (8 n) + M^-1
+// (8 k(k+1)/2) + window (8 T n / group size) + chunk partials.
+//
+// The iterates are those of k_admm_grp's fused form (FUSE) up to summation order: same
+// stopping rule, adaptive rho (NEED_REFACTOR), min_iter / max_iter and per-call iteration
+// budget.  Replaces qpsolvers.solve_problem (src/qp_problems.py:211-214) for the sweep's
+// batched solve (src/optimization.py:168-174 per risk aversion).
+#include "common.h"
+#include "capi_util.h"
+
+// (experiment builds only) PQ_SW_X = 1: no state traffic in the updates; 2: no MFMA passes
+#ifndef PQ_SW_X
+#define PQ_SW_X 0
+#endif
+
+namespace pq {
+namespace {
+
+constexpr int SW_T = 512;            // threads of the pass workgroup (8 waves)
+constexpr int SW_G = 64;             // problems per group (4 MFMA column tiles)
+constexpr int SW_K = 256;            // window rows (padded; T <= 256)
+constexpr int SW_SA = 16;            // assets per sub-chunk (one MFMA row tile)
+constexpr int SW_PX = SW_SA + 1;     // LDS pitch of the window slab
+constexpr int SW_CH = 256;           // assets per workgroup chunk
+constexpr int SW_PV = SW_G + 1;      // LDS pitch of the x~ / v slabs
+constexpr int SW_MG = 4;             // general rows (register-resident)
+constexpr int SW_MT = 256;           // threads of the mid workgroup
+constexpr int SR_N = 80;             // per-problem scalar record (doubles)
+constexpr int RP_N = 16;             // per-(chunk, problem) partial record (doubles)
+// scalar record
+enum {
+  S_RHO = 0, S_DINV, S_RB, S_SPS, S_SU, S_ACT, S_IT, S_END, S_STAT, S_QMAX, S_PD, S_ACT0,
+  S_RMV = 12,                        // 3: general-row residual terms of the next iteration
+  S_CW = 16, S_RGZ = 20, S_YG = 24, S_WG = 28, S_WGP = 32, S_ZG = 36, S_CGX = 40, S_CGV = 44,
+  S_RG = 48, S_LG = 52, S_UG = 56, S_CMU = 60, S_MUV = 64
+};
+// partial record: mode 1 (iteration) [0..5] residual maxima, [6] mu.v, [8..11] Cg.v;
+// mode 0 (prologue) [0] max |q|, [1..4] Cg.mu, [6] mu.v, [8..11] Cg.v, [12..15] Cg.x
+// per-problem LDS scalars of the pass kernel
+constexpr int SC_N = 4 + 5 * SW_MG;
+enum { C_DINV = 0, C_RB, C_SU, C_ACT, C_CW = 4, C_RGZ = 8, C_YG = 12, C_WG = 16, C_WGP = 20 };
+
+__device__ __forceinline__ double sw_grho(double l, double u, double rho, const pq_settings& s) {
+  if (l == u) return rho * s.eq_scale;
+  if (isinf(l) && isinf(u)) return s.rho_min;
+  return rho;
+}
+
+// reductions over the 16 lanes of a row (xor offsets < 16 stay inside it)
+__device__ __forceinline__ double qsum16(double v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double qmax16(double v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- per-problem setup (one thread per problem slot of every group) ------------------------
+__global__ __launch_bounds__(256) void k_sw_setup(pq_lowrank lr, pq_problem pb, pq_state st, pq_settings s,
+                                                  const int32_t* gdates, int ngroups, double* SR,
+                                                  int iters_call) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int grp = e / SW_G, g = e - grp * SW_G;
+  if (grp >= ngroups) return;
+  const int b0 = gdates[grp];
+  if (g >= gdates[grp + 1] - b0) return;
+  const int b = b0 + g;
+  double* R = SR + (int64_t)b * SR_N;
+  const int stt = st.status[b];
+  const int act = (stt == PQ_UNSOLVED || stt == PQ_NEED_REFACTOR);
+  const double rho = st.rho[b];
+  const double rb = pb.lb ? sw_grho(pb.lb[(int64_t)b * pb.box_stride], pb.ub[(int64_t)b * pb.box_stride], rho, s)
+                          : 0.0;
+  const double pd = pb.p_diag ? pb.p_diag[b] : 0.0;
+  const double ps = (pb.p_scale ? pb.p_scale[b] : 1.0) * (lr.w_scale ? lr.w_scale[b] : 1.0);
+  R[S_RHO] = rho;
+  R[S_DINV] = 1.0 / (s.sigma + pd + rb);
+  R[S_RB] = rb;
+  R[S_SPS] = sqrt(fmax(ps, 0.0));
+  R[S_SU] = 0.0;
+  R[S_ACT] = act;
+  R[S_ACT0] = act;
+  R[S_IT] = st.iters[b];
+  R[S_END] = min(s.max_iter, st.iters[b] + iters_call);
+  R[S_STAT] = stt;
+  R[S_PD] = pd;
+  for (int r = 0; r < 3; ++r) R[S_RMV + r] = 0.0;
+  for (int r = 0; r < SW_MG; ++r) {
+    double zg = 0, yg = 0, lgv = 0, ugv = 0, rg = 0;
+    if (r < pb.mg) {
+      zg = st.z[(int64_t)b * st.m_ld + r];
+      yg = st.y[(int64_t)b * st.m_ld + r];
+      lgv = pb.lg[(int64_t)b * pb.g_stride + r];
+      ugv = pb.ug[(int64_t)b * pb.g_stride + r];
+      rg = sw_grho(lgv, ugv, rho, s);
+    }
+    R[S_ZG + r] = zg;
+    R[S_YG + r] = yg;
+    R[S_LG + r] = lgv;
+    R[S_UG + r] = ugv;
+    R[S_RG + r] = rg;
+    R[S_WG + r] = rg * zg - yg;
+    R[S_WGP + r] = rg * zg - yg;
+    R[S_CW + r] = 0.0;
+    R[S_RGZ + r] = 0.0;
+    R[S_CGX + r] = 0.0;
+    R[S_CGV + r] = 0.0;
+    R[S_CMU + r] = 0.0;
+  }
+}
+
+// ---- the fused pass: [pass 2 + updates of iteration k] + rhs / pass 1 of iteration k + 1 ----
+// MODE 0: the prologue (rhs of the first iteration and its pass 1 only).  One 512-thread
+// workgroup per CU walks its chunk in 16-asset sub-chunks.  The window slab of a sub-chunk
+// (256 rows x 16 assets) is staged in LDS, where both passes read it, and the next slab and
+// the next sub-chunk's x / Px / z / y are loaded into registers while the current one
+// computes (a whole sub-chunk of MFMA and update work covers the HBM latency).
+//   pass 2: wave w = (column tile w >> 1, K half w & 1) -- Ut of its half in registers;
+//   update: thread t = (asset t & 15, problems (t >> 4) + 32 e), 16-lane reductions;
+//   pass 1: wave w owns window-row tiles 2w, 2w + 1 and all four column tiles.
+template <int MODE, int MGR>
+__global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, pq_state st, pq_settings s,
+                                                  const int32_t* gdates, int nch, const double* SR,
+                                                  const double* Ut, double* Wp, double* Rp, int q_shared) {
+  __shared__ __attribute__((aligned(16))) double Xs[2 * SW_K * SW_PX];   // window slabs [buf][u][asset]
+  __shared__ __attribute__((aligned(16))) double XV[2 * SW_SA * SW_PV];  // x~ of the two K halves; half 0 then v
+  __shared__ double p_sc[SW_G * SC_N];
+  __shared__ double p_red[SW_G * RP_N];
+  __shared__ int s_row[SW_K];
+  __shared__ int s_any;
+
+  const int slot = xcd_slot(blockIdx.x, gridDim.x);
+  const int grp = slot / nch, ch = slot - grp * nch;
+  const int b0 = gdates[grp];
+  const int G = gdates[grp + 1] - b0;
+  const int t = threadIdx.x;
+  const int n = pb.n, ld = pb.ld, mg = pb.mg, tmax = lr.tmax;
+  const int T = lr.tlen[b0];
+  const double sigma = s.sigma, alpha = s.alpha;
+
+  if (t < SW_G) {
+    const int g = t;
+    double* sc = p_sc + g * SC_N;
+    if (g < G) {
+      const double* R = SR + (int64_t)(b0 + g) * SR_N;
+      sc[C_DINV] = R[S_DINV];
+      sc[C_RB] = R[S_RB];
+      sc[C_SU] = R[S_SU];
+      sc[C_ACT] = R[S_ACT];
+#pragma unroll
+      for (int r = 0; r < SW_MG; ++r) {
+        sc[C_CW + r] = R[S_CW + r];
+        sc[C_RGZ + r] = R[S_RGZ + r];
+        sc[C_YG + r] = R[S_YG + r];
+        sc[C_WG + r] = R[S_WG + r];
+        sc[C_WGP + r] = R[S_WGP + r];
+      }
+    } else {
+      for (int e = 0; e < SC_N; ++e) sc[e] = 0.0;
+    }
+  }
+  for (int e = t; e < SW_G * RP_N; e += SW_T) p_red[e] = 0.0;
+  for (int u = t; u < SW_K; u += SW_T) s_row[u] = u < T ? lr.rows[(int64_t)b0 * tmax + u] : -1;
+  __syncthreads();
+  if (t == 0) {
+    int any = 0;
+    for (int g = 0; g < G; ++g) any |= p_sc[g * SC_N + C_ACT] != 0.0;
+    s_any = any;
+  }
+  __syncthreads();
+  if (!s_any) return;   // uniform: nothing left to iterate in this group
+
+  const int w = t >> 6, l = t & 63;
+  const int m16 = l & 15, k4 = l >> 4;
+  const double* __restrict__ panel = lr.panel;
+  const int64_t ldp = lr.ldp;
+  const int c0 = ch * SW_CH;
+  const int c1 = min(c0 + SW_CH, n);
+
+  // pass-2 operand: wave w holds Ut[128 kh + 4 s + k4][16 gt + m16], s < 32
+  const int kh = w & 1, gt = w >> 1;
+  double ut[32];
+  if constexpr (MODE == 1) {
+    const double* Ug = Ut + (int64_t)grp * SW_K * SW_G;
+#pragma unroll
+    for (int s2 = 0; s2 < 32; ++s2) ut[s2] = Ug[(128 * kh + 4 * s2 + k4) * SW_G + 16 * gt + m16];
+  }
+  (void)ut;
+
+  f64x4 wacc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wacc[a][c] = f64x4{0.0, 0.0, 0.0, 0.0};
+
+  // slab loader: thread t -> window row t >> 1, assets 8 (t & 1) .. + 8 of the sub-chunk
+  const int lrow = t >> 1, lhalf = t & 1;
+  const int lr_id = s_row[lrow];
+  const double* lsrc = panel + (int64_t)(lr_id < 0 ? 0 : lr_id) * ldp + 8 * lhalf;
+  double sl[8];
+  auto slab_load = [&](int i0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ia = i0 + 8 * lhalf + e;
+      sl[e] = (lr_id >= 0 && ia < n) ? lsrc[i0 + e] : 0.0;
+    }
+  };
+  auto slab_store = [&](int buf) {
+    double* d = Xs + buf * (SW_K * SW_PX) + lrow * SW_PX + 8 * lhalf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = sl[e];
+  };
+
+  // update roles: asset i0 + (t & 15), problems g = (t >> 4) + 32 e
+  const int ui = t & 15, ug = t >> 4;
+  const double* mu0 = lr.mu ? lr.mu + (int64_t)b0 * lr.mu_stride : nullptr;
+  const double* Cg0 = mg ? pb.Cg : nullptr;   // shared rows (host-checked Cg_stride == 0)
+  double px_[2], x_[2], zb_[2], yb_[2], q_[2];
+  auto state_load = [&](int i0) {
+    const int ia = i0 + ui;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int g = ug + 32 * e;
+      const bool ok = g < G && ia < n && p_sc[g * SC_N + C_ACT] != 0.0;
+      const int b = b0 + (g < G ? g : 0);
+      x_[e] = ok ? st.x[(int64_t)b * ld + ia] : 0.0;
+      zb_[e] = ok ? st.z[(int64_t)b * st.m_ld + st.mg_pad + ia] : 0.0;
+      yb_[e] = ok ? st.y[(int64_t)b * st.m_ld + st.mg_pad + ia] : 0.0;
+      px_[e] = (MODE == 1 && ok) ? st.Px[(int64_t)b * ld + ia] : 0.0;
+      q_[e] = ok ? pb.q[(int64_t)(q_shared ? b0 : b) * pb.q_stride + ia] : 0.0;
+    }
+  };
+
+  slab_load(c0);
+  slab_store(0);
+  state_load(c0);
+  __syncthreads();
+  int cur = 0;
+  for (int i0 = c0; i0 < c1; i0 += SW_SA) {
+    const bool more = i0 + SW_SA < c1;
+    if (more) slab_load(i0 + SW_SA);   // lands during this sub-chunk; stored at its end
+    const double* X = Xs + cur * (SW_K * SW_PX);
+
+    if constexpr (MODE == 1) {
+      // ---- pass 2: x~raw[i][g] = sum_u X[u][i] Ut[u][g] over this wave's K half ----------
+      f64x4 xa = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s2 = 0; s2 < 32; ++s2)
+        xa = __builtin_amdgcn_mfma_f64_16x16x4f64(X[(128 * kh + 4 * s2 + k4) * SW_PX + m16], ut[s2], xa, 0, 0, 0);
+      double* xv = XV + kh * (SW_SA * SW_PV);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xv[(k4 + 4 * r) * SW_PV + 16 * gt + m16] = xa[r];
+      __syncthreads();
+    }
+
+    // ---- per-element updates (MODE 1) / first rhs (MODE 0); v = rhs / c into half 0 ---------
+    {
+      const int ia = i0 + ui;
+      const bool inb = ia < n;
+      const double mui = (mu0 && inb) ? mu0[ia] : 0.0;
+      const double lo = inb ? pb.lb[ia] : 0.0, up = inb ? pb.ub[ia] : 0.0;   // (uniform box rows)
+      double cgi[MGR > 0 ? MGR : 1];
+#pragma unroll
+      for (int r = 0; r < (MGR > 0 ? MGR : 1); ++r) cgi[r] = (r < mg && inb) ? Cg0[(int64_t)r * ld + ia] : 0.0;
+      double xs[2], zs[2], ys[2], pxs[2], qs[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        xs[e] = x_[e];
+        zs[e] = zb_[e];
+        ys[e] = yb_[e];
+        pxs[e] = px_[e];
+        qs[e] = q_[e];
+      }
+      if (more) state_load(i0 + SW_SA);   // the next sub-chunk's state, in flight from here
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int g = ug + 32 * e;
+        const double* sc = p_sc + g * SC_N;
+        const bool act = sc[C_ACT] != 0.0;   // (0 for g >= G)
+        const int b = b0 + (g < G ? g : 0);
+        double v = 0.0;
+        double red[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) red[k] = 0.0;
+        double cgx[MGR > 0 ? MGR : 1];
+#pragma unroll
+        for (int r = 0; r < (MGR > 0 ? MGR : 1); ++r) cgx[r] = 0.0;
+        if (act && inb) {
+          const double qi = qs[e], x = xs[e], zb = zs[e], yb = ys[e];
+          const double rb = sc[C_RB], dinv = sc[C_DINV];
+          // this iteration's rhs (the expression that produced the pass-1 operand)
+          double cgwp = 0.0;
+#pragma unroll
+          for (int r = 0; r < MGR; ++r) cgwp = fma(cgi[r], sc[C_WGP + r], cgwp);
+          double rr0 = sigma * x - qi + cgwp;
+          rr0 += rb * zb - yb;
+          if constexpr (MODE == 0) {
+            v = rr0 * dinv;
+            red[0] = fabs(qi);
+#pragma unroll
+            for (int r = 0; r < MGR; ++r) {
+              red[1 + r] = cgi[r] * mui;
+              red[8 + r] = cgi[r] * v;
+              cgx[r] = cgi[r] * x;
+            }
+            red[6] = mui * v;
+          } else {
+            const double px = pxs[e];
+            const double xr = XV[ui * SW_PV + g] + XV[SW_SA * SW_PV + ui * SW_PV + g];
+            double corr = xr - sc[C_SU] * mui;
+#pragma unroll
+            for (int r = 0; r < MGR; ++r) corr = fma(sc[C_CW + r], cgi[r], corr);
+            const double xt = (rr0 - corr) * dinv;
+            double pxt = rr0 - sigma * xt - rb * xt;
+            double cgy = 0.0, cgw = 0.0;
+#pragma unroll
+            for (int r = 0; r < MGR; ++r) {
+              pxt -= cgi[r] * sc[C_RGZ + r];
+              cgy = fma(cgi[r], sc[C_YG + r], cgy);
+              cgw = fma(cgi[r], sc[C_WG + r], cgw);
+            }
+            const double xn = alpha * xt + (1.0 - alpha) * x;
+            const double pxn = alpha * pxt + (1.0 - alpha) * px;
+            double rr = sigma * xn - qi + cgw;
+            const double zh = alpha * xt + (1.0 - alpha) * zb;
+            const double zn = fmin(fmax(zh + yb / rb, lo), up);
+            const double yn = yb + rb * (zh - zn);
+#if PQ_SW_X != 1
+            st.z[(int64_t)b * st.m_ld + st.mg_pad + ia] = zn;
+            st.y[(int64_t)b * st.m_ld + st.mg_pad + ia] = yn;
+            st.x[(int64_t)b * ld + ia] = xn;
+            st.Px[(int64_t)b * ld + ia] = pxn;
+#endif
+            rr += rb * zn - yn;
+            red[0] = fabs(xn - zn);
+            red[1] = fabs(xn);
+            red[2] = fabs(zn);
+            const double cy = yn + cgy;
+            red[3] = fabs((pxn + qi + yn) + (cy - yn));
+            red[4] = fabs(pxn);
+            red[5] = fabs(cy);
+            v = rr * dinv;
+            red[6] = mui * v;
+#pragma unroll
+            for (int r = 0; r < MGR; ++r) red[8 + r] = cgi[r] * v;
+          }
+        }
+        XV[ui * SW_PV + g] = v;   // the element this thread read (half 0), now v
+        // 16-lane reductions (the lanes of a row share problem g); one owner per g
+        double* pr = p_red + g * RP_N;
+        if constexpr (MODE == 1) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) red[k] = qmax16(red[k]);
+          red[6] = qsum16(red[6]);
+#pragma unroll
+          for (int r = 0; r < MGR; ++r) red[8 + r] = qsum16(red[8 + r]);
+          if (ui == 0) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) pr[k] = fmax(pr[k], red[k]);
+            pr[6] += red[6];
+#pragma unroll
+            for (int r = 0; r < MGR; ++r) pr[8 + r] += red[8 + r];
+          }
+        } else {
+          red[0] = qmax16(red[0]);
+          red[6] = qsum16(red[6]);
+#pragma unroll
+          for (int r = 0; r < MGR; ++r) {
+            red[1 + r] = qsum16(red[1 + r]);
+            red[8 + r] = qsum16(red[8 + r]);
+            cgx[r] = qsum16(cgx[r]);
+          }
+          if (ui == 0) {
+            pr[0] = fmax(pr[0], red[0]);
+            pr[6] += red[6];
+#pragma unroll
+            for (int r = 0; r < MGR; ++r) {
+              pr[1 + r] += red[1 + r];
+              pr[8 + r] += red[8 + r];
+              pr[12 + r] += cgx[r];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- pass 1: W[u][g] += sum_i X[u][i] v[i][g] (window-row tiles 2w, 2w + 1) -------------
+#pragma unroll
+    for (int s2 = 0; s2 < SW_SA / 4; ++s2) {
+      const int ii = 4 * s2 + k4;
+      const double a0 = X[(32 * w + m16) * SW_PX + ii];
+      const double a1 = X[(32 * w + 16 + m16) * SW_PX + ii];
+      const double* vrow = XV + ii * SW_PV + m16;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double bv = vrow[16 * c];
+        wacc[0][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv, wacc[0][c], 0, 0, 0);
+        wacc[1][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv, wacc[1][c], 0, 0, 0);
+      }
+    }
+    if (more) slab_store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- chunk partials: W (problem-major rows of SW_K) and the per-problem sums --------------
+  {
+    double* wp = Wp + ((int64_t)(grp * nch + ch) * SW_G) * SW_K;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wp[(16 * c + m16) * SW_K + 32 * w + 16 * a + k4 + 4 * r] = wacc[a][c][r];
+    double* rp = Rp + ((int64_t)(grp * nch + ch) * SW_G) * RP_N;
+    for (int e = t; e < SW_G * RP_N; e += SW_T) rp[e] = p_red[e];
+  }
+}
+
+// ---- per problem: convergence of iteration k, W, u = M^-1 kw, Ut, general rows of k + 1 -----
+template <int MODE, int MGR>
+__global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, pq_settings s,
+                                                  const int32_t* gdates, int nch, double* SR, double* Ut,
+                                                  const double* Wp, const double* Rp, const double* Minv_all,
+                                                  int k_ld, int64_t M_stride, const double* pc, int64_t ldpc,
+                                                  int r0, const double* cc) {
+  __shared__ double kw[SW_K + 8];
+  __shared__ double uv[SW_K + 8];
+  __shared__ double s_dot[SW_K + 8];
+  __shared__ double s_part[4 * SW_K];
+  __shared__ double red[RP_N];
+  __shared__ double s_red[8];
+  __shared__ int s_cont;
+
+  const int grp = blockIdx.x / SW_G, g = blockIdx.x - grp * SW_G;
+  const int b0 = gdates[grp];
+  if (g >= gdates[grp + 1] - b0) return;
+  const int b = b0 + g;
+  double* R = SR + (int64_t)b * SR_N;
+  if (R[S_ACT] == 0.0) return;   // uniform
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  const int mg = pb.mg, tmax = lr.tmax, T = lr.tlen[b0];
+  const int k = tmax + mg;
+
+  // chunk partials of this problem, in chunk order
+  if (t < RP_N) {   // four chunks' loads in flight at a time, combined in chunk order
+    const bool is_max = MODE == 1 ? t < 6 : t == 0;
+    const double* rp = Rp + ((int64_t)grp * nch * SW_G + g) * RP_N + t;
+    const int64_t cs = (int64_t)SW_G * RP_N;
+    double a = 0.0;
+    int c = 0;
+    for (; c + 4 <= nch; c += 4) {
+      const double v0 = rp[c * cs], v1 = rp[(c + 1) * cs], v2 = rp[(c + 2) * cs], v3 = rp[(c + 3) * cs];
+      a = is_max ? fmax(fmax(fmax(fmax(a, v0), v1), v2), v3) : (((a + v0) + v1) + v2) + v3;
+    }
+    for (; c < nch; ++c) {
+      const double v = rp[c * cs];
+      a = is_max ? fmax(a, v) : a + v;
+    }
+    red[t] = a;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int cont = 1;
+    if constexpr (MODE == 1) {
+      const double mv0 = fmax(red[0], R[S_RMV + 0]), mv1 = fmax(red[1], R[S_RMV + 1]),
+                   mv2 = fmax(red[2], R[S_RMV + 2]);
+      const double mv3 = red[3], mv4 = red[4], mv5 = red[5], mv6 = R[S_QMAX];
+      const double rho = R[S_RHO];
+      const int it = (int)R[S_IT] + 1;
+      int stat = PQ_UNSOLVED;
+      const double eps_p = s.eps_abs + s.eps_rel * fmax(mv1, mv2);
+      const double eps_d = s.eps_abs + s.eps_rel * fmax(mv4, fmax(mv5, mv6));
+      double rnew = rho;
+      if (it >= s.min_iter && mv0 <= eps_p && mv3 <= eps_d) {
+        stat = PQ_SOLVED;
+      } else if (s.adapt_interval > 0 && it % s.adapt_interval == 0) {
+        const double rp = mv0 / (fmax(mv1, mv2) + 1e-30);
+        const double rd = mv3 / (fmax(mv4, fmax(mv5, mv6)) + 1e-30);
+        double rn = rho * sqrt(rp / (rd + 1e-30));
+        rn = fmin(fmax(rn, s.rho_min), s.rho_max);
+        if (rn > rho * s.adapt_tol || rn < rho / s.adapt_tol) {
+          rnew = rn;
+          stat = PQ_NEED_REFACTOR;
+        }
+      }
+      if (stat == PQ_UNSOLVED && it >= s.max_iter) stat = PQ_MAX_ITER;
+      cont = (stat == PQ_UNSOLVED) && it < (int)R[S_END];
+      R[S_IT] = it;
+      R[S_RHO] = rnew;
+      R[S_STAT] = stat;
+      R[S_ACT] = cont;
+      R[S_MUV] = red[6];
+#pragma unroll
+      for (int r = 0; r < SW_MG; ++r)
+        if (r < mg) R[S_CGV + r] = red[8 + r];
+    } else {
+      R[S_QMAX] = red[0];
+      R[S_MUV] = red[6];
+#pragma unroll
+      for (int r = 0; r < SW_MG; ++r)
+        if (r < mg) {
+          R[S_CMU + r] = red[1 + r];
+          R[S_CGV + r] = red[8 + r];
+          R[S_CGX + r] = red[12 + r];
+        }
+    }
+    s_cont = cont;
+  }
+  __syncthreads();
+  if (!s_cont) return;
+
+  const double sps = R[S_SPS], muv = red[6], dinv = R[S_DINV];
+  (void)dinv;
+  // kw = [sps (W - mu.v) over the window rows | sqrt(rho_r) Cg_r.v]
+  for (int j = t; j < SW_K; j += SW_MT) {
+    double a = 0.0;
+    if (j < T) {   // the chunk partials in chunk order, four loads in flight
+      const double* wp = Wp + ((int64_t)grp * nch * SW_G + g) * SW_K + j;
+      const int64_t cs = (int64_t)SW_G * SW_K;
+      double W = 0.0;
+      int c = 0;
+      for (; c + 4 <= nch; c += 4) {
+        const double v0 = wp[c * cs], v1 = wp[(c + 1) * cs], v2 = wp[(c + 2) * cs], v3 = wp[(c + 3) * cs];
+        W = (((W + v0) + v1) + v2) + v3;
+      }
+      for (; c < nch; ++c) W += wp[c * cs];
+      a = sps * (W - muv);
+    } else if (j >= tmax && j < k) {
+      a = sqrt(R[S_RG + (j - tmax)]) * red[8 + (j - tmax)];
+    }
+    kw[j] = a;
+  }
+  __syncthreads();
+
+  // u = M^-1 kw (lower triangle, row pitch k_ld): rows j = w + 4 e; lane l holds columns
+  // l + 64 q -- a dot part per row (its entries c <= j) and an axpy part (c < j) in registers
+  {
+    const double* Mi = Minv_all + (int64_t)b * M_stride;
+    double rv[4], acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = l + 64 * q;
+      rv[q] = c < k ? kw[c] : 0.0;
+      acc[q] = 0.0;
+    }
+    constexpr int RU = 4;
+    double m0[RU][4], m1[RU][4];
+    auto rload = [&](double (&M)[RU][4], int j0) {
+#pragma unroll
+      for (int e = 0; e < RU; ++e) {
+        const int j = j0 + 4 * e;
+        const double* rp = Mi + (int64_t)(j < k ? j : 0) * k_ld;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = l + 64 * q;
+          M[e][q] = (j < k && c <= j) ? rp[c] : 0.0;
+        }
+      }
+    };
+    auto rblock = [&](const double (&M)[RU][4], int j0) {
+      double dd[RU];
+#pragma unroll
+      for (int e = 0; e < RU; ++e) {
+        const int j = j0 + 4 * e;
+        const double a = j < k ? kw[j] : 0.0;
+        double sd = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = l + 64 * q;
+          sd = fma(M[e][q], rv[q], sd);
+          acc[q] = fma(a, c < j ? M[e][q] : 0.0, acc[q]);
+        }
+        dd[e] = sd;
+      }
+#pragma unroll
+      for (int e = 0; e < RU; ++e) dd[e] = wave_sum(dd[e]);
+      if (l == 0) {
+#pragma unroll
+        for (int e = 0; e < RU; ++e) {
+          const int j = j0 + 4 * e;
+          if (j < k) s_dot[j] = dd[e];
+        }
+      }
+    };
+    rload(m0, w);
+    for (int j0 = w; j0 < k; j0 += 8 * RU) {
+      rload(m1, j0 + 4 * RU);
+      rblock(m0, j0);
+      rload(m0, j0 + 8 * RU);
+      rblock(m1, j0 + 4 * RU);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s_part[w * SW_K + l + 64 * q] = acc[q];
+  }
+  __syncthreads();
+  for (int c = t; c < SW_K; c += SW_MT) {
+    double u = 0.0;
+    if (c < k) {
+      u = s_dot[c];
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) u += s_part[ww * SW_K + c];
+    }
+    uv[c] = u;
+  }
+  __syncthreads();
+
+  // Ut column of this problem (zero outside the window rows), su, Cg x~ terms
+  double su = 0.0, pcu[SW_MG] = {0.0, 0.0, 0.0, 0.0};
+  {
+    double* Ug = Ut + (int64_t)grp * SW_K * SW_G;
+    for (int j = t; j < SW_K; j += SW_MT) {
+      const double uu = j < T ? sps * uv[j] : 0.0;
+      Ug[j * SW_G + g] = uu;
+      su += uu;
+      if (j < T) {
+        const int row = lr.rows[(int64_t)b0 * tmax + j];
+#pragma unroll
+        for (int r = 0; r < MGR; ++r)
+          if (r < mg) pcu[r] = fma(pc[(int64_t)(row - r0) * ldpc + r], uu, pcu[r]);
+      }
+    }
+  }
+  su = wave_sum(su);
+#pragma unroll
+  for (int r = 0; r < MGR; ++r) pcu[r] = wave_sum(pcu[r]);
+  if (l == 0) {
+    s_part[w] = su;
+#pragma unroll
+    for (int r = 0; r < MGR; ++r) s_part[4 + 4 * r + w] = pcu[r];
+  }
+  __syncthreads();
+  if (t == 0) {
+    double sut = 0.0;
+    for (int ww = 0; ww < 4; ++ww) sut += s_part[ww];
+    R[S_SU] = sut;
+    double cw[SW_MG] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < MGR; ++r) {
+      const double rg = R[S_RG + r];
+      cw[r] = r < mg ? sqrt(rg) * uv[tmax + r] : 0.0;
+      R[S_CW + r] = cw[r];
+    }
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+#pragma unroll
+    for (int r = 0; r < MGR; ++r) {
+      if (r >= mg) break;
+      double a = 0.0;
+      for (int ww = 0; ww < 4; ++ww) a += s_part[4 + 4 * r + ww];
+      double cwr = 0.0;
+      for (int r2 = 0; r2 < mg; ++r2) cwr = fma(cc[r * mg + r2], cw[r2], cwr);
+      const double zt = R[S_CGV + r] - dinv * (a - sut * R[S_CMU + r] + cwr);
+      const double rg = R[S_RG + r], zg = R[S_ZG + r], yg = R[S_YG + r];
+      const double zh = s.alpha * zt + (1.0 - s.alpha) * zg;
+      const double zn = fmin(fmax(zh + yg / rg, R[S_LG + r]), R[S_UG + r]);
+      const double yn = yg + rg * (zh - zn);
+      const double cx = s.alpha * zt + (1.0 - s.alpha) * R[S_CGX + r];
+      m0 = fmax(m0, fabs(cx - zn));
+      m1 = fmax(m1, fabs(cx));
+      m2 = fmax(m2, fabs(zn));
+      R[S_RGZ + r] = rg * zt;
+      R[S_ZG + r] = zn;
+      R[S_YG + r] = yn;
+      R[S_CGX + r] = cx;
+      R[S_WGP + r] = R[S_WG + r];
+      R[S_WG + r] = rg * zn - yn;
+    }
+    R[S_RMV + 0] = m0;
+    R[S_RMV + 1] = m1;
+    R[S_RMV + 2] = m2;
+  }
+}
+
+// ---- any problem still iterating (one workgroup) ---------------------------------------------
+__global__ __launch_bounds__(256) void k_sw_any(const int32_t* gdates, int ngroups, const double* SR, int* flag) {
+  __shared__ int s_a;
+  if (threadIdx.x == 0) s_a = 0;
+  __syncthreads();
+  const int b0 = gdates[0], b1 = gdates[ngroups];
+  int a = 0;
+  for (int b = b0 + threadIdx.x; b < b1; b += 256) a |= SR[(int64_t)b * SR_N + S_ACT] != 0.0;
+  if (a) s_a = 1;   // benign race: every writer stores 1
+  __syncthreads();
+  if (threadIdx.x == 0) flag[0] = s_a;
+}
+
+// ---- write back the per-problem scalars and the general rows -----------------------------
+__global__ __launch_bounds__(256) void k_sw_final(pq_problem pb, pq_state st, const int32_t* gdates, int ngroups,
+                                                  const double* SR) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int grp = e / SW_G, g = e - grp * SW_G;
+  if (grp >= ngroups) return;
+  const int b0 = gdates[grp];
+  if (g >= gdates[grp + 1] - b0) return;
+  const int b = b0 + g;
+  const double* R = SR + (int64_t)b * SR_N;
+  if (R[S_ACT0] != 0.0) {
+    st.iters[b] = (int)R[S_IT];
+    st.status[b] = (int)R[S_STAT];
+    st.rho[b] = R[S_RHO];
+  }
+  for (int r = 0; r < pb.mg; ++r) {
+    st.z[(int64_t)b * st.m_ld + r] = R[S_ZG + r];
+    st.y[(int64_t)b * st.m_ld + r] = R[S_YG + r];
+  }
+}
+
+}  // namespace
+}  // namespace pq
+
+// Scratch of pq_admm_lr_sweep in doubles (per-problem records, chunk partials, Ut, a flag).
+extern "C" int64_t pq_sweep_scratch_doubles(int32_t n, int32_t batch, int32_t ngroups) {
+  const int64_t nch = (n + pq::SW_CH - 1) / pq::SW_CH;
+  return (int64_t)batch * pq::SR_N + (int64_t)ngroups * nch * pq::SW_G * (pq::SW_K + pq::RP_N) +
+         (int64_t)ngroups * pq::SW_K * pq::SW_G + 64;
+}
+
+extern "C" int pq_admm_lr_sweep(const pq_lowrank* lr, const pq_problem* pb, pq_state* st, const double* Minv,
+                                int32_t k_ld, int64_t M_stride, const int32_t* gdates, int32_t ngroups,
+                                const pq_settings* s, int32_t iters_this_call, const double* pc, int64_t ldpc,
+                                int32_t r0, const double* cc, int32_t q_shared, double* scratch,
+                                int64_t scratch_doubles, void* stream) {
+  PQ_CHECK_ARG(lr && pb && st && s && Minv && gdates && scratch, "pq_admm_lr_sweep: null argument");
+  PQ_CHECK_ARG(lr->panel && lr->rows && lr->tlen && lr->tmax > 0 && lr->tmax <= pq::SW_K,
+               "pq_admm_lr_sweep: needs a window of at most %d rows (tmax=%d)", pq::SW_K, lr->tmax);
+  PQ_CHECK_ARG(pb->mg >= 0 && pb->mg <= pq::SW_MG && (pb->mg == 0 || (pb->Cg && pb->lg && pb->ug && pc && cc)),
+               "pq_admm_lr_sweep: needs 0 <= mg <= %d shared general rows with pc / cc (mg=%d)", pq::SW_MG, pb->mg);
+  PQ_CHECK_ARG(pb->mg == 0 || pb->Cg_stride == 0, "pq_admm_lr_sweep: the general rows must be shared");
+  PQ_CHECK_ARG(pb->lb && pb->ub && pb->box_stride == 0, "pq_admm_lr_sweep: needs shared box rows");
+  const int k = lr->tmax + pb->mg;
+  PQ_CHECK_ARG(k <= k_ld && k_ld <= pq::SW_K, "pq_admm_lr_sweep: need k <= k_ld <= %d (k=%d)", pq::SW_K, k);
+  PQ_CHECK_ARG(scratch_doubles >= pq_sweep_scratch_doubles(pb->n, pb->batch, ngroups),
+               "pq_admm_lr_sweep: scratch too small");
+  if (ngroups <= 0 || iters_this_call <= 0) return 0;
+  hipStream_t str = (hipStream_t)stream;
+  const int nch = (pb->n + pq::SW_CH - 1) / pq::SW_CH;
+  double* SR = scratch;
+  double* Wp = SR + (int64_t)pb->batch * pq::SR_N;
+  double* Rp = Wp + (int64_t)ngroups * nch * pq::SW_G * pq::SW_K;
+  double* Ut = Rp + (int64_t)ngroups * nch * pq::SW_G * pq::RP_N;
+  int* flag = reinterpret_cast<int*>(Ut + (int64_t)ngroups * pq::SW_K * pq::SW_G);
+  const int nslot = ngroups * pq::SW_G;
+  PQ_CHECK_HIP(hipMemsetAsync(Ut, 0, sizeof(double) * (size_t)ngroups * pq::SW_K * pq::SW_G, str));
+  hipLaunchKernelGGL(pq::k_sw_setup, dim3((nslot + 255) / 256), dim3(256), 0, str, *lr, *pb, *st, *s, gdates, ngroups,
+                     SR, (int)iters_this_call);
+  const bool mg1 = pb->mg <= 1;
+  auto pass = [&](int mode) {
+    const dim3 grid(ngroups * nch), blk(pq::SW_T);
+    if (mode == 0) {
+      if (mg1) hipLaunchKernelGGL((pq::k_sw_pass<0, 1>), grid, blk, 0, str, *lr, *pb, *st, *s, gdates, nch, SR, Ut, Wp, Rp, (int)q_shared);
+      else hipLaunchKernelGGL((pq::k_sw_pass<0, 4>), grid, blk, 0, str, *lr, *pb, *st, *s, gdates, nch, SR, Ut, Wp, Rp, (int)q_shared);
+    } else {
+      if (mg1) hipLaunchKernelGGL((pq::k_sw_pass<1, 1>), grid, blk, 0, str, *lr, *pb, *st, *s, gdates, nch, SR, Ut, Wp, Rp, (int)q_shared);
+      else hipLaunchKernelGGL((pq::k_sw_pass<1, 4>), grid, blk, 0, str, *lr, *pb, *st, *s, gdates, nch, SR, Ut, Wp, Rp, (int)q_shared);
+    }
+  };
+  auto mid = [&](int mode) {
+    const dim3 grid(nslot), blk(pq::SW_MT);
+#define PQ_SW_MID(MD, MG)                                                                                     \
+  hipLaunchKernelGGL((pq::k_sw_mid<MD, MG>), grid, blk, 0, str, *lr, *pb, *s, gdates, nch, SR, Ut, Wp, Rp, Minv, \
+                     k_ld, M_stride, pc, ldpc, r0, cc)
+    if (mode == 0) {
+      if (mg1) PQ_SW_MID(0, 1); else PQ_SW_MID(0, 4);
+    } else {
+      if (mg1) PQ_SW_MID(1, 1); else PQ_SW_MID(1, 4);
+    }
+#undef PQ_SW_MID
+  };
+  pass(0);
+  mid(0);
+  // iterations in blocks; one flag read between blocks (the first block covers the usual
+  // loose-stop run, later blocks are short)
+  int done = 0, blockn = 12;
+  while (done < iters_this_call) {
+    const int nb = blockn < iters_this_call - done ? blockn : iters_this_call - done;
+    for (int j = 0; j < nb; ++j) {
+      pass(1);
+      mid(1);
+    }
+    done += nb;
+    blockn = 4;
+    if (done >= iters_this_call) break;
+    hipLaunchKernelGGL(pq::k_sw_any, dim3(1), dim3(256), 0, str, gdates, ngroups, SR, flag);
+    int h = 0;
+    PQ_CHECK_HIP(hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, str));
+    PQ_CHECK_HIP(hipStreamSynchronize(str));
+    if (!h) break;
+  }
+  hipLaunchKernelGGL(pq::k_sw_final, dim3((nslot + 255) / 256), dim3(256), 0, str, *pb, *st, gdates, ngroups, SR);
+  PQ_CHECK_LAUNCH("pq_admm_lr_sweep");
+  return 0;
+}

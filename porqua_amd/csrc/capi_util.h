@@ -25,3 +25,12 @@ void set_error(const char* fmt, ...);
       return -2;                                                                \
     }                                                                           \
   } while (0)
+
+#define PQ_CHECK_HIP(call)                                                      \
+  do {                                                                          \
+    hipError_t e_ = (call);                                                     \
+    if (e_ != hipSuccess) {                                                     \
+      pq::set_error("%s: %s", #call, hipGetErrorString(e_));                    \
+      return -2;                                                                \
+    }                                                                           \
+  } while (0)

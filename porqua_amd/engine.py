@@ -959,7 +959,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                   fuse: bool = True, grouped_polish: bool = True, gcap: bool = True,
                   eig: "EigCap | None" = None, wide_polish: bool = True, sync_free: bool = False,
                   graphs: "StageGraphs | None" = None, sf_rounds: int | None = None,
-                  host_work=None) -> BatchResult:
+                  host_work=None, sweep: "SweepPlan | None" = None) -> BatchResult:
     """Woodbury-form solve for T + mg < n: K2 = capacitance SYRK + Cholesky/inverse of the
     k x k matrices M, K3 = low-rank ADMM over the shared window rows (grouped over sliding
     windows when a GroupPlan is given), K4 = window-form polish.  qb.P is never read (it
@@ -973,7 +973,9 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
     rounds, the per-date polish and the ADMM retry, exactly as without it).  With ``graphs``
     (StageGraphs) the sync-free stages are captured once and replayed.  ``host_work`` (a
     callable, sync-free only): the caller's host work that needs no result, run while the
-    device works, just before the flag read."""
+    device works, just before the flag read.  ``sweep`` (SweepPlan: groups of up to 64
+    problems sharing one window, porqua_amd.sweep): the fused ADMM runs as pq_admm_lr_sweep
+    (two chip-wide launches per iteration) instead of one workgroup per group."""
     if sync_free and not (gcap and eig is None and groups is not None and grouped_polish and polish):
         sync_free = False
     tl = _Timeline(events, graphs if sync_free else None)
@@ -1085,6 +1087,12 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
                                        nzmax, strm)
         if grouped:   # every group relaunches; solved dates are skipped inside
             fz = bd is not None and fuse and qb.mg <= 32   # uniform D + shared Cg: the fused form
+            if fz and sweep is not None and sweep.applicable(qb, lr, k_ld):
+                scr = sweep.buffer(qb, lib)
+                return lib.pq_admm_lr_sweep(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
+                                            _ptr(sweep.gdates), sweep.ngroups, SS, int(s.max_iter),
+                                            bd["pc"].data_ptr(), bd["pc"].stride(0), bd["r0"], bd["cc"].data_ptr(),
+                                            int(sweep.q_shared), scr.data_ptr(), scr.numel(), strm)
             nzr, nzv, nzmax = sparse_cols
             return lib.pq_admm_lr_grouped(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
                                           _ptr(groups.gdates), groups.ngroups, _ptr(groups.urows),
@@ -1399,6 +1407,39 @@ GCAP_MAX_DATES = int(os.environ.get("PQ_GCAP_GMAX", "32"))
 GCAP32_WIDE = os.environ.get("PQ_GCAP32_WIDE", "1") != "0"
 GCAP_FACTOR = os.environ.get("PQ_GCAP_FACTOR", "batched")   # (A/B) "large": K2L for the group factor
 GROUP_MAX_UNION = 320    # union rows per group (admm_grp.hip UMAXG)
+
+
+SWEEP_ADMM = os.environ.get("PQ_SWEEP_ADMM", "1") != "0"   # (A/B) 0: the sweep's groups on k_admm_grp
+
+
+class SweepPlan:
+    """Problem groups for pq_admm_lr_sweep (admm_sweep.hip): runs of up to 64 consecutive
+    problems that share one window and its centring (the risk-aversion row of a rebalance
+    date, porqua_amd.sweep), with the kernel's scratch (per-problem records, per-chunk
+    partials, the pass-2 operand).  ``q_shared``: the problems of a group share q as well."""
+
+    GMAX = 64
+
+    def __init__(self, counts, device, q_shared: bool = False):
+        self.q_shared = bool(q_shared)
+        starts, b = [], 0
+        for c in counts:
+            starts.extend(range(b, b + int(c), self.GMAX))
+            b += int(c)
+        starts.append(b)
+        self.gdates = torch.tensor(starts, dtype=torch.int32, device=device)
+        self.ngroups = len(starts) - 1
+        self.scratch = None
+
+    def applicable(self, qb: "QPBatch", lr: "LowRank", k_ld: int) -> bool:
+        return (SWEEP_ADMM and self.ngroups > 0 and lr.tmax <= 256 and k_ld <= 256 and qb.mg <= 4
+                and qb.lb is not None and qb.ub is not None and qb.shared)
+
+    def buffer(self, qb: "QPBatch", lib) -> torch.Tensor:
+        need = int(lib.pq_sweep_scratch_doubles(qb.n, qb.batch, self.ngroups))
+        if self.scratch is None or self.scratch.numel() < need:
+            self.scratch = torch.empty(need, dtype=F64, device=qb.device)
+        return self.scratch
 
 
 class GroupPlan:

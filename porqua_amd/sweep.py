@@ -117,6 +117,9 @@ class MeanVarianceSweep:
         self.k_ld = k_ld
         self.pdate = torch.arange(nd, dtype=torch.int32, device=dev).repeat_interleave(L)
         self.gp = engine.GroupPlan(rows_p, tlen_p, dev, gmax=gmax) if (group and B) else None
+        # the ADMM's own groups: the risk aversions of a date (up to 64 per group) on one window
+        # and one q = -mu_d, two chip-wide launches per iteration (engine.SweepPlan, admm_sweep.hip)
+        self.sp = engine.SweepPlan([L] * nd, dev, q_shared=True) if (group and B) else None
         self.settings = settings if settings is not None else engine.Settings.from_params(SWEEP_SETTINGS)
         self.ws = ws if ws is not None else engine.Workspace(qb, dense=False)
 
@@ -148,7 +151,7 @@ class MeanVarianceSweep:
             eig = tl("eig", lambda: engine.EigCap(pan, self.r_d, self.t_d, self.mu_c, self.qb, self.pdate, self.k_ld,
                                                   backend=self.eig_backend))
         res = engine.solve_lowrank(self.qb, self.lr, self.settings, ws=self.ws, groups=self.gp, events=events,
-                                   eig=eig)
+                                   eig=eig, sweep=self.sp)
         gp = self.gp
         meta = {"dates": self.nd, "lambdas": self.lam, "grouped": gp is not None and gp.ok,
                 "ngroups": None if gp is None else gp.ngroups, "capacitance": res.capacitance,
