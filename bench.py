@@ -421,6 +421,18 @@ def main():
         k_u = u_mean + qb.mg
         it_bytes = (2 * 8.0 * u_mean * n + 8.0 * k_u * (k_u + 1) / 2) / g_mean + 12 * 8.0 * n
         admm_bytes = it_bytes * total_iters
+    elif grouped and getattr(ws, "sweep_admm", None) is not None:
+        # risk-aversion sweep (admm_sweep.hip, k_sw_pass + k_sw_mid), per problem-iteration: the
+        # ADMM state read + written (x, Px, z, y: 8 n-vectors), the lower-triangle M_b^-1, the
+        # problem's rows of the chunk partials of W (written + read), and per group of G
+        # problems the window (T n) and q once
+        sp = ws.sweep_admm
+        kern = "k_sw_pass"
+        g_mean = D / sp.ngroups
+        nch = (n + 255) // 256
+        it_bytes = (8.0 * 8 * n + 8.0 * k_lr * (k_lr + 1) / 2 + 2 * 8.0 * 256 * nch
+                    + 8.0 * (T * n + n) / g_mean)
+        admm_bytes = it_bytes * total_iters
     elif grouped:
         # HBM level: the date's lower-triangle M^-1 (the only per-date O(k^2) stream; 4749 x
         # 512 KB is far beyond the caches) + the ADMM state read and written (x, z, y, Px);
@@ -477,7 +489,8 @@ def main():
         traffic, traffic_src = pm["kernels"][kern]["hbm_bytes_per_admm_iteration"], os.path.relpath(f, ROOT)
         if "mfma_busy_fraction" in pm:
             mfma_busy = {kk: pm["mfma_busy_fraction"][kk] for kk in
-                         ("k_band_gram", "k_factor", "k_gcap_prep", "k_admm_grp", "k_admm_gcap", "k_polish_w",
+                         ("k_band_gram", "k_factor", "k_gcap_prep", "k_admm_grp", "k_admm_gcap", "k_sw_pass",
+                          "k_sw_mid", "k_polish_w",
                           "k_pg_form", "k_pg_form_grp", "k_pg_solve", "k_pg_passA", "k_pg_passB")
                          if kk in pm["mfma_busy_fraction"]}
             mfma_src = traffic_src
@@ -506,7 +519,8 @@ def main():
                    "dates_per_gpu": D, "global_batch": D_all,
                    "parallelism": (f"dates-sharded x{world} (every lambda of a date on its rank)"
                                    if wname == "config5" else f"dates-sharded x{world}")},
-        "roofline": {"bound": "hbm", "kernel": kern + (" (K3, grouped low-rank)" if grouped else " (K3)"),
+        "roofline": {"bound": "hbm", "kernel": kern + (" + k_sw_mid (K3, risk-aversion sweep)" if kern == "k_sw_pass"
+                                                       else " (K3, grouped low-rank)" if grouped else " (K3)"),
                      "achieved": admm_gbs,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": admm_gbs / HBM_PEAK_GBS,
                      "traffic": traffic,
@@ -522,6 +536,9 @@ def main():
                      "algorithmic_bytes_note": ("per date-iteration: (union rows 2 x 8Un + lower-triangle M_U^-1 "
                                                 "8k(k+1)/2, k = U + mg) / dates per group + ADMM state 12 x 8n"
                                                 if kern == "k_admm_gcap" else
+                                                "per problem-iteration: ADMM state 8 x 8n + lower-triangle M_b^-1 "
+                                                "8k(k+1)/2 + W chunk partials 2 x 8 x 256 x ceil(n/256) + (window "
+                                                "8Tn + q 8n) / problems per group" if kern == "k_sw_pass" else
                                                 "per date-iteration: lower-triangle M^-1 8k(k+1)/2 (k = T + mg) "
                                                 "+ ADMM state 8 x 8n" if grouped else
                                                 "per date-iteration: window rows 2 x 8Tn + M^-1 8k(k+1)/2"
@@ -530,6 +547,8 @@ def main():
                      "l2_window_gbs": None if l2_bytes is None else l2_bytes * total_iters / tk["admm"] / 1e9,
                      "path": ("lowrank grouped, group capacitance (one M_U^-1 per slide group + per-date "
                               "Woodbury correction; MFMA passes over the union rows)" if kern == "k_admm_gcap" else
+                              "lowrank, risk-aversion sweep (the date's problems as MFMA columns of fused "
+                              "chunk passes over its window; per-problem M_b^-1)" if kern == "k_sw_pass" else
                               "lowrank grouped (Woodbury; MFMA passes over the union of sliding windows)"
                               if grouped else "lowrank (Woodbury: window rows + M^-1)" if use_lr
                               else "dense K^-1 (lower)"),

@@ -27,9 +27,26 @@
 #include "common.h"
 #include "capi_util.h"
 
-// (experiment builds only) PQ_SW_X = 1: no state traffic in the updates; 2: no MFMA passes
+// (experiment builds only) PQ_SW_X = 1: no state stores in the updates; 4: no pass-2 MFMA;
+// 5: no pass-1 MFMA
 #ifndef PQ_SW_X
 #define PQ_SW_X 0
+#endif
+#ifndef PQ_SW_RU
+#define PQ_SW_RU 4
+#endif
+// (experiment builds only) PQ_SW_PROF: phase clocks of k_sw_pass in the spare partial slots
+#ifdef PQ_SW_PROF
+#define SW_STAMP(k)                        \
+  do {                                     \
+    if (threadIdx.x == 0) {                \
+      const long long now_ = clock64();    \
+      pclk[k] += (double)(now_ - tclk);    \
+      tclk = now_;                         \
+    }                                      \
+  } while (0)
+#else
+#define SW_STAMP(k) do { } while (0)
 #endif
 
 namespace pq {
@@ -56,8 +73,8 @@ enum {
 // partial record: mode 1 (iteration) [0..5] residual maxima, [6] mu.v, [8..11] Cg.v;
 // mode 0 (prologue) [0] max |q|, [1..4] Cg.mu, [6] mu.v, [8..11] Cg.v, [12..15] Cg.x
 // per-problem LDS scalars of the pass kernel
-constexpr int SC_N = 4 + 5 * SW_MG;
-enum { C_DINV = 0, C_RB, C_SU, C_ACT, C_CW = 4, C_RGZ = 8, C_YG = 12, C_WG = 16, C_WGP = 20 };
+constexpr int SC_N = 5 + 5 * SW_MG;
+enum { C_DINV = 0, C_RB, C_SU, C_ACT, C_CW = 4, C_RGZ = 8, C_YG = 12, C_WG = 16, C_WGP = 20, C_RBI = 24 };
 
 __device__ __forceinline__ double sw_grho(double l, double u, double rho, const pq_settings& s) {
   if (l == u) return rho * s.eq_scale;
@@ -138,7 +155,8 @@ __global__ __launch_bounds__(256) void k_sw_setup(pq_lowrank lr, pq_problem pb, 
 // the next sub-chunk's x / Px / z / y are loaded into registers while the current one
 // computes (a whole sub-chunk of MFMA and update work covers the HBM latency).
 //   pass 2: wave w = (column tile w >> 1, K half w & 1) -- Ut of its half in registers;
-//   update: thread t = (asset t & 15, problems (t >> 4) + 32 e), 16-lane reductions;
+//   update: thread t = (asset t & 15, problems (t >> 4) + 32 e); residual terms and sums
+//           kept per thread over the chunk, 16-lane reductions once at its end;
 //   pass 1: wave w owns window-row tiles 2w, 2w + 1 and all four column tiles.
 template <int MODE, int MGR>
 __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, pq_state st, pq_settings s,
@@ -147,7 +165,7 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
   __shared__ __attribute__((aligned(16))) double Xs[2 * SW_K * SW_PX];   // window slabs [buf][u][asset]
   __shared__ __attribute__((aligned(16))) double XV[2 * SW_SA * SW_PV];  // x~ of the two K halves; half 0 then v
   __shared__ double p_sc[SW_G * SC_N];
-  __shared__ double p_red[SW_G * RP_N];
+  __shared__ double racc_l[10 * SW_T];   // per-thread residual maxima / mu.v, [slot][e][thread]
   __shared__ int s_row[SW_K];
   __shared__ int s_any;
 
@@ -159,6 +177,10 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
   const int n = pb.n, ld = pb.ld, mg = pb.mg, tmax = lr.tmax;
   const int T = lr.tlen[b0];
   const double sigma = s.sigma, alpha = s.alpha;
+#ifdef PQ_SW_PROF
+  double pclk[4] = {0.0, 0.0, 0.0, 0.0};
+  long long tclk = clock64();
+#endif
 
   if (t < SW_G) {
     const int g = t;
@@ -167,6 +189,7 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
       const double* R = SR + (int64_t)(b0 + g) * SR_N;
       sc[C_DINV] = R[S_DINV];
       sc[C_RB] = R[S_RB];
+      sc[C_RBI] = 1.0 / R[S_RB];   // (the box projection multiplies by 1 / rho_box)
       sc[C_SU] = R[S_SU];
       sc[C_ACT] = R[S_ACT];
 #pragma unroll
@@ -181,7 +204,6 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
       for (int e = 0; e < SC_N; ++e) sc[e] = 0.0;
     }
   }
-  for (int e = t; e < SW_G * RP_N; e += SW_T) p_red[e] = 0.0;
   for (int u = t; u < SW_K; u += SW_T) s_row[u] = u < T ? lr.rows[(int64_t)b0 * tmax + u] : -1;
   __syncthreads();
   if (t == 0) {
@@ -237,26 +259,46 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
   const int ui = t & 15, ug = t >> 4;
   const double* mu0 = lr.mu ? lr.mu + (int64_t)b0 * lr.mu_stride : nullptr;
   const double* Cg0 = mg ? pb.Cg : nullptr;   // shared rows (host-checked Cg_stride == 0)
-  double px_[2], x_[2], zb_[2], yb_[2], q_[2];
+  constexpr int MGA = MGR > 0 ? MGR : 1;
+  // prefetched one sub-chunk ahead: the element state and the asset's shared values (every
+  // value the updates read from memory, so their waits never cover the next prefetch)
+  double px_[2], x_[2], zb_[2], yb_[2], q_[2], mu_, lo_, up_, cg_[MGA];
   auto state_load = [&](int i0) {
     const int ia = i0 + ui;
+    const bool inb = ia < n;
+    mu_ = (mu0 && inb) ? mu0[ia] : 0.0;
+    lo_ = inb ? pb.lb[ia] : 0.0;   // (shared box rows, host-checked)
+    up_ = inb ? pb.ub[ia] : 0.0;
+#pragma unroll
+    for (int r = 0; r < MGA; ++r) cg_[r] = (r < mg && inb) ? Cg0[(int64_t)r * ld + ia] : 0.0;
+    const double qa = (q_shared && inb) ? pb.q[(int64_t)b0 * pb.q_stride + ia] : 0.0;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int g = ug + 32 * e;
-      const bool ok = g < G && ia < n && p_sc[g * SC_N + C_ACT] != 0.0;
+      const bool ok = g < G && inb && p_sc[g * SC_N + C_ACT] != 0.0;
       const int b = b0 + (g < G ? g : 0);
-      x_[e] = ok ? st.x[(int64_t)b * ld + ia] : 0.0;
-      zb_[e] = ok ? st.z[(int64_t)b * st.m_ld + st.mg_pad + ia] : 0.0;
-      yb_[e] = ok ? st.y[(int64_t)b * st.m_ld + st.mg_pad + ia] : 0.0;
-      px_[e] = (MODE == 1 && ok) ? st.Px[(int64_t)b * ld + ia] : 0.0;
-      q_[e] = ok ? pb.q[(int64_t)(q_shared ? b0 : b) * pb.q_stride + ia] : 0.0;
+      // 32-bit element offsets (host-checked < 2^31): SGPR base + VGPR offset addressing
+      const unsigned ox = (unsigned)(b * ld + ia), oz = (unsigned)(b * st.m_ld + st.mg_pad + ia);
+      x_[e] = ok ? st.x[ox] : 0.0;
+      zb_[e] = ok ? st.z[oz] : 0.0;
+      yb_[e] = ok ? st.y[oz] : 0.0;
+      px_[e] = (MODE == 1 && ok) ? st.Px[ox] : 0.0;
+      q_[e] = q_shared ? qa : (ok ? pb.q[(unsigned)(b * pb.q_stride + ia)] : 0.0);
     }
   };
+
+  double rcg[2][MGA], rcm[2][MGA], rcx[2][MGA];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int r = 0; r < MGA; ++r) rcg[e][r] = rcm[e][r] = rcx[e][r] = 0.0;
+  for (int k = 0; k < 10; ++k) racc_l[k * SW_T + t] = 0.0;   // (own slots: no barrier needed)
 
   slab_load(c0);
   slab_store(0);
   state_load(c0);
   __syncthreads();
+  SW_STAMP(3);
   int cur = 0;
   for (int i0 = c0; i0 < c1; i0 += SW_SA) {
     const bool more = i0 + SW_SA < c1;
@@ -265,25 +307,31 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
 
     if constexpr (MODE == 1) {
       // ---- pass 2: x~raw[i][g] = sum_u X[u][i] Ut[u][g] over this wave's K half ----------
-      f64x4 xa = f64x4{0.0, 0.0, 0.0, 0.0};
+      // two accumulation chains (even / odd k-steps): a dependent f64 MFMA chain issues at half rate
+      f64x4 xa = f64x4{0.0, 0.0, 0.0, 0.0}, xb = f64x4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int s2 = 0; s2 < 32; ++s2)
+      for (int s2 = 0; s2 < 32; s2 += 2) {
+        if (PQ_SW_X == 4) break;
         xa = __builtin_amdgcn_mfma_f64_16x16x4f64(X[(128 * kh + 4 * s2 + k4) * SW_PX + m16], ut[s2], xa, 0, 0, 0);
+        xb = __builtin_amdgcn_mfma_f64_16x16x4f64(X[(128 * kh + 4 * s2 + 4 + k4) * SW_PX + m16], ut[s2 + 1], xb, 0,
+                                                  0, 0);
+      }
+      xa += xb;
       double* xv = XV + kh * (SW_SA * SW_PV);
 #pragma unroll
       for (int r = 0; r < 4; ++r) xv[(k4 + 4 * r) * SW_PV + 16 * gt + m16] = xa[r];
       __syncthreads();
+      SW_STAMP(0);
     }
 
     // ---- per-element updates (MODE 1) / first rhs (MODE 0); v = rhs / c into half 0 ---------
     {
       const int ia = i0 + ui;
       const bool inb = ia < n;
-      const double mui = (mu0 && inb) ? mu0[ia] : 0.0;
-      const double lo = inb ? pb.lb[ia] : 0.0, up = inb ? pb.ub[ia] : 0.0;   // (uniform box rows)
-      double cgi[MGR > 0 ? MGR : 1];
+      const double mui = mu_, lo = lo_, up = up_;
+      double cgi[MGA];
 #pragma unroll
-      for (int r = 0; r < (MGR > 0 ? MGR : 1); ++r) cgi[r] = (r < mg && inb) ? Cg0[(int64_t)r * ld + ia] : 0.0;
+      for (int r = 0; r < MGA; ++r) cgi[r] = cg_[r];
       double xs[2], zs[2], ys[2], pxs[2], qs[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -345,13 +393,14 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
             const double pxn = alpha * pxt + (1.0 - alpha) * px;
             double rr = sigma * xn - qi + cgw;
             const double zh = alpha * xt + (1.0 - alpha) * zb;
-            const double zn = fmin(fmax(zh + yb / rb, lo), up);
+            const double zn = fmin(fmax(fma(yb, sc[C_RBI], zh), lo), up);
             const double yn = yb + rb * (zh - zn);
 #if PQ_SW_X != 1
-            st.z[(int64_t)b * st.m_ld + st.mg_pad + ia] = zn;
-            st.y[(int64_t)b * st.m_ld + st.mg_pad + ia] = yn;
-            st.x[(int64_t)b * ld + ia] = xn;
-            st.Px[(int64_t)b * ld + ia] = pxn;
+            const unsigned ox = (unsigned)(b * ld + ia), oz = (unsigned)(b * st.m_ld + st.mg_pad + ia);
+            st.z[oz] = zn;
+            st.y[oz] = yn;
+            st.x[ox] = xn;
+            st.Px[ox] = pxn;
 #endif
             rr += rb * zn - yn;
             red[0] = fabs(xn - zn);
@@ -368,44 +417,32 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
           }
         }
         XV[ui * SW_PV + g] = v;   // the element this thread read (half 0), now v
-        // 16-lane reductions (the lanes of a row share problem g); one owner per g
-        double* pr = p_red + g * RP_N;
+        // residual terms / sums accumulate per thread over the chunk (reduced once, below):
+        // the maxima and mu.v in this thread's own LDS slots, the general-row sums in registers.
+        // |x|, |z| and |Px|, |C'y| only enter the test as max(|x|, |z|), max(|Px|, |C'y|, |q|)
+        double* ra = racc_l + (2 * 0 + e) * SW_T + t;
         if constexpr (MODE == 1) {
+          ra[0] = fmax(ra[0], red[0]);
+          ra[2 * SW_T] = fmax(ra[2 * SW_T], fmax(red[1], red[2]));
+          ra[4 * SW_T] = fmax(ra[4 * SW_T], red[3]);
+          ra[6 * SW_T] = fmax(ra[6 * SW_T], fmax(red[4], red[5]));
+          ra[8 * SW_T] += red[6];
 #pragma unroll
-          for (int k = 0; k < 6; ++k) red[k] = qmax16(red[k]);
-          red[6] = qsum16(red[6]);
-#pragma unroll
-          for (int r = 0; r < MGR; ++r) red[8 + r] = qsum16(red[8 + r]);
-          if (ui == 0) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) pr[k] = fmax(pr[k], red[k]);
-            pr[6] += red[6];
-#pragma unroll
-            for (int r = 0; r < MGR; ++r) pr[8 + r] += red[8 + r];
-          }
+          for (int r = 0; r < MGR; ++r) rcg[e][r] += red[8 + r];
         } else {
-          red[0] = qmax16(red[0]);
-          red[6] = qsum16(red[6]);
+          ra[0] = fmax(ra[0], red[0]);
+          ra[8 * SW_T] += red[6];
 #pragma unroll
           for (int r = 0; r < MGR; ++r) {
-            red[1 + r] = qsum16(red[1 + r]);
-            red[8 + r] = qsum16(red[8 + r]);
-            cgx[r] = qsum16(cgx[r]);
-          }
-          if (ui == 0) {
-            pr[0] = fmax(pr[0], red[0]);
-            pr[6] += red[6];
-#pragma unroll
-            for (int r = 0; r < MGR; ++r) {
-              pr[1 + r] += red[1 + r];
-              pr[8 + r] += red[8 + r];
-              pr[12 + r] += cgx[r];
-            }
+            rcm[e][r] += red[1 + r];
+            rcg[e][r] += red[8 + r];
+            rcx[e][r] += cgx[r];
           }
         }
       }
     }
     __syncthreads();
+    SW_STAMP(1);
 
     // ---- pass 1: W[u][g] += sum_i X[u][i] v[i][g] (window-row tiles 2w, 2w + 1) -------------
 #pragma unroll
@@ -417,12 +454,17 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const double bv = vrow[16 * c];
+        if (PQ_SW_X == 5) {
+          wacc[0][c][0] += a0 * bv;
+          continue;
+        }
         wacc[0][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv, wacc[0][c], 0, 0, 0);
         wacc[1][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv, wacc[1][c], 0, 0, 0);
       }
     }
     if (more) slab_store(cur ^ 1);
     __syncthreads();
+    SW_STAMP(2);
     cur ^= 1;
   }
 
@@ -435,8 +477,47 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int r = 0; r < 4; ++r) wp[(16 * c + m16) * SW_K + 32 * w + 16 * a + k4 + 4 * r] = wacc[a][c][r];
+    // the chunk's per-problem terms: 16-lane reductions of the per-thread partials, in the
+    // partial-record layout (unused slots zero)
     double* rp = Rp + ((int64_t)(grp * nch + ch) * SW_G) * RP_N;
-    for (int e = t; e < SW_G * RP_N; e += SW_T) rp[e] = p_red[e];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int g = ug + 32 * e;
+      double o[RP_N];
+#pragma unroll
+      for (int k = 0; k < RP_N; ++k) o[k] = 0.0;
+      const double* ra = racc_l + e * SW_T + t;
+      if constexpr (MODE == 1) {   // (slots 2 and 5 stay 0: merged into 1 and 4)
+        o[0] = qmax16(ra[0]);
+        o[1] = qmax16(ra[2 * SW_T]);
+        o[3] = qmax16(ra[4 * SW_T]);
+        o[4] = qmax16(ra[6 * SW_T]);
+        o[6] = qsum16(ra[8 * SW_T]);
+#pragma unroll
+        for (int r = 0; r < MGR; ++r) o[8 + r] = qsum16(rcg[e][r]);
+      } else {
+        o[0] = qmax16(ra[0]);
+        o[6] = qsum16(ra[8 * SW_T]);
+#pragma unroll
+        for (int r = 0; r < MGR; ++r) {
+          o[1 + r] = qsum16(rcm[e][r]);
+          o[8 + r] = qsum16(rcg[e][r]);
+          o[12 + r] = qsum16(rcx[e][r]);
+        }
+      }
+      if (ui == 0) {
+#pragma unroll
+        for (int k = 0; k < RP_N; ++k) rp[g * RP_N + k] = o[k];
+      }
+    }
+#ifdef PQ_SW_PROF
+    if (t == 0) {   // pass 2, updates, pass 1, setup (clock64 ticks) in problem 0's spare slots
+      rp[7] = pclk[0];
+      rp[13] = pclk[1];
+      rp[14] = pclk[2];
+      rp[15] = pclk[3];
+    }
+#endif
   }
 }
 
@@ -452,7 +533,7 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   __shared__ double s_dot[SW_K + 8];
   __shared__ double s_part[4 * SW_K];
   __shared__ double red[RP_N];
-  __shared__ double s_red[8];
+  __shared__ double sr[SR_N];
   __shared__ int s_cont;
 
   const int grp = blockIdx.x / SW_G, g = blockIdx.x - grp * SW_G;
@@ -464,8 +545,47 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   const int t = threadIdx.x, w = t >> 6, l = t & 63;
   const int mg = pb.mg, tmax = lr.tmax, T = lr.tlen[b0];
   const int k = tmax + mg;
+  static_assert(SW_MT == SW_K, "one window row per thread");
 
-  // chunk partials of this problem, in chunk order
+  // Every load that depends on nothing else is issued before the first barrier: the chunk
+  // partials (residual terms, this thread's window row of W), this thread's row id and pc
+  // entries, and the first M^-1 rows -- one HBM round trip instead of one per phase.
+  const double* Mi = Minv_all + (int64_t)b * M_stride;
+  constexpr int RU = PQ_SW_RU;   // rows per M^-1 load batch (two batches in flight)
+  double m0[RU][4], m1[RU][4];
+  // rows j = w + 4 e of this wave; lane l holds columns l + 64 q.  A 64-column block is loaded
+  // when any of it is in the lower triangle (a wave-uniform test), masked in the arithmetic
+  auto rload = [&](double (&M)[RU][4], int j0) {
+#pragma unroll
+    for (int e = 0; e < RU; ++e) {
+      const int j = j0 + 4 * e;
+      const double* rp = Mi + (int64_t)(j < k ? j : 0) * k_ld + l;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) M[e][q] = (j < k && 64 * q <= j) ? rp[64 * q] : 0.0;
+    }
+  };
+  rload(m0, w);
+  double Wj = 0.0;
+  int rowj = 0;
+  double pcv[MGR > 0 ? MGR : 1];
+  {
+    const int j = t;   // SW_MT == SW_K: one window row per thread
+    if (j < T) {       // the chunk partials in chunk order, four loads in flight
+      const double* wp = Wp + ((int64_t)grp * nch * SW_G + g) * SW_K + j;
+      const int64_t cs = (int64_t)SW_G * SW_K;
+      int c = 0;
+      for (; c + 4 <= nch; c += 4) {
+        const double v0 = wp[c * cs], v1 = wp[(c + 1) * cs], v2 = wp[(c + 2) * cs], v3 = wp[(c + 3) * cs];
+        Wj = (((Wj + v0) + v1) + v2) + v3;
+      }
+      for (; c < nch; ++c) Wj += wp[c * cs];
+      rowj = lr.rows[(int64_t)b0 * tmax + j];
+    }
+#pragma unroll
+    for (int r = 0; r < (MGR > 0 ? MGR : 1); ++r)
+      pcv[r] = (j < T && r < mg) ? pc[(int64_t)(rowj - r0) * ldpc + r] : 0.0;
+  }
+  if (t < SR_N) sr[t] = R[t];
   if (t < RP_N) {   // four chunks' loads in flight at a time, combined in chunk order
     const bool is_max = MODE == 1 ? t < 6 : t == 0;
     const double* rp = Rp + ((int64_t)grp * nch * SW_G + g) * RP_N + t;
@@ -486,11 +606,11 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   if (t == 0) {
     int cont = 1;
     if constexpr (MODE == 1) {
-      const double mv0 = fmax(red[0], R[S_RMV + 0]), mv1 = fmax(red[1], R[S_RMV + 1]),
-                   mv2 = fmax(red[2], R[S_RMV + 2]);
-      const double mv3 = red[3], mv4 = red[4], mv5 = red[5], mv6 = R[S_QMAX];
-      const double rho = R[S_RHO];
-      const int it = (int)R[S_IT] + 1;
+      const double mv0 = fmax(red[0], sr[S_RMV + 0]), mv1 = fmax(red[1], sr[S_RMV + 1]),
+                   mv2 = fmax(red[2], sr[S_RMV + 2]);
+      const double mv3 = red[3], mv4 = red[4], mv5 = red[5], mv6 = sr[S_QMAX];
+      const double rho = sr[S_RHO];
+      const int it = (int)sr[S_IT] + 1;
       int stat = PQ_UNSOLVED;
       const double eps_p = s.eps_abs + s.eps_rel * fmax(mv1, mv2);
       const double eps_d = s.eps_abs + s.eps_rel * fmax(mv4, fmax(mv5, mv6));
@@ -508,7 +628,7 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
         }
       }
       if (stat == PQ_UNSOLVED && it >= s.max_iter) stat = PQ_MAX_ITER;
-      cont = (stat == PQ_UNSOLVED) && it < (int)R[S_END];
+      cont = (stat == PQ_UNSOLVED) && it < (int)sr[S_END];
       R[S_IT] = it;
       R[S_RHO] = rnew;
       R[S_STAT] = stat;
@@ -516,16 +636,16 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
       R[S_MUV] = red[6];
 #pragma unroll
       for (int r = 0; r < SW_MG; ++r)
-        if (r < mg) R[S_CGV + r] = red[8 + r];
+        if (r < mg) R[S_CGV + r] = sr[S_CGV + r] = red[8 + r];
     } else {
       R[S_QMAX] = red[0];
       R[S_MUV] = red[6];
 #pragma unroll
       for (int r = 0; r < SW_MG; ++r)
         if (r < mg) {
-          R[S_CMU + r] = red[1 + r];
-          R[S_CGV + r] = red[8 + r];
-          R[S_CGX + r] = red[12 + r];
+          R[S_CMU + r] = sr[S_CMU + r] = red[1 + r];
+          R[S_CGV + r] = sr[S_CGV + r] = red[8 + r];
+          R[S_CGX + r] = sr[S_CGX + r] = red[12 + r];
         }
     }
     s_cont = cont;
@@ -533,33 +653,20 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   __syncthreads();
   if (!s_cont) return;
 
-  const double sps = R[S_SPS], muv = red[6], dinv = R[S_DINV];
-  (void)dinv;
+  const double sps = sr[S_SPS], muv = red[6], dinv = sr[S_DINV];
   // kw = [sps (W - mu.v) over the window rows | sqrt(rho_r) Cg_r.v]
-  for (int j = t; j < SW_K; j += SW_MT) {
+  {
+    const int j = t;
     double a = 0.0;
-    if (j < T) {   // the chunk partials in chunk order, four loads in flight
-      const double* wp = Wp + ((int64_t)grp * nch * SW_G + g) * SW_K + j;
-      const int64_t cs = (int64_t)SW_G * SW_K;
-      double W = 0.0;
-      int c = 0;
-      for (; c + 4 <= nch; c += 4) {
-        const double v0 = wp[c * cs], v1 = wp[(c + 1) * cs], v2 = wp[(c + 2) * cs], v3 = wp[(c + 3) * cs];
-        W = (((W + v0) + v1) + v2) + v3;
-      }
-      for (; c < nch; ++c) W += wp[c * cs];
-      a = sps * (W - muv);
-    } else if (j >= tmax && j < k) {
-      a = sqrt(R[S_RG + (j - tmax)]) * red[8 + (j - tmax)];
-    }
+    if (j < T) a = sps * (Wj - muv);
+    else if (j >= tmax && j < k) a = sqrt(sr[S_RG + (j - tmax)]) * red[8 + (j - tmax)];
     kw[j] = a;
   }
   __syncthreads();
 
-  // u = M^-1 kw (lower triangle, row pitch k_ld): rows j = w + 4 e; lane l holds columns
-  // l + 64 q -- a dot part per row (its entries c <= j) and an axpy part (c < j) in registers
+  // u = M^-1 kw (lower triangle, row pitch k_ld): a dot part per row (entries c <= j) and an
+  // axpy part (c < j) in registers
   {
-    const double* Mi = Minv_all + (int64_t)b * M_stride;
     double rv[4], acc[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -567,20 +674,6 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
       rv[q] = c < k ? kw[c] : 0.0;
       acc[q] = 0.0;
     }
-    constexpr int RU = 4;
-    double m0[RU][4], m1[RU][4];
-    auto rload = [&](double (&M)[RU][4], int j0) {
-#pragma unroll
-      for (int e = 0; e < RU; ++e) {
-        const int j = j0 + 4 * e;
-        const double* rp = Mi + (int64_t)(j < k ? j : 0) * k_ld;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c = l + 64 * q;
-          M[e][q] = (j < k && c <= j) ? rp[c] : 0.0;
-        }
-      }
-    };
     auto rblock = [&](const double (&M)[RU][4], int j0) {
       double dd[RU];
 #pragma unroll
@@ -591,7 +684,7 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c = l + 64 * q;
-          sd = fma(M[e][q], rv[q], sd);
+          sd = fma(c <= j ? M[e][q] : 0.0, rv[q], sd);
           acc[q] = fma(a, c < j ? M[e][q] : 0.0, acc[q]);
         }
         dd[e] = sd;
@@ -606,7 +699,6 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
         }
       }
     };
-    rload(m0, w);
     for (int j0 = w; j0 < k; j0 += 8 * RU) {
       rload(m1, j0 + 4 * RU);
       rblock(m0, j0);
@@ -617,7 +709,8 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
     for (int q = 0; q < 4; ++q) s_part[w * SW_K + l + 64 * q] = acc[q];
   }
   __syncthreads();
-  for (int c = t; c < SW_K; c += SW_MT) {
+  {
+    const int c = t;
     double u = 0.0;
     if (c < k) {
       u = s_dot[c];
@@ -631,18 +724,12 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   // Ut column of this problem (zero outside the window rows), su, Cg x~ terms
   double su = 0.0, pcu[SW_MG] = {0.0, 0.0, 0.0, 0.0};
   {
-    double* Ug = Ut + (int64_t)grp * SW_K * SW_G;
-    for (int j = t; j < SW_K; j += SW_MT) {
-      const double uu = j < T ? sps * uv[j] : 0.0;
-      Ug[j * SW_G + g] = uu;
-      su += uu;
-      if (j < T) {
-        const int row = lr.rows[(int64_t)b0 * tmax + j];
+    const int j = t;
+    const double uu = j < T ? sps * uv[j] : 0.0;
+    Ut[((int64_t)grp * SW_K + j) * SW_G + g] = uu;
+    su = uu;
 #pragma unroll
-        for (int r = 0; r < MGR; ++r)
-          if (r < mg) pcu[r] = fma(pc[(int64_t)(row - r0) * ldpc + r], uu, pcu[r]);
-      }
-    }
+    for (int r = 0; r < MGR; ++r) pcu[r] = pcv[r] * uu;
   }
   su = wave_sum(su);
 #pragma unroll
@@ -660,7 +747,7 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
     double cw[SW_MG] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int r = 0; r < MGR; ++r) {
-      const double rg = R[S_RG + r];
+      const double rg = sr[S_RG + r];
       cw[r] = r < mg ? sqrt(rg) * uv[tmax + r] : 0.0;
       R[S_CW + r] = cw[r];
     }
@@ -672,12 +759,12 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
       for (int ww = 0; ww < 4; ++ww) a += s_part[4 + 4 * r + ww];
       double cwr = 0.0;
       for (int r2 = 0; r2 < mg; ++r2) cwr = fma(cc[r * mg + r2], cw[r2], cwr);
-      const double zt = R[S_CGV + r] - dinv * (a - sut * R[S_CMU + r] + cwr);
-      const double rg = R[S_RG + r], zg = R[S_ZG + r], yg = R[S_YG + r];
+      const double zt = sr[S_CGV + r] - dinv * (a - sut * sr[S_CMU + r] + cwr);
+      const double rg = sr[S_RG + r], zg = sr[S_ZG + r], yg = sr[S_YG + r];
       const double zh = s.alpha * zt + (1.0 - s.alpha) * zg;
-      const double zn = fmin(fmax(zh + yg / rg, R[S_LG + r]), R[S_UG + r]);
+      const double zn = fmin(fmax(zh + yg / rg, sr[S_LG + r]), sr[S_UG + r]);
       const double yn = yg + rg * (zh - zn);
-      const double cx = s.alpha * zt + (1.0 - s.alpha) * R[S_CGX + r];
+      const double cx = s.alpha * zt + (1.0 - s.alpha) * sr[S_CGX + r];
       m0 = fmax(m0, fabs(cx - zn));
       m1 = fmax(m1, fabs(cx));
       m2 = fmax(m2, fabs(zn));
@@ -685,7 +772,7 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
       R[S_ZG + r] = zn;
       R[S_YG + r] = yn;
       R[S_CGX + r] = cx;
-      R[S_WGP + r] = R[S_WG + r];
+      R[S_WGP + r] = sr[S_WG + r];
       R[S_WG + r] = rg * zn - yn;
     }
     R[S_RMV + 0] = m0;
@@ -750,6 +837,9 @@ extern "C" int pq_admm_lr_sweep(const pq_lowrank* lr, const pq_problem* pb, pq_s
                "pq_admm_lr_sweep: needs 0 <= mg <= %d shared general rows with pc / cc (mg=%d)", pq::SW_MG, pb->mg);
   PQ_CHECK_ARG(pb->mg == 0 || pb->Cg_stride == 0, "pq_admm_lr_sweep: the general rows must be shared");
   PQ_CHECK_ARG(pb->lb && pb->ub && pb->box_stride == 0, "pq_admm_lr_sweep: needs shared box rows");
+  PQ_CHECK_ARG((int64_t)pb->batch * (st->m_ld > pb->ld ? st->m_ld : pb->ld) < (int64_t)1 << 31 &&
+                   (int64_t)pb->batch * pb->q_stride < (int64_t)1 << 31,
+               "pq_admm_lr_sweep: state arrays beyond 32-bit element offsets");
   const int k = lr->tmax + pb->mg;
   PQ_CHECK_ARG(k <= k_ld && k_ld <= pq::SW_K, "pq_admm_lr_sweep: need k <= k_ld <= %d (k=%d)", pq::SW_K, k);
   PQ_CHECK_ARG(scratch_doubles >= pq_sweep_scratch_doubles(pb->n, pb->batch, ngroups),

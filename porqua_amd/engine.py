@@ -1088,6 +1088,7 @@ def solve_lowrank(qb: QPBatch, lr: LowRank, settings: Settings | None = None,
         if grouped:   # every group relaunches; solved dates are skipped inside
             fz = bd is not None and fuse and qb.mg <= 32   # uniform D + shared Cg: the fused form
             if fz and sweep is not None and sweep.applicable(qb, lr, k_ld):
+                ws.sweep_admm = sweep   # (the bench's roofline reads which kernel ran)
                 scr = sweep.buffer(qb, lib)
                 return lib.pq_admm_lr_sweep(L_, P_, S_, M["Minv"].data_ptr(), k_ld, k_ld * k_ld,
                                             _ptr(sweep.gdates), sweep.ngroups, SS, int(s.max_iter),

@@ -20,7 +20,8 @@ from porqua_amd.workloads import SweepBacktest  # noqa: E402
 
 
 def main():
-    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    iters = int(args[0]) if args else 12
     wl = SweepBacktest()
     wl.step()
     torch.cuda.synchronize()
@@ -32,6 +33,7 @@ def main():
     x0, z0, y0 = ws.x.clone(), ws.z.clone(), ws.y.clone()
     s = engine.Settings.from_params({"eps_abs": 1e-12, "eps_rel": 1e-12}).to_c()
     s.max_iter = 100000
+    s.min_iter = 10 ** 9   # no stop: every variant runs the same iterations
     pb, lrs = qb.c_struct(), lr.c_struct()
 
     def reset():
@@ -58,7 +60,8 @@ def main():
                                       bd["pc"].data_ptr(), bd["pc"].stride(0), bd["r0"], bd["cc"].data_ptr(), None,
                                       None, 0, strm)
 
-    for name, fn in (("sweep", run_sweep), ("grouped", run_grp)):
+    runs = (("sweep", run_sweep),) if "--sweep-only" in sys.argv else (("sweep", run_sweep), ("grouped", run_grp))
+    for name, fn in runs:
         ts = []
         for rep in range(4):
             reset()
@@ -72,6 +75,16 @@ def main():
         it = ws.iters.float().mean().item()
         print("%-8s %d iterations: %s ms  (%.3f ms / iteration, mean iters %.1f)"
               % (name, iters, " ".join("%.2f" % t for t in ts), min(ts[1:]) / iters, it), flush=True)
+        if name == "sweep" and "--prof" in sys.argv:   # PQ_SW_PROF build: the last pass's phase clocks
+            scr = sw.sp.buffer(qb, lib)
+            nch = (qb.n + 255) // 256
+            ng = sw.sp.ngroups
+            off = qb.batch * 80 + ng * nch * 64 * 256
+            rp = scr[off:off + ng * nch * 64 * 16].view(ng * nch, 64, 16)[:, 0, :].cpu().numpy()
+            ph = rp[:, [7, 13, 14, 15]]
+            tot = ph.sum(1)
+            print("k_sw_pass phase clocks per workgroup (last launch): pass 2 %.0f, updates %.0f, pass 1 %.0f,"
+                  " setup %.0f, total %.0f (max %.0f)" % (*ph.mean(0), tot.mean(), tot.max()), flush=True)
 
 
 if __name__ == "__main__":

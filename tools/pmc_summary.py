@@ -86,6 +86,10 @@ def main():
         adm["hbm_bytes_first_dispatch"] = 2.0 * f1[kern] * 1024.0 + w1.get(kern, 0.0) * 1024.0
         adm["hbm_bytes_per_admm_iteration"] = adm["hbm_bytes_first_dispatch"] / iters
         adm["algorithmic_bytes_per_admm_iteration"] = float(bench_pmc["roofline"]["algorithmic_bytes_per_iteration"])
+        if kern == "k_sw_pass":   # the sweep's ADMM: two launches per iteration, all of the step's
+            mid = out["kernels"].get("k_sw_mid", {})
+            adm["hbm_bytes_per_admm_iteration"] = (adm["hbm_bytes_per_step"] + mid.get("hbm_bytes_per_step", 0.0)) / iters
+            adm["hbm_bytes_note"] = "k_sw_pass + k_sw_mid, every dispatch of the step / problem-iterations"
     out["admm_kernel"] = kern
     # optional MFMA pass (SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-busy cycles summed over every
     # SIMD; GRBM_GUI_ACTIVE counts the dispatch's cycles summed over the 8 XCDs): busy
