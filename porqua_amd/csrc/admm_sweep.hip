@@ -33,7 +33,7 @@
 #define PQ_SW_X 0
 #endif
 #ifndef PQ_SW_RU
-#define PQ_SW_RU 4
+#define PQ_SW_RU 2
 #endif
 // (experiment builds only) PQ_SW_PROF: phase clocks of k_sw_pass in the spare partial slots
 #ifdef PQ_SW_PROF
