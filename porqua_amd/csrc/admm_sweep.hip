@@ -536,7 +536,10 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   __shared__ double sr[SR_N];
   __shared__ int s_cont;
 
-  const int grp = blockIdx.x / SW_G, g = blockIdx.x - grp * SW_G;
+  // XCD-contiguous slots: a group's problems on one XCD, so the 8-byte column writes of its Ut
+  // merge in one L2 (and its chunk partials were written on the same XCD by k_sw_pass)
+  const int slot = xcd_slot(blockIdx.x, gridDim.x);
+  const int grp = slot / SW_G, g = slot - grp * SW_G;
   const int b0 = gdates[grp];
   if (g >= gdates[grp + 1] - b0) return;
   const int b = b0 + g;

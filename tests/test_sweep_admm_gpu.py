@@ -124,3 +124,24 @@ def test_sweep_kernel_skips_solved_problems(device):
     assert torch.equal(ws.iters[done], it0[done])
     assert bool((ws.iters[~done] == it0[~done] + 6).all())
     assert bool((res.x[~done] - x0[~done]).abs().amax() > 0)
+
+
+def test_sweep_kernel_adaptive_rho_matches_grouped_kernel(device):
+    """Adaptive rho inside the sweep kernel: the rho requests (NEED_REFACTOR), the engine's
+    refactorisation and the resumed iterations agree with the grouped kernel's."""
+    lambdas = np.logspace(-1, 2, 24)
+    st = engine.Settings.from_params({**SWEEP_SETTINGS, "polish": 0, "max_iter": 14, "eps_grouped": 0.0,
+                                      "eps_abs": 1e-12, "eps_rel": 1e-12, "adapt_interval": 4,
+                                      "adapt_tol": 1.5})
+    sw_a, ra = _sweep(600, 2, lambdas, st, device, True)
+    sw_b, rb = _sweep(600, 2, lambdas, st, device, False)
+    assert ra.refactors > 0 and ra.refactors == rb.refactors, (ra.refactors, rb.refactors)
+    xa, _, _, ia, sa = _state(sw_a, ra)
+    xb, _, _, ib, sb = _state(sw_b, rb)
+    assert np.array_equal(ia, ib) and np.array_equal(sa, sb)
+    # the requested rho is a ratio of residual maxima, which carry the iterates' rounding
+    # differences (up to ~1e-7 relative after a few iterations, the first test above)
+    rho_a, rho_b = sw_a.ws.rho.cpu().numpy(), sw_b.ws.rho.cpu().numpy()
+    assert np.abs(rho_a / rho_b - 1.0).max() <= 1e-5, np.abs(rho_a / rho_b - 1.0).max()
+    sc = np.maximum(np.abs(xb).max(1), 1e-300)
+    assert (np.abs(xa - xb).max(1) / sc).max() <= 1e-6
