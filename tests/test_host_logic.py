@@ -456,3 +456,27 @@ def test_loose_stop_eps_rule():
     assert engine.loose_stop_eps(off, False, 9749, mg=21) == 0.0
     own = engine.Settings(eps_grouped_tracking=3e-2)
     assert engine.loose_stop_eps(own, False, 13) == 3e-2 and engine.loose_stop_eps(own, False, 4544) == 3e-2
+
+
+def test_sweep_plan_groups_and_applicability():
+    """engine.SweepPlan (the risk-aversion groups of pq_admm_lr_sweep): rows of up to 64
+    problems, a longer row split, and the kernel's shape conditions."""
+    sp = engine.SweepPlan([40, 70, 64], "cpu")
+    assert sp.gdates.tolist() == [0, 40, 104, 110, 174] and sp.ngroups == 4
+    assert engine.SweepPlan([], "cpu").ngroups == 0
+    n = 300
+    qb = engine.QPBatch(n, 174, 1, device="cpu", P=torch.empty(0, dtype=torch.float64))
+
+    class LR:
+        tmax = 252
+    assert sp.applicable(qb, LR(), 256)
+    LR.tmax = 300                       # window beyond the kernel's 256 rows
+    assert not sp.applicable(qb, LR(), 256)
+    LR.tmax = 252
+    assert not sp.applicable(qb, LR(), 320)   # capacitance beyond k_ld 256
+    q5 = engine.QPBatch(n, 174, 5, device="cpu", P=torch.empty(0, dtype=torch.float64))
+    assert not sp.applicable(q5, LR(), 256)   # more than 4 general rows
+    qs = engine.QPBatch(n, 174, 1, device="cpu", shared_constraints=False, P=torch.empty(0, dtype=torch.float64))
+    assert not sp.applicable(qs, LR(), 256)   # per-problem rows / boxes
+    need = _lib.load().pq_sweep_scratch_doubles(5000, 4096, 64)
+    assert need == 4096 * 80 + 64 * 20 * 64 * (256 + 16) + 64 * 256 * 64 + 64
