@@ -242,17 +242,20 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
   const int lr_id = s_row[lrow];
   const double* lsrc = panel + (int64_t)(lr_id < 0 ? 0 : lr_id) * ldp + 8 * lhalf;
   double sl[8];
+  // unconditional loads from clamped addresses, zeroed when stored: a conditional load is an
+  // exec-masked block whose else-branch zeroes the destination, a write-after-write that makes
+  // the compiler wait for every outstanding load there (s_waitcnt vmcnt(0)), which would
+  // expose the latency of the prefetches issued before it
+  int sl_i0 = 0;
   auto slab_load = [&](int i0) {
+    sl_i0 = i0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int ia = i0 + 8 * lhalf + e;
-      sl[e] = (lr_id >= 0 && ia < n) ? lsrc[i0 + e] : 0.0;
-    }
+    for (int e = 0; e < 8; ++e) sl[e] = lsrc[min(i0 + 8 * lhalf + e, n - 1) - 8 * lhalf];
   };
   auto slab_store = [&](int buf) {
     double* d = Xs + buf * (SW_K * SW_PX) + lrow * SW_PX + 8 * lhalf;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) d[e] = sl[e];
+    for (int e = 0; e < 8; ++e) d[e] = (lr_id >= 0 && sl_i0 + 8 * lhalf + e < n) ? sl[e] : 0.0;
   };
 
   // update roles: asset i0 + (t & 15), problems g = (t >> 4) + 32 e
@@ -263,27 +266,27 @@ __global__ __launch_bounds__(SW_T) void k_sw_pass(pq_lowrank lr, pq_problem pb, 
   // prefetched one sub-chunk ahead: the element state and the asset's shared values (every
   // value the updates read from memory, so their waits never cover the next prefetch)
   double px_[2], x_[2], zb_[2], yb_[2], q_[2], mu_, lo_, up_, cg_[MGA];
+  // (unconditional loads from clamped addresses, as for the slab: values of inactive or
+  // out-of-range elements are loaded but never used -- the updates run under act && inb)
   auto state_load = [&](int i0) {
-    const int ia = i0 + ui;
-    const bool inb = ia < n;
-    mu_ = (mu0 && inb) ? mu0[ia] : 0.0;
-    lo_ = inb ? pb.lb[ia] : 0.0;   // (shared box rows, host-checked)
-    up_ = inb ? pb.ub[ia] : 0.0;
+    const int ia = min(i0 + ui, n - 1);
+    mu_ = mu0 ? mu0[ia] : 0.0;
+    lo_ = pb.lb[ia];   // (shared box rows, host-checked)
+    up_ = pb.ub[ia];
 #pragma unroll
-    for (int r = 0; r < MGA; ++r) cg_[r] = (r < mg && inb) ? Cg0[(int64_t)r * ld + ia] : 0.0;
-    const double qa = (q_shared && inb) ? pb.q[(int64_t)b0 * pb.q_stride + ia] : 0.0;
+    for (int r = 0; r < MGA; ++r) cg_[r] = r < mg ? Cg0[(int64_t)r * ld + ia] : 0.0;
+    const double qa = q_shared ? pb.q[(int64_t)b0 * pb.q_stride + ia] : 0.0;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int g = ug + 32 * e;
-      const bool ok = g < G && inb && p_sc[g * SC_N + C_ACT] != 0.0;
       const int b = b0 + (g < G ? g : 0);
       // 32-bit element offsets (host-checked < 2^31): SGPR base + VGPR offset addressing
       const unsigned ox = (unsigned)(b * ld + ia), oz = (unsigned)(b * st.m_ld + st.mg_pad + ia);
-      x_[e] = ok ? st.x[ox] : 0.0;
-      zb_[e] = ok ? st.z[oz] : 0.0;
-      yb_[e] = ok ? st.y[oz] : 0.0;
-      px_[e] = (MODE == 1 && ok) ? st.Px[ox] : 0.0;
-      q_[e] = q_shared ? qa : (ok ? pb.q[(unsigned)(b * pb.q_stride + ia)] : 0.0);
+      x_[e] = st.x[ox];
+      zb_[e] = st.z[oz];
+      yb_[e] = st.y[oz];
+      px_[e] = MODE == 1 ? st.Px[ox] : 0.0;
+      q_[e] = q_shared ? qa : pb.q[(unsigned)(b * pb.q_stride + ia)];
     }
   };
 
