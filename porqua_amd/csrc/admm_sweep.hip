@@ -559,15 +559,18 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   const double* Mi = Minv_all + (int64_t)b * M_stride;
   constexpr int RU = PQ_SW_RU;   // rows per M^-1 load batch (two batches in flight)
   double m0[RU][4], m1[RU][4];
-  // rows j = w + 4 e of this wave; lane l holds columns l + 64 q.  A 64-column block is loaded
-  // when any of it is in the lower triangle (a wave-uniform test), masked in the arithmetic
+  // rows j = w + 4 e of this wave; lane l holds columns l + 64 q.  Blocks above the diagonal
+  // block (and rows past k) load the diagonal block again (an L2 hit, no HBM bytes): every load
+  // is unconditional, since a skipped load is an exec-masked branch whose zeroing of the
+  // destination makes the compiler wait for all outstanding loads; the arithmetic masks c <= j
   auto rload = [&](double (&M)[RU][4], int j0) {
 #pragma unroll
     for (int e = 0; e < RU; ++e) {
       const int j = j0 + 4 * e;
-      const double* rp = Mi + (int64_t)(j < k ? j : 0) * k_ld + l;
+      const int jj = j < k ? j : 0;
+      const double* rp = Mi + (int64_t)jj * k_ld + l;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) M[e][q] = (j < k && 64 * q <= j) ? rp[64 * q] : 0.0;
+      for (int q = 0; q < 4; ++q) M[e][q] = rp[64 * min(q, jj >> 6)];
     }
   };
   rload(m0, w);
@@ -576,20 +579,23 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
   double pcv[MGR > 0 ? MGR : 1];
   {
     const int j = t;   // SW_MT == SW_K: one window row per thread
-    if (j < T) {       // the chunk partials in chunk order, four loads in flight
+    {   // the chunk partials in chunk order, eight unconditional loads in flight (clamped to
+        // the last chunk, added as 0 past it: the same sums)
       const double* wp = Wp + ((int64_t)grp * nch * SW_G + g) * SW_K + j;
       const int64_t cs = (int64_t)SW_G * SW_K;
-      int c = 0;
-      for (; c + 4 <= nch; c += 4) {
-        const double v0 = wp[c * cs], v1 = wp[(c + 1) * cs], v2 = wp[(c + 2) * cs], v3 = wp[(c + 3) * cs];
-        Wj = (((Wj + v0) + v1) + v2) + v3;
+      for (int c = 0; c < nch; c += 8) {
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = wp[min(c + e, nch - 1) * cs];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Wj += c + e < nch ? v[e] : 0.0;
       }
-      for (; c < nch; ++c) Wj += wp[c * cs];
-      rowj = lr.rows[(int64_t)b0 * tmax + j];
+      if (j >= T) Wj = 0.0;
+      rowj = lr.rows[(int64_t)b0 * tmax + (j < T ? j : 0)];
     }
 #pragma unroll
     for (int r = 0; r < (MGR > 0 ? MGR : 1); ++r)
-      pcv[r] = (j < T && r < mg) ? pc[(int64_t)(rowj - r0) * ldpc + r] : 0.0;
+      pcv[r] = r < mg ? pc[(int64_t)(rowj - r0) * ldpc + r] : 0.0;   // (rows past T: times u = 0)
   }
   if (t < SR_N) sr[t] = R[t];
   if (t < RP_N) {   // four chunks' loads in flight at a time, combined in chunk order
@@ -597,14 +603,13 @@ __global__ __launch_bounds__(SW_MT) void k_sw_mid(pq_lowrank lr, pq_problem pb, 
     const double* rp = Rp + ((int64_t)grp * nch * SW_G + g) * RP_N + t;
     const int64_t cs = (int64_t)SW_G * RP_N;
     double a = 0.0;
-    int c = 0;
-    for (; c + 4 <= nch; c += 4) {
-      const double v0 = rp[c * cs], v1 = rp[(c + 1) * cs], v2 = rp[(c + 2) * cs], v3 = rp[(c + 3) * cs];
-      a = is_max ? fmax(fmax(fmax(fmax(a, v0), v1), v2), v3) : (((a + v0) + v1) + v2) + v3;
-    }
-    for (; c < nch; ++c) {
-      const double v = rp[c * cs];
-      a = is_max ? fmax(a, v) : a + v;
+    for (int c = 0; c < nch; c += 8) {   // (as the chunk partials above)
+      double v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = rp[min(c + e, nch - 1) * cs];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c + e < nch) a = is_max ? fmax(a, v[e]) : a + v[e];
     }
     red[t] = a;
   }

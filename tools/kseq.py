@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-dispatch kernel timeline of one bench step from a rocprofv3 kernel trace:
-python tools/kseq.py <run_kernel_trace.csv> [step index, default 1] [name prefix filter]"""
+python tools/kseq.py <run_kernel_trace.csv> [step index, default 1] [name prefix filter]
+[step's first kernel, default k_window_moments_grp; k_window_mean for the risk-aversion sweep]"""
 import collections
 import csv
 import sys
@@ -10,17 +11,18 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     step = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     pref = sys.argv[3] if len(sys.argv) > 3 else "k_"
+    first = sys.argv[4] if len(sys.argv) > 4 else "k_window_moments_grp"
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     seq = []
     for r in rows:
         k = r["Kernel_Name"]
-        for pre in ("void pq::", "pq::(anonymous namespace)::", "pq::", "k_"):   # (-T: truncated names)
+        for pre in ("void pq::", "pq::(anonymous namespace)::", "pq::", ""):   # (-T: truncated names)
             if k.startswith(pre):
-                k = (k if pre == "k_" else k[len(pre):]).split("(")[0]
+                k = k[len(pre):].split("(")[0]
                 seq.append((k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3,
                             int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
                 break
-    starts = [i for i, (k, *_) in enumerate(seq) if k.startswith("k_window_moments_grp")]
+    starts = [i for i, (k, *_) in enumerate(seq) if k.startswith(first)]
     i0 = starts[step]
     i1 = starts[step + 1] if len(starts) > step + 1 else len(seq)
     tot = collections.defaultdict(float)
