@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-dispatch kernel timeline of one bench step from a rocprofv3 kernel trace:
 python tools/kseq.py <run_kernel_trace.csv> [step index, default 1] [name prefix filter]
-[step's first kernel, default k_window_moments_grp; k_window_mean for the risk-aversion sweep]"""
+[step's first kernel, default k_window_moments_grp; k_window_mean:2 for the risk-aversion sweep,
+whose steps launch it twice]"""
 import collections
 import csv
 import sys
@@ -12,6 +13,8 @@ def main():
     step = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     pref = sys.argv[3] if len(sys.argv) > 3 else "k_"
     first = sys.argv[4] if len(sys.argv) > 4 else "k_window_moments_grp"
+    first, _, per = first.partition(":")
+    per = int(per or 1)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     seq = []
     for r in rows:
@@ -22,7 +25,7 @@ def main():
                 seq.append((k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3,
                             int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
                 break
-    starts = [i for i, (k, *_) in enumerate(seq) if k.startswith(first)]
+    starts = [i for i, (k, *_) in enumerate(seq) if k.startswith(first)][::per]
     i0 = starts[step]
     i1 = starts[step + 1] if len(starts) > step + 1 else len(seq)
     tot = collections.defaultdict(float)
