@@ -950,28 +950,47 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
         f64x4 z[NB];
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) z[nb] = f64x4{0.0, 0.0, 0.0, 0.0};
-        // unconditional loads (clamped row / column; rows past kU unused, B zero past NE), the
-        // next step's issued before this step's MFMA: NE reaches ~130 for monthly windows
-        auto edge_a = [&](int e0) -> double {
-          const int e = e0 + kq;
-          const int cu = e < NH ? e : T0 + (e - NH);
-          return Mi[(int64_t)(e < NE ? cu : 0) * k_ld + (ua < kU ? ua : 0)];
-        };
-        double av_next = edge_a(0);
-        for (int e0 = 0; e0 < NE; e0 += 4) {
-          const int e = e0 + kq;
-          const int cu = e < NH ? e : T0 + (e - NH);   // union row of edge e
-          const double av = av_next;
-          av_next = edge_a(e0 + 4);
+        // unconditional loads (clamped row / column; rows past kU unused, B zero past NE): the
+        // epilogue's q_b entries first, then the A entries of EB steps at a time before their
+        // MFMAs -- one step ahead left one load in flight, a memory round trip per step (NE is
+        // ~62 for daily windows, ~130 monthly), and the q_b loads under the epilogue's
+        // conditions were waited for one by one
+        double qv[NB][4];
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb) {
-            const int gl = gl0 + 16 * nb;
-            double bv = 0.0;
-            if (e < NE && gact[nb]) {
-              if (e < NH) bv = e < offg[nb] ? g_y[gl * CH_MAX + e] : 0.0;
-              else bv = cu >= offg[nb] + T0 ? g_y[gl * CH_MAX + (cu - T0)] : 0.0;
+        for (int nb = 0; nb < NB; ++nb) {
+          const int gl = gl0 + 16 * nb;
+          const double* Q = gc.aq + (int64_t)(d0 + (gl < G ? gl : 0)) * gc.aq_stride + k_ld;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int u = tile * 16 + kq + 4 * r;
+            qv[nb][r] = Q[u < kU ? u : 0];
+          }
+        }
+        constexpr int EB = 8;
+        for (int e00 = 0; e00 < NE; e00 += 4 * EB) {
+          double av[EB];
+#pragma unroll
+          for (int s = 0; s < EB; ++s) {
+            const int e = e00 + 4 * s + kq;
+            const int cu = e < NH ? e : T0 + (e - NH);
+            av[s] = Mi[(int64_t)(e < NE ? cu : 0) * k_ld + (ua < kU ? ua : 0)];
+          }
+#pragma unroll
+          for (int s = 0; s < EB; ++s) {
+            const int e0 = e00 + 4 * s;
+            if (e0 >= NE) break;   // (uniform)
+            const int e = e0 + kq;
+            const int cu = e < NH ? e : T0 + (e - NH);   // union row of edge e
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) {
+              const int gl = gl0 + 16 * nb;
+              double bv = 0.0;
+              if (e < NE && gact[nb]) {
+                if (e < NH) bv = e < offg[nb] ? g_y[gl * CH_MAX + e] : 0.0;
+                else bv = cu >= offg[nb] + T0 ? g_y[gl * CH_MAX + (cu - T0)] : 0.0;
+              }
+              z[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv, z[nb], 0, 0, 0);
             }
-            z[nb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, z[nb], 0, 0, 0);
           }
         }
         // lane holds rows tile * 16 + kq + 4 r of date gl
@@ -980,12 +999,11 @@ __global__ __launch_bounds__(CT * NB) __attribute__((amdgpu_waves_per_eu(2, 2)))
           const int gl = gl0 + 16 * nb;
           if (gact[nb]) {
             const double coef = g_coef[gl];
-            const double* Q = gc.aq + (int64_t)(d0 + gl) * gc.aq_stride + k_ld;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int u = tile * 16 + kq + 4 * r;
               if (u < kU) {
-                const double v = WU[u * CG + gl] - z[nb][r] + coef * Q[u];
+                const double v = WU[u * CG + gl] - z[nb][r] + coef * qv[nb][r];
                 if (u < U) UT[u * CG + gl] = gk.sqc * v;
                 else g_cw[gl * MGG + (u - U)] = s_sr[u - U] * v;
               }
