@@ -148,10 +148,19 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
   // ---- stable compaction of the free variables: wave w owns a contiguous index range ----
   const int seg = ((n + PW * 64 - 1) / (PW * 64)) * 64;
   const int lo = w * seg, hi = min(n, lo + seg);
+  // (every loop over a date's n entries below issues four steps' loads before using them,
+  // from clamped addresses: one load round trip per step made the setup ~140 serial round
+  // trips at n = 5000)
   int c = 0;
-  for (int i0 = lo; i0 < hi; i0 += 64) {
-    const int i = i0 + l;
-    c += __popcll(__ballot(i < hi && wk.fl[i] == 0));
+  for (int i0 = lo; i0 < hi; i0 += 4 * 64) {
+    int fv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 64 * u + l;
+      fv[u] = wk.fl[i < hi ? i : lo];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c += __popcll(__ballot(i0 + 64 * u + l < hi && fv[u] == 0));
   }
   if (l == 0) wcnt[w] = c;
   if (t == 0) {
@@ -212,12 +221,21 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     if (t == 0) R[R_STATE] = PQ_PG_FALLBACK;
     return;
   }
-  for (int i0 = lo; i0 < hi; i0 += 64) {
-    const int i = i0 + l;
-    const bool f = i < hi && wk.fl[i] == 0;
-    const unsigned long long m = __ballot(f);
-    if (f) wk.Fl[base + __popcll(m & ((1ull << l) - 1ull))] = i;
-    base += __popcll(m);
+  for (int i0 = lo; i0 < hi; i0 += 4 * 64) {
+    int fv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 64 * u + l;
+      fv[u] = wk.fl[i < hi ? i : lo];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 64 * u + l;
+      const bool f = i < hi && fv[u] == 0;
+      const unsigned long long m = __ballot(f);
+      if (f) wk.Fl[base + __popcll(m & ((1ull << l) - 1ull))] = i;
+      base += __popcll(m);
+    }
   }
   // ---- P_FF reuse: every free variable in the free list of the last form (the usual later
   //      round only fixes variables) -> the solve gathers P_FF from K ---------------------------
@@ -230,12 +248,26 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
   }
   // ---- fixed values, nzb -------------------------------------------------------------------
   int nzb = 0;
-  for (int i = t; i < ld; i += PT) {
-    const int f = wk.fl[i];
-    const double v = i < n ? (f == 1 ? lb[i] : (f == 2 ? ub[i] : 0.0)) : 0.0;
-    wk.xb[i] = v;
-    if (k == 0) wk.xs[i] = v;
-    nzb |= (v != 0.0);
+  for (int i0 = t; i0 < ld; i0 += 4 * PT) {
+    int fv[4];
+    double lv[4], uv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * PT, ic = i < n ? i : 0;
+      fv[u] = wk.fl[i < ld ? i : 0];
+      lv[u] = has_box ? lb[ic] : 0.0;
+      uv[u] = has_box ? ub[ic] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * PT;
+      if (i >= ld) continue;
+      const int f = fv[u];
+      const double v = i < n ? (f == 1 ? lv[u] : (f == 2 ? uv[u] : 0.0)) : 0.0;
+      wk.xb[i] = v;
+      if (k == 0) wk.xs[i] = v;
+      nzb |= (v != 0.0);
+    }
   }
   nzb = block_or(nzb, red);   // barrier: Fl complete below
   // ---- d_a = rhs_a - C_aB x_B ----------------------------------------------------------------
@@ -243,7 +275,18 @@ __global__ __launch_bounds__(PT) void k_pg_setup(pq_problem pb, pq_state st, dou
     const int r = s_al[a];
     const double* cr = Cg + (int64_t)r * ld;
     double sum = 0.0;
-    for (int j = l; j < n; j += 64) sum += cr[j] * wk.xb[j];
+    for (int j0 = l; j0 < n; j0 += 8 * 64) {   // (the same per-lane order, eight loads ahead)
+      double cv[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + 64 * u, jc = j < n ? j : 0;
+        cv[u] = cr[jc];
+        xv[u] = wk.xb[jc];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j0 + 64 * u < n) sum += cv[u] * xv[u];
+    }
     sum = wave_sum(sum);
     if (l == 0) R[R_DA + a] = (R[R_ACT + r] == 1.0 ? lg[r] : ug[r]) - sum;
   }
@@ -2076,6 +2119,25 @@ __global__ __launch_bounds__(QT) void k_pg_passB(pq_lowrank lr, pq_problem pb, p
 // per-date passes are load-latency bound, 4 loads per thread and vector at n = 1000 instead
 // of 16 with one wave)
 constexpr int PPT = 256;
+// sum over j = hl, hl + PPT, ... < n of a[j] b[j], in that order: four steps' loads issued
+// together (clamped, unconditional), so a long row (n = 5000: 20 steps) is 5 load round trips
+// instead of 20 -- the same sum
+__device__ __forceinline__ double row_dot4(const double* a, const double* b, int n, int hl) {
+  double sum = 0.0;
+  for (int j0 = hl; j0 < n; j0 += 4 * PPT) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * PPT, jc = j < n ? j : 0;
+      av[u] = a[jc];
+      bv[u] = b[jc];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (j0 + u * PPT < n) sum += av[u] * bv[u];
+  }
+  return sum;
+}
 template <int MODE>
 __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, pq_state st, double* rec,
                                                 pq_settings s, const int32_t* gdates, int ngroups,
@@ -2183,8 +2245,7 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
   // general rows: Cg x, activity checks (lane 0 decides, as the reference kernel's lane 0)
   for (int r = 0; r < mg; ++r) {
     const double* cr = Cg + (int64_t)r * ld;
-    double sum = 0.0;
-    for (int j = hl; j < n; j += PPT) sum += cr[j] * wk.xs[j];
+    double sum = row_dot4(cr, wk.xs, n, hl);
     sum = block_sum(sum, red);
     // a vertex whose bound variables overshoot its equality row (the round before fixed
     // several free variables at their upper bounds at once, e.g. two weights past 1 under a
@@ -2229,24 +2290,44 @@ __global__ __launch_bounds__(PPT) void k_pg_post(pq_lowrank lr, pq_problem pb, p
   double* sz = st.z + (int64_t)b * st.m_ld;
   double* sy = st.y + (int64_t)b * st.m_ld;
   double xpx = 0.0, qx = 0.0, pres = 0.0, dres = 0.0, gapb = 0.0;
-  for (int i = hl; i < n; i += PPT) {
-    const double xi = wk.xs[i];
-    double zb = 0.0;
-    if (has_box) zb = wk.fl[i] ? -wk.g[i] : 0.0;
-    xpx += xi * wk.Px[i];
-    qx += q[i] * xi;
-    dres = fmax(dres, fabs(wk.g[i] + zb));
-    if (has_box) {
-      if (!isinf(lb[i])) { pres = fmax(pres, lb[i] - xi); gapb += lb[i] * fmin(zb, 0.0); }
-      if (!isinf(ub[i])) { pres = fmax(pres, xi - ub[i]); gapb += ub[i] * fmax(zb, 0.0); }
-      sy[st.mg_pad + i] = zb;
+  // (four of the thread's elements per step, every load issued first, as in the checks above;
+  // the same sums in the same order)
+  for (int i0 = hl; i0 < n; i0 += 4 * PPT) {
+    double xv[4], pv[4], gv[4], qv[4], lbv[4], ubv[4];
+    int fv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * PPT, ic = i < n ? i : 0;
+      xv[j] = wk.xs[ic];
+      pv[j] = wk.Px[ic];
+      gv[j] = wk.g[ic];
+      qv[j] = q[ic];
+      fv[j] = wk.fl[ic];
+      lbv[j] = has_box ? lb[ic] : 0.0;
+      ubv[j] = has_box ? ub[ic] : 0.0;
     }
-    sx[i] = xi;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * PPT;
+      if (i >= n) continue;
+      const double xi = xv[j];
+      double zb = 0.0;
+      if (has_box) zb = fv[j] ? -gv[j] : 0.0;
+      xpx += xi * pv[j];
+      qx += qv[j] * xi;
+      dres = fmax(dres, fabs(gv[j] + zb));
+      if (has_box) {
+        const double lbi = lbv[j], ubi = ubv[j];
+        if (!isinf(lbi)) { pres = fmax(pres, lbi - xi); gapb += lbi * fmin(zb, 0.0); }
+        if (!isinf(ubi)) { pres = fmax(pres, xi - ubi); gapb += ubi * fmax(zb, 0.0); }
+        sy[st.mg_pad + i] = zb;
+      }
+      sx[i] = xi;
+    }
   }
   for (int r = 0; r < mg; ++r) {
     const double* cr = Cg + (int64_t)r * ld;
-    double sum = 0.0;
-    for (int j = hl; j < n; j += PPT) sum += cr[j] * wk.xs[j];
+    double sum = row_dot4(cr, wk.xs, n, hl);
     sum = block_sum(sum, red);
     const double lam = lamof(r);
     double v;
