@@ -24,10 +24,22 @@ __global__ __launch_bounds__(256) void k_window_mean(const double* panel, int64_
   const int T = tlen[b];
   const int32_t* rw = rows + (int64_t)b * tmax;
   double s = 0.0;
-  if (geo) {
-    for (int k = 0; k < T; ++k) s += log(1.0 + panel[(int64_t)rw[k] * ldp + j]);
+  // (unrolled: eight rows' loads in flight per thread instead of one round trip per row -- the
+  // same sums in the same order)
+  if (geo) {   // (the loads gathered before the logarithms, whose branches would otherwise
+               // wait for every outstanding load)
+    int k = 0;
+    for (; k + 8 <= T; k += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = panel[(int64_t)rw[k + u] * ldp + j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += log(1.0 + v[u]);
+    }
+    for (; k < T; ++k) s += log(1.0 + panel[(int64_t)rw[k] * ldp + j]);
     mu[(int64_t)b * mu_stride + j] = exp(s / T) - 1.0;
   } else {
+#pragma unroll 8
     for (int k = 0; k < T; ++k) s += panel[(int64_t)rw[k] * ldp + j];
     mu[(int64_t)b * mu_stride + j] = s / T;
   }
@@ -45,6 +57,7 @@ __global__ __launch_bounds__(256) void k_window_sumsq(const double* panel, int64
   const int32_t* rw = rows + (int64_t)b * tmax;
   const double m = mu ? mu[(int64_t)b * mu_stride + j] : 0.0;
   double s = 0.0;
+#pragma unroll 8
   for (int k = 0; k < T; ++k) {
     const double d = panel[(int64_t)rw[k] * ldp + j] - m;
     s = fma(d, d, s);
@@ -117,17 +130,43 @@ __global__ __launch_bounds__(256) void k_window_geomean_grp(const double* panel,
   const int d0 = gdates[g], d1 = gdates[g + 1];
   const int32_t* ur = urows + (int64_t)g * umax;
   const int T = tlen[d0];
-  auto lx = [&](int u) { return log(1.0 + panel[(int64_t)ur[u] * ldp + j]); };
+  // the rows' loads gathered before their logarithms (whose branches would otherwise wait for
+  // every outstanding load): 8 at a time for the first window, 4 for the entering / leaving
+  // runs -- the same sums in the same order
+  auto xv = [&](int u) { return panel[(int64_t)ur[u] * ldp + j]; };
   int lo = uoff[d0], hi = lo + T;
   double s = 0.0;
-#pragma unroll 8
-  for (int u = lo; u < hi; ++u) s += lx(u);
+  {
+    int u = lo;
+    for (; u + 8 <= hi; u += 8) {
+      double v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = xv(u + e);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += log(1.0 + v[e]);
+    }
+    for (; u < hi; ++u) s += log(1.0 + xv(u));
+  }
   for (int b = d0;; ) {
     mu[(int64_t)b * mu_stride + j] = exp(s / T) - 1.0;
     if (++b >= d1) break;
     const int nlo = uoff[b], nhi = nlo + T;
-    for (int u = hi; u < nhi; ++u) s += lx(u);    // entering
-    for (int u = lo; u < nlo; ++u) s -= lx(u);    // leaving
+    for (int u = hi; u < nhi; u += 4) {   // entering
+      double v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = xv(min(u + e, nhi - 1));
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (u + e < nhi) s += log(1.0 + v[e]);
+    }
+    for (int u = lo; u < nlo; u += 4) {   // leaving
+      double v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = xv(min(u + e, nlo - 1));
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (u + e < nlo) s -= log(1.0 + v[e]);
+    }
     lo = nlo;
     hi = nhi;
   }
