@@ -157,41 +157,62 @@ __global__ __launch_bounds__(256) void k_band_gram(const double* panel, int64_t 
   if (J < 0 || TB * Jd - (TB - 1) >= W) return;   // uniform: no lag of this tile in [0, W)
   const int t = threadIdx.x, i = t >> 2, cc = (t & 3) * 4;
   const int ra = I * TB + i, rb = J * TB + i;
-  const double* pa = ra < nrows ? panel + (int64_t)(r0 + ra) * ldp : nullptr;
-  const double* pq_ = rb < nrows ? panel + (int64_t)(r0 + rb) * ldp : nullptr;
+  // unconditional loads from clamped rows / columns, zeroed when staged, and a ring of four
+  // chunks in registers: each chunk's loads are issued four chunks ahead of its MFMAs (one
+  // chunk ahead under lane conditions waited for every load, a round trip per 16 columns)
+  const bool aok = ra < nrows, bok = rb < nrows;
+  const double* pa = panel + (int64_t)(r0 + (aok ? ra : 0)) * ldp;
+  const double* pq_ = panel + (int64_t)(r0 + (bok ? rb : 0)) * ldp;
   auto load = [&](double (&v)[4], const double* p, int c0) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int c = c0 + cc + e;
-      v[e] = (p && c < n) ? p[c] : 0.0;
+      v[e] = p[c < n ? c : 0];
     }
   };
-  auto store = [&](const double (&v)[4], double* S) {
+  auto store = [&](const double (&v)[4], double* S, bool ok, int c0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) S[(cc + e) * LDW + i] = v[e];
+    for (int e = 0; e < 4; ++e) S[(cc + e) * LDW + i] = (ok && c0 + cc + e < n) ? v[e] : 0.0;
   };
+  constexpr int D = 4;
+  const int nc = (n + KC - 1) / KC;
   Acc acc;
   acc.zero();
-  double va[4], vb[4];
-  load(va, pa, 0);
-  load(vb, pq_, 0);
-  store(va, smem);
-  store(vb, smem + STAGE);
+  double va[D][4], vb[D][4];
+  load(va[0], pa, 0);
+  load(vb[0], pq_, 0);
+#pragma unroll
+  for (int s2 = 1; s2 < D; ++s2)
+    if (s2 < nc) {   // (uniform)
+      load(va[s2], pa, s2 * KC);
+      load(vb[s2], pq_, s2 * KC);
+    }
+  store(va[0], smem, aok, 0);
+  store(vb[0], smem + STAGE, bok, 0);
+  if (D < nc) {
+    load(va[0], pa, D * KC);
+    load(vb[0], pq_, D * KC);
+  }
   __syncthreads();
   int buf = 0;
-  for (int c0 = 0; c0 < n; c0 += KC) {
-    const bool more = c0 + KC < n;
-    if (more) {
-      load(va, pa, c0 + KC);
-      load(vb, pq_, c0 + KC);
+  for (int c = 0; c < nc; c += D) {
+#pragma unroll
+    for (int s2 = 0; s2 < D; ++s2) {
+      const int cur = c + s2;
+      if (cur >= nc) break;   // (uniform)
+      mma_lds(acc, smem + buf * 2 * STAGE, smem + buf * 2 * STAGE + STAGE, KC);
+      const int nx = cur + 1;   // chunk nx lives in slot nx % D = (s2 + 1) % D
+      if (nx < nc) {
+        store(va[(s2 + 1) % D], smem + (buf ^ 1) * 2 * STAGE, aok, nx * KC);
+        store(vb[(s2 + 1) % D], smem + (buf ^ 1) * 2 * STAGE + STAGE, bok, nx * KC);
+        if (nx + D < nc) {   // refill the slot with chunk nx + D
+          load(va[(s2 + 1) % D], pa, (nx + D) * KC);
+          load(vb[(s2 + 1) % D], pq_, (nx + D) * KC);
+        }
+      }
+      __syncthreads();
+      buf ^= 1;
     }
-    mma_lds(acc, smem + buf * 2 * STAGE, smem + buf * 2 * STAGE + STAGE, KC);
-    if (more) {
-      store(va, smem + (buf ^ 1) * 2 * STAGE);
-      store(vb, smem + (buf ^ 1) * 2 * STAGE + STAGE);
-    }
-    __syncthreads();
-    buf ^= 1;
   }
 #pragma unroll
   for (int m = 0; m < 2; ++m)
